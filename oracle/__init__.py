@@ -1,0 +1,135 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes bindings of the fp64 C restatement
+(oracle/frt_oracle.c -> oracle/liboracle.so).
+
+Importable only from tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, as the checker.  The product (first_raytracer_amd) never
+imports this package.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+_lib = None
+
+
+class Counters(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "node_visits", "box_passes", "tri_tests", "sphere_tests",
+        "camera_rays", "extension_rays", "shadow_rays", "samples")]
+
+    @property
+    def rays(self):
+        return self.camera_rays + self.extension_rays + self.shadow_rays
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+
+
+class SceneInfo(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "n_tris", "n_spheres", "n_materials", "n_lights", "n_nodes", "world_kind", "n_list", "bvh_depth")]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("oracle/liboracle.so missing: run `make -C oracle` (or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        dp = ctypes.POINTER(ctypes.c_double)
+        L.ora_load_scene.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_double, ctypes.POINTER(ctypes.c_void_p)]
+        L.ora_free_scene.argtypes = [ctypes.c_void_p]
+        L.ora_scene_get_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(SceneInfo)]
+        L.ora_scene_export_bvh.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.ora_scene_export_tris.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.ora_render.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
+                                 ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(Counters)]
+        L.ora_world_hit.argtypes = [ctypes.c_void_p, dp, dp, ctypes.c_double, ctypes.c_double, dp,
+                                    ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(Counters)]
+        L.ora_rng_uniform.argtypes = [ctypes.c_uint32] * 4
+        L.ora_rng_uniform.restype = ctypes.c_double
+        L.ora_kat_tri_hit.argtypes = [dp, dp, ctypes.c_int, dp, dp, ctypes.c_double, ctypes.c_double, dp]
+        L.ora_kat_sphere_hit.argtypes = [dp, ctypes.c_double, dp, dp, ctypes.c_double, ctypes.c_double, dp]
+        L.ora_kat_aabb_hit.argtypes = [dp, dp, dp, dp, ctypes.c_double, ctypes.c_double]
+        L.ora_kat_camera.argtypes = [dp, dp, dp, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                     ctypes.c_double, ctypes.c_double, dp, dp]
+        L.ora_kat_cosine.argtypes = [dp, dp, dp]
+        L.ora_kat_tri_sample.argtypes = [dp, dp, ctypes.c_int, ctypes.c_int, dp, dp, dp]
+        L.ora_kat_sphere_sample.argtypes = [dp, ctypes.c_double, dp, dp, dp]
+        L.ora_kat_miweight.argtypes = [ctypes.c_double, ctypes.c_double]
+        L.ora_kat_miweight.restype = ctypes.c_double
+        L.ora_kat_fromsrgb.argtypes = [ctypes.c_double]
+        L.ora_kat_fromsrgb.restype = ctypes.c_double
+        L.ora_kat_atof.argtypes = [ctypes.c_char_p]
+        L.ora_kat_atof.restype = ctypes.c_float
+        L.ora_kat_pick.argtypes = [ctypes.c_double, ctypes.c_int]
+        L.ora_kat_sort.argtypes = [dp, ctypes.c_int, ctypes.c_void_p]
+        L.ora_kat_list_hit.argtypes = [ctypes.c_int, ctypes.c_int, dp, dp, dp, dp]
+        L.ora_write_pfm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, dp]
+        _lib = L
+    return _lib
+
+
+def darr(x):
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+    return a, a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+class OracleScene:
+    """Scene built by the restated reference constructors (main.cpp:222-314)."""
+
+    def __init__(self, kind, obj_path, aspect):
+        self.ptr = ctypes.c_void_p()
+        rc = lib().ora_load_scene(kind.encode(), obj_path.encode(), float(aspect), ctypes.byref(self.ptr))
+        if rc != 0:
+            raise RuntimeError(f"ora_load_scene({kind}, {obj_path}) failed: {rc}")
+        self.info = SceneInfo()
+        lib().ora_scene_get_info(self.ptr, ctypes.byref(self.info))
+
+    def __del__(self):
+        if getattr(self, "ptr", None) and lib is not None:
+            try:
+                lib().ora_free_scene(self.ptr)
+            except Exception:
+                pass
+            self.ptr = None
+
+    def bvh(self):
+        n = self.info.n_nodes
+        boxes = np.zeros((max(n, 1), 6)); left = np.zeros(max(n, 1), np.int32); right = np.zeros(max(n, 1), np.int32)
+        lib().ora_scene_export_bvh(self.ptr, boxes.ctypes.data, left.ctypes.data, right.ctypes.data)
+        return boxes[:n], left[:n], right[:n]
+
+    def tris(self):
+        n = self.info.n_tris
+        v = np.zeros((max(n, 1), 9)); m = np.zeros(max(n, 1), np.int32)
+        lib().ora_scene_export_tris(self.ptr, v.ctypes.data, m.ctypes.data)
+        return v[:n], m[:n]
+
+    def render(self, nx, ny, spp, seed=0, pixels=None, nthreads=None):
+        """Mean radiance per pixel (viewer::add_sample semantics) + counters."""
+        if pixels is None:
+            pixels = np.arange(nx * ny, dtype=np.int32)
+        pixels = np.ascontiguousarray(pixels, dtype=np.int32)
+        out = np.zeros((len(pixels), 3))
+        cnt = Counters()
+        nthreads = nthreads or min(16, os.cpu_count() or 1)
+        rc = lib().ora_render(self.ptr, nx, ny, spp, seed, pixels.ctypes.data, len(pixels), nthreads,
+                              out.ctypes.data, ctypes.byref(cnt))
+        if rc != 0:
+            raise RuntimeError(f"ora_render failed: {rc}")
+        return out, cnt
+
+    def world_hit(self, o, d, tmin, tmax):
+        oa, op = darr(o); da, dptr = darr(d)
+        t = ctypes.c_double(); prim = ctypes.c_int32(); cnt = Counters()
+        ok = lib().ora_world_hit(self.ptr, op, dptr, tmin, tmax, ctypes.byref(t), ctypes.byref(prim), ctypes.byref(cnt))
+        return bool(ok), t.value, prim.value, cnt
+
+
+def rng_uniform(seed, pixel, sample, dim):
+    return lib().ora_rng_uniform(seed, pixel, sample, dim)

@@ -1,0 +1,1284 @@
+/*
+ * frt_oracle.c -- TEST INFRASTRUCTURE ONLY.  See frt_oracle.h.
+ *
+ * fp64 CPU restatement of jammm/first_raytracer's path::Li hot path.  Every
+ * arithmetic expression keeps the reference's operand order so the component
+ * functions are bit-identical to the reference's own code (pinned by
+ * tests/golden/kat_*.json, produced by oracle/_ref/ref_kat built from the
+ * reference sources).  File:line citations are relative to
+ * /root/reference/first_ray/.
+ *
+ * Build: see oracle/Makefile (gcc -O2 -ffp-contract=off, no -march: the
+ * reference's x86-64 doubles are not FMA-contracted either).
+ */
+#define _GNU_SOURCE
+#include "frt_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#ifndef M_PI
+#define M_PI 3.14159265358979323846
+#endif
+
+/* util.h:10-12 */
+static const double EPSILON = 1e-4;
+static const double SHADOW_EPSILON = (double)1e-3f;
+
+/* ------------------------------------------------------------------------ */
+/* RNG stream spec (DESIGN.md "RNG stream spec"; identical in csrc/frt_rng.h) */
+/* ------------------------------------------------------------------------ */
+static inline uint32_t mix32(uint32_t x)
+{
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x;
+}
+typedef struct { uint32_t k0, k1; } rng_key;
+static inline rng_key rng_make(uint32_t seed, uint32_t pixel, uint32_t sample)
+{
+    uint32_t a = mix32(seed ^ 0x2545F491U);
+    rng_key k;
+    k.k0 = mix32(mix32(a ^ pixel) + sample * 0x9E3779B9U);
+    k.k1 = mix32(mix32(a + pixel * 0x632BE5ABU) ^ (sample * 0x85157AF5U + 0x5851F42DU));
+    return k;
+}
+static inline double rng_u(rng_key k, uint32_t dim)
+{
+    uint32_t h = mix32(mix32(k.k0 ^ (dim * 0x85EBCA77U + 0xC2B2AE3DU)) + k.k1);
+    return (double)(h >> 8) * (1.0 / 16777216.0);
+}
+double ora_rng_uniform(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t dim)
+{
+    return rng_u(rng_make(seed, pixel, sample), dim);
+}
+/* dimension layout: camera 0..3 (path.cpp:131-133); bounce at depth d uses
+ * base = 4 + 8 d: scatter get3d +0..2 (path.cpp:36), light pick get1d +3
+ * (path.cpp:39), light sample get2d +4..5 (path.cpp:45), bsdf get2d +6..7
+ * (path.cpp:99). */
+#define DIM_BOUNCE(d) (4u + 8u * (uint32_t)(d))
+
+/* ------------------------------------------------------------------------ */
+/* Vector3f (geometry.h:297-547), fp64                                       */
+/* ------------------------------------------------------------------------ */
+typedef struct { double e[3]; } v3;
+static inline v3 mk(double x, double y, double z) { v3 r; r.e[0] = x; r.e[1] = y; r.e[2] = z; return r; }
+static inline v3 vadd(v3 a, v3 b) { return mk(a.e[0] + b.e[0], a.e[1] + b.e[1], a.e[2] + b.e[2]); }
+static inline v3 vsub(v3 a, v3 b) { return mk(a.e[0] - b.e[0], a.e[1] - b.e[1], a.e[2] - b.e[2]); }
+static inline v3 vmul(v3 a, v3 b) { return mk(a.e[0] * b.e[0], a.e[1] * b.e[1], a.e[2] * b.e[2]); }
+static inline v3 smul(double t, v3 v) { return mk(t * v.e[0], t * v.e[1], t * v.e[2]); }  /* t*v and v*t */
+static inline v3 sdiv(v3 v, double t) { return mk(v.e[0] / t, v.e[1] / t, v.e[2] / t); }  /* v / t      */
+static inline v3 vneg(v3 v) { return mk(-v.e[0], -v.e[1], -v.e[2]); }
+static inline double dot(v3 a, v3 b) { return a.e[0] * b.e[0] + a.e[1] * b.e[1] + a.e[2] * b.e[2]; }
+static inline v3 cross(v3 a, v3 b)
+{
+    return mk((a.e[1] * b.e[2]) - (a.e[2] * b.e[1]),
+              (a.e[2] * b.e[0]) - (a.e[0] * b.e[2]),
+              (a.e[0] * b.e[1]) - (a.e[1] * b.e[0]));
+}
+static inline double vlen(v3 v) { return sqrt(v.e[0] * v.e[0] + v.e[1] * v.e[1] + v.e[2] * v.e[2]); }
+static inline double vlen2(v3 v) { return v.e[0] * v.e[0] + v.e[1] * v.e[1] + v.e[2] * v.e[2]; }
+static inline v3 unit(v3 v) { return sdiv(v, vlen(v)); }                       /* geometry.h:468 */
+static inline v3 make_unit(v3 v)                                             /* geometry.h:372 */
+{
+    double k = 1.0 / sqrt(v.e[0] * v.e[0] + v.e[1] * v.e[1] + v.e[2] * v.e[2]);
+    return mk(v.e[0] * k, v.e[1] * k, v.e[2] * k);
+}
+static inline v3 vscale_inplace(v3 v, double t) { return mk(v.e[0] * t, v.e[1] * t, v.e[2] * t); } /* *= t */
+static inline v3 vdiv_inplace(v3 v, double t)                                /* /= t: *= 1/t */
+{
+    double k = 1.0 / t;
+    return mk(v.e[0] * k, v.e[1] * k, v.e[2] * k);
+}
+static inline v3 vload(const double *p) { return mk(p[0], p[1], p[2]); }
+static inline void vstore(double *p, v3 v) { p[0] = v.e[0]; p[1] = v.e[1]; p[2] = v.e[2]; }
+static inline double std_max(double a, double b) { return (a < b) ? b : a; }   /* std::max */
+
+/* util.h:55-60 */
+static inline double miWeight(double pdf1, double pdf2)
+{
+    pdf1 *= pdf1;
+    pdf2 *= pdf2;
+    return pdf1 / (pdf1 + pdf2);
+}
+/* util.h:62-66 */
+static inline double FromSrgb(double v)
+{
+    if (v <= 0.04045) return v * (1.0 / 12.92);
+    return pow((v + 0.055) * (1.0 / 1.055), 2.4);
+}
+
+/* ------------------------------------------------------------------------ */
+/* ray / aabb / onb                                                         */
+/* ------------------------------------------------------------------------ */
+typedef struct { v3 o, d; } ray;
+static inline v3 ray_at(const ray *r, double t) { return vadd(r->o, smul(t, r->d)); } /* ray.h:13 */
+
+typedef struct { v3 min, max, size; } aabb;                                   /* aabb.h:6-68 */
+static inline aabb aabb_mk(v3 lo, v3 hi) { aabb b; b.min = lo; b.max = hi; b.size = vsub(hi, lo); return b; }
+static inline int aabb_hit(const aabb *b, const ray *r, double tmin, double tmax) /* aabb.h:14-31 */
+{
+    for (int i = 0; i < 3; ++i) {
+        double invD = 1.0 / r->d.e[i];
+        double t0 = (b->min.e[i] - r->o.e[i]) * invD;
+        double t1 = (b->max.e[i] - r->o.e[i]) * invD;
+        if (invD < 0.0) { double tt = t0; t0 = t1; t1 = tt; }
+        tmin = t0 > tmin ? t0 : tmin;
+        tmax = t1 < tmax ? t1 : tmax;
+        if (tmax < tmin) return 0;
+    }
+    return 1;
+}
+static inline int aabb_longest_axis(const aabb *b)                           /* aabb.h:33-43 */
+{
+    int axis = 0;
+    if (b->size.e[1] > b->size.e[0]) axis = 1;
+    else if (b->size.e[2] > b->size.e[0]) axis = 2;
+    return axis;
+}
+static inline double aabb_area(const aabb *b)                                /* aabb.h:46-49 */
+{
+    return 2 * ((b->size.e[0] * b->size.e[1]) + (b->size.e[1] * b->size.e[2]) + (b->size.e[0] * b->size.e[2]));
+}
+static inline aabb surrounding_box(aabb b0, aabb b1)                         /* aabb.h:57-68 */
+{
+    v3 small = mk(fmin(b0.min.e[0], b1.min.e[0]), fmin(b0.min.e[1], b1.min.e[1]), fmin(b0.min.e[2], b1.min.e[2]));
+    v3 big = mk(fmax(b0.max.e[0], b1.max.e[0]), fmax(b0.max.e[1], b1.max.e[1]), fmax(b0.max.e[2], b1.max.e[2]));
+    return aabb_mk(small, big);
+}
+
+typedef struct { v3 axis[3]; } onb;                                          /* onb.h:6-33 */
+static inline onb onb_from_w(v3 n)
+{
+    onb b;
+    b.axis[2] = n;
+    if (fabs(n.e[0]) > fabs(n.e[1])) {
+        double invLen = 1.0 / sqrt(n.e[0] * n.e[0] + n.e[2] * n.e[2]);
+        b.axis[1] = mk(n.e[2] * invLen, (double)0.0f, -n.e[0] * invLen);
+    } else {
+        double invLen = 1.0 / sqrt(n.e[1] * n.e[1] + n.e[2] * n.e[2]);
+        b.axis[1] = mk(0.0, n.e[2] * invLen, -n.e[1] * invLen);
+    }
+    b.axis[0] = cross(b.axis[1], b.axis[2]);
+    return b;
+}
+static inline v3 onb_from_local(const onb *b, v3 a)                          /* onb.h:16 */
+{
+    return vadd(vadd(smul(a.e[0], b->axis[0]), smul(a.e[1], b->axis[1])), smul(a.e[2], b->axis[2]));
+}
+
+/* pdf.h:13-23 */
+static inline v3 hemisphere_to_cosine_direction(double r0, double r1)
+{
+    const double r = sqrt(r0);
+    const double phi = 2 * (double)M_PI * r1;
+    const double x = r * cos(phi);
+    const double y = r * sin(phi);
+    return mk(x, y, sqrt(1 - r0));
+}
+/* pdf.h:38-44 */
+static inline v3 uniform_sample_sphere(double u0, double u1)
+{
+    const double z = 1 - 2 * u0;
+    const double r = sqrt(std_max((double)0, (double)1 - z * z));
+    const double phi = 2 * (double)M_PI * u1;
+    return mk(r * cos(phi), r * sin(phi), z);
+}
+/* pdf.h:46-56 */
+static inline v3 random_to_sphere(double radius, double distance_squared, double r1, double r2)
+{
+    double z = 1 + r2 * (sqrt(1 - radius * radius / distance_squared) - 1);
+    double phi = 2 * (double)M_PI * r1;
+    double x = cos(phi) * sqrt(1 - z * z);
+    double y = sin(phi) * sqrt(1 - z * z);
+    return mk(x, y, z);
+}
+/* cosine_pdf (pdf.h:80-97): value uses uvw.w() == the normal */
+static inline double cosine_pdf_value(v3 w, v3 direction)
+{
+    double c = dot(w, unit(direction));
+    double cosine = (c < 0.0) ? 0.0 : c;   /* std::max<double>(c, 0.0) */
+    return cosine / (double)M_PI;
+}
+
+/* util.h:21-41 */
+static inline void random_in_unit_disk(double s0, double s1, double *ox, double *oy)
+{
+    double a = s0 * 2.0 - 1.0, b = s1 * 2.0 - 1.0;
+    if (a == 0.0 && b == 0.0) { *ox = 0.0; *oy = 0.0; return; }
+    double a2 = a * a, b2 = b * b, phi, r;
+    if (a2 > b2) { r = a; phi = (M_PI / 4.0) * (b / a); }
+    else { r = b; phi = (M_PI / 2.0) - (M_PI / 4.0) * (a / b); }
+    double cosphi = cos(phi), sinphi = sin(phi);
+    *ox = r * cosphi; *oy = r * sinphi;
+}
+
+/* ------------------------------------------------------------------------ */
+/* camera (camera.h:10-35)                                                  */
+/* ------------------------------------------------------------------------ */
+typedef struct { v3 origin, llc, horizontal, vertical, u, v, w; double lens_radius; } camera;
+static camera camera_mk(v3 lookfrom, v3 lookat, v3 vup, double vfov, double aspect, double aperture, double focus_dist)
+{
+    camera c;
+    c.lens_radius = aperture / 2;
+    double theta = vfov * (double)M_PI / 180.0;
+    double half_height = tan(theta / 2);
+    double half_width = aspect * half_height;
+    c.origin = lookfrom;
+    c.w = unit(vsub(lookfrom, lookat));
+    c.u = unit(cross(vup, c.w));
+    c.v = cross(c.w, c.u);
+    c.llc = vsub(vsub(vsub(c.origin, smul(half_width * focus_dist, c.u)), smul(half_height * focus_dist, c.v)),
+                 smul(focus_dist, c.w));
+    c.horizontal = smul(2 * half_width * focus_dist, c.u);
+    c.vertical = smul(2 * half_height * focus_dist, c.v);
+    return c;
+}
+static inline ray camera_get_ray(const camera *c, double s, double t, double l0, double l1)
+{
+    double rx, ry;
+    if (c->lens_radius == 0) { rx = c->lens_radius; ry = c->lens_radius; }
+    else { random_in_unit_disk(l0, l1, &rx, &ry); rx = c->lens_radius * rx; ry = c->lens_radius * ry; }
+    v3 offset = vadd(smul(rx, c->u), smul(ry, c->v));
+    ray r;
+    r.o = vadd(c->origin, offset);
+    r.d = vsub(vsub(vadd(vadd(c->llc, smul(s, c->horizontal)), smul(t, c->vertical)), c->origin), offset);
+    return r;
+}
+
+/* ------------------------------------------------------------------------ */
+/* scene                                                                    */
+/* ------------------------------------------------------------------------ */
+enum { MAT_LAMBERT = 0, MAT_LIGHT = 1, MAT_PHONG = 2, MAT_DIELECTRIC = 3 };
+typedef struct { int type; v3 albedo; v3 emit; double ks[3], ior, shininess; } material;
+
+typedef struct {
+    v3 v0, v1, v2, e1, e2;      /* triangle.h:58-66 (edges from the fp64 vertices) */
+    v3 n0, n1, n2;              /* vertex normals (mesh->normals)                  */
+    double inv_area;            /* 1/(0.5 |e1 x e2| nTriangles_of_mesh)            */
+    int mat, geo;               /* material, use_geometry_normals                  */
+} tri;
+typedef struct { v3 c; double r; int mat; } sphere;
+
+typedef struct { aabb box; int32_t left, right; } bnode;                     /* child<0: ~prim_ref */
+
+#define REF_SPHERE (1 << 30)
+enum { WORLD_BVH = 0, WORLD_LIST = 1 };
+
+struct ora_scene {
+    tri *tris; int ntris;
+    sphere *sph; int nsph;
+    material *mats; int nmats;
+    int world_kind;
+    bnode *nodes; int nnodes; int32_t root;   /* root >= 0 node, < 0 single prim leaf */
+    int32_t *list; int nlist;                 /* prim refs, list worlds         */
+    int32_t *lights; int nlights;             /* prim refs (Scene::lights)       */
+    camera cam;
+    v3 env;
+    int bvh_depth;
+};
+
+typedef struct {
+    double t;
+    v3 p, normal;
+    int32_t obj;     /* prim ref */
+    int mat;
+} hit_record;
+
+/* triangle::hit (triangle.h:69-118) */
+static int tri_hit(const tri *tr, const ray *r, double t_min, double t_max, hit_record *hrec, double *uo, double *vo)
+{
+    double a, f, u, v;
+    const v3 h = cross(r->d, tr->e2);
+    a = dot(tr->e1, h);
+    if (a == 0) return 0;
+    f = 1.0 / a;
+    v3 s = vsub(r->o, tr->v0);
+    u = f * dot(s, h);
+    if (u < 0.0 || u > 1.0) return 0;
+    v3 q = cross(s, tr->e1);
+    v = f * dot(r->d, q);
+    if (v >= 0.0 && u + v <= 1.0) {
+        double t = f * dot(tr->e2, q);
+        if (t > t_min && t < t_max) {
+            hrec->t = t;
+            hrec->p = ray_at(r, t);
+            if (tr->geo)
+                hrec->normal = unit(cross(tr->e1, tr->e2));
+            else
+                hrec->normal = unit(vadd(vadd(smul((1 - u - v), tr->n0), smul(u, tr->n1)), smul(v, tr->n2)));
+            hrec->mat = tr->mat;
+            if (uo) { *uo = u; *vo = v; }
+            return 1;
+        }
+    }
+    return 0;
+}
+/* sphere::hit (sphere.h:26-56) */
+static int sphere_hit(const sphere *sp, const ray *r, double t_min, double t_max, hit_record *rec)
+{
+    v3 oc = vsub(r->o, sp->c);
+    const double a = dot(r->d, r->d);
+    const double b = dot(oc, r->d);
+    const double c = dot(oc, oc) - sp->r * sp->r;
+    double discriminant = b * b - a * c;
+    if (discriminant >= 0.0) {
+        discriminant = sqrt(discriminant);
+        double t = (-b - discriminant) / a;
+        if (t < t_min) t = (-b + discriminant) / a;
+        if (t < t_min || t > t_max) return 0;
+        rec->t = t;
+        rec->p = ray_at(r, rec->t);
+        rec->normal = sdiv(vsub(rec->p, sp->c), sp->r);
+        if (vlen2(vsub(r->o, sp->c)) < sp->r * sp->r) rec->normal = vneg(rec->normal);
+        rec->mat = sp->mat;
+        return 1;
+    }
+    return 0;
+}
+
+static inline aabb prim_box(const ora_scene *s, int32_t ref)
+{
+    if (ref & REF_SPHERE) {                                                  /* sphere.h:58-62 */
+        const sphere *sp = &s->sph[ref & ~REF_SPHERE];
+        v3 rr = mk(sp->r, sp->r, sp->r);
+        return aabb_mk(vsub(sp->c, rr), vadd(sp->c, rr));
+    }
+    const tri *t = &s->tris[ref];                                            /* triangle.h:120-137 */
+    v3 mn = mk(fmin(fmin(t->v0.e[0], t->v1.e[0]), t->v2.e[0]),
+               fmin(fmin(t->v0.e[1], t->v1.e[1]), t->v2.e[1]),
+               fmin(fmin(t->v0.e[2], t->v1.e[2]), t->v2.e[2]));
+    v3 mx = mk(fmax(fmax(t->v0.e[0], t->v1.e[0]), t->v2.e[0]),
+               fmax(fmax(t->v0.e[1], t->v1.e[1]), t->v2.e[1]),
+               fmax(fmax(t->v0.e[2], t->v1.e[2]), t->v2.e[2]));
+    return aabb_mk(mn, mx);
+}
+
+static inline int prim_hit(const ora_scene *s, int32_t ref, const ray *r, double tmin, double tmax,
+                           hit_record *rec, ora_counters *cnt)
+{
+    int ok;
+    if (ref & REF_SPHERE) {
+        cnt->sphere_tests++;
+        ok = sphere_hit(&s->sph[ref & ~REF_SPHERE], r, tmin, tmax, rec);
+    } else {
+        cnt->tri_tests++;
+        ok = tri_hit(&s->tris[ref], r, tmin, tmax, rec, NULL, NULL);
+    }
+    if (ok) rec->obj = ref;
+    return ok;
+}
+
+/* parallel_bvh_node::hit (parallel_bvh.h:39-64) */
+static int bvh_hit(const ora_scene *s, int32_t node, const ray *r, double t_min, double t_max,
+                   hit_record *rec, ora_counters *cnt)
+{
+    if (node < 0) return prim_hit(s, ~node, r, t_min, t_max, rec, cnt);
+    const bnode *nd = &s->nodes[node];
+    cnt->node_visits++;
+    if (aabb_hit(&nd->box, r, t_min, t_max)) {
+        cnt->box_passes++;
+        double ray_min_t = t_min;
+        if (ray_min_t == EPSILON)
+            ray_min_t *= std_max(std_max(std_max(fabs(r->o.e[0]), fabs(r->o.e[1])), fabs(r->o.e[2])), EPSILON);
+        if (ray_min_t > t_min) t_min = ray_min_t;
+        if (bvh_hit(s, nd->left, r, t_min, t_max, rec, cnt)) {
+            bvh_hit(s, nd->right, r, t_min, rec->t, rec, cnt);
+            return 1;
+        }
+        return bvh_hit(s, nd->right, r, t_min, t_max, rec, cnt);
+    }
+    return 0;
+}
+/* hitable_list::hit (hitable_list.cpp:4-21) */
+static int list_hit(const ora_scene *s, const ray *r, double t_min, double t_max, hit_record *rec, ora_counters *cnt)
+{
+    hit_record temp;
+    int hit_anything = 0;
+    double closest = t_max;
+    for (int i = 0; i < s->nlist; ++i) {
+        if (prim_hit(s, s->list[i], r, t_min, closest, &temp, cnt)) {
+            hit_anything = 1;
+            closest = temp.t;
+            *rec = temp;
+        }
+    }
+    return hit_anything;
+}
+static inline int world_hit(const ora_scene *s, const ray *r, double t_min, double t_max, hit_record *rec,
+                            ora_counters *cnt)
+{
+    if (s->world_kind == WORLD_LIST) return list_hit(s, r, t_min, t_max, rec, cnt);
+    return bvh_hit(s, s->root, r, t_min, t_max, rec, cnt);
+}
+
+/* pdf_direct_sampling: triangle.h:139-144; sphere.h:64-78 */
+static double prim_pdf_direct(const ora_scene *s, int32_t ref, const hit_record *lrec, v3 to_light)
+{
+    if (!(ref & REF_SPHERE)) return s->tris[ref].inv_area;
+    const sphere *sp = &s->sph[ref & ~REF_SPHERE];
+    ray rr; rr.o = lrec->p; rr.d = to_light;
+    const v3 o = ray_at(&rr, -lrec->t);
+    const v3 direction = vsub(sp->c, o);
+    const double distance_squared = vlen2(direction);
+    const double radius_squared = sp->r * sp->r;
+    if (distance_squared <= radius_squared) return 1 / (4 * M_PI * sp->r * sp->r);
+    const double cos_theta_max = sqrt(1 - radius_squared / vlen2(direction));
+    const double solid_angle = 2 * M_PI * (1 - cos_theta_max);
+    return (1 / solid_angle) * fabs(dot(to_light, lrec->normal)) / vlen2(direction);
+}
+/* sample_direct: triangle.h:145-175; sphere.h:80-107.  Fills lrec (t, p, normal, mat, obj). */
+static v3 prim_sample_direct(const ora_scene *s, int32_t ref, hit_record *rec, v3 o, double u0, double u1)
+{
+    if (!(ref & REF_SPHERE)) {
+        const tri *t = &s->tris[ref];
+        double su0 = sqrt(u0);
+        double b0 = 1 - su0;
+        double b1 = u1 * su0;
+        v3 random_point = vadd(vadd(smul((1 - b0 - b1), t->v0), smul(b0, t->v1)), smul(b1, t->v2));
+        rec->t = 1.0;
+        rec->p = random_point;
+        if (t->geo) rec->normal = unit(cross(t->e1, t->e2));
+        else rec->normal = unit(vadd(vadd(smul((1 - b0 - b1), t->n0), smul(b0, t->n1)), smul(b1, t->n2)));
+        rec->mat = t->mat;
+        rec->obj = ref;
+        return vsub(random_point, o);
+    }
+    const sphere *sp = &s->sph[ref & ~REF_SPHERE];
+    const v3 direction = vsub(sp->c, o);
+    const double distance_squared = vlen2(direction);
+    onb uvw = onb_from_w(direction);
+    if (distance_squared <= sp->r * sp->r) {
+        v3 p = vadd(sp->c, smul(sp->r, uniform_sample_sphere(u0, u1)));
+        rec->p = p;
+        rec->mat = sp->mat;
+        rec->normal = unit(vsub(sp->c, p));
+        rec->obj = ref;
+        return vsub(p, o);
+    }
+    v3 p = onb_from_local(&uvw, random_to_sphere(sp->r, distance_squared, u0, u1));
+    rec->mat = sp->mat;
+    rec->normal = unit(p);
+    rec->obj = ref;
+    return p;
+}
+/* diffuse_light::emitted (material.h:184-190); other materials emit 0 */
+static inline v3 mat_emitted(const ora_scene *s, int mat, v3 d, v3 normal)
+{
+    const material *m = &s->mats[mat];
+    if (m->type == MAT_LIGHT && dot(normal, d) < 0) return m->emit;
+    return mk(0, 0, 0);
+}
+/* hitable_list::pick_sample (hitable_list.cpp:64-70) */
+static inline int pick_sample(double sample, int list_size)
+{
+    int index = (int)(sample * list_size);
+    if (index == list_size) index -= 1;
+    return index;
+}
+
+typedef struct { const ora_scene *s; rng_key key; ora_counters *cnt; } li_ctx;
+
+/* path::Li (path.cpp:4-116), recursive like the reference so the
+ * association order of every product/sum matches.  Only the non-specular
+ * (lambertian) scatter branch and diffuse_light emission are reachable in the
+ * hot-path scenes; other material types are rejected at load. */
+static v3 Li(li_ctx *c, const ray *r, int depth, const hit_record *prev, double prev_bsdf_pdf)
+{
+    const ora_scene *s = c->s;
+    hit_record hrec;
+    if (depth == 0) c->cnt->camera_rays++; else c->cnt->extension_rays++;
+    if (world_hit(s, r, EPSILON, FLT_MAX, &hrec, c->cnt)) {
+        v3 Le = mat_emitted(s, hrec.mat, r->d, hrec.normal);
+        if ((Le.e[0] != 0.0) || (Le.e[1] != 0.0) || (Le.e[2] != 0.0)) {
+            if (depth == 0 || s->mats[prev->mat].type == MAT_PHONG || s->mats[prev->mat].type == MAT_DIELECTRIC)
+                return Le;
+            const double cos_wo = dot(hrec.normal, vneg(unit(r->d)));
+            double distance_squared = vlen2(vsub(hrec.p, prev->p));
+            if (distance_squared <= EPSILON) distance_squared = EPSILON;
+            double surface_bsdf_pdf = prev_bsdf_pdf;
+            const double light_pdf = prim_pdf_direct(s, hrec.obj, &hrec, r->d) * distance_squared / fabs(cos_wo);
+            const double weight = miWeight(surface_bsdf_pdf, light_pdf);
+            return smul(weight, Le);
+        }
+        const material *m = &s->mats[hrec.mat];
+        /* lambertian::scatter always succeeds; diffuse_light::scatter fails (material.h:55-60,183) */
+        if (depth <= 33 && m->type == MAT_LAMBERT) {
+            const uint32_t base = DIM_BOUNCE(depth);
+            const int index = pick_sample(rng_u(c->key, base + 3), s->nlights);
+            if (index >= 0) {
+                hit_record lrec;
+                v3 offset_origin = vadd(hrec.p, smul(EPSILON, hrec.normal));
+                v3 to_light = prim_sample_direct(s, s->lights[index], &lrec, offset_origin,
+                                                 rng_u(c->key, base + 4), rng_u(c->key, base + 5));
+                const double dist_to_light = vlen(to_light);
+                ray shadow; shadow.o = offset_origin; shadow.d = to_light;
+                c->cnt->shadow_rays++;
+                if (!world_hit(s, &shadow, EPSILON, 1 - SHADOW_EPSILON, &lrec, c->cnt)) {
+                    to_light = make_unit(to_light);
+                    shadow.d = to_light;
+                    v3 surface_bsdf = sdiv(m->albedo, M_PI);
+                    const double cos_wi = dot(hrec.normal, unit(to_light));
+                    const double cos_wo = dot(lrec.normal, vneg(unit(to_light)));
+                    if (cos_wo != 0) {
+                        double distance_squared = dist_to_light * dist_to_light;
+                        surface_bsdf = vscale_inplace(surface_bsdf, cos_wi);
+                        const double light_pdf = prim_pdf_direct(s, s->lights[index], &hrec, to_light)
+                                                 * distance_squared / fabs(cos_wo);
+                        const double surface_bsdf_pdf = cosine_pdf_value(hrec.normal, to_light);
+                        const double weight = miWeight(light_pdf, surface_bsdf_pdf);
+                        v3 em = mat_emitted(s, lrec.mat, shadow.d, lrec.normal);
+                        Le = vadd(Le, sdiv(smul(weight, vmul(em, surface_bsdf)), light_pdf));
+                    }
+                }
+            }
+            /* diffuse bounce (path.cpp:96-110) */
+            onb uvw = onb_from_w(hrec.normal);
+            ray wo;
+            wo.o = vadd(hrec.p, smul(EPSILON, hrec.normal));
+            wo.d = onb_from_local(&uvw, hemisphere_to_cosine_direction(rng_u(c->key, base + 6),
+                                                                        rng_u(c->key, base + 7)));
+            const double surface_bsdf_pdf = cosine_pdf_value(hrec.normal, wo.d);
+            const v3 surface_bsdf = sdiv(m->albedo, M_PI);
+            if (surface_bsdf_pdf == 0) return mk(0, 0, 0);
+            const double cos_wo = fabs(dot(hrec.normal, unit(wo.d)));
+            v3 li = Li(c, &wo, depth + 1, &hrec, surface_bsdf_pdf);
+            return vadd(Le, sdiv(smul(cos_wo, vmul(surface_bsdf, li)), surface_bsdf_pdf));
+        }
+        return Le;
+    }
+    /* environment_map::eval with a constant texture (material.h:219-232) */
+    return s->env;
+}
+
+/* one pixel, path.cpp:120-143 (loop over s, add_sample divides by ns: *= 1/ns) */
+static void render_pixel(const ora_scene *s, int nx, int ny, int spp, uint32_t seed, int x, int y,
+                         double *out, ora_counters *cnt)
+{
+    v3 col = mk(0.0, 0.0, 0.0);
+    const uint32_t pixel = (uint32_t)y * (uint32_t)nx + (uint32_t)x;
+    for (int smp = 0; smp < spp; ++smp) {
+        li_ctx c; c.s = s; c.cnt = cnt; c.key = rng_make(seed, pixel, (uint32_t)smp);
+        double u = (double)(x + rng_u(c.key, 0)) / (double)nx;
+        double v = (double)(y + rng_u(c.key, 1)) / (double)ny;
+        ray r = camera_get_ray(&s->cam, u, v, rng_u(c.key, 2), rng_u(c.key, 3));
+        hit_record h; memset(&h, 0, sizeof(h)); h.mat = 0;
+        v3 sample = Li(&c, &r, 0, &h, 0.0);
+        col = vadd(col, sample);
+        cnt->samples++;
+    }
+    col = vdiv_inplace(col, (double)spp);
+    vstore(out, col);
+}
+
+typedef struct {
+    const ora_scene *s; int nx, ny, spp; uint32_t seed;
+    const int32_t *pixels; int npix; int tid, nth;
+    double *out; ora_counters cnt;
+} job;
+static void *render_worker(void *arg)
+{
+    job *j = (job *)arg;
+    memset(&j->cnt, 0, sizeof(j->cnt));
+    for (int i = j->tid; i < j->npix; i += j->nth) {
+        int p = j->pixels[i];
+        render_pixel(j->s, j->nx, j->ny, j->spp, j->seed, p % j->nx, p / j->nx, &j->out[3 * (size_t)i], &j->cnt);
+    }
+    return NULL;
+}
+int ora_render(const ora_scene *s, int nx, int ny, int spp, uint32_t seed, const int32_t *pixels, int npix,
+               int nthreads, double *out_rgb, ora_counters *cnt)
+{
+    if (!s || nx <= 0 || ny <= 0 || spp <= 0 || npix < 0) return -1;
+    for (int i = 0; i < npix; ++i)
+        if (pixels[i] < 0 || pixels[i] >= nx * ny) return -2;
+    if (nthreads < 1) nthreads = 1;
+    job *jobs = (job *)calloc((size_t)nthreads, sizeof(job));
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    for (int t = 0; t < nthreads; ++t) {
+        jobs[t].s = s; jobs[t].nx = nx; jobs[t].ny = ny; jobs[t].spp = spp; jobs[t].seed = seed;
+        jobs[t].pixels = pixels; jobs[t].npix = npix; jobs[t].tid = t; jobs[t].nth = nthreads; jobs[t].out = out_rgb;
+        if (nthreads > 1) pthread_create(&th[t], NULL, render_worker, &jobs[t]);
+    }
+    if (nthreads == 1) render_worker(&jobs[0]);
+    ora_counters tot; memset(&tot, 0, sizeof(tot));
+    for (int t = 0; t < nthreads; ++t) {
+        if (nthreads > 1) pthread_join(th[t], NULL);
+        tot.node_visits += jobs[t].cnt.node_visits; tot.box_passes += jobs[t].cnt.box_passes;
+        tot.tri_tests += jobs[t].cnt.tri_tests; tot.sphere_tests += jobs[t].cnt.sphere_tests;
+        tot.camera_rays += jobs[t].cnt.camera_rays; tot.extension_rays += jobs[t].cnt.extension_rays;
+        tot.shadow_rays += jobs[t].cnt.shadow_rays; tot.samples += jobs[t].cnt.samples;
+    }
+    if (cnt) *cnt = tot;
+    free(jobs); free(th);
+    return 0;
+}
+
+int ora_world_hit(const ora_scene *s, const double *o, const double *d, double tmin, double tmax,
+                  double *t_out, int32_t *prim_out, ora_counters *cnt)
+{
+    ora_counters local; memset(&local, 0, sizeof(local));
+    ray r; r.o = vload(o); r.d = vload(d);
+    hit_record h;
+    int ok = world_hit(s, &r, tmin, tmax, &h, cnt ? cnt : &local);
+    if (ok) { *t_out = h.t; *prim_out = h.obj; } else { *t_out = 0; *prim_out = -1; }
+    return ok;
+}
+
+/* ------------------------------------------------------------------------ */
+/* BVH build: parallel_bvh_node ctor (parallel_bvh.h:67-160) with glibc      */
+/* qsort and the bvh.h:6-55 comparators.  Subtrees are built depth-first,    */
+/* the left child first, exactly like the sequential taskflow schedule.      */
+/* ------------------------------------------------------------------------ */
+typedef struct { const ora_scene *s; int axis; } cmp_ctx;
+static int box_cmp(const void *a, const void *b, void *arg)
+{
+    const cmp_ctx *c = (const cmp_ctx *)arg;
+    aabb bl = prim_box(c->s, *(const int32_t *)a);
+    aabb br = prim_box(c->s, *(const int32_t *)b);
+    if (bl.min.e[c->axis] - br.min.e[c->axis] < 0.0) return -1;
+    return 1;
+}
+typedef struct { aabb *boxes; double *left_area, *right_area; } bscratch;
+
+static int32_t build_rec(ora_scene *s, int32_t *l, int n, int g_index, bscratch *g, int depth)
+{
+    if (depth > s->bvh_depth) s->bvh_depth = depth;
+    int32_t me = s->nnodes++;
+    aabb *boxes = g->boxes + g_index;
+    double *left_area = g->left_area + g_index;
+    double *right_area = g->right_area + g_index;
+
+    aabb main_box = prim_box(s, l[0]);
+    for (int i = 1; i < n; ++i) {
+        aabb nb = prim_box(s, l[i]);
+        main_box = surrounding_box(nb, main_box);
+    }
+    cmp_ctx cc; cc.s = s; cc.axis = aabb_longest_axis(&main_box);
+    qsort_r(l, (size_t)n, sizeof(int32_t), box_cmp, &cc);
+    for (int i = 0; i < n; ++i) boxes[i] = prim_box(s, l[i]);
+    left_area[0] = aabb_area(&boxes[0]);
+    aabb left_box = boxes[0];
+    for (int i = 1; i < n - 1; ++i) { left_box = surrounding_box(left_box, boxes[i]); left_area[i] = aabb_area(&left_box); }
+    right_area[n - 1] = aabb_area(&boxes[n - 1]);
+    aabb right_box = boxes[n - 1];
+    for (int i = n - 2; i > 0; --i) { right_box = surrounding_box(right_box, boxes[i]); right_area[i] = aabb_area(&right_box); }
+    double min_SAH = FLT_MAX;
+    int min_idx = 0;
+    for (int i = 0; i < n - 1; ++i) {
+        double SAH = i * left_area[i] + (n - i - 1) * right_area[i + 1];
+        if (SAH < min_SAH) { min_idx = i; min_SAH = SAH; }
+    }
+    s->nodes[me].box = main_box;
+    int32_t left, right;
+    if (min_idx == 0) left = ~l[0];
+    else left = build_rec(s, l, min_idx + 1, g_index, g, depth + 1);
+    if (min_idx == n - 2) right = ~l[min_idx + 1];
+    else right = build_rec(s, l + min_idx + 1, n - min_idx - 1, g_index + min_idx + 1, g, depth + 1);
+    s->nodes[me].left = left;
+    s->nodes[me].right = right;
+    return me;
+}
+static int build_bvh(ora_scene *s, int32_t *prims, int n)
+{
+    s->nodes = (bnode *)calloc((size_t)(n > 1 ? n - 1 : 1), sizeof(bnode));
+    s->nnodes = 0; s->bvh_depth = 0;
+    if (n <= 0) return -1;
+    if (n == 1) { s->root = ~prims[0]; return 0; }   /* the reference reads an uninitialised index here */
+    bscratch g;
+    g.boxes = (aabb *)malloc(sizeof(aabb) * (size_t)n);
+    g.left_area = (double *)malloc(sizeof(double) * (size_t)n);
+    g.right_area = (double *)malloc(sizeof(double) * (size_t)n);
+    s->root = build_rec(s, prims, n, 0, &g, 1);
+    free(g.boxes); free(g.left_area); free(g.right_area);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* OBJ/MTL ingest: Assimp 5.0.1 ObjFileParser + post-processing restated     */
+/* (mesh split per object/material, fast_atoreal_move float parsing, quad   */
+/* triangulation, GenSmoothNormals for meshes without vn), then             */
+/* mesh_loader.cpp:59-112 material mapping.  Assimp is absent: parity at    */
+/* this boundary is "unpinned" (SURVEY.md 8(c)).                             */
+/* ------------------------------------------------------------------------ */
+static const double fast_atof_table[16] = {
+    0.0, 0.1, 0.01, 0.001, 0.0001, 0.00001, 0.000001, 0.0000001, 0.00000001, 0.000000001,
+    0.0000000001, 0.00000000001, 0.000000000001, 0.0000000000001, 0.00000000000001, 0.000000000000001};
+static uint64_t strtoul10_64(const char *in, const char **out, unsigned *max_inout)
+{
+    unsigned cur = 0;
+    uint64_t value = 0;
+    while (*in >= '0' && *in <= '9') {
+        const uint64_t new_value = (value * 10) + (uint64_t)(*in - '0');
+        if (new_value < value) break;   /* overflow: Assimp throws; keep value */
+        value = new_value;
+        ++in; ++cur;
+        if (max_inout && *max_inout == cur) {
+            while (*in >= '0' && *in <= '9') ++in;
+            break;
+        }
+    }
+    if (out) *out = in;
+    if (max_inout) *max_inout = cur;
+    return value;
+}
+static const char *fast_atof_float(const char *c, float *outv)
+{
+    float f = 0;
+    int inv = (*c == '-');
+    if (inv || *c == '+') ++c;
+    if (!((*c >= '0' && *c <= '9') || ((*c == '.' || *c == ',') && c[1] >= '0' && c[1] <= '9'))) {
+        *outv = 0; return c;
+    }
+    if (!(*c == '.' || *c == ',')) f = (float)strtoul10_64(c, &c, NULL);
+    if ((*c == '.' || *c == ',') && c[1] >= '0' && c[1] <= '9') {
+        ++c;
+        unsigned diff = 15;  /* AI_FAST_ATOF_RELAVANT_DECIMALS */
+        double pl = (double)strtoul10_64(c, &c, &diff);
+        pl *= fast_atof_table[diff];
+        f += (float)pl;
+    } else if (*c == '.') {
+        ++c;
+    }
+    if (*c == 'e' || *c == 'E') {
+        ++c;
+        int einv = (*c == '-');
+        if (einv || *c == '+') ++c;
+        float ex = (float)strtoul10_64(c, &c, NULL);
+        if (einv) ex = -ex;
+        f *= powf(10.0f, ex);
+    }
+    if (inv) f = -f;
+    *outv = f;
+    return c;
+}
+float ora_kat_atof(const char *s) { float f; fast_atof_float(s, &f); return f; }
+
+typedef struct { char name[128]; float kd[3], ks[3], ke[3]; float d, ni, ns; int has_kd; } mtl;
+typedef struct { int mtl; int nfaces; int *faces; int cap; } omesh;   /* faces: triangles, vertex idx */
+
+typedef struct {
+    float *v; int nv, capv;              /* positions */
+    float *vn; int nvn, capvn;           /* normals (vn) */
+    mtl *mats; int nmats;
+    omesh *meshes; int nmeshes, capm;
+    int *fv_n;                            /* per triangle corner: normal index or -1 (parallel to faces) */
+} objdata;
+
+static void trim(char *s)
+{
+    size_t n = strlen(s);
+    while (n && (s[n - 1] == '\n' || s[n - 1] == '\r' || s[n - 1] == ' ' || s[n - 1] == '\t')) s[--n] = 0;
+}
+static int load_mtl(const char *path, objdata *od)
+{
+    FILE *f = fopen(path, "rb");
+    if (!f) return -1;
+    char line[1024];
+    mtl *cur = NULL;
+    while (fgets(line, sizeof line, f)) {
+        char *p = line;
+        while (*p == ' ' || *p == '\t') ++p;
+        trim(p);
+        if (!strncmp(p, "newmtl", 6)) {
+            od->mats = (mtl *)realloc(od->mats, sizeof(mtl) * (size_t)(od->nmats + 1));
+            cur = &od->mats[od->nmats++];
+            memset(cur, 0, sizeof(*cur));
+            const char *nm = p + 6; while (*nm == ' ' || *nm == '\t') ++nm;
+            snprintf(cur->name, sizeof cur->name, "%s", nm);
+            cur->kd[0] = cur->kd[1] = cur->kd[2] = 0.6f;  /* ObjFile::Material defaults */
+            cur->d = 1.0f; cur->ni = 1.0f;
+            continue;
+        }
+        if (!cur) continue;
+        const char *q;
+        float *dst = NULL; int n3 = 0;
+        if (p[0] == 'K' && p[1] == 'd' && (p[2] == ' ' || p[2] == '\t')) { dst = cur->kd; n3 = 1; cur->has_kd = 1; }
+        else if (p[0] == 'K' && p[1] == 's' && (p[2] == ' ' || p[2] == '\t')) { dst = cur->ks; n3 = 1; }
+        else if (p[0] == 'K' && p[1] == 'e' && (p[2] == ' ' || p[2] == '\t')) { dst = cur->ke; n3 = 1; }
+        else if (p[0] == 'd' && (p[1] == ' ' || p[1] == '\t')) dst = &cur->d;
+        else if (p[0] == 'N' && p[1] == 'i') dst = &cur->ni;
+        else if (p[0] == 'N' && p[1] == 's') dst = &cur->ns;
+        else if (p[0] == 'T' && p[1] == 'r') { q = p + 2; while (*q == ' ' || *q == '\t') ++q; float tr; fast_atof_float(q, &tr); cur->d = 1.0f - tr; continue; }
+        if (!dst) continue;
+        q = p + (n3 ? 2 : (p[0] == 'd' ? 1 : 2));
+        for (int k = 0; k < (n3 ? 3 : 1); ++k) {
+            while (*q == ' ' || *q == '\t') ++q;
+            q = fast_atof_float(q, &dst[k]);
+        }
+    }
+    fclose(f);
+    return 0;
+}
+static int find_mtl(const objdata *od, const char *name)
+{
+    for (int i = 0; i < od->nmats; ++i) if (!strcmp(od->mats[i].name, name)) return i;
+    return -1;
+}
+static omesh *new_mesh(objdata *od, int mtl_idx)
+{
+    if (od->nmeshes == od->capm) { od->capm = od->capm ? 2 * od->capm : 16; od->meshes = (omesh *)realloc(od->meshes, sizeof(omesh) * (size_t)od->capm); }
+    omesh *m = &od->meshes[od->nmeshes++];
+    memset(m, 0, sizeof(*m));
+    m->mtl = mtl_idx;
+    return m;
+}
+static void mesh_push(omesh *m, int a, int b, int c, int na, int nb, int nc)
+{
+    if (m->nfaces == m->cap) { m->cap = m->cap ? 2 * m->cap : 64; m->faces = (int *)realloc(m->faces, sizeof(int) * 6 * (size_t)m->cap); }
+    int *f = &m->faces[6 * m->nfaces++];
+    f[0] = a; f[1] = b; f[2] = c; f[3] = na; f[4] = nb; f[5] = nc;
+}
+static inline void fsub3(const float *a, const float *b, float *o) { o[0] = a[0] - b[0]; o[1] = a[1] - b[1]; o[2] = a[2] - b[2]; }
+static inline void fdivs3(float *v, float f)   /* aiVector3t::operator/= */
+{
+    if (f == 1.0f) return;
+    const float invF = 1.0f / f;
+    v[0] *= invF; v[1] *= invF; v[2] *= invF;
+}
+static inline void fnorm3(float *v)   /* aiVector3D::Normalize */
+{
+    fdivs3(v, sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]));
+}
+static inline float fdot3(const float *a, const float *b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+
+/* TriangulateProcess quad rule: fan from the concave vertex (or 0). */
+static int quad_start(const objdata *od, const int *vi)
+{
+    for (int i = 0; i < 4; ++i) {
+        const float *v0 = &od->v[3 * vi[(i + 3) % 4]], *v1 = &od->v[3 * vi[(i + 2) % 4]];
+        const float *v2 = &od->v[3 * vi[(i + 1) % 4]], *v = &od->v[3 * vi[i]];
+        float left[3], diag[3], right[3];
+        fsub3(v0, v, left); fsub3(v1, v, diag); fsub3(v2, v, right);
+        fnorm3(left); fnorm3(diag); fnorm3(right);
+        const float angle = acosf(fdot3(left, diag)) + acosf(fdot3(right, diag));
+        if (angle > (float)M_PI) return i;
+    }
+    return 0;
+}
+
+static int parse_obj(const char *path, objdata *od)
+{
+    FILE *f = fopen(path, "rb");
+    if (!f) return -1;
+    char line[4096];
+    omesh *cur = NULL;
+    int cur_mtl = -2;          /* -2: no material selected yet (NoMaterial) */
+    int cur_has_obj = 0;
+    char group[512] = "";
+    while (fgets(line, sizeof line, f)) {
+        char *p = line;
+        while (*p == ' ' || *p == '\t') ++p;
+        trim(p);
+        if (p[0] == 'v' && (p[1] == ' ' || p[1] == '\t')) {
+            if (od->nv == od->capv) { od->capv = od->capv ? 2 * od->capv : 1024; od->v = (float *)realloc(od->v, sizeof(float) * 3 * (size_t)od->capv); }
+            const char *q = p + 1;
+            for (int k = 0; k < 3; ++k) { while (*q == ' ' || *q == '\t') ++q; q = fast_atof_float(q, &od->v[3 * od->nv + k]); }
+            od->nv++;
+        } else if (p[0] == 'v' && p[1] == 'n') {
+            if (od->nvn == od->capvn) { od->capvn = od->capvn ? 2 * od->capvn : 1024; od->vn = (float *)realloc(od->vn, sizeof(float) * 3 * (size_t)od->capvn); }
+            const char *q = p + 2;
+            for (int k = 0; k < 3; ++k) { while (*q == ' ' || *q == '\t') ++q; q = fast_atof_float(q, &od->vn[3 * od->nvn + k]); }
+            od->nvn++;
+        } else if (!strncmp(p, "mtllib", 6)) {
+            const char *nm = p + 6; while (*nm == ' ' || *nm == '\t') ++nm;
+            char dir[2048]; snprintf(dir, sizeof dir, "%s", path);
+            char *slash = strrchr(dir, '/');
+            char full[4096];
+            if (slash) { slash[1] = 0; snprintf(full, sizeof full, "%s%s", dir, nm); } else snprintf(full, sizeof full, "%s", nm);
+            load_mtl(full, od);
+        } else if ((p[0] == 'g' || p[0] == 'o') && (p[1] == ' ' || p[1] == '\t' || p[1] == 0)) {
+            /* ObjFileParser::getGroupName/createObject: a new group name starts a new
+             * object + mesh inheriting the current material */
+            const char *nm = p + 1; while (*nm == ' ' || *nm == '\t') ++nm;
+            if (cur && !strcmp(nm, group)) continue;
+            snprintf(group, sizeof group, "%s", nm);
+            cur = new_mesh(od, cur_mtl);
+            cur_has_obj = 1;
+        } else if (!strncmp(p, "usemtl", 6)) {
+            const char *nm = p + 6; while (*nm == ' ' || *nm == '\t') ++nm;
+            int idx = find_mtl(od, nm);
+            if (idx < 0) {  /* unknown name: Assimp creates a named default material */
+                od->mats = (mtl *)realloc(od->mats, sizeof(mtl) * (size_t)(od->nmats + 1));
+                mtl *m = &od->mats[od->nmats];
+                memset(m, 0, sizeof(*m));
+                snprintf(m->name, sizeof m->name, "%s", nm);
+                m->kd[0] = m->kd[1] = m->kd[2] = 0.6f; m->d = 1.0f; m->ni = 1.0f;
+                idx = od->nmats++;
+            }
+            if (idx == cur_mtl && cur) continue;   /* same material: ignored */
+            cur_mtl = idx;
+            if (!cur) { cur = new_mesh(od, cur_mtl); cur_has_obj = 1; continue; }
+            if (cur->mtl != -2 && cur->mtl != idx && cur->nfaces > 0) cur = new_mesh(od, cur_mtl);  /* needsNewMesh */
+            else cur->mtl = idx;
+        } else if (p[0] == 'f' && (p[1] == ' ' || p[1] == '\t')) {
+            if (!cur) { cur = new_mesh(od, cur_mtl); cur_has_obj = 1; }
+            int vi[64], ni[64], nvtx = 0;
+            const char *q = p + 1;
+            while (*q && nvtx < 64) {
+                while (*q == ' ' || *q == '\t') ++q;
+                if (!*q) break;
+                long a = strtol(q, (char **)&q, 10), nn = 0;
+                if (*q == '/') {
+                    ++q;
+                    if (*q != '/') strtol(q, (char **)&q, 10);
+                    if (*q == '/') { ++q; nn = strtol(q, (char **)&q, 10); }
+                }
+                while (*q && *q != ' ' && *q != '\t') ++q;
+                vi[nvtx] = (int)(a < 0 ? od->nv + a : a - 1);
+                ni[nvtx] = nn == 0 ? -1 : (int)(nn < 0 ? od->nvn + nn : nn - 1);
+                nvtx++;
+            }
+            if (nvtx == 3) mesh_push(cur, vi[0], vi[1], vi[2], ni[0], ni[1], ni[2]);
+            else if (nvtx == 4) {
+                int s0 = quad_start(od, vi);
+                int t[4] = {vi[s0], vi[(s0 + 1) % 4], vi[(s0 + 2) % 4], vi[(s0 + 3) % 4]};
+                int tn[4] = {ni[s0], ni[(s0 + 1) % 4], ni[(s0 + 2) % 4], ni[(s0 + 3) % 4]};
+                mesh_push(cur, t[0], t[1], t[2], tn[0], tn[1], tn[2]);
+                mesh_push(cur, t[0], t[2], t[3], tn[0], tn[2], tn[3]);
+            } else if (nvtx > 4) {
+                for (int k = 1; k + 1 < nvtx; ++k) mesh_push(cur, vi[0], vi[k], vi[k + 1], ni[0], ni[k], ni[k + 1]);
+            }
+        }
+    }
+    (void)cur_has_obj;
+    fclose(f);
+    return 0;
+}
+
+/* GenVertexNormalsProcess with the default 175 degree limit: every corner
+ * gets the normalised sum of the face normals of all corners at (nearly) the
+ * same position inside the mesh. */
+static void smooth_normals(const objdata *od, const omesh *m, float *cn /* 9 per face */)
+{
+    int nc = 3 * m->nfaces;
+    float *fnrm = (float *)malloc(sizeof(float) * 3 * (size_t)m->nfaces);
+    float lo[3] = {1e30f, 1e30f, 1e30f}, hi[3] = {-1e30f, -1e30f, -1e30f};
+    for (int fi = 0; fi < m->nfaces; ++fi) {
+        const int *f = &m->faces[6 * fi];
+        const float *a = &od->v[3 * f[0]], *b = &od->v[3 * f[1]], *c = &od->v[3 * f[2]];
+        float e1[3], e2[3];
+        fsub3(b, a, e1); fsub3(c, a, e2);
+        float n[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+        float l = sqrtf(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+        if (l > 0.0f) fdivs3(n, l);   /* NormalizeSafe */
+        memcpy(&fnrm[3 * fi], n, sizeof n);
+        for (int k = 0; k < 3; ++k) {
+            const float *v = &od->v[3 * f[k]];
+            for (int d = 0; d < 3; ++d) { if (v[d] < lo[d]) lo[d] = v[d]; if (v[d] > hi[d]) hi[d] = v[d]; }
+        }
+    }
+    float dd[3] = {hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]};
+    float eps = sqrtf(dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2]) * 1e-4f;
+    float eps2 = eps * eps;
+    for (int i = 0; i < nc; ++i) {
+        const float *pi = &od->v[3 * m->faces[6 * (i / 3) + (i % 3)]];
+        float acc[3] = {0, 0, 0};
+        for (int j = 0; j < nc; ++j) {
+            const float *pj = &od->v[3 * m->faces[6 * (j / 3) + (j % 3)]];
+            float d3[3]; fsub3(pj, pi, d3);
+            if (d3[0] * d3[0] + d3[1] * d3[1] + d3[2] * d3[2] < eps2) {
+                acc[0] += fnrm[3 * (j / 3)]; acc[1] += fnrm[3 * (j / 3) + 1]; acc[2] += fnrm[3 * (j / 3) + 2];
+            }
+        }
+        float l = sqrtf(acc[0] * acc[0] + acc[1] * acc[1] + acc[2] * acc[2]);
+        if (l > 0.0f) fdivs3(acc, l);
+        memcpy(&cn[3 * i], acc, sizeof acc);
+    }
+    free(fnrm);
+}
+
+/* create_triangle_mesh (triangle.cpp:9-23) + mesh_loader material mapping */
+static int add_obj(ora_scene *s, const char *path, int geo, int32_t **lights, int *nlights)
+{
+    objdata od; memset(&od, 0, sizeof(od));
+    if (parse_obj(path, &od) != 0) return -1;
+    for (int mi = 0; mi < od.nmeshes; ++mi) {
+        omesh *m = &od.meshes[mi];
+        if (m->nfaces == 0) continue;   /* Assimp drops empty meshes */
+        /* material (mesh_loader.cpp:59-112) */
+        material mat; memset(&mat, 0, sizeof(mat));
+        const mtl *mt = (m->mtl >= 0) ? &od.mats[m->mtl] : NULL;
+        if (!mt) {
+            mat.type = MAT_LAMBERT; mat.albedo = mk(0.5, 0.5, 0.5);
+        } else if (mt->ke[0] != 0 || mt->ke[1] != 0 || mt->ke[2] != 0) {
+            mat.type = MAT_LIGHT; mat.emit = mk(mt->ke[0], mt->ke[1], mt->ke[2]);
+        } else if (mt->ks[0] != 0 || mt->ks[1] != 0 || mt->ks[2] != 0) {
+            mat.type = (mt->d < 1.0f) ? MAT_DIELECTRIC : MAT_PHONG;
+            mat.albedo = mk(FromSrgb(mt->kd[0]), FromSrgb(mt->kd[1]), FromSrgb(mt->kd[2]));
+            mat.ks[0] = FromSrgb(mt->ks[0]); mat.ks[1] = FromSrgb(mt->ks[1]); mat.ks[2] = FromSrgb(mt->ks[2]);
+            mat.ior = mt->ni; mat.shininess = mt->ns;
+        } else {
+            mat.type = MAT_LAMBERT;
+            mat.albedo = mk(FromSrgb(mt->kd[0]), FromSrgb(mt->kd[1]), FromSrgb(mt->kd[2]));
+        }
+        s->mats = (material *)realloc(s->mats, sizeof(material) * (size_t)(s->nmats + 1));
+        s->mats[s->nmats] = mat;
+        int mat_idx = s->nmats++;
+        /* normals: vn when every corner has one, else GenSmoothNormals */
+        int has_vn = 1;
+        for (int fi = 0; fi < m->nfaces && has_vn; ++fi)
+            for (int k = 0; k < 3; ++k) if (m->faces[6 * fi + 3 + k] < 0) has_vn = 0;
+        float *cn = (float *)malloc(sizeof(float) * 9 * (size_t)m->nfaces);
+        if (has_vn) {
+            for (int fi = 0; fi < m->nfaces; ++fi)
+                for (int k = 0; k < 3; ++k) memcpy(&cn[9 * fi + 3 * k], &od.vn[3 * m->faces[6 * fi + 3 + k]], 3 * sizeof(float));
+        } else if (!geo) {
+            smooth_normals(&od, m, cn);
+        } else {
+            memset(cn, 0, sizeof(float) * 9 * (size_t)m->nfaces);
+        }
+        s->tris = (tri *)realloc(s->tris, sizeof(tri) * (size_t)(s->ntris + m->nfaces));
+        for (int fi = 0; fi < m->nfaces; ++fi) {
+            tri *t = &s->tris[s->ntris + fi];
+            const int *f = &m->faces[6 * fi];
+            t->v0 = mk(od.v[3 * f[0]], od.v[3 * f[0] + 1], od.v[3 * f[0] + 2]);
+            t->v1 = mk(od.v[3 * f[1]], od.v[3 * f[1] + 1], od.v[3 * f[1] + 2]);
+            t->v2 = mk(od.v[3 * f[2]], od.v[3 * f[2] + 1], od.v[3 * f[2] + 2]);
+            t->n0 = mk(cn[9 * fi], cn[9 * fi + 1], cn[9 * fi + 2]);
+            t->n1 = mk(cn[9 * fi + 3], cn[9 * fi + 4], cn[9 * fi + 5]);
+            t->n2 = mk(cn[9 * fi + 6], cn[9 * fi + 7], cn[9 * fi + 8]);
+            t->e1 = vsub(t->v1, t->v0);
+            t->e2 = vsub(t->v2, t->v0);
+            t->inv_area = 1 / (0.5 * vlen(cross(t->e1, t->e2)) * m->nfaces);
+            t->mat = mat_idx;
+            t->geo = geo;
+            if (mat.type == MAT_LIGHT) {
+                *lights = (int32_t *)realloc(*lights, sizeof(int32_t) * (size_t)(*nlights + 1));
+                (*lights)[(*nlights)++] = s->ntris + fi;
+            }
+        }
+        s->ntris += m->nfaces;
+        free(cn);
+    }
+    for (int i = 0; i < od.nmeshes; ++i) free(od.meshes[i].faces);
+    free(od.meshes); free(od.v); free(od.vn); free(od.mats);
+    return 0;
+}
+
+static int add_material(ora_scene *s, int type, v3 albedo, v3 emit)
+{
+    s->mats = (material *)realloc(s->mats, sizeof(material) * (size_t)(s->nmats + 1));
+    memset(&s->mats[s->nmats], 0, sizeof(material));
+    s->mats[s->nmats].type = type; s->mats[s->nmats].albedo = albedo; s->mats[s->nmats].emit = emit;
+    return s->nmats++;
+}
+static int add_sphere(ora_scene *s, v3 c, double r, int mat)
+{
+    s->sph = (sphere *)realloc(s->sph, sizeof(sphere) * (size_t)(s->nsph + 1));
+    s->sph[s->nsph].c = c; s->sph[s->nsph].r = r; s->sph[s->nsph].mat = mat;
+    return s->nsph++;
+}
+
+int ora_load_scene(const char *kind, const char *obj_path, double aspect, ora_scene **out)
+{
+    ora_scene *s = (ora_scene *)calloc(1, sizeof(ora_scene));
+    int32_t *lights = NULL; int nlights = 0;
+    s->env = mk(0.0, 0.0, 0.0);
+    if (!strcmp(kind, "cornell_box_obj") || !strcmp(kind, "obj_geo") || !strcmp(kind, "obj_smooth")) {
+        /* main.cpp:222-252 */
+        if (add_obj(s, obj_path, strcmp(kind, "obj_smooth") != 0, &lights, &nlights) != 0) { free(s); return -1; }
+        s->world_kind = WORLD_BVH;
+        int32_t *prims = (int32_t *)malloc(sizeof(int32_t) * (size_t)s->ntris);
+        for (int i = 0; i < s->ntris; ++i) prims[i] = i;
+        build_bvh(s, prims, s->ntris);
+        free(prims);
+        s->cam = camera_mk(mk(0, 1, (double)3.9f), mk(0, 1, 0), mk(0, 1, 0), 40.0, aspect, 0.0, 10.0);
+    } else if (!strcmp(kind, "veach_mis")) {
+        /* main.cpp:281-314: list world = mesh triangles + 5 spheres; lights = mesh
+         * emitters + 5 separate (identical) sphere objects; black env. */
+        if (add_obj(s, obj_path, 0, &lights, &nlights) != 0) { free(s); return -1; }
+        const double cx[5] = {10, (double)-1.25f, (double)-3.75f, (double)1.25f, (double)3.75f};
+        const double cy[5] = {10, 0, 0, 0, 0};
+        const double cz[5] = {4, 0, 0, 0, 0};
+        const double rad[5] = {0.5, (double)0.1f, (double)0.03333f, (double)0.3f, (double)0.9f};
+        const double em[5] = {800, 100, (double)901.803f, (double)11.1111f, 1.23457};
+        s->world_kind = WORLD_LIST;
+        s->nlist = s->ntris + 5;
+        s->list = (int32_t *)malloc(sizeof(int32_t) * (size_t)s->nlist);
+        for (int i = 0; i < s->ntris; ++i) s->list[i] = i;
+        for (int k = 0; k < 5; ++k) {
+            int m = add_material(s, MAT_LIGHT, mk(0, 0, 0), mk(em[k], em[k], em[k]));
+            s->list[s->ntris + k] = REF_SPHERE | add_sphere(s, mk(cx[k], cy[k], cz[k]), rad[k], m);
+        }
+        for (int k = 0; k < 5; ++k) {
+            int m = add_material(s, MAT_LIGHT, mk(0, 0, 0), mk(em[k], em[k], em[k]));
+            int id = add_sphere(s, mk(cx[k], cy[k], cz[k]), rad[k], m);
+            lights = (int32_t *)realloc(lights, sizeof(int32_t) * (size_t)(nlights + 1));
+            lights[nlights++] = REF_SPHERE | id;
+        }
+        s->cam = camera_mk(mk(0, 2, 15), mk(0, -2, 2.5), mk(0, 1, 0), 28.0, aspect, 0.0, 50.0);
+    } else {
+        free(s);
+        return -3;
+    }
+    s->lights = lights; s->nlights = nlights;
+    for (int i = 0; i < s->nmats; ++i)
+        if (s->mats[i].type != MAT_LAMBERT && s->mats[i].type != MAT_LIGHT) { ora_free_scene(s); return -4; }
+    *out = s;
+    return 0;
+}
+void ora_free_scene(ora_scene *s)
+{
+    if (!s) return;
+    free(s->tris); free(s->sph); free(s->mats); free(s->nodes); free(s->list); free(s->lights); free(s);
+}
+void ora_scene_get_info(const ora_scene *s, ora_scene_info *info)
+{
+    info->n_tris = s->ntris; info->n_spheres = s->nsph; info->n_materials = s->nmats;
+    info->n_lights = s->nlights; info->n_nodes = s->nnodes; info->world_kind = s->world_kind;
+    info->n_list = s->nlist; info->bvh_depth = s->bvh_depth;
+}
+/* nodes were allocated in pre-order (left subtree first) = left-first DFS order */
+int ora_scene_export_bvh(const ora_scene *s, double *boxes, int32_t *left, int32_t *right)
+{
+    for (int i = 0; i < s->nnodes; ++i) {
+        vstore(&boxes[6 * i], s->nodes[i].box.min);
+        vstore(&boxes[6 * i + 3], s->nodes[i].box.max);
+        left[i] = s->nodes[i].left; right[i] = s->nodes[i].right;
+    }
+    return s->nnodes;
+}
+int ora_scene_export_tris(const ora_scene *s, double *v9, int32_t *mat)
+{
+    for (int i = 0; i < s->ntris; ++i) {
+        vstore(&v9[9 * i], s->tris[i].v0); vstore(&v9[9 * i + 3], s->tris[i].v1); vstore(&v9[9 * i + 6], s->tris[i].v2);
+        mat[i] = s->tris[i].mat;
+    }
+    return s->ntris;
+}
+
+/* ------------------------------------------------------------------------ */
+/* known-answer entry points                                                */
+/* ------------------------------------------------------------------------ */
+static tri kat_tri(const double *v9, const double *n9, int geo, int nmesh)
+{
+    tri t; memset(&t, 0, sizeof t);
+    t.v0 = vload(v9); t.v1 = vload(v9 + 3); t.v2 = vload(v9 + 6);
+    if (n9) { t.n0 = vload(n9); t.n1 = vload(n9 + 3); t.n2 = vload(n9 + 6); }
+    t.e1 = vsub(t.v1, t.v0); t.e2 = vsub(t.v2, t.v0);
+    t.inv_area = 1 / (0.5 * vlen(cross(t.e1, t.e2)) * nmesh);
+    t.geo = geo;
+    return t;
+}
+int ora_kat_tri_hit(const double *v9, const double *n9, int geo, const double *o, const double *d,
+                    double tmin, double tmax, double *out)
+{
+    tri t = kat_tri(v9, n9, geo, 1);
+    ray r; r.o = vload(o); r.d = vload(d);
+    hit_record h; double u = 0, v = 0;
+    int ok = tri_hit(&t, &r, tmin, tmax, &h, &u, &v);
+    memset(out, 0, sizeof(double) * 10);
+    out[0] = ok;
+    if (ok) { out[1] = h.t; vstore(out + 2, h.p); vstore(out + 5, h.normal); out[8] = u; out[9] = v; }
+    return ok;
+}
+int ora_kat_sphere_hit(const double *c, double r, const double *o, const double *d, double tmin, double tmax, double *out)
+{
+    sphere sp; sp.c = vload(c); sp.r = r; sp.mat = 0;
+    ray ry; ry.o = vload(o); ry.d = vload(d);
+    hit_record h;
+    int ok = sphere_hit(&sp, &ry, tmin, tmax, &h);
+    memset(out, 0, sizeof(double) * 8);
+    out[0] = ok;
+    if (ok) { out[1] = h.t; vstore(out + 2, h.p); vstore(out + 5, h.normal); }
+    return ok;
+}
+int ora_kat_aabb_hit(const double *lo, const double *hi, const double *o, const double *d, double tmin, double tmax)
+{
+    aabb b = aabb_mk(vload(lo), vload(hi));
+    ray r; r.o = vload(o); r.d = vload(d);
+    return aabb_hit(&b, &r, tmin, tmax);
+}
+void ora_kat_camera(const double *from, const double *at, const double *vup, double vfov, double aspect,
+                    double aperture, double focus, double s, double t, const double *smp, double *out6)
+{
+    camera c = camera_mk(vload(from), vload(at), vload(vup), vfov, aspect, aperture, focus);
+    ray r = camera_get_ray(&c, s, t, smp[0], smp[1]);
+    vstore(out6, r.o); vstore(out6 + 3, r.d);
+}
+void ora_kat_cosine(const double *n, const double *smp, double *out4)
+{
+    onb b = onb_from_w(vload(n));
+    v3 d = onb_from_local(&b, hemisphere_to_cosine_direction(smp[0], smp[1]));
+    vstore(out4, d);
+    out4[3] = cosine_pdf_value(vload(n), d);
+}
+void ora_kat_tri_sample(const double *v9, const double *n9, int geo, int n_tris_in_mesh, const double *o,
+                        const double *smp, double *out10)
+{
+    ora_scene s; memset(&s, 0, sizeof s);
+    tri t = kat_tri(v9, n9, geo, n_tris_in_mesh);
+    s.tris = &t; s.ntris = 1;
+    hit_record rec;
+    v3 tl = prim_sample_direct(&s, 0, &rec, vload(o), smp[0], smp[1]);
+    vstore(out10, rec.p); vstore(out10 + 3, rec.normal); vstore(out10 + 6, tl);
+    out10[9] = prim_pdf_direct(&s, 0, &rec, tl);
+}
+void ora_kat_sphere_sample(const double *c, double r, const double *o, const double *smp, double *out7)
+{
+    ora_scene s; memset(&s, 0, sizeof s);
+    sphere sp; sp.c = vload(c); sp.r = r; sp.mat = 0;
+    s.sph = &sp; s.nsph = 1;
+    hit_record rec; memset(&rec, 0, sizeof rec);
+    v3 tl = prim_sample_direct(&s, REF_SPHERE, &rec, vload(o), smp[0], smp[1]);
+    vstore(out7, tl); vstore(out7 + 3, rec.normal);
+    /* pdf_direct_sampling(lrec, to_light) as evaluated at a BSDF hit: lrec.p = o + 1*tl, t = 1 */
+    hit_record l2; l2.t = 1.0; l2.p = vadd(vload(o), tl); l2.normal = rec.normal;
+    out7[6] = prim_pdf_direct(&s, REF_SPHERE, &l2, tl);
+}
+double ora_kat_miweight(double a, double b) { return miWeight(a, b); }
+double ora_kat_fromsrgb(double v) { return FromSrgb(v); }
+int ora_kat_pick(double u, int n) { return pick_sample(u, n); }
+static int key_cmp(const void *a, const void *b, void *arg)
+{
+    const double *k = (const double *)arg;
+    if (k[*(const int32_t *)a] - k[*(const int32_t *)b] < 0.0) return -1;
+    return 1;
+}
+void ora_kat_sort(const double *keys, int n, int32_t *perm_out)
+{
+    for (int i = 0; i < n; ++i) perm_out[i] = i;
+    qsort_r(perm_out, (size_t)n, sizeof(int32_t), key_cmp, (void *)keys);
+}
+
+
+/* hitable_list::hit over ntri triangles (9 doubles each, geometric normals)
+ * followed by nsph spheres (c[3], r): out = hit, winner index, t */
+void ora_kat_list_hit(int ntri, int nsph, const double *geom, const double *o, const double *d, double *out3)
+{
+    ora_scene s; memset(&s, 0, sizeof s);
+    s.tris = (tri *)calloc((size_t)ntri + 1, sizeof(tri));
+    s.sph = (sphere *)calloc((size_t)nsph + 1, sizeof(sphere));
+    s.list = (int32_t *)calloc((size_t)(ntri + nsph) + 1, sizeof(int32_t));
+    for (int i = 0; i < ntri; ++i) { s.tris[i] = kat_tri(geom + 9 * i, NULL, 1, 1); s.list[i] = i; }
+    for (int k = 0; k < nsph; ++k) {
+        const double *g = geom + 9 * ntri + 4 * k;
+        s.sph[k].c = vload(g); s.sph[k].r = g[3];
+        s.list[ntri + k] = REF_SPHERE | k;
+    }
+    s.ntris = ntri; s.nsph = nsph; s.nlist = ntri + nsph; s.world_kind = WORLD_LIST;
+    ray r; r.o = vload(o); r.d = vload(d);
+    hit_record h; ora_counters cnt; memset(&cnt, 0, sizeof cnt);
+    int ok = world_hit(&s, &r, EPSILON, FLT_MAX, &h, &cnt);
+    out3[0] = ok; out3[1] = -1; out3[2] = 0;
+    if (ok) {
+        out3[1] = (h.obj & REF_SPHERE) ? ntri + (h.obj & ~REF_SPHERE) : h.obj;
+        out3[2] = h.t;
+    }
+    free(s.tris); free(s.sph); free(s.list);
+}
+
+/* image_pfm::save_image (image.h:89-118): "PF\n<w> <h>\n-1\n" + float rows y=0..h-1 */
+int ora_write_pfm(const char *path, int nx, int ny, const double *rgb)
+{
+    FILE *f = fopen(path, "wb");
+    if (!f) return -1;
+    fprintf(f, "PF\n%d %d\n-1\n", nx, ny);
+    for (int i = 0; i < nx * ny * 3; ++i) { float v = (float)rgb[i]; fwrite(&v, sizeof v, 1, f); }
+    fclose(f);
+    return 0;
+}

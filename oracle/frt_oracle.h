@@ -1,0 +1,114 @@
+/*
+ * frt_oracle.h -- TEST INFRASTRUCTURE ONLY (the checker, never the product).
+ *
+ * CPU restatement, in plain C and fp64, of jammm/first_raytracer's hot path
+ * (`path::Li`, first_ray/path.cpp:4-116) together with everything it reaches:
+ * camera (camera.h:10-35), parallel_bvh traversal + SAH build
+ * (parallel_bvh.h:39-175, bvh.h:6-55), triangle / sphere / aabb / list
+ * queries, lambertian + diffuse_light + constant environment, cosine pdf,
+ * onb, MIS weights, the OBJ/MTL ingest semantics of mesh_loader.cpp:5-162
+ * (Assimp 5.0.1 behaviour restated) and the film / PFM output
+ * (viewer.cpp:109-132, image.h:89-118).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load this library.  The product path (first_raytracer_amd/, libfrt.so)
+ * never links or calls it.
+ *
+ * The reference draws std::mt19937 per thread (sampler.h:17-34, path.cpp:122)
+ * and cannot be replayed; the restatement and the HIP kernels instead share
+ * the counter-based RNG specified in DESIGN.md ("RNG stream spec").
+ */
+#ifndef FRT_ORACLE_H
+#define FRT_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ora_scene ora_scene;
+
+typedef struct ora_counters {
+    /* reference-algorithm counters (Scene.h:18-22 semantics, 64-bit) */
+    uint64_t node_visits;     /* parallel_bvh_node::hit calls (parallel_bvh.h:41) */
+    uint64_t box_passes;      /* passed node box tests (parallel_bvh.h:45)        */
+    uint64_t tri_tests;       /* triangle::hit calls (triangle.h:71)              */
+    uint64_t sphere_tests;    /* sphere::hit calls                                */
+    /* top-level scene queries = "rays" (path.cpp:10 and :50)                     */
+    uint64_t camera_rays;
+    uint64_t extension_rays;
+    uint64_t shadow_rays;
+    uint64_t samples;
+} ora_counters;
+
+typedef struct ora_scene_info {
+    int32_t n_tris, n_spheres, n_materials, n_lights, n_nodes, world_kind, n_list;
+    int32_t bvh_depth;
+} ora_scene_info;
+
+/* Scene constructors (main.cpp:222-252 cornell_box_obj, main.cpp:281-314 veach_mis).
+ * `kind`: "cornell_box_obj" | "veach_mis" | "obj_geo" | "obj_smooth".
+ * For obj_* the camera is the cornell one.  Returns 0 on success. */
+int  ora_load_scene(const char *kind, const char *obj_path, double aspect, ora_scene **out);
+void ora_free_scene(ora_scene *s);
+void ora_scene_get_info(const ora_scene *s, ora_scene_info *info);
+
+/* Flattened export of the reference-topology BVH in left-first DFS order:
+ * node i: box lo[3],hi[3] (6 doubles), left, right (child >= 0 = node index,
+ * child < 0 = ~prim_ref).  prim_ref: triangle t -> t, sphere k -> (1<<30)|k. */
+int  ora_scene_export_bvh(const ora_scene *s, double *boxes, int32_t *left, int32_t *right);
+/* triangles: 9 doubles (v0,v1,v2) each; materials per triangle */
+int  ora_scene_export_tris(const ora_scene *s, double *v9, int32_t *mat);
+
+/* Render pixels (linear index y*nx+x, y=0 bottom row) with `spp` samples each,
+ * frame seed `seed`, on `nthreads` threads.  out_rgb[3*i..] = mean radiance
+ * (viewer::add_sample semantics).  Returns 0 on success. */
+int  ora_render(const ora_scene *s, int nx, int ny, int spp, uint32_t seed,
+                const int32_t *pixels, int npix, int nthreads,
+                double *out_rgb, ora_counters *cnt);
+
+/* Single query of the world (closest or any hit) with reference counters. */
+int  ora_world_hit(const ora_scene *s, const double *o, const double *d, double tmin, double tmax,
+                   double *t_out, int32_t *prim_out, ora_counters *cnt);
+
+/* RNG stream spec (shared with the HIP kernels). */
+double   ora_rng_uniform(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t dim);
+
+/* ---- component known-answer entry points (checked against oracle/_ref) ---- */
+/* tri: 9 doubles v0 v1 v2; geo=1 geometric normal, else normals n9.
+ * out: hit, t, p[3], normal[3], u, v  (10 doubles) */
+int  ora_kat_tri_hit(const double *v9, const double *n9, int geo, const double *o, const double *d,
+                     double tmin, double tmax, double *out);
+/* sphere c[3], r; out: hit, t, p[3], normal[3] */
+int  ora_kat_sphere_hit(const double *c, double r, const double *o, const double *d,
+                        double tmin, double tmax, double *out);
+/* out: 1/0 */
+int  ora_kat_aabb_hit(const double *lo, const double *hi, const double *o, const double *d,
+                      double tmin, double tmax);
+/* camera: lookfrom, lookat, vup, vfov, aspect, aperture, focus, s, t, sample2 -> o[3], d[3] */
+void ora_kat_camera(const double *from, const double *at, const double *vup, double vfov, double aspect,
+                    double aperture, double focus, double s, double t, const double *smp, double *out6);
+/* cosine pdf around unit normal n: generate(sample2) -> dir[3], value(dir) */
+void ora_kat_cosine(const double *n, const double *smp, double *out4);
+/* triangle sample_direct from o: out p[3], normal[3], to_light[3], pdf */
+void ora_kat_tri_sample(const double *v9, const double *n9, int geo, int n_tris_in_mesh, const double *o,
+                        const double *smp, double *out10);
+/* sphere sample_direct + pdf_direct_sampling: out to_light[3], rec.normal[3], pdf(of lrec=...)  */
+void ora_kat_sphere_sample(const double *c, double r, const double *o, const double *smp, double *out7);
+double ora_kat_miweight(double a, double b);
+double ora_kat_fromsrgb(double v);
+float  ora_kat_atof(const char *s);
+int    ora_kat_pick(double u, int n);
+/* glibc-qsort ordering with the reference comparator (bvh.h:6-55) on keys */
+void   ora_kat_sort(const double *keys, int n, int32_t *perm_out);
+
+void   ora_kat_list_hit(int ntri, int nsph, const double *geom, const double *o, const double *d, double *out3);
+
+/* PFM writer with image_pfm::save_image byte layout (image.h:89-118). */
+int  ora_write_pfm(const char *path, int nx, int ny, const double *rgb);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
