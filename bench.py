@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s of the MI355X path integrator on the BASELINE.json config
+(CornellBox-Original, 1920x1080, 512 spp, path + NEE + MIS), with the image
+tiles sharded over N GPUs (one process per GPU, RCCL all-gather of the tile
+radiance over xGMI), plus the roofline of the path megakernel and the CPU
+baseline (the fp64 C restatement, oracle/, timed on this host's cores).
+
+One "step" = one full frame: every rank renders its tiles (tile t -> rank
+t mod N) into HBM, then the per-rank slot buffers are all-gathered and rank 0
+scatters them into the film.  Scene upload and BVH build happen before the
+timed region.
+
+    python bench.py [--gpus N --steps K --warmup W] [--scene cornell|cornell_1m|veach]
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mrays/sec + RMSE vs CPU ref, CornellBox 1080p 512spp, 1/2/4/8 MI355X"
+SCENES = os.path.join(ROOT, "tests", "golden", "scenes")
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+NODE_BYTES, TRI_BYTES, RAY_BYTES = 32, 48, 32   # B_ray = 32 V + 48 T + 32
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def scene_spec(name, workdir):
+    if name == "cornell":
+        return "cornell_box_obj", os.path.join(SCENES, "CornellBox-Original.obj"), "CornellBox-Original"
+    if name == "veach":
+        return "veach_mis", os.path.join(SCENES, "veach_mi.obj"), "veach_mi"
+    if name == "cornell_1m":
+        import first_raytracer_amd as frt
+        dst = os.path.join(workdir, "cornell_1m_k172.obj")
+        if not os.path.exists(dst):
+            frt.write_tessellated_obj(os.path.join(SCENES, "CornellBox-Original.obj"), 172, dst)
+        return "cornell_box_obj", dst, "cornell_1m (k=172, 1,005,858 tris)"
+    raise ValueError(name)
+
+
+def load_traversal_stats(key):
+    path = os.path.join(ROOT, "profiles", "traversal_stats.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            return json.load(f).get(key)
+    return None
+
+
+def cpu_baseline(kind, obj, nx, ny, spp, seed, npix, threads, film):
+    """The oracle (fp64 C restatement) on a bounded pixel sample of the same
+    frame and RNG streams: CPU Mrays/s, reference traversal counters (for
+    B_ray) and the RMSE of the GPU film on those pixels."""
+    import oracle
+    sc = oracle.OracleScene(kind, obj, nx / ny)
+    pix = np.unique(np.linspace(0, nx * ny - 1, npix).astype(np.int32))
+    t0 = time.perf_counter()
+    out, cnt = sc.render(nx, ny, spp, seed=seed, pixels=pix, nthreads=threads)
+    dt = time.perf_counter() - t0
+    rays = cnt.rays
+    gpu = film.reshape(-1, 3)[pix].astype(np.float64)
+    rmse = float(np.sqrt(np.mean((gpu - out) ** 2)))
+    return {
+        "mrays": rays / dt / 1e6, "seconds": dt, "rays": rays, "npix": len(pix),
+        "V": cnt.node_visits / rays, "T": (cnt.tri_tests + cnt.sphere_tests) / rays,
+        "rays_per_sample": rays / cnt.samples, "rmse": rmse,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="cornell", choices=["cornell", "cornell_1m", "veach"])
+    ap.add_argument("--res", default="1920x1080")
+    ap.add_argument("--spp", type=int, default=512)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--tile", type=int, default=32)
+    ap.add_argument("--cpu-pixels", type=int, default=12288, help="pixels in the CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pfm", default="", help="write the rank-0 film here")
+    args = ap.parse_args()
+    nx, ny = (int(x) for x in args.res.lower().split("x"))
+
+    import torch
+    import torch.distributed as dist
+
+    import first_raytracer_amd as frt
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    workdir = os.path.join(ROOT, "gpurun_out") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else "/tmp"
+    kind, obj, scene_name = scene_spec(args.scene, workdir)
+    t0 = time.perf_counter()
+    hs = frt.HostScene(kind, obj, nx / ny)
+    ctx = frt.Context(local)
+    ctx.upload(hs)
+    setup_s = time.perf_counter() - t0
+
+    params = frt.RenderParams.make(nx, ny, args.spp, seed=args.seed, tile_size=args.tile,
+                                   shard_index=rank, shard_count=world)
+    slot_counts = [int(frt.lib().frt_shard_slot_count(
+        frt.RenderParams.make(nx, ny, args.spp, tile_size=args.tile, shard_index=r, shard_count=world)))
+        for r in range(world)]
+    max_slots = max(slot_counts)
+    my_slots = torch.zeros(max_slots * 3, dtype=torch.float32, device=dev)
+    gathered = torch.zeros(world * max_slots * 3, dtype=torch.float32, device=dev) if world > 1 else None
+    film = torch.zeros(nx * ny * 3, dtype=torch.float32, device=dev)
+    if rank == 0:
+        maps = []
+        for r in range(world):
+            m = frt.shard_slots(frt.RenderParams.make(nx, ny, args.spp, tile_size=args.tile, shard_index=r,
+                                                      shard_count=world))
+            pad = np.full(max_slots, -1, np.int32)
+            pad[:len(m)] = m
+            maps.append(pad)
+        slot_pix = torch.from_numpy(np.concatenate(maps).astype(np.int64)).to(dev)
+        valid = slot_pix >= 0
+        dst_idx = slot_pix[valid]
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        st = ctx.render_device(params, my_slots.data_ptr(), stream.cuda_stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, my_slots)
+            src = gathered
+        else:
+            src = my_slots
+        if rank == 0:
+            film.view(-1, 3)[dst_idx] = src.view(-1, 3)[valid]
+        return st
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t_start = time.perf_counter()
+    rays = 0
+    kernel_ms = []
+    last = None
+    for k in range(args.steps):
+        st = step()
+        rays += st.rays
+        kernel_ms.append(st.kernel_ms)
+        last = st
+        log(f"rank {rank} step {k}: {st.rays / 1e9:.3f} Grays, kernel {st.kernel_ms:.1f} ms")
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        r = torch.tensor([float(rays)], dtype=torch.float64, device=dev)
+        dist.all_reduce(r, op=dist.ReduceOp.SUM)
+        rays = int(r.item())
+
+    if rank == 0:
+        value = rays / elapsed / 1e6
+        film_np = film.cpu().numpy()
+        key = f"{args.scene}:{nx}x{ny}"
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            cpu = cpu_baseline(kind, obj, nx, ny, args.spp, args.seed, args.cpu_pixels, threads, film_np)
+            cpu["threads"] = threads
+        ts = load_traversal_stats(key)
+        if cpu is not None:
+            V, T = cpu["V"], cpu["T"]
+        elif ts is not None:
+            V, T = ts["V"], ts["T"]
+        else:
+            V = T = None
+        avg_kernel_s = float(np.mean(kernel_ms)) * 1e-3
+        rays_per_launch = last.rays
+        roofline = None
+        if V is not None:
+            b_ray = NODE_BYTES * V + TRI_BYTES * T + RAY_BYTES
+            achieved = rays_per_launch * b_ray / avg_kernel_s / 1e9
+            traffic = None
+            pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            if os.path.exists(pmc):
+                with open(pmc) as f:
+                    traffic = json.load(f).get(f"{key}:n{world}")
+            roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "kernel": "path_megakernel", "bytes_per_ray": round(b_ray, 1),
+                        "V_node": round(V, 3), "T_tri": round(T, 3), "rays_per_launch": int(rays_per_launch),
+                        "avg_launch_ms": round(avg_kernel_s * 1e3, 3)}
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "Mrays/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"{scene_name} {nx}x{ny} {args.spp}spp path+NEE+MIS", "scene": args.scene,
+                       "nx": nx, "ny": ny, "spp": args.spp, "seed": args.seed, "tile": args.tile,
+                       "parallelism": f"tiles-interleaved x{world} + rccl all-gather"},
+            "rmse": None if cpu is None else cpu["rmse"],
+            "rays_per_step": int(rays // args.steps),
+            "setup_s": round(setup_s, 2),
+            "image_mean": [round(float(x), 6) for x in film_np.reshape(-1, 3).mean(0)],
+            "roofline": roofline,
+            "cpu_baseline": None if cpu is None else {
+                "value": round(cpu["mrays"], 3), "unit": "Mrays/s", "cores": cpu["threads"], "kind": "port",
+                "sample": f"{cpu['npix']} evenly spaced pixels of the same {nx}x{ny} frame at {args.spp} spp "
+                          f"({cpu['rays']} rays, {cpu['seconds']:.1f} s); fp64 C restatement of path::Li"},
+        }
+        if args.pfm:
+            frt.write_pfm(args.pfm, film_np.reshape(ny, nx, 3))
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

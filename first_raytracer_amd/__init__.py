@@ -1,0 +1,236 @@
+"""first_raytracer_amd -- MI355X-native path-tracing integrator (drop-in for
+jammm/first_raytracer's path::Li / path::Render hot path).
+
+The product is native: libfrt.so (HIP kernels for gfx950 + the C++ host scene
+pipeline) behind the C-ABI in include/frt.h.  This module is a thin ctypes
+binding used by the tests, bench.py and scripts; it never falls back to a CPU
+path -- if libfrt.so is missing or no gfx950 device is present, it raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libfrt.so")
+
+FRT_WORLD_BVH, FRT_WORLD_LIST = 0, 1
+FRT_MAT_LAMBERTIAN, FRT_MAT_DIFFUSE_LIGHT = 0, 1
+FRT_PRIM_SPHERE = 1 << 30
+
+ERRORS = {0: "ok", -1: "invalid", -2: "hip", -3: "no scene", -4: "unsupported", -5: "io", -6: "no gfx950 device"}
+
+
+class FrtError(RuntimeError):
+    pass
+
+
+class Material(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("albedo", ctypes.c_double * 3), ("emit", ctypes.c_double * 3)]
+
+
+class SceneView(ctypes.Structure):
+    _fields_ = [
+        ("world_kind", ctypes.c_int32),
+        ("n_tris", ctypes.c_int32),
+        ("tri_v", ctypes.c_void_p), ("tri_n", ctypes.c_void_p), ("tri_material", ctypes.c_void_p),
+        ("tri_geometry_normal", ctypes.c_void_p), ("tri_inv_area", ctypes.c_void_p),
+        ("n_spheres", ctypes.c_int32), ("sphere", ctypes.c_void_p), ("sphere_material", ctypes.c_void_p),
+        ("n_materials", ctypes.c_int32), ("materials", ctypes.c_void_p),
+        ("n_nodes", ctypes.c_int32), ("root", ctypes.c_int32),
+        ("node_box", ctypes.c_void_p), ("node_child", ctypes.c_void_p),
+        ("n_list", ctypes.c_int32), ("list", ctypes.c_void_p),
+        ("n_lights", ctypes.c_int32), ("lights", ctypes.c_void_p),
+        ("cam_origin", ctypes.c_double * 3), ("cam_lower_left", ctypes.c_double * 3),
+        ("cam_horizontal", ctypes.c_double * 3), ("cam_vertical", ctypes.c_double * 3),
+        ("cam_u", ctypes.c_double * 3), ("cam_v", ctypes.c_double * 3),
+        ("cam_lens_radius", ctypes.c_double),
+        ("env_color", ctypes.c_double * 3),
+    ]
+
+
+class RenderParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("nx", "ny", "spp")] + [("seed", ctypes.c_uint32)] + [
+        (n, ctypes.c_int32) for n in ("max_depth", "integrator", "tile_size", "shard_index", "shard_count",
+                                      "samples_per_item", "flags")]
+
+    @classmethod
+    def make(cls, nx, ny, spp, seed=0, max_depth=33, tile_size=32, shard_index=0, shard_count=1,
+             samples_per_item=0):
+        return cls(nx=nx, ny=ny, spp=spp, seed=seed, max_depth=max_depth, integrator=0, tile_size=tile_size,
+                   shard_index=shard_index, shard_count=shard_count, samples_per_item=samples_per_item, flags=0)
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in ("camera_rays", "extension_rays", "shadow_rays", "samples",
+                                               "pixels", "work_items")] + [
+        ("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double)]
+
+    @property
+    def rays(self):
+        return self.camera_rays + self.extension_rays + self.shadow_rays
+
+    def as_dict(self):
+        d = {n: getattr(self, n) for n, _ in self._fields_}
+        d["rays"] = self.rays
+        return d
+
+
+class HostSceneInfo(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("n_tris", "n_spheres", "n_materials", "n_lights", "n_nodes",
+                                              "world_kind", "n_list", "bvh_depth")] + [
+        ("load_ms", ctypes.c_double), ("build_ms", ctypes.c_double)]
+
+
+_lib = None
+
+# every symbol include/frt.h declares
+EXPORTS = ("frt_get_abi_version", "frt_create", "frt_destroy", "frt_last_error", "frt_upload_scene",
+           "frt_shard_slot_count", "frt_shard_slots", "frt_render", "frt_render_device", "frt_scene_create",
+           "frt_scene_view_get", "frt_scene_info", "frt_scene_destroy", "frt_write_tessellated_obj",
+           "frt_write_pfm")
+
+
+def lib():
+    """Load libfrt.so (built in-tree by __graft_entry__.build()).  Raises if missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FrtError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(LIB_PATH)
+    vp = ctypes.c_void_p
+    L.frt_get_abi_version.restype = ctypes.c_int
+    L.frt_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    L.frt_destroy.argtypes = [vp]
+    L.frt_last_error.argtypes = [vp]
+    L.frt_last_error.restype = ctypes.c_char_p
+    L.frt_upload_scene.argtypes = [vp, ctypes.POINTER(SceneView)]
+    L.frt_shard_slot_count.argtypes = [ctypes.POINTER(RenderParams)]
+    L.frt_shard_slot_count.restype = ctypes.c_int64
+    L.frt_shard_slots.argtypes = [ctypes.POINTER(RenderParams), vp]
+    L.frt_render.argtypes = [vp, ctypes.POINTER(RenderParams), vp, ctypes.POINTER(Stats)]
+    L.frt_render_device.argtypes = [vp, ctypes.POINTER(RenderParams), vp, vp, ctypes.POINTER(Stats)]
+    L.frt_scene_create.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_double, ctypes.POINTER(vp)]
+    L.frt_scene_view_get.argtypes = [vp, ctypes.POINTER(SceneView)]
+    L.frt_scene_info.argtypes = [vp, ctypes.POINTER(HostSceneInfo)]
+    L.frt_scene_destroy.argtypes = [vp]
+    L.frt_scene_destroy.restype = None
+    L.frt_write_tessellated_obj.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p]
+    L.frt_write_pfm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, vp]
+    _lib = L
+    return L
+
+
+def _check(rc, what, ctx=None):
+    if rc != 0:
+        msg = ""
+        if ctx is not None:
+            msg = lib().frt_last_error(ctx).decode(errors="replace")
+        raise FrtError(f"{what} failed: {ERRORS.get(rc, rc)} {msg}")
+
+
+class HostScene:
+    """Scene built natively (main.cpp scene constructors + mesh_loader + create_bvh)."""
+
+    def __init__(self, kind, obj_path, aspect):
+        self.ptr = ctypes.c_void_p()
+        _check(lib().frt_scene_create(kind.encode(), obj_path.encode(), float(aspect), ctypes.byref(self.ptr)),
+               f"frt_scene_create({kind})")
+        self.info = HostSceneInfo()
+        lib().frt_scene_info(self.ptr, ctypes.byref(self.info))
+
+    def view(self):
+        v = SceneView()
+        _check(lib().frt_scene_view_get(self.ptr, ctypes.byref(v)), "frt_scene_view_get")
+        return v
+
+    def arrays(self):
+        """numpy views of the flattened scene (copies)."""
+        v = self.view()
+
+        def arr(ptr, n, dt, w=1):
+            if n == 0 or not ptr:
+                return np.zeros((0, w) if w > 1 else 0, dt)
+            a = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(np.ctypeslib.as_ctypes_type(dt))),
+                                      shape=(n * w,)).copy()
+            return a.reshape(n, w) if w > 1 else a
+        return {
+            "tri_v": arr(v.tri_v, v.n_tris, np.float64, 9),
+            "tri_material": arr(v.tri_material, v.n_tris, np.int32),
+            "node_box": arr(v.node_box, v.n_nodes, np.float64, 6),
+            "node_child": arr(v.node_child, v.n_nodes, np.int32, 2),
+            "root": v.root,
+            "lights": arr(v.lights, v.n_lights, np.int32),
+            "list": arr(v.list, v.n_list, np.int32),
+        }
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            try:
+                lib().frt_scene_destroy(self.ptr)
+            except Exception:
+                pass
+            self.ptr = None
+
+
+class Context:
+    """One GPU (frt_ctx).  Raises FrtError when no gfx950 device is present."""
+
+    def __init__(self, device=0):
+        self.ptr = ctypes.c_void_p()
+        _check(lib().frt_create(int(device), ctypes.byref(self.ptr)), f"frt_create(device={device})")
+
+    def upload(self, scene):
+        view = scene.view() if isinstance(scene, HostScene) else scene
+        _check(lib().frt_upload_scene(self.ptr, ctypes.byref(view)), "frt_upload_scene", self.ptr)
+
+    def render(self, params, film=None):
+        """Render into a full film (nx*ny*3 float32, y=0 bottom row).  Returns (film, stats)."""
+        if film is None:
+            film = np.zeros((params.ny, params.nx, 3), np.float32)
+        assert film.dtype == np.float32 and film.flags.c_contiguous and film.size == params.nx * params.ny * 3
+        st = Stats()
+        _check(lib().frt_render(self.ptr, ctypes.byref(params), film.ctypes.data, ctypes.byref(st)),
+               "frt_render", self.ptr)
+        return film, st
+
+    def render_device(self, params, dev_ptr, stream_ptr=None):
+        """Render this shard's slots into device memory at dev_ptr (slot_count*3 floats)."""
+        st = Stats()
+        _check(lib().frt_render_device(self.ptr, ctypes.byref(params), ctypes.c_void_p(dev_ptr),
+                                       ctypes.c_void_p(stream_ptr) if stream_ptr else None, ctypes.byref(st)),
+               "frt_render_device", self.ptr)
+        return st
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            lib().frt_destroy(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def shard_slots(params):
+    """Linear film index (y*nx+x) held by each output slot of a shard (-1 = padding)."""
+    n = lib().frt_shard_slot_count(ctypes.byref(params))
+    if n < 0:
+        raise FrtError("bad render params")
+    out = np.zeros(n, np.int32)
+    _check(lib().frt_shard_slots(ctypes.byref(params), out.ctypes.data), "frt_shard_slots")
+    return out
+
+
+def write_pfm(path, film):
+    film = np.ascontiguousarray(film, dtype=np.float32)
+    ny, nx = film.shape[0], film.shape[1]
+    _check(lib().frt_write_pfm(path.encode(), nx, ny, film.ctypes.data), "frt_write_pfm")
+
+
+def write_tessellated_obj(src_obj, k, dst_obj):
+    _check(lib().frt_write_tessellated_obj(src_obj.encode(), int(k), dst_obj.encode()), "frt_write_tessellated_obj")

@@ -1,0 +1,184 @@
+// frt_device.hpp -- fp32 device math shared by the path megakernel.
+// All functions are __host__ __device__ so the same code can be compiled for
+// the host-side self tests (frt_selftest_* in frt_render.hip).
+//
+// Reference semantics restated (fp64 there, fp32 here), first_ray/:
+//   aabb::hit           aabb.h:14-31       (slab test, NaN-tolerant)
+//   triangle::hit       triangle.h:69-118  (Moller-Trumbore)
+//   sphere::hit         sphere.h:26-56
+//   onb::build_from_w   onb.h:18-30
+//   hemisphere_to_cosine_direction pdf.h:13-23, cosine_pdf pdf.h:80-97
+//   miWeight            util.h:55-60
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define FRT_HD __host__ __device__ __forceinline__
+
+namespace frt {
+
+constexpr float kEps = 1e-4f;              // util.h:10 EPSILON
+constexpr float kShadowEps = 1e-3f;        // util.h:11 SHADOW_EPSILON
+constexpr float kPi = 3.14159265358979323846f;
+constexpr float kInvPi = 0.318309886183790671538f;
+constexpr float kTMaxClosest = 3.40282347e+38f;   // FLT_MAX (path.cpp:10)
+
+struct f3 { float x, y, z; };
+FRT_HD f3 mk3(float x, float y, float z) { return f3{x, y, z}; }
+FRT_HD f3 operator+(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+FRT_HD f3 operator-(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+FRT_HD f3 operator*(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+FRT_HD f3 operator*(float t, f3 v) { return f3{t * v.x, t * v.y, t * v.z}; }
+FRT_HD f3 operator-(f3 v) { return f3{-v.x, -v.y, -v.z}; }
+FRT_HD float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+FRT_HD f3 cross(f3 a, f3 b) { return f3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+FRT_HD float len2(f3 v) { return dot(v, v); }
+FRT_HD float rlen(f3 v) { return 1.0f / sqrtf(len2(v)); }
+FRT_HD f3 normalize(f3 v) { return rlen(v) * v; }
+FRT_HD bool nonzero(f3 v) { return v.x != 0.0f || v.y != 0.0f || v.z != 0.0f; }
+FRT_HD f3 xyz(float4 v) { return f3{v.x, v.y, v.z}; }
+
+// ---------------------------------------------------------------------------
+// RNG stream spec (identical to oracle/frt_oracle.c rng_make/rng_u)
+// ---------------------------------------------------------------------------
+FRT_HD uint32_t mix32(uint32_t x)
+{
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x;
+}
+struct RngKey { uint32_t k0, k1; };
+FRT_HD RngKey rng_key(uint32_t seed, uint32_t pixel, uint32_t sample)
+{
+    const uint32_t a = mix32(seed ^ 0x2545F491U);
+    RngKey k;
+    k.k0 = mix32(mix32(a ^ pixel) + sample * 0x9E3779B9U);
+    k.k1 = mix32(mix32(a + pixel * 0x632BE5ABU) ^ (sample * 0x85157AF5U + 0x5851F42DU));
+    return k;
+}
+// uniform in [0,1) with 24 bits: exact in fp32 and fp64
+FRT_HD float rng_u(RngKey k, uint32_t dim)
+{
+    const uint32_t h = mix32(mix32(k.k0 ^ (dim * 0x85EBCA77U + 0xC2B2AE3DU)) + k.k1);
+    return (float)(h >> 8) * (1.0f / 16777216.0f);
+}
+// dimension layout: camera 0..3; bounce d: base 4 + 8d (+3 light pick,
+// +4..5 light sample, +6..7 bsdf direction; +0..2 reserved for get3d)
+FRT_HD uint32_t dim_bounce(int depth) { return 4u + 8u * (uint32_t)depth; }
+
+// ---------------------------------------------------------------------------
+// geometry
+// ---------------------------------------------------------------------------
+// reciprocal direction for the slab test.  Zero components are nudged to
+// +-1e-30 so no 0*inf NaN can arise; the reference's NaN-tolerant compare
+// (aabb.h:24-25) keeps the interval unchanged in that case, and so does this
+// (the near-parallel slab then spans +-huge).  Device boxes are padded
+// outward, so the degenerate "origin exactly on a face" case cannot cull.
+FRT_HD f3 safe_inv(f3 d)
+{
+    const float tiny = 1e-30f;
+    const float dx = fabsf(d.x) > tiny ? d.x : copysignf(tiny, d.x);
+    const float dy = fabsf(d.y) > tiny ? d.y : copysignf(tiny, d.y);
+    const float dz = fabsf(d.z) > tiny ? d.z : copysignf(tiny, d.z);
+    return f3{1.0f / dx, 1.0f / dy, 1.0f / dz};
+}
+// slab test of a box against [tmin, tmax]; returns entry distance or +inf on
+// miss (aabb.h:14-31: the reference's per-axis early exit decides the same).
+FRT_HD float slab_entry(float lox, float loy, float loz, float hix, float hiy, float hiz,
+                        f3 o, f3 invd, float tmin, float tmax)
+{
+    const float tx0 = (lox - o.x) * invd.x, tx1 = (hix - o.x) * invd.x;
+    const float ty0 = (loy - o.y) * invd.y, ty1 = (hiy - o.y) * invd.y;
+    const float tz0 = (loz - o.z) * invd.z, tz1 = (hiz - o.z) * invd.z;
+    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
+    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+    return (tf < tn) ? __builtin_inff() : tn;
+}
+
+// Moller-Trumbore (triangle.h:69-118): returns t, or -1 on miss.  Accepts
+// t in (tmin, tmax] -- the caller resolves t == tmax with the DFS rank tie rule.
+FRT_HD float tri_intersect(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float tmin, float tmax, float &u, float &v)
+{
+    const f3 h = cross(d, e2);
+    const float a = dot(e1, h);
+    if (a == 0.0f) return -1.0f;
+    const float f = 1.0f / a;
+    const f3 s = o - v0;
+    u = f * dot(s, h);
+    if (u < 0.0f || u > 1.0f) return -1.0f;
+    const f3 q = cross(s, e1);
+    v = f * dot(d, q);
+    if (!(v >= 0.0f && u + v <= 1.0f)) return -1.0f;
+    const float t = f * dot(e2, q);
+    return (t > tmin && t <= tmax) ? t : -1.0f;
+}
+
+// sphere::hit (sphere.h:26-56): returns t or -1; accepts t in [tmin, tmax]
+FRT_HD float sphere_intersect(f3 o, f3 d, f3 c, float r, float tmin, float tmax)
+{
+    const f3 oc = o - c;
+    const float a = dot(d, d);
+    const float b = dot(oc, d);
+    const float cc = dot(oc, oc) - r * r;
+    float disc = b * b - a * cc;
+    if (!(disc >= 0.0f)) return -1.0f;
+    disc = sqrtf(disc);
+    float t = (-b - disc) / a;
+    if (t < tmin) t = (-b + disc) / a;
+    if (t < tmin || t > tmax) return -1.0f;
+    return t;
+}
+
+// onb::build_from_w (onb.h:18-30) + fromLocal
+struct Onb { f3 u, v, w; };
+FRT_HD Onb onb_from_w(f3 n)
+{
+    Onb b;
+    b.w = n;
+    if (fabsf(n.x) > fabsf(n.y)) {
+        const float inv = 1.0f / sqrtf(n.x * n.x + n.z * n.z);
+        b.v = f3{n.z * inv, 0.0f, -n.x * inv};
+    } else {
+        const float inv = 1.0f / sqrtf(n.y * n.y + n.z * n.z);
+        b.v = f3{0.0f, n.z * inv, -n.y * inv};
+    }
+    b.u = cross(b.v, b.w);
+    return b;
+}
+FRT_HD f3 onb_local(const Onb &b, f3 a) { return a.x * b.u + a.y * b.v + a.z * b.w; }
+
+// pdf.h:13-23
+FRT_HD f3 cosine_direction(float r0, float r1)
+{
+    const float r = sqrtf(r0);
+    const float phi = 2.0f * kPi * r1;
+    float sp, cp;
+    sincosf(phi, &sp, &cp);
+    return f3{r * cp, r * sp, sqrtf(1.0f - r0)};
+}
+// pdf.h:38-44
+FRT_HD f3 uniform_sphere(float u0, float u1)
+{
+    const float z = 1.0f - 2.0f * u0;
+    const float r = sqrtf(fmaxf(0.0f, 1.0f - z * z));
+    float sp, cp;
+    sincosf(2.0f * kPi * u1, &sp, &cp);
+    return f3{r * cp, r * sp, z};
+}
+// pdf.h:46-56
+FRT_HD f3 random_to_sphere(float radius, float dist2, float r1, float r2)
+{
+    const float z = 1.0f + r2 * (sqrtf(1.0f - radius * radius / dist2) - 1.0f);
+    float sp, cp;
+    sincosf(2.0f * kPi * r1, &sp, &cp);
+    const float s = sqrtf(1.0f - z * z);
+    return f3{cp * s, sp * s, z};
+}
+// util.h:55-60
+FRT_HD float mi_weight(float p1, float p2)
+{
+    p1 *= p1;
+    p2 *= p2;
+    return p1 / (p1 + p2);
+}
+
+}  // namespace frt

@@ -1,0 +1,836 @@
+// scene.cpp -- native host-side scene pipeline behind include/frt.h:
+//   * OBJ/MTL ingest with the semantics of mesh_loader::load_obj
+//     (first_ray/mesh_loader.cpp:5-162) on top of Assimp 5.0.1's OBJ import
+//     (object/material mesh split, fast_atoreal_move parsing, quad
+//     triangulation, GenSmoothNormals) -- Assimp is absent from this image,
+//     its behaviour is restated ("unpinned at the Assimp boundary");
+//   * create_triangle_mesh (triangle.cpp:9-23): one triangle per face,
+//     emissive meshes feed Scene::lights;
+//   * parallel_bvh_node::create_bvh (parallel_bvh.h:67-175): the SAH split
+//     rule with glibc's merge-sort qsort order (bvh.h:6-55 comparators),
+//     built with std::thread subtrees instead of taskflow subflows;
+//   * scene constructors cornell_box_obj (main.cpp:222-252) and veach_mis
+//     (main.cpp:281-314), camera (camera.h:10-28);
+//   * the cornell_1m tessellation generator and the PFM writer (image.h:89-118).
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "frt.h"
+
+namespace {
+
+constexpr double kPi = 3.14159265358979323846;
+
+struct V3 {
+    double x = 0, y = 0, z = 0;
+};
+inline V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline V3 operator*(double t, V3 v) { return {t * v.x, t * v.y, t * v.z}; }
+inline V3 cross(V3 a, V3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+inline double length(V3 v) { return std::sqrt(v.x * v.x + v.y * v.y + v.z * v.z); }
+inline V3 unit(V3 v)
+{
+    const double l = length(v);
+    return {v.x / l, v.y / l, v.z / l};
+}
+
+// ---------------------------------------------------------------------------
+// Assimp fast_atoreal_move<float> (restated): integer part -> float, up to 15
+// fractional digits as an integer scaled by a double table, added in float.
+// ---------------------------------------------------------------------------
+const double kAtofTable[16] = {0.0, 0.1, 0.01, 0.001, 0.0001, 0.00001, 0.000001, 0.0000001, 0.00000001, 0.000000001,
+                               0.0000000001, 0.00000000001, 0.000000000001, 0.0000000000001, 0.00000000000001,
+                               0.000000000000001};
+uint64_t strtoul10_64(const char *in, const char **out, unsigned *max_inout)
+{
+    unsigned cur = 0;
+    uint64_t value = 0;
+    while (*in >= '0' && *in <= '9') {
+        const uint64_t nv = value * 10 + (uint64_t)(*in - '0');
+        if (nv < value) break;
+        value = nv;
+        ++in;
+        ++cur;
+        if (max_inout && *max_inout == cur) {
+            while (*in >= '0' && *in <= '9') ++in;
+            break;
+        }
+    }
+    if (out) *out = in;
+    if (max_inout) *max_inout = cur;
+    return value;
+}
+const char *parse_float(const char *c, float &out)
+{
+    float f = 0.0f;
+    const bool inv = (*c == '-');
+    if (inv || *c == '+') ++c;
+    if (!((*c >= '0' && *c <= '9') || ((*c == '.' || *c == ',') && c[1] >= '0' && c[1] <= '9'))) {
+        out = 0.0f;
+        return c;
+    }
+    if (!(*c == '.' || *c == ',')) f = (float)strtoul10_64(c, &c, nullptr);
+    if ((*c == '.' || *c == ',') && c[1] >= '0' && c[1] <= '9') {
+        ++c;
+        unsigned diff = 15;
+        double pl = (double)strtoul10_64(c, &c, &diff);
+        pl *= kAtofTable[diff];
+        f += (float)pl;
+    } else if (*c == '.') {
+        ++c;
+    }
+    if (*c == 'e' || *c == 'E') {
+        ++c;
+        const bool einv = (*c == '-');
+        if (einv || *c == '+') ++c;
+        float ex = (float)strtoul10_64(c, &c, nullptr);
+        if (einv) ex = -ex;
+        f *= std::pow(10.0f, ex);
+    }
+    out = inv ? -f : f;
+    return c;
+}
+inline const char *skip_ws(const char *p)
+{
+    while (*p == ' ' || *p == '\t') ++p;
+    return p;
+}
+
+struct Mtl {
+    std::string name;
+    float kd[3] = {0.6f, 0.6f, 0.6f}, ks[3] = {0, 0, 0}, ke[3] = {0, 0, 0};
+    float d = 1.0f, ni = 1.0f, ns = 0.0f;
+};
+struct ObjMesh {
+    int mtl = -2;  // -2: no material
+    std::vector<int> v;   // 3 per face
+    std::vector<int> vn;  // 3 per face (-1 = none)
+};
+struct ObjData {
+    std::vector<float> v, vn;
+    std::vector<Mtl> mats;
+    std::vector<ObjMesh> meshes;
+};
+
+std::string dir_of(const std::string &path)
+{
+    const size_t s = path.find_last_of('/');
+    return s == std::string::npos ? std::string() : path.substr(0, s + 1);
+}
+std::string rstrip(std::string s)
+{
+    while (!s.empty() && (s.back() == '\n' || s.back() == '\r' || s.back() == ' ' || s.back() == '\t')) s.pop_back();
+    return s;
+}
+
+bool load_mtl(const std::string &path, ObjData &od)
+{
+    std::ifstream f(path);
+    if (!f) return false;
+    std::string line;
+    Mtl *cur = nullptr;
+    while (std::getline(f, line)) {
+        line = rstrip(line);
+        const char *p = skip_ws(line.c_str());
+        if (!strncmp(p, "newmtl", 6)) {
+            od.mats.emplace_back();
+            cur = &od.mats.back();
+            cur->name = skip_ws(p + 6);
+            continue;
+        }
+        if (!cur) continue;
+        float *dst = nullptr;
+        int n = 1;
+        const char *q = nullptr;
+        if (p[0] == 'K' && (p[2] == ' ' || p[2] == '\t')) {
+            if (p[1] == 'd') dst = cur->kd;
+            else if (p[1] == 's') dst = cur->ks;
+            else if (p[1] == 'e') dst = cur->ke;
+            n = 3;
+            q = p + 2;
+        } else if (p[0] == 'd' && (p[1] == ' ' || p[1] == '\t')) {
+            dst = &cur->d; q = p + 1;
+        } else if (p[0] == 'N' && p[1] == 'i') {
+            dst = &cur->ni; q = p + 2;
+        } else if (p[0] == 'N' && p[1] == 's') {
+            dst = &cur->ns; q = p + 2;
+        } else if (p[0] == 'T' && p[1] == 'r') {
+            float tr;
+            parse_float(skip_ws(p + 2), tr);
+            cur->d = 1.0f - tr;
+            continue;
+        }
+        if (!dst) continue;
+        for (int k = 0; k < n; ++k) q = parse_float(skip_ws(q), dst[k]);
+    }
+    return true;
+}
+
+inline void fdivs(float *v, float f)  // aiVector3t::operator/=
+{
+    if (f == 1.0f) return;
+    const float inv = 1.0f / f;
+    v[0] *= inv; v[1] *= inv; v[2] *= inv;
+}
+
+// TriangulateProcess: a quad is fanned from its concave vertex (or vertex 0)
+int quad_start(const ObjData &od, const int *vi)
+{
+    for (int i = 0; i < 4; ++i) {
+        const float *v0 = &od.v[3 * vi[(i + 3) % 4]], *v1 = &od.v[3 * vi[(i + 2) % 4]];
+        const float *v2 = &od.v[3 * vi[(i + 1) % 4]], *v = &od.v[3 * vi[i]];
+        float l[3] = {v0[0] - v[0], v0[1] - v[1], v0[2] - v[2]};
+        float dg[3] = {v1[0] - v[0], v1[1] - v[1], v1[2] - v[2]};
+        float r[3] = {v2[0] - v[0], v2[1] - v[1], v2[2] - v[2]};
+        fdivs(l, std::sqrt(l[0] * l[0] + l[1] * l[1] + l[2] * l[2]));
+        fdivs(dg, std::sqrt(dg[0] * dg[0] + dg[1] * dg[1] + dg[2] * dg[2]));
+        fdivs(r, std::sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]));
+        const float angle = std::acos(l[0] * dg[0] + l[1] * dg[1] + l[2] * dg[2]) +
+                            std::acos(r[0] * dg[0] + r[1] * dg[1] + r[2] * dg[2]);
+        if (angle > (float)kPi) return i;
+    }
+    return 0;
+}
+
+bool parse_obj(const std::string &path, ObjData &od)
+{
+    std::ifstream f(path);
+    if (!f) return false;
+    std::string line, group;
+    ObjMesh *cur = nullptr;
+    int cur_mtl = -2;
+    bool any_group = false;
+    auto new_mesh = [&](int m) {
+        od.meshes.emplace_back();
+        od.meshes.back().mtl = m;
+        return &od.meshes.back();
+    };
+    while (std::getline(f, line)) {
+        const char *p = skip_ws(line.c_str());
+        if (p[0] == 'v' && (p[1] == ' ' || p[1] == '\t')) {
+            const char *q = p + 1;
+            for (int k = 0; k < 3; ++k) {
+                float x;
+                q = parse_float(skip_ws(q), x);
+                od.v.push_back(x);
+            }
+        } else if (p[0] == 'v' && p[1] == 'n') {
+            const char *q = p + 2;
+            for (int k = 0; k < 3; ++k) {
+                float x;
+                q = parse_float(skip_ws(q), x);
+                od.vn.push_back(x);
+            }
+        } else if (!strncmp(p, "mtllib", 6)) {
+            load_mtl(dir_of(path) + rstrip(skip_ws(p + 6)), od);
+        } else if ((p[0] == 'g' || p[0] == 'o') && (p[1] == ' ' || p[1] == '\t' || p[1] == 0 || p[1] == '\r')) {
+            // ObjFileParser: a new group name starts a new object whose first mesh inherits the material
+            const std::string nm = rstrip(skip_ws(p + 1));
+            if (cur && any_group && nm == group) continue;
+            group = nm;
+            any_group = true;
+            cur = new_mesh(cur_mtl);
+        } else if (!strncmp(p, "usemtl", 6)) {
+            const std::string nm = rstrip(skip_ws(p + 6));
+            int idx = -1;
+            for (size_t i = 0; i < od.mats.size(); ++i)
+                if (od.mats[i].name == nm) idx = (int)i;
+            if (idx < 0) {  // unknown: a named default material
+                od.mats.emplace_back();
+                od.mats.back().name = nm;
+                idx = (int)od.mats.size() - 1;
+            }
+            if (idx == cur_mtl && cur) continue;
+            cur_mtl = idx;
+            if (!cur) {
+                cur = new_mesh(cur_mtl);
+                continue;
+            }
+            if (cur->mtl != -2 && cur->mtl != idx && !cur->v.empty()) cur = new_mesh(cur_mtl);  // needsNewMesh
+            else cur->mtl = idx;
+        } else if (p[0] == 'f' && (p[1] == ' ' || p[1] == '\t')) {
+            if (!cur) cur = new_mesh(cur_mtl);
+            int vi[64], ni[64], nv = 0;
+            const char *q = p + 1;
+            const int nverts = (int)(od.v.size() / 3), nnorm = (int)(od.vn.size() / 3);
+            while (*q && nv < 64) {
+                q = skip_ws(q);
+                if (!*q || *q == '\r' || *q == '\n') break;
+                char *e;
+                long a = strtol(q, &e, 10);
+                q = e;
+                long nn = 0;
+                if (*q == '/') {
+                    ++q;
+                    if (*q != '/') { strtol(q, &e, 10); q = e; }
+                    if (*q == '/') { ++q; nn = strtol(q, &e, 10); q = e; }
+                }
+                while (*q && *q != ' ' && *q != '\t') ++q;
+                vi[nv] = (int)(a < 0 ? nverts + a : a - 1);
+                ni[nv] = nn == 0 ? -1 : (int)(nn < 0 ? nnorm + nn : nn - 1);
+                ++nv;
+            }
+            auto push = [&](int a, int b, int c) {
+                cur->v.insert(cur->v.end(), {vi[a], vi[b], vi[c]});
+                cur->vn.insert(cur->vn.end(), {ni[a], ni[b], ni[c]});
+            };
+            if (nv == 3) {
+                push(0, 1, 2);
+            } else if (nv == 4) {
+                const int s = quad_start(od, vi);
+                push(s, (s + 1) % 4, (s + 2) % 4);
+                push(s, (s + 2) % 4, (s + 3) % 4);
+            } else if (nv > 4) {
+                for (int k = 1; k + 1 < nv; ++k) push(0, k, k + 1);
+            }
+        }
+    }
+    return true;
+}
+
+// GenVertexNormalsProcess, default 175 degree limit: every corner gets the
+// normalised sum of the face normals of all corners within epsilon of it.
+void smooth_normals(const ObjData &od, const ObjMesh &m, std::vector<float> &cn)
+{
+    const size_t nf = m.v.size() / 3, nc = m.v.size();
+    std::vector<float> fn(3 * nf);
+    float lo[3] = {1e30f, 1e30f, 1e30f}, hi[3] = {-1e30f, -1e30f, -1e30f};
+    for (size_t f = 0; f < nf; ++f) {
+        const float *a = &od.v[3 * m.v[3 * f]], *b = &od.v[3 * m.v[3 * f + 1]], *c = &od.v[3 * m.v[3 * f + 2]];
+        const float e1[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+        const float e2[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
+        float n[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+        const float l = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+        if (l > 0.0f) fdivs(n, l);
+        memcpy(&fn[3 * f], n, sizeof n);
+        for (int k = 0; k < 3; ++k) {
+            const float *v = &od.v[3 * m.v[3 * f + k]];
+            for (int d = 0; d < 3; ++d) { lo[d] = std::min(lo[d], v[d]); hi[d] = std::max(hi[d], v[d]); }
+        }
+    }
+    const float dd[3] = {hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]};
+    const float eps = std::sqrt(dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2]) * 1e-4f;
+    const float eps2 = eps * eps;
+    // grid hashing with cell = eps (neighbour cells searched)
+    const float cell = eps > 0.0f ? eps : 1.0f;
+    auto key = [&](int64_t ix, int64_t iy, int64_t iz) {
+        return (uint64_t)(ix * 73856093LL) ^ (uint64_t)(iy * 19349663LL) ^ (uint64_t)(iz * 83492791LL);
+    };
+    std::unordered_multimap<uint64_t, size_t> grid;
+    grid.reserve(nc * 2);
+    auto cell_of = [&](const float *v, int64_t *c3) {
+        for (int d = 0; d < 3; ++d) c3[d] = (int64_t)std::floor((v[d] - lo[d]) / cell);
+    };
+    for (size_t i = 0; i < nc; ++i) {
+        int64_t c3[3];
+        cell_of(&od.v[3 * m.v[i]], c3);
+        grid.emplace(key(c3[0], c3[1], c3[2]), i);
+    }
+    cn.assign(3 * nc, 0.0f);
+    std::vector<size_t> found;
+    for (size_t i = 0; i < nc; ++i) {
+        const float *pi = &od.v[3 * m.v[i]];
+        int64_t c3[3];
+        cell_of(pi, c3);
+        found.clear();
+        for (int dx = -1; dx <= 1; ++dx)
+            for (int dy = -1; dy <= 1; ++dy)
+                for (int dz = -1; dz <= 1; ++dz) {
+                    auto r = grid.equal_range(key(c3[0] + dx, c3[1] + dy, c3[2] + dz));
+                    for (auto it = r.first; it != r.second; ++it) {
+                        const float *pj = &od.v[3 * m.v[it->second]];
+                        const float d3[3] = {pj[0] - pi[0], pj[1] - pi[1], pj[2] - pi[2]};
+                        if (d3[0] * d3[0] + d3[1] * d3[1] + d3[2] * d3[2] < eps2) found.push_back(it->second);
+                    }
+                }
+        std::sort(found.begin(), found.end());
+        found.erase(std::unique(found.begin(), found.end()), found.end());
+        float acc[3] = {0, 0, 0};
+        for (size_t j : found) {
+            acc[0] += fn[3 * (j / 3)];
+            acc[1] += fn[3 * (j / 3) + 1];
+            acc[2] += fn[3 * (j / 3) + 2];
+        }
+        const float l = std::sqrt(acc[0] * acc[0] + acc[1] * acc[1] + acc[2] * acc[2]);
+        if (l > 0.0f) fdivs(acc, l);
+        memcpy(&cn[3 * i], acc, sizeof acc);
+    }
+}
+
+inline double from_srgb(double v)  // util.h:62-66
+{
+    if (v <= 0.04045) return v * (1.0 / 12.92);
+    return std::pow((v + 0.055) * (1.0 / 1.055), 2.4);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// host scene
+// ---------------------------------------------------------------------------
+struct frt_host_scene {
+    std::vector<double> tri_v, tri_n, tri_inv_area;
+    std::vector<int32_t> tri_mat;
+    std::vector<uint8_t> tri_geo;
+    std::vector<double> sphere;
+    std::vector<int32_t> sphere_mat;
+    std::vector<frt_material> mats;
+    std::vector<double> node_box;
+    std::vector<int32_t> node_child;
+    int32_t root = 0;
+    int32_t world_kind = FRT_WORLD_BVH;
+    std::vector<int32_t> list, lights;
+    double cam[6][3] = {};
+    double lens_radius = 0;
+    double env[3] = {0, 0, 0};
+    int bvh_depth = 0;
+    double load_ms = 0, build_ms = 0;
+
+    int add_material(int type, V3 albedo, V3 emit)
+    {
+        frt_material m{};
+        m.type = type;
+        m.albedo[0] = albedo.x; m.albedo[1] = albedo.y; m.albedo[2] = albedo.z;
+        m.emit[0] = emit.x; m.emit[1] = emit.y; m.emit[2] = emit.z;
+        mats.push_back(m);
+        return (int)mats.size() - 1;
+    }
+    int add_sphere(V3 c, double r, int mat)
+    {
+        sphere.insert(sphere.end(), {c.x, c.y, c.z, r});
+        sphere_mat.push_back(mat);
+        return (int)sphere_mat.size() - 1;
+    }
+    void set_camera(V3 lookfrom, V3 lookat, V3 vup, double vfov, double aspect, double aperture, double focus)
+    {
+        // camera.h:10-28 (fp64, same operation order)
+        lens_radius = aperture / 2;
+        const double theta = vfov * kPi / 180.0;
+        const double hh = std::tan(theta / 2);
+        const double hw = aspect * hh;
+        const V3 w = unit(lookfrom - lookat);
+        const V3 u = unit(cross(vup, w));
+        const V3 v = cross(w, u);
+        const V3 llc = ((lookfrom - (hw * focus) * u) - (hh * focus) * v) - focus * w;
+        const V3 h = (2 * hw * focus) * u;
+        const V3 vv = (2 * hh * focus) * v;
+        const V3 all[6] = {lookfrom, llc, h, vv, u, v};
+        for (int i = 0; i < 6; ++i) { cam[i][0] = all[i].x; cam[i][1] = all[i].y; cam[i][2] = all[i].z; }
+    }
+};
+
+namespace {
+
+// mesh_loader::load_obj + create_triangle_mesh
+bool add_obj(frt_host_scene &s, const std::string &path, bool geo)
+{
+    ObjData od;
+    if (!parse_obj(path, od)) return false;
+    for (const ObjMesh &m : od.meshes) {
+        const size_t nf = m.v.size() / 3;
+        if (nf == 0) continue;  // Assimp drops empty meshes
+        const Mtl *mt = (m.mtl >= 0) ? &od.mats[m.mtl] : nullptr;
+        int type;
+        V3 albedo, emit;
+        if (!mt) {  // DefaultMaterial -> lambertian 0.5 (mesh_loader.cpp:107-111)
+            type = FRT_MAT_LAMBERTIAN;
+            albedo = {0.5, 0.5, 0.5};
+        } else if (mt->ke[0] != 0 || mt->ke[1] != 0 || mt->ke[2] != 0) {
+            type = FRT_MAT_DIFFUSE_LIGHT;
+            emit = {mt->ke[0], mt->ke[1], mt->ke[2]};
+        } else if (mt->ks[0] != 0 || mt->ks[1] != 0 || mt->ks[2] != 0) {
+            type = (mt->d < 1.0f) ? 4 : 2;  // dielectric / modified_phong: outside the hot path
+            albedo = {from_srgb(mt->kd[0]), from_srgb(mt->kd[1]), from_srgb(mt->kd[2])};
+        } else {
+            type = FRT_MAT_LAMBERTIAN;
+            albedo = {from_srgb(mt->kd[0]), from_srgb(mt->kd[1]), from_srgb(mt->kd[2])};
+        }
+        const int mat = s.add_material(type, albedo, emit);
+        bool has_vn = true;
+        for (int x : m.vn) if (x < 0) { has_vn = false; break; }
+        std::vector<float> cn;
+        if (has_vn) {
+            cn.resize(3 * m.vn.size());
+            for (size_t i = 0; i < m.vn.size(); ++i) memcpy(&cn[3 * i], &od.vn[3 * m.vn[i]], 3 * sizeof(float));
+        } else if (!geo) {
+            smooth_normals(od, m, cn);
+        } else {
+            cn.assign(3 * m.v.size(), 0.0f);
+        }
+        const int base = (int)s.tri_mat.size();
+        for (size_t f = 0; f < nf; ++f) {
+            double v[9], n[9];
+            for (int k = 0; k < 3; ++k)
+                for (int d = 0; d < 3; ++d) {
+                    v[3 * k + d] = od.v[3 * m.v[3 * f + k] + d];
+                    n[3 * k + d] = cn[3 * (3 * f + k) + d];
+                }
+            s.tri_v.insert(s.tri_v.end(), v, v + 9);
+            s.tri_n.insert(s.tri_n.end(), n, n + 9);
+            const V3 e1{v[3] - v[0], v[4] - v[1], v[5] - v[2]}, e2{v[6] - v[0], v[7] - v[1], v[8] - v[2]};
+            s.tri_inv_area.push_back(1 / (0.5 * length(cross(e1, e2)) * (double)nf));  // triangle.h:65
+            s.tri_mat.push_back(mat);
+            s.tri_geo.push_back(geo ? 1 : 0);
+            if (type == FRT_MAT_DIFFUSE_LIGHT) s.lights.push_back(base + (int)f);
+        }
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// parallel_bvh_node construction (parallel_bvh.h:67-160)
+// ---------------------------------------------------------------------------
+struct Box {
+    double lo[3], hi[3];
+};
+inline double box_area(const Box &b)  // aabb.h:46-49 (size = max - min)
+{
+    const double sx = b.hi[0] - b.lo[0], sy = b.hi[1] - b.lo[1], sz = b.hi[2] - b.lo[2];
+    return 2 * ((sx * sy) + (sy * sz) + (sx * sz));
+}
+inline Box surround(const Box &a, const Box &b)  // aabb.h:57-68
+{
+    Box r;
+    for (int k = 0; k < 3; ++k) { r.lo[k] = std::fmin(a.lo[k], b.lo[k]); r.hi[k] = std::fmax(a.hi[k], b.hi[k]); }
+    return r;
+}
+inline int longest_axis(const Box &b)  // aabb.h:33-43
+{
+    const double sx = b.hi[0] - b.lo[0], sy = b.hi[1] - b.lo[1], sz = b.hi[2] - b.lo[2];
+    if (sy > sx) return 1;
+    if (sz > sx) return 2;
+    return 0;
+}
+
+struct Builder {
+    const std::vector<Box> &pbox;          // per primitive-ref slot
+    std::vector<double> node_box;
+    std::vector<int32_t> node_child;
+    std::atomic<int> n_nodes{0};
+    std::atomic<int> max_depth{0};
+    std::vector<int32_t> refs;             // slot -> prim ref
+
+    explicit Builder(const std::vector<Box> &b) : pbox(b) {}
+
+    // glibc msort_with_tmp (stdlib/msort.c) with the bvh.h comparator:
+    // cmp(a,b) = (key[a] - key[b] < 0) ? -1 : 1; "<= 0" takes from the left run.
+    static void msort(int32_t *b, size_t n, int32_t *tmp, const Box *boxes, int axis)
+    {
+        if (n <= 1) return;
+        const size_t n1 = n / 2, n2 = n - n1;
+        int32_t *b1 = b, *b2 = b + n1;
+        msort(b1, n1, tmp, boxes, axis);
+        msort(b2, n2, tmp, boxes, axis);
+        size_t i = n1, j = n2;
+        int32_t *t = tmp;
+        while (i > 0 && j > 0) {
+            if (boxes[*b1].lo[axis] - boxes[*b2].lo[axis] < 0.0) { *t++ = *b1++; --i; }
+            else { *t++ = *b2++; --j; }
+        }
+        if (i > 0) memcpy(t, b1, i * sizeof(int32_t));
+        memcpy(b, tmp, (n - j) * sizeof(int32_t));
+    }
+
+    int32_t build(int32_t *l, int n, int depth)
+    {
+        int md = max_depth.load();
+        while (depth > md && !max_depth.compare_exchange_weak(md, depth)) {}
+        const int me = n_nodes.fetch_add(1);
+        const Box *B = pbox.data();
+        Box main_box = B[l[0]];
+        for (int i = 1; i < n; ++i) main_box = surround(B[l[i]], main_box);
+        const int axis = longest_axis(main_box);
+        std::vector<int32_t> tmp(n);
+        msort(l, (size_t)n, tmp.data(), B, axis);
+        std::vector<double> left_area(n), right_area(n);
+        left_area[0] = box_area(B[l[0]]);
+        Box lb = B[l[0]];
+        for (int i = 1; i < n - 1; ++i) { lb = surround(lb, B[l[i]]); left_area[i] = box_area(lb); }
+        right_area[n - 1] = box_area(B[l[n - 1]]);
+        Box rb = B[l[n - 1]];
+        for (int i = n - 2; i > 0; --i) { rb = surround(rb, B[l[i]]); right_area[i] = box_area(rb); }
+        double min_sah = 3.40282346638528859812e+38;  // FLT_MAX
+        int idx = 0;
+        for (int i = 0; i < n - 1; ++i) {
+            const double sah = i * left_area[i] + (n - i - 1) * right_area[i + 1];
+            if (sah < min_sah) { idx = i; min_sah = sah; }
+        }
+        tmp.clear(); tmp.shrink_to_fit();
+        left_area.clear(); left_area.shrink_to_fit();
+        right_area.clear(); right_area.shrink_to_fit();
+        int32_t left = 0, right = 0;
+        auto do_left = [&] { left = (idx == 0) ? ~l[0] : build(l, idx + 1, depth + 1); };
+        auto do_right = [&] { right = (idx == n - 2) ? ~l[idx + 1] : build(l + idx + 1, n - idx - 1, depth + 1); };
+        if (n > 65536 && depth < 6) {  // large subtrees on their own thread (taskflow subflows in the reference)
+            std::thread th(do_left);
+            do_right();
+            th.join();
+        } else {
+            do_left();
+            do_right();
+        }
+        for (int k = 0; k < 3; ++k) { node_box[6 * me + k] = main_box.lo[k]; node_box[6 * me + 3 + k] = main_box.hi[k]; }
+        node_child[2 * me] = left;
+        node_child[2 * me + 1] = right;
+        return me;
+    }
+};
+
+// leaves hold the slot index; map slots back to prim refs afterwards
+void build_bvh(frt_host_scene &s, const std::vector<int32_t> &prims)
+{
+    const int n = (int)prims.size();
+    std::vector<Box> boxes(n);
+    for (int i = 0; i < n; ++i) {
+        const int ref = prims[i];
+        Box &b = boxes[i];
+        if (ref & FRT_PRIM_SPHERE) {
+            const double *sp = &s.sphere[4 * (ref & ~FRT_PRIM_SPHERE)];
+            for (int k = 0; k < 3; ++k) { b.lo[k] = sp[k] - sp[3]; b.hi[k] = sp[k] + sp[3]; }
+        } else {
+            const double *v = &s.tri_v[9 * ref];
+            for (int k = 0; k < 3; ++k) {  // triangle.h:120-137
+                b.lo[k] = std::fmin(std::fmin(v[k], v[3 + k]), v[6 + k]);
+                b.hi[k] = std::fmax(std::fmax(v[k], v[3 + k]), v[6 + k]);
+            }
+        }
+    }
+    s.node_box.clear();
+    s.node_child.clear();
+    if (n == 0) { s.root = 0; return; }
+    if (n == 1) { s.root = ~prims[0]; s.bvh_depth = 0; return; }
+    Builder b(boxes);
+    b.node_box.assign(6 * (size_t)(n - 1), 0.0);
+    b.node_child.assign(2 * (size_t)(n - 1), 0);
+    std::vector<int32_t> slots(n);
+    for (int i = 0; i < n; ++i) slots[i] = i;
+    const int root = b.build(slots.data(), n, 1);
+    for (auto &c : b.node_child)
+        if (c < 0) c = ~prims[~c];
+    s.node_box = std::move(b.node_box);
+    s.node_child = std::move(b.node_child);
+    s.root = root;
+    s.bvh_depth = b.max_depth.load();
+}
+
+}  // namespace
+
+extern "C" int frt_scene_create(const char *kind, const char *obj_path, double aspect, frt_host_scene **out)
+{
+    if (!kind || !obj_path || !out) return FRT_E_INVALID;
+    *out = nullptr;
+    auto s = std::make_unique<frt_host_scene>();
+    const std::string k = kind;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (k == "cornell_box_obj" || k == "obj_geo" || k == "obj_smooth") {
+        if (!add_obj(*s, obj_path, k != "obj_smooth")) return FRT_E_IO;
+        s->world_kind = FRT_WORLD_BVH;
+        s->set_camera({0, 1, (double)3.9f}, {0, 1, 0}, {0, 1, 0}, 40.0, aspect, 0.0, 10.0);  // main.cpp:236-242
+    } else if (k == "veach_mis") {
+        if (!add_obj(*s, obj_path, false)) return FRT_E_IO;
+        // main.cpp:292-302: five emissive spheres in the world list, and five
+        // separate identical sphere objects in Scene::lights
+        const double cx[5] = {10, (double)-1.25f, (double)-3.75f, (double)1.25f, (double)3.75f};
+        const double cy[5] = {10, 0, 0, 0, 0}, cz[5] = {4, 0, 0, 0, 0};
+        const double rad[5] = {0.5, (double)0.1f, (double)0.03333f, (double)0.3f, (double)0.9f};
+        const double em[5] = {800, 100, (double)901.803f, (double)11.1111f, 1.23457};
+        s->world_kind = FRT_WORLD_LIST;
+        for (int i = 0; i < (int)s->tri_mat.size(); ++i) s->list.push_back(i);
+        std::vector<int32_t> light_refs;
+        for (int j = 0; j < 5; ++j) {
+            const int m = s->add_material(FRT_MAT_DIFFUSE_LIGHT, {}, {em[j], em[j], em[j]});
+            s->list.push_back(FRT_PRIM_SPHERE | s->add_sphere({cx[j], cy[j], cz[j]}, rad[j], m));
+        }
+        for (int j = 0; j < 5; ++j) {
+            const int m = s->add_material(FRT_MAT_DIFFUSE_LIGHT, {}, {em[j], em[j], em[j]});
+            s->lights.push_back(FRT_PRIM_SPHERE | s->add_sphere({cx[j], cy[j], cz[j]}, rad[j], m));
+        }
+        s->set_camera({0, 2, 15}, {0, -2, 2.5}, {0, 1, 0}, 28.0, aspect, 0.0, 50.0);
+    } else {
+        return FRT_E_INVALID;
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    if (s->world_kind == FRT_WORLD_BVH) {
+        std::vector<int32_t> prims(s->tri_mat.size());
+        for (size_t i = 0; i < prims.size(); ++i) prims[i] = (int32_t)i;
+        build_bvh(*s, prims);
+    }
+    const auto t2 = std::chrono::steady_clock::now();
+    s->load_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    s->build_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+    *out = s.release();
+    return FRT_OK;
+}
+
+extern "C" int frt_scene_view_get(const frt_host_scene *s, frt_scene_view *v)
+{
+    if (!s || !v) return FRT_E_INVALID;
+    memset(v, 0, sizeof(*v));
+    v->world_kind = s->world_kind;
+    v->n_tris = (int32_t)s->tri_mat.size();
+    v->tri_v = s->tri_v.data();
+    v->tri_n = s->tri_n.data();
+    v->tri_material = s->tri_mat.data();
+    v->tri_geometry_normal = s->tri_geo.data();
+    v->tri_inv_area = s->tri_inv_area.data();
+    v->n_spheres = (int32_t)s->sphere_mat.size();
+    v->sphere = s->sphere.data();
+    v->sphere_material = s->sphere_mat.data();
+    v->n_materials = (int32_t)s->mats.size();
+    v->materials = s->mats.data();
+    v->n_nodes = (int32_t)(s->node_child.size() / 2);
+    v->root = s->root;
+    v->node_box = s->node_box.data();
+    v->node_child = s->node_child.data();
+    v->n_list = (int32_t)s->list.size();
+    v->list = s->list.data();
+    v->n_lights = (int32_t)s->lights.size();
+    v->lights = s->lights.data();
+    for (int k = 0; k < 3; ++k) {
+        v->cam_origin[k] = s->cam[0][k];
+        v->cam_lower_left[k] = s->cam[1][k];
+        v->cam_horizontal[k] = s->cam[2][k];
+        v->cam_vertical[k] = s->cam[3][k];
+        v->cam_u[k] = s->cam[4][k];
+        v->cam_v[k] = s->cam[5][k];
+        v->env_color[k] = s->env[k];
+    }
+    v->cam_lens_radius = s->lens_radius;
+    return FRT_OK;
+}
+
+extern "C" int frt_scene_info(const frt_host_scene *s, frt_host_scene_info *info)
+{
+    if (!s || !info) return FRT_E_INVALID;
+    info->n_tris = (int32_t)s->tri_mat.size();
+    info->n_spheres = (int32_t)s->sphere_mat.size();
+    info->n_materials = (int32_t)s->mats.size();
+    info->n_lights = (int32_t)s->lights.size();
+    info->n_nodes = (int32_t)(s->node_child.size() / 2);
+    info->world_kind = s->world_kind;
+    info->n_list = (int32_t)s->list.size();
+    info->bvh_depth = s->bvh_depth;
+    info->load_ms = s->load_ms;
+    info->build_ms = s->build_ms;
+    return FRT_OK;
+}
+
+extern "C" void frt_scene_destroy(frt_host_scene *s) { delete s; }
+
+// ---------------------------------------------------------------------------
+// cornell_1m generator: non-emissive quads -> k x k cells
+// ---------------------------------------------------------------------------
+extern "C" int frt_write_tessellated_obj(const char *src_obj, int k, const char *dst_obj)
+{
+    if (!src_obj || !dst_obj || k < 1) return FRT_E_INVALID;
+    std::ifstream in(src_obj);
+    if (!in) return FRT_E_IO;
+    std::string dst = dst_obj;
+    std::string mtl_dst = dst.substr(0, dst.size() >= 4 ? dst.size() - 4 : dst.size()) + ".mtl";
+    // find and copy the material library next to the output
+    std::vector<std::string> lines;
+    std::string line, mtllib;
+    while (std::getline(in, line)) {
+        lines.push_back(line);
+        const char *p = skip_ws(line.c_str());
+        if (!strncmp(p, "mtllib", 6)) mtllib = rstrip(skip_ws(p + 6));
+    }
+    std::map<std::string, bool> emissive;
+    if (!mtllib.empty()) {
+        ObjData od;
+        load_mtl(dir_of(src_obj) + mtllib, od);
+        for (auto &m : od.mats) emissive[m.name] = (m.ke[0] != 0 || m.ke[1] != 0 || m.ke[2] != 0);
+        std::ifstream mi(dir_of(src_obj) + mtllib, std::ios::binary);
+        std::ofstream mo(mtl_dst, std::ios::binary);
+        if (!mi || !mo) return FRT_E_IO;
+        mo << mi.rdbuf();
+    }
+    FILE *f = fopen(dst_obj, "w");
+    if (!f) return FRT_E_IO;
+    const size_t slash = mtl_dst.find_last_of('/');
+    fprintf(f, "# cornell-shaped tessellation (k=%d) of %s\nmtllib %s\n", k, src_obj,
+            (slash == std::string::npos ? mtl_dst : mtl_dst.substr(slash + 1)).c_str());
+    std::vector<std::string> vtok;  // raw vertex tokens of the source (positions)
+    std::string cur_mtl;
+    long long written = 0;
+    for (const std::string &ln : lines) {
+        const char *p = skip_ws(ln.c_str());
+        if (p[0] == 'v' && (p[1] == ' ' || p[1] == '\t')) {
+            vtok.push_back(rstrip(skip_ws(p + 1)));
+        } else if (!strncmp(p, "usemtl", 6)) {
+            cur_mtl = rstrip(skip_ws(p + 6));
+            fprintf(f, "%s\n", rstrip(p).c_str());
+        } else if ((p[0] == 'g' || p[0] == 'o') && (p[1] == ' ' || p[1] == '\t')) {
+            fprintf(f, "%s\n", rstrip(p).c_str());
+        } else if (p[0] == 'f' && (p[1] == ' ' || p[1] == '\t')) {
+            std::istringstream ss(p + 1);
+            std::vector<long> idx;
+            std::string t;
+            while (ss >> t) idx.push_back(std::stol(t));
+            const long nv = (long)vtok.size();
+            std::vector<std::array<double, 3>> P;
+            for (long a : idx) {
+                const long i = a < 0 ? nv + a : a - 1;
+                float x, y, z;
+                const char *q = vtok[i].c_str();
+                q = parse_float(skip_ws(q), x);
+                q = parse_float(skip_ws(q), y);
+                parse_float(skip_ws(q), z);
+                P.push_back({x, y, z});
+            }
+            const bool keep = emissive.count(cur_mtl) && emissive[cur_mtl];
+            if (P.size() != 4 || keep || k == 1) {  // lights (and non-quads) stay as they are
+                for (auto &pt : P) fprintf(f, "v %.9g %.9g %.9g\n", pt[0], pt[1], pt[2]);
+                fprintf(f, "f");
+                for (size_t i = 0; i < P.size(); ++i) fprintf(f, " %ld", (long)i - (long)P.size());
+                fprintf(f, "\n");
+                continue;
+            }
+            // bilinear grid (k+1)^2 over p0..p3, cells as quads (fanned like the source quads)
+            for (int j = 0; j <= k; ++j)
+                for (int i = 0; i <= k; ++i) {
+                    const double s = (double)i / k, tt = (double)j / k;
+                    double q[3];
+                    for (int d = 0; d < 3; ++d)
+                        q[d] = (1 - s) * (1 - tt) * P[0][d] + s * (1 - tt) * P[1][d] + s * tt * P[2][d] + (1 - s) * tt * P[3][d];
+                    fprintf(f, "v %.9g %.9g %.9g\n", q[0], q[1], q[2]);
+                }
+            const long nvert = (long)(k + 1) * (k + 1);
+            for (int j = 0; j < k; ++j)
+                for (int i = 0; i < k; ++i) {
+                    const long a = j * (k + 1) + i, b = a + 1, c = a + (k + 1) + 1, d = a + (k + 1);
+                    fprintf(f, "f %ld %ld %ld %ld\n", a - nvert, b - nvert, c - nvert, d - nvert);
+                    ++written;
+                }
+        }
+    }
+    fclose(f);
+    (void)written;
+    return FRT_OK;
+}
+
+extern "C" int frt_write_pfm(const char *path, int nx, int ny, const float *rgb)
+{
+    if (!path || !rgb || nx <= 0 || ny <= 0) return FRT_E_INVALID;
+    FILE *f = fopen(path, "wb");
+    if (!f) return FRT_E_IO;
+    fprintf(f, "PF\n%d %d\n-1\n", nx, ny);
+    const size_t n = (size_t)nx * ny * 3;
+    const bool ok = fwrite(rgb, sizeof(float), n, f) == n;
+    fclose(f);
+    return ok ? FRT_OK : FRT_E_IO;
+}

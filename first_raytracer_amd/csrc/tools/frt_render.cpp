@@ -1,0 +1,55 @@
+// frt_render -- command-line renderer: the reference's main() (main.cpp:483-525)
+// with the scene, resolution, spp, seed and GPU count as flags instead of
+// compile-time choices.  Writes the linear film as PFM (image.h:89-118).
+//
+//   frt_render --scene cornell|veach|obj --obj FILE [--res 1920x1080] [--ns 512]
+//              [--seed 0] [--gpus 1] [--out out.pfm]
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "frt_integrator.hpp"
+
+int main(int argc, char **argv)
+{
+    std::string scene = "cornell", obj, out = "out.pfm";
+    int nx = 512, ny = 512, gpus = 1;
+    long ns = 100;
+    unsigned seed = 0;
+    for (int i = 1; i < argc; ++i) {
+        const std::string a = argv[i];
+        auto next = [&]() -> const char * {
+            if (i + 1 >= argc) { std::fprintf(stderr, "missing value for %s\n", a.c_str()); std::exit(2); }
+            return argv[++i];
+        };
+        if (a == "--scene") scene = next();
+        else if (a == "--obj") obj = next();
+        else if (a == "--res") { if (std::sscanf(next(), "%dx%d", &nx, &ny) != 2) return 2; }
+        else if (a == "--ns") ns = std::atol(next());
+        else if (a == "--seed") seed = (unsigned)std::strtoul(next(), nullptr, 10);
+        else if (a == "--gpus") gpus = std::atoi(next());
+        else if (a == "--out") out = next();
+        else { std::fprintf(stderr, "unknown flag %s\n", a.c_str()); return 2; }
+    }
+    if (obj.empty()) { std::fprintf(stderr, "--obj is required\n"); return 2; }
+    try {
+        std::printf("Resolution: %dx%d\nSetting number of samples to %ld\n", nx, ny, ns);
+        const std::string kind = scene == "cornell" ? "cornell_box_obj" : scene == "veach" ? "veach_mis" : "obj_smooth";
+        frt::Scene s(kind, obj, double(nx) / double(ny));
+        std::printf("BVH construction took me %g seconds (%d triangles, depth %d).\n", s.info().build_ms * 1e-3,
+                    s.info().n_tris, s.info().bvh_depth);
+        frt::viewer film(nx, ny, (uint64_t)ns);
+        frt::renderer<frt::path_gpu> render;
+        render.devices.clear();
+        for (int g = 0; g < gpus; ++g) render.devices.push_back(g);
+        render.seed = seed;
+        render.Render(&s, film);
+        film.save_pfm(out);
+        std::printf("Saved %s\n", out.c_str());
+    } catch (const std::exception &e) {
+        std::fprintf(stderr, "frt_render: %s\n", e.what());
+        return 1;
+    }
+    return 0;
+}

@@ -1,0 +1,167 @@
+/*
+ * frt.h -- C-ABI of the MI355X path-tracing integrator (the drop-in boundary).
+ *
+ * Replaces, for one GPU, the work the reference enqueues in
+ *   path::Render(Scene*, viewer*, tf::Taskflow&)         first_ray/path.cpp:118-148
+ *   path::Li(ray, Scene*, depth, prev_hrec, pdf, sampler) first_ray/path.cpp:4-116
+ * as driven by renderer<path>::Render                    first_ray/integrator.h:14-46
+ * and writes the film that viewer::add_sample fills       first_ray/viewer.cpp:109-132.
+ *
+ * The caller flattens its Scene (Scene.h:10-26) once into an frt_scene_view
+ * (plain host arrays, fp64 like the reference's Vector3f), uploads it, and
+ * renders tiles of the frame.  No torch / HIP C++ types cross this boundary;
+ * a hip stream is passed as an opaque pointer.  See INTEGRATION.md for the
+ * reference-side `path_gpu` binding.
+ *
+ * Errors: every call returns 0 on success or a negative FRT_E* code;
+ * frt_last_error(ctx) describes the last failure (the reference throws
+ * std::runtime_error, e.g. triangle.cpp:34, image.h:102; the C++ host
+ * wrapper include/frt_integrator.hpp converts codes back into exceptions).
+ */
+#ifndef FRT_H
+#define FRT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FRT_ABI_VERSION 1
+
+enum {
+    FRT_OK = 0,
+    FRT_E_INVALID = -1,      /* bad argument / malformed scene view        */
+    FRT_E_HIP = -2,          /* HIP runtime failure (message in last_error) */
+    FRT_E_NO_SCENE = -3,     /* frt_render before frt_upload_scene          */
+    FRT_E_UNSUPPORTED = -4,  /* material/feature outside the hot path       */
+    FRT_E_IO = -5,           /* file could not be read / written            */
+    FRT_E_NO_DEVICE = -6     /* no gfx950 device / bad device index         */
+};
+
+enum { FRT_WORLD_BVH = 0, FRT_WORLD_LIST = 1 };          /* parallel_bvh_node | hitable_list */
+enum { FRT_MAT_LAMBERTIAN = 0, FRT_MAT_DIFFUSE_LIGHT = 1 }; /* material.h:50-73, 179-192 */
+enum { FRT_INTEGRATOR_PATH = 0 };                         /* path.h:8-18 */
+
+/* primitive reference: triangle t -> t ; sphere k -> FRT_PRIM_SPHERE | k */
+#define FRT_PRIM_SPHERE (1 << 30)
+
+typedef struct frt_material {
+    int32_t type;            /* FRT_MAT_*                                     */
+    int32_t reserved;
+    double albedo[3];        /* lambertian: constant_texture colour (linear)  */
+    double emit[3];          /* diffuse_light: constant_texture colour        */
+} frt_material;
+
+typedef struct frt_scene_view {
+    int32_t world_kind;                 /* FRT_WORLD_BVH or FRT_WORLD_LIST              */
+    /* triangles (triangle.h:55-66, one entry per `triangle` object) */
+    int32_t n_tris;
+    const double *tri_v;                /* 9 per tri: v0, v1, v2                        */
+    const double *tri_n;                /* 9 per tri: vertex normals, or NULL           */
+    const int32_t *tri_material;        /* index into materials                         */
+    const uint8_t *tri_geometry_normal; /* use_geometry_normals per tri, NULL = all 1   */
+    const double *tri_inv_area;         /* 1/(0.5|e1 x e2| nTriangles_of_mesh)           */
+    /* spheres (sphere.h:8-24) */
+    int32_t n_spheres;
+    const double *sphere;               /* 4 per sphere: centre, radius                 */
+    const int32_t *sphere_material;
+    /* materials */
+    int32_t n_materials;
+    const frt_material *materials;
+    /* BVH world: the parallel_bvh_node tree (parallel_bvh.h:8-27) */
+    int32_t n_nodes;
+    int32_t root;                       /* node index, or ~prim_ref for a 1-prim world  */
+    const double *node_box;             /* 6 per node: min, max                         */
+    const int32_t *node_child;          /* 2 per node: left, right; >=0 node, <0 ~prim  */
+    /* list world (hitable_list, hitable_list.cpp:4-21) */
+    int32_t n_list;
+    const int32_t *list;                /* prim refs in list order                      */
+    /* Scene::lights (hitable_list of emitters) */
+    int32_t n_lights;
+    const int32_t *lights;              /* prim refs                                    */
+    /* camera (camera.h:10-28), already constructed */
+    double cam_origin[3], cam_lower_left[3], cam_horizontal[3], cam_vertical[3];
+    double cam_u[3], cam_v[3];
+    double cam_lens_radius;
+    /* environment_map with a constant texture (material.h:206-232) */
+    double env_color[3];
+} frt_scene_view;
+
+typedef struct frt_render_params {
+    int32_t nx, ny;          /* film size (viewer nx, ny)                                  */
+    int32_t spp;             /* samples per pixel (viewer ns)                              */
+    uint32_t seed;           /* frame seed of the counter RNG (DESIGN.md "RNG stream spec") */
+    int32_t max_depth;       /* scatter while depth <= max_depth; reference: 33 (path.cpp:36) */
+    int32_t integrator;      /* FRT_INTEGRATOR_PATH                                        */
+    int32_t tile_size;       /* square tiles, multiple of 8; 0 = 32                        */
+    int32_t shard_index;     /* this call renders tiles t with t % shard_count == index    */
+    int32_t shard_count;     /* 1 = whole frame                                            */
+    int32_t samples_per_item;/* work granule in samples; 0 = automatic                     */
+    int32_t flags;           /* reserved, 0                                                */
+} frt_render_params;
+
+typedef struct frt_stats {
+    uint64_t camera_rays;    /* top-level scene queries, path.cpp:10 at depth 0 */
+    uint64_t extension_rays; /* path.cpp:10 at depth > 0                        */
+    uint64_t shadow_rays;    /* path.cpp:50                                     */
+    uint64_t samples;
+    uint64_t pixels;
+    uint64_t work_items;
+    double kernel_ms;        /* path megakernel, HIP events on its stream       */
+    double total_ms;         /* whole call                                      */
+} frt_stats;
+
+int frt_get_abi_version(void);
+
+/* ---- context: one per GPU, not thread-safe ---- */
+typedef struct frt_ctx frt_ctx;
+int frt_create(int hip_device, frt_ctx **out);
+int frt_destroy(frt_ctx *ctx);
+const char *frt_last_error(const frt_ctx *ctx);
+
+/* Copy the scene to HBM (fp32 device layout, DESIGN.md "Data layout").  The
+ * view's arrays are only read during the call. */
+int frt_upload_scene(frt_ctx *ctx, const frt_scene_view *scene);
+
+/* Shard geometry: number of output slots of a shard (tiles * tile_size^2) and,
+ * per slot, the linear film index y*nx+x it holds (or -1 for padding). */
+int64_t frt_shard_slot_count(const frt_render_params *p);
+int frt_shard_slots(const frt_render_params *p, int32_t *slot_pixel);
+
+/* Render this shard.  `film_rgb` is the caller's full film (nx*ny*3 floats,
+ * index (y*nx+x)*3, y = 0 bottom row, as viewer::fout_image); only this
+ * shard's pixels are written, with the mean radiance (viewer.cpp:111). */
+int frt_render(frt_ctx *ctx, const frt_render_params *p, float *film_rgb, frt_stats *st);
+
+/* Device variant: writes the shard's slots (frt_shard_slot_count * 3 floats,
+ * slot order) into device memory `slots_rgb` on `hip_stream` (NULL = the
+ * context's stream) and returns after the work has completed. */
+int frt_render_device(frt_ctx *ctx, const frt_render_params *p, float *slots_rgb, void *hip_stream,
+                      frt_stats *st);
+
+/* ---- host-side scene pipeline (native C++; what main.cpp + mesh_loader +
+ *      parallel_bvh_node::create_bvh do in the reference) ---- */
+typedef struct frt_host_scene frt_host_scene;
+typedef struct frt_host_scene_info {
+    int32_t n_tris, n_spheres, n_materials, n_lights, n_nodes, world_kind, n_list, bvh_depth;
+    double load_ms, build_ms;
+} frt_host_scene_info;
+/* kind: "cornell_box_obj" (main.cpp:222-252), "veach_mis" (main.cpp:281-314),
+ *       "obj_geo" / "obj_smooth" (any OBJ, cornell camera, geometric / vertex normals) */
+int frt_scene_create(const char *kind, const char *obj_path, double aspect, frt_host_scene **out);
+int frt_scene_view_get(const frt_host_scene *s, frt_scene_view *view);
+int frt_scene_info(const frt_host_scene *s, frt_host_scene_info *info);
+void frt_scene_destroy(frt_host_scene *s);
+
+/* cornell_1m generator: every non-emissive quad of `src_obj` bilinearly
+ * tessellated into k x k cells, written as OBJ + MTL. */
+int frt_write_tessellated_obj(const char *src_obj, int k, const char *dst_obj);
+
+/* image_pfm::save_image layout (image.h:89-118), path used as given. */
+int frt_write_pfm(const char *path, int nx, int ny, const float *rgb);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FRT_H */

@@ -1,0 +1,182 @@
+// frt_integrator.hpp -- C++ host API over the C-ABI (include/frt.h) that keeps
+// the reference's integrator concept, so code written against
+//   template <class I> struct renderer : I { double Render(Scene*, viewer&); }  (integrator.h:11-47)
+//   struct path { void Render(Scene*, viewer*, ...); using_custom_viewer; }      (path.h:8-18)
+//   struct viewer { add_sample(...); save_and_destroy(...); }                     (viewer.h:9-26)
+// reads the same against frt::renderer<frt::path_gpu>.  Errors become
+// exceptions (frt::error), as the reference throws std::runtime_error.
+#pragma once
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "frt.h"
+
+namespace frt {
+
+struct error : std::runtime_error {
+    int code;
+    error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+inline void check(int rc, const char *what, const frt_ctx *ctx = nullptr)
+{
+    if (rc != FRT_OK)
+        throw error(rc, std::string(what) + " failed (" + std::to_string(rc) + ")" +
+                            (ctx ? std::string(": ") + frt_last_error(ctx) : std::string()));
+}
+
+// Scene (Scene.h:10-26): world + lights + camera + environment, built natively
+// by the reference's scene constructors (main.cpp:222-252, 281-314).
+class Scene {
+public:
+    Scene(const std::string &kind, const std::string &obj_path, double aspect)
+    {
+        frt_host_scene *s = nullptr;
+        check(frt_scene_create(kind.c_str(), obj_path.c_str(), aspect, &s), "frt_scene_create");
+        scene_.reset(s);
+        check(frt_scene_info(s, &info_), "frt_scene_info");
+    }
+    static Scene cornell_box_obj(const std::string &obj, double aspect) { return Scene("cornell_box_obj", obj, aspect); }
+    static Scene veach_mis(const std::string &obj, double aspect) { return Scene("veach_mis", obj, aspect); }
+
+    frt_scene_view view() const
+    {
+        frt_scene_view v;
+        check(frt_scene_view_get(scene_.get(), &v), "frt_scene_view_get");
+        return v;
+    }
+    const frt_host_scene_info &info() const { return info_; }
+
+private:
+    struct del { void operator()(frt_host_scene *s) const { frt_scene_destroy(s); } };
+    std::unique_ptr<frt_host_scene, del> scene_;
+    frt_host_scene_info info_{};
+};
+
+// viewer (viewer.h:9-26, viewer.cpp:109-140) without the GL window: the linear
+// film (fout_image, doubles) and the tonemapped u8 image (out_image).
+struct viewer {
+    viewer(int nx, int ny, uint64_t ns, int num_channels = 3)
+        : nx(nx), ny(ny), ns(ns), num_channels(num_channels), out_image((size_t)nx * ny * num_channels, 0),
+          fout_image((size_t)nx * ny * num_channels, 0.0)
+    {
+    }
+    // add_sample(pixel, sum) (viewer.cpp:109-132): sum *= 1/ns, store linear + tonemapped
+    void add_sample(int x, int y, double r, double g, double b)
+    {
+        const double k = 1.0 / double(ns);
+        store_mean(x, y, r * k, g * k, b * k);
+    }
+    // the GPU already returns the per-pixel mean (sum * 1/ns)
+    void store_mean(int x, int y, double fr, double fg, double fb)
+    {
+        const size_t idx = ((size_t)y * nx + x) * num_channels;
+        out_image[idx] = (uint8_t)int(std::pow(1 - std::exp(-fr), 1 / 2.2) * 255 + .5);
+        out_image[idx + 1] = (uint8_t)int(std::pow(1 - std::exp(-fg), 1 / 2.2) * 255 + .5);
+        out_image[idx + 2] = (uint8_t)int(std::pow(1 - std::exp(-fb), 1 / 2.2) * 255 + .5);
+        fout_image[idx] = fr;
+        fout_image[idx + 1] = fg;
+        fout_image[idx + 2] = fb;
+    }
+    // image_pfm::save_image layout (image.h:89-118); path used as given (no $HOME prefix)
+    void save_pfm(const std::string &path) const
+    {
+        std::vector<float> f(fout_image.begin(), fout_image.end());
+        check(frt_write_pfm(path.c_str(), nx, ny, f.data()), "frt_write_pfm");
+    }
+    const int nx, ny;
+    const uint64_t ns;
+    const int num_channels;
+    bool to_exit = false;
+    std::vector<uint8_t> out_image;
+    std::vector<double> fout_image;
+};
+
+// path_gpu: the drop-in for `path` (path.h:8-18).  Render() renders every tile
+// of the frame on the listed GPUs (tile t -> device t % n, one host thread per
+// device, disjoint film writes) and stores the per-pixel means in the viewer.
+struct path_gpu {
+    std::vector<int> devices{0};
+    uint32_t seed = 0;
+    int max_depth = 33;     // path.cpp:36
+    int tile_size = 32;
+    frt_stats last_stats{};
+    static constexpr bool using_custom_viewer = false;
+
+    void Render(Scene *scene, viewer *film)
+    {
+        const int n = (int)devices.size();
+        std::vector<frt_stats> st(n);
+        std::vector<std::string> errs(n);
+        std::vector<std::vector<float>> films(n, std::vector<float>((size_t)film->nx * film->ny * 3, 0.0f));
+        const frt_scene_view view = scene->view();
+        auto work = [&](int i) {
+            frt_ctx *ctx = nullptr;
+            try {
+                check(frt_create(devices[i], &ctx), "frt_create");
+                check(frt_upload_scene(ctx, &view), "frt_upload_scene", ctx);
+                frt_render_params p{};
+                p.nx = film->nx; p.ny = film->ny; p.spp = (int)film->ns; p.seed = seed;
+                p.max_depth = max_depth; p.integrator = FRT_INTEGRATOR_PATH; p.tile_size = tile_size;
+                p.shard_index = i; p.shard_count = n;
+                check(frt_render(ctx, &p, films[i].data(), &st[i]), "frt_render", ctx);
+            } catch (const std::exception &e) {
+                errs[i] = e.what();
+            }
+            if (ctx) frt_destroy(ctx);
+        };
+        std::vector<std::thread> th;
+        for (int i = 1; i < n; ++i) th.emplace_back(work, i);
+        work(0);
+        for (auto &t : th) t.join();
+        for (int i = 0; i < n; ++i)
+            if (!errs[i].empty()) throw error(FRT_E_HIP, errs[i]);
+        // gather: shard i owns tiles t % n == i
+        const int T = tile_size, ntx = (film->nx + T - 1) / T;
+        for (int y = 0; y < film->ny; ++y)
+            for (int x = 0; x < film->nx; ++x) {
+                const int owner = ((y / T) * ntx + (x / T)) % n;
+                const float *px = &films[owner][3 * ((size_t)y * film->nx + x)];
+                film->store_mean(x, y, px[0], px[1], px[2]);
+            }
+        last_stats = frt_stats{};
+        for (const frt_stats &s : st) {
+            last_stats.camera_rays += s.camera_rays; last_stats.extension_rays += s.extension_rays;
+            last_stats.shadow_rays += s.shadow_rays; last_stats.samples += s.samples;
+            last_stats.pixels += s.pixels; last_stats.work_items += s.work_items;
+            last_stats.kernel_ms = std::max(last_stats.kernel_ms, s.kernel_ms);
+            last_stats.total_ms = std::max(last_stats.total_ms, s.total_ms);
+        }
+    }
+};
+
+// renderer<I> (integrator.h:11-47): time I::Render, print the statistics the
+// reference prints -- with true 64-bit ray counts instead of node visits.
+template <typename integrator>
+struct renderer : public integrator {
+    double Render(Scene *scene, viewer &film)
+    {
+        const auto t1 = std::chrono::high_resolution_clock::now();
+        integrator::Render(scene, &film);
+        const auto t2 = std::chrono::high_resolution_clock::now();
+        const double secs = std::chrono::duration<double>(t2 - t1).count();
+        const frt_stats &s = integrator::last_stats;
+        const double rays = double(s.camera_rays + s.extension_rays + s.shadow_rays);
+        std::printf("\nIt took me %g seconds to render.\n", secs);
+        std::printf(" Camera rays: %llu\n Extension rays: %llu\n Shadow rays: %llu\n",
+                    (unsigned long long)s.camera_rays, (unsigned long long)s.extension_rays,
+                    (unsigned long long)s.shadow_rays);
+        std::printf(" Kernel time: %.3f ms\n Rays/second: %.1fM/sec (kernel %.1fM/sec)\n", s.kernel_ms,
+                    rays / secs / 1e6, rays / (s.kernel_ms * 1e-3) / 1e6);
+        return secs;
+    }
+};
+
+}  // namespace frt

@@ -46,6 +46,10 @@ def lib():
         L.ora_scene_get_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(SceneInfo)]
         L.ora_scene_export_bvh.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.ora_scene_export_tris.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.ora_scene_export_camera.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.ora_scene_export_camera.restype = None
+        L.ora_scene_export_lights.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.ora_scene_export_materials.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.ora_render.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
                                  ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(Counters)]
         L.ora_world_hit.argtypes = [ctypes.c_void_p, dp, dp, ctypes.c_double, ctypes.c_double, dp,
@@ -109,6 +113,21 @@ class OracleScene:
         v = np.zeros((max(n, 1), 9)); m = np.zeros(max(n, 1), np.int32)
         lib().ora_scene_export_tris(self.ptr, v.ctypes.data, m.ctypes.data)
         return v[:n], m[:n]
+
+    def camera(self):
+        out = np.zeros(19)
+        lib().ora_scene_export_camera(self.ptr, out.ctypes.data)
+        return out
+
+    def lights(self):
+        out = np.zeros(max(self.info.n_lights, 1), np.int32)
+        lib().ora_scene_export_lights(self.ptr, out.ctypes.data)
+        return out[:self.info.n_lights]
+
+    def materials(self):
+        out = np.zeros((max(self.info.n_materials, 1), 7))
+        lib().ora_scene_export_materials(self.ptr, out.ctypes.data)
+        return out[:self.info.n_materials]
 
     def render(self, nx, ny, spp, seed=0, pixels=None, nthreads=None):
         """Mean radiance per pixel (viewer::add_sample semantics) + counters."""

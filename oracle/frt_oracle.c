@@ -1151,6 +1151,29 @@ int ora_scene_export_tris(const ora_scene *s, double *v9, int32_t *mat)
     return s->ntris;
 }
 
+
+/* camera as constructed (camera.h:10-28): origin, llc, horizontal, vertical, u, v, lens_radius (19 doubles) */
+void ora_scene_export_camera(const ora_scene *s, double *out19)
+{
+    vstore(out19, s->cam.origin); vstore(out19 + 3, s->cam.llc); vstore(out19 + 6, s->cam.horizontal);
+    vstore(out19 + 9, s->cam.vertical); vstore(out19 + 12, s->cam.u); vstore(out19 + 15, s->cam.v);
+    out19[18] = s->cam.lens_radius;
+}
+/* lights (prim refs) and materials (type, albedo[3], emit[3] -> 7 doubles each) */
+int ora_scene_export_lights(const ora_scene *s, int32_t *refs)
+{
+    for (int i = 0; i < s->nlights; ++i) refs[i] = s->lights[i];
+    return s->nlights;
+}
+int ora_scene_export_materials(const ora_scene *s, double *out7)
+{
+    for (int i = 0; i < s->nmats; ++i) {
+        out7[7 * i] = s->mats[i].type;
+        vstore(out7 + 7 * i + 1, s->mats[i].albedo); vstore(out7 + 7 * i + 4, s->mats[i].emit);
+    }
+    return s->nmats;
+}
+
 /* ------------------------------------------------------------------------ */
 /* known-answer entry points                                                */
 /* ------------------------------------------------------------------------ */

@@ -61,6 +61,10 @@ int  ora_scene_export_bvh(const ora_scene *s, double *boxes, int32_t *left, int3
 /* triangles: 9 doubles (v0,v1,v2) each; materials per triangle */
 int  ora_scene_export_tris(const ora_scene *s, double *v9, int32_t *mat);
 
+void ora_scene_export_camera(const ora_scene *s, double *out19);
+int  ora_scene_export_lights(const ora_scene *s, int32_t *refs);
+int  ora_scene_export_materials(const ora_scene *s, double *out7);
+
 /* Render pixels (linear index y*nx+x, y=0 bottom row) with `spp` samples each,
  * frame seed `seed`, on `nthreads` threads.  out_rgb[3*i..] = mean radiance
  * (viewer::add_sample semantics).  Returns 0 on success. */

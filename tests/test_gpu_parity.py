@@ -1,0 +1,127 @@
+"""GPU parity: the HIP path (through the C-ABI) against the fp64 C restatement
+of path::Li (oracle/) on the same counter-RNG streams.
+
+Tolerance (BASELINE.json north_star): image RMSE <= 1e-3 on linear radiance
+over all pixels and channels.  The GPU computes in fp32, the oracle in fp64;
+the only differences are rounding and the rare path that rounding sends down
+a different branch.  Integer quantities (sample counts, shard geometry) are
+exact; the image is bit-reproducible run to run and across shard counts."""
+import os
+
+import numpy as np
+import pytest
+
+import first_raytracer_amd as frt
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+RMSE_TOL = 1e-3
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = frt.Context(0)
+    yield c
+    c.close()
+
+
+def rmse(a, b):
+    return float(np.sqrt(np.mean((np.asarray(a, np.float64).reshape(-1, 3) - np.asarray(b, np.float64).reshape(-1, 3)) ** 2)))
+
+
+def render_pair(ctx, kind, obj, nx, ny, spp, seed=0, **kw):
+    hs = frt.HostScene(kind, obj, nx / ny)
+    ctx.upload(hs)
+    film, st = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=seed, **kw))
+    ref, cnt = oracle.OracleScene(kind, obj, nx / ny).render(nx, ny, spp, seed=seed)
+    return film, st, ref, cnt
+
+
+def test_cornell_c1_config(ctx, cornell_obj):
+    """C1: CornellBox 256x256, 16 spp, path + NEE + MIS."""
+    film, st, ref, cnt = render_pair(ctx, "cornell_box_obj", cornell_obj, 256, 256, 16, seed=0)
+    e = rmse(film, ref)
+    print("cornell 256x256x16 rmse", e, "rays", st.rays, cnt.rays)
+    assert st.samples == 256 * 256 * 16 == cnt.samples
+    assert st.camera_rays == cnt.camera_rays
+    assert abs(st.rays - cnt.rays) / cnt.rays < 1e-3
+    assert abs(st.shadow_rays - cnt.shadow_rays) / cnt.shadow_rays < 1e-3
+    assert e <= RMSE_TOL
+    assert np.isfinite(film).all()
+
+
+def test_cornell_widescreen_more_spp(ctx, cornell_obj):
+    film, st, ref, cnt = render_pair(ctx, "cornell_box_obj", cornell_obj, 160, 90, 64, seed=3)
+    assert rmse(film, ref) <= RMSE_TOL
+
+
+def test_veach_mis_c3_geometry(ctx, veach_obj):
+    """C3 geometry: list world, 5 sphere lights (NEE contributes 0, MIS via bsdf hits)."""
+    film, st, ref, cnt = render_pair(ctx, "veach_mis", veach_obj, 96, 64, 64, seed=5)
+    e = rmse(film, ref)
+    print("veach rmse", e, "mean", film.reshape(-1, 3).mean(0), ref.mean(0))
+    assert st.samples == cnt.samples
+    assert abs(st.rays - cnt.rays) / cnt.rays < 2e-3
+    assert e <= RMSE_TOL * max(1.0, float(np.abs(ref).mean()) * 10)
+
+
+def test_tessellated_cornell(ctx, cornell_obj, tmp_path):
+    dst = str(tmp_path / "tess.obj")
+    frt.write_tessellated_obj(cornell_obj, 8, dst)
+    film, st, ref, cnt = render_pair(ctx, "cornell_box_obj", dst, 64, 64, 16, seed=11)
+    assert rmse(film, ref) <= RMSE_TOL
+
+
+def test_deterministic_and_shard_invariant(ctx, cornell_obj):
+    nx, ny, spp = 100, 70, 8
+    ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, nx / ny))
+    a, _ = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=9, samples_per_item=4))
+    b, _ = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=9, samples_per_item=4))
+    assert np.array_equal(a, b)
+    film = np.zeros_like(a)
+    for r in range(3):
+        ctx.render(frt.RenderParams.make(nx, ny, spp, seed=9, samples_per_item=4, shard_index=r, shard_count=3), film)
+    assert np.array_equal(a, film)                     # same (pixel, sample) streams, same sum order
+    c, _ = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=9, samples_per_item=1, tile_size=16))
+    assert np.allclose(a, c, rtol=1e-5, atol=1e-6)     # chunking only regroups the fp32 sums
+
+
+def test_device_output_slots(ctx, cornell_obj):
+    import torch
+    nx, ny, spp = 64, 48, 4
+    ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, nx / ny))
+    p = frt.RenderParams.make(nx, ny, spp, seed=2, shard_index=1, shard_count=2, tile_size=16)
+    slots = frt.shard_slots(p)
+    out = torch.zeros(len(slots) * 3, dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream()
+    st = ctx.render_device(p, out.data_ptr(), stream.cuda_stream)
+    film, _ = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=2, tile_size=16))
+    got = out.cpu().numpy().reshape(-1, 3)
+    valid = slots >= 0
+    assert np.array_equal(got[valid], film.reshape(-1, 3)[slots[valid]])
+    assert st.pixels == valid.sum()
+
+
+@pytest.mark.parametrize("nx,ny,spp,depth", [(7, 5, 1, 33), (33, 17, 3, 0), (8, 8, 2, -1)])
+def test_edge_cases(ctx, cornell_obj, nx, ny, spp, depth):
+    """ragged frames, 1 spp, direct-only (max_depth 0) and emission-only (-1)."""
+    hs = frt.HostScene("cornell_box_obj", cornell_obj, nx / ny)
+    ctx.upload(hs)
+    film, st = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=4, max_depth=depth, tile_size=8))
+    assert st.samples == nx * ny * spp and st.pixels == nx * ny
+    assert np.isfinite(film).all()
+    if depth == -1:
+        assert st.shadow_rays == 0 and st.extension_rays == 0
+    if depth == 33:
+        ref, _ = oracle.OracleScene("cornell_box_obj", cornell_obj, nx / ny).render(nx, ny, spp, seed=4)
+        assert rmse(film, ref) <= 5 * RMSE_TOL   # tiny frame: one diverged sample weighs more
+
+
+def test_unsupported_material_rejected(ctx, tmp_path):
+    obj = tmp_path / "m.obj"
+    (tmp_path / "m.mtl").write_text("newmtl glossy\nKd 0.5 0.5 0.5\nKs 0.5 0.5 0.5\n")
+    obj.write_text("mtllib m.mtl\nv 0 0 0\nv 1 0 0\nv 0 1 0\ng a\nusemtl glossy\nf 1 2 3\n")
+    hs = frt.HostScene("obj_geo", str(obj), 1.0)
+    with pytest.raises(frt.FrtError, match="unsupported"):
+        ctx.upload(hs)
