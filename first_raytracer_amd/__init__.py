@@ -89,7 +89,7 @@ _lib = None
 EXPORTS = ("frt_get_abi_version", "frt_create", "frt_destroy", "frt_last_error", "frt_upload_scene",
            "frt_shard_slot_count", "frt_shard_slots", "frt_render", "frt_render_device", "frt_scene_create",
            "frt_scene_view_get", "frt_scene_info", "frt_scene_destroy", "frt_write_tessellated_obj",
-           "frt_write_pfm")
+           "frt_write_pfm", "frt_selftest_path_host")
 
 
 def lib():
@@ -119,6 +119,8 @@ def lib():
     L.frt_scene_destroy.restype = None
     L.frt_write_tessellated_obj.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p]
     L.frt_write_pfm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, vp]
+    L.frt_selftest_path_host.argtypes = [ctypes.POINTER(SceneView), ctypes.POINTER(RenderParams), vp,
+                                         ctypes.c_int, vp, ctypes.POINTER(Stats)]
     _lib = L
     return L
 
@@ -224,6 +226,18 @@ def shard_slots(params):
     out = np.zeros(n, np.int32)
     _check(lib().frt_shard_slots(ctypes.byref(params), out.ctypes.data), "frt_shard_slots")
     return out
+
+
+def selftest_path_host(scene, params, pixels):
+    """Self-test hook: the megakernel's per-lane path code run on the host
+    (CPU unit tests of the device logic; never a render path)."""
+    pixels = np.ascontiguousarray(pixels, dtype=np.int32)
+    out = np.zeros((len(pixels), 3), np.float32)
+    st = Stats()
+    view = scene.view()
+    _check(lib().frt_selftest_path_host(ctypes.byref(view), ctypes.byref(params), pixels.ctypes.data, len(pixels),
+                                        out.ctypes.data, ctypes.byref(st)), "frt_selftest_path_host")
+    return out, st
 
 
 def write_pfm(path, film):

@@ -1,0 +1,340 @@
+// frt_path.hpp -- per-path logic of the integrator, __host__ __device__ so the
+// HIP megakernel and the host self-test (frt_selftest_path_host) run the very
+// same code.  Restates, in fp32 (first_ray/ is fp64):
+//   path::Li                  path.cpp:4-116 (iterative: one ray per step)
+//   parallel_bvh_node::hit    parallel_bvh.h:39-64 (ordered stack traversal)
+//   hitable_list::hit         hitable_list.cpp:4-21
+//   triangle / sphere sample_direct + pdf_direct_sampling
+//                             triangle.h:139-175, sphere.h:64-107
+//   lambertian, diffuse_light material.h:50-73, 179-192
+//   camera::get_ray           camera.h:30-35
+#pragma once
+#include "frt.h"
+#include "frt_device.hpp"
+
+namespace frt {
+
+FRT_HD int f2i(float f) { return __builtin_bit_cast(int, f); }
+FRT_HD float i2f(int i) { return __builtin_bit_cast(float, i); }
+
+constexpr int kSentinel = 0x7fffffff;   // "stack empty"; never a node index
+
+// device scene (fp32, HBM-resident; DESIGN.md "Data layout")
+struct DevScene {
+    const float4 *nodes;     // 4 x float4 per interior node: child0 box | child1 box | (child0, child1) refs
+    const float4 *tris;      // 3 x float4 per triangle: v0 | e1 | e2 (48 B), DFS leaf order
+    const float4 *tshade;    // 2 x float4 per triangle: (n_geo, inv_area) | (mat, geo, -, -)
+    const float4 *tnorm;     // 3 x float4 per triangle: vertex normals (smooth shading only)
+    const float4 *spheres;   // (centre, radius)
+    const int *sphere_mat;
+    const float4 *mats;      // 2 x float4 per material: (albedo, type) | (emit, -)
+    const int *lights;       // device prim refs
+    const int *list;         // device prim refs (list worlds)
+    int root;                // node index, or ~prim for a single-leaf world
+    int n_lights, n_list, world_kind;
+    float root_lo[3], root_hi[3];
+    f3 cam_o, cam_llc, cam_h, cam_v, cam_u, cam_vv;
+    float lens_r;
+    f3 env;
+};
+
+struct Hit {
+    int prim;     // device prim ref, -1 = miss
+    float t, u, v;
+};
+
+FRT_HD float prim_t(const DevScene &S, int ref, f3 o, f3 d, float tmin, float tmax, float &u, float &v)
+{
+    if (ref & FRT_PRIM_SPHERE) {
+        const float4 sp = S.spheres[ref & ~FRT_PRIM_SPHERE];
+        u = v = 0.0f;
+        return sphere_intersect(o, d, xyz(sp), sp.w, tmin, tmax);
+    }
+    const float4 a = S.tris[3 * ref], b = S.tris[3 * ref + 1], c = S.tris[3 * ref + 2];
+    return tri_intersect(o, d, xyz(a), xyz(b), xyz(c), tmin, tmax, u, v);
+}
+
+// parallel_bvh_node::hit as an ordered stack traversal.  Closest hit keeps the
+// reference's answer: minimum t, exact ties to the leaf that comes first in
+// the left-first DFS (device triangle ids ARE that order).  Boxes are padded
+// outward, so culling never removes a hit.  `stk` entry k lives at
+// stk[k * STRIDE] (LDS column per lane on the GPU, a plain array on the host).
+template <int STRIDE>
+FRT_HD Hit trace_bvh(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int *stk)
+{
+    Hit h{-1, tmax, 0.0f, 0.0f};
+    const f3 invd = safe_inv(d);
+    // root box with the unscaled EPSILON (parallel_bvh.h:43), then
+    // t_min = EPSILON * max(1, |o|_inf) (parallel_bvh.h:46-51)
+    if (slab_entry(S.root_lo[0], S.root_lo[1], S.root_lo[2], S.root_hi[0], S.root_hi[1], S.root_hi[2], o, invd,
+                   kEps, tmax) == __builtin_inff())
+        return h;
+    const float tmin = kEps * fmaxf(1.0f, fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z))));
+    int node = S.root;
+    int sp = 0;
+    for (;;) {
+        while ((unsigned)node < (unsigned)kSentinel) {   // interior node
+            const float4 n0 = S.nodes[4 * node], n1 = S.nodes[4 * node + 1];
+            const float4 n2 = S.nodes[4 * node + 2], n3 = S.nodes[4 * node + 3];
+            const float t0 = slab_entry(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, invd, tmin, h.t);
+            const float t1 = slab_entry(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, invd, tmin, h.t);
+            const int c0 = f2i(n3.x), c1 = f2i(n3.y);
+            const bool h0 = t0 != __builtin_inff(), h1 = t1 != __builtin_inff();
+            if (h0 && h1) {
+                const bool first0 = t0 <= t1;
+                stk[sp * STRIDE] = first0 ? c1 : c0;
+                ++sp;
+                node = first0 ? c0 : c1;
+            } else if (h0) {
+                node = c0;
+            } else if (h1) {
+                node = c1;
+            } else {
+                node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel;
+            }
+        }
+        if (node == kSentinel) break;
+        // leaf: one primitive (single-prim leaves, parallel_bvh.h:129-149)
+        const int ref = ~node;
+        float u, v;
+        const float t = prim_t(S, ref, o, d, tmin, h.t, u, v);
+        if (t > 0.0f) {
+            const bool better = (t < h.t) || (h.prim >= 0 && ((ref & FRT_PRIM_SPHERE) || ref < h.prim));
+            if (better) {
+                h.prim = ref; h.t = t; h.u = u; h.v = v;
+                if (anyhit) return h;
+            }
+        }
+        node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel;
+        if (node == kSentinel) break;
+    }
+    return h;
+}
+
+// hitable_list::hit: in list order, triangles strict '<', spheres inclusive (sphere.h:34)
+FRT_HD Hit trace_list(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit)
+{
+    Hit h{-1, tmax, 0.0f, 0.0f};
+    for (int i = 0; i < S.n_list; ++i) {
+        const int ref = S.list[i];
+        float u, v;
+        const float t = prim_t(S, ref, o, d, kEps, h.t, u, v);
+        if (t > 0.0f && ((ref & FRT_PRIM_SPHERE) || t < h.t)) {
+            h.prim = ref; h.t = t; h.u = u; h.v = v;
+            if (anyhit) return h;
+        }
+    }
+    return h;
+}
+
+template <int WORLD, int STRIDE>
+FRT_HD Hit trace(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int *stk)
+{
+    if constexpr (WORLD == FRT_WORLD_LIST) return trace_list(S, o, d, tmax, anyhit);
+    else return trace_bvh<STRIDE>(S, o, d, tmax, anyhit, stk);
+}
+
+// hit record of a primitive: shading normal + material
+FRT_HD void prim_shade(const DevScene &S, int ref, f3 ro, f3 p, float u, float v, f3 &n, int &mat)
+{
+    if (ref & FRT_PRIM_SPHERE) {                               // sphere.h:47-50
+        const int k = ref & ~FRT_PRIM_SPHERE;
+        const float4 sp = S.spheres[k];
+        n = (1.0f / sp.w) * (p - xyz(sp));
+        if (len2(ro - xyz(sp)) < sp.w * sp.w) n = -n;          // origin inside: flip
+        mat = S.sphere_mat[k];
+        return;
+    }
+    const float4 s0 = S.tshade[2 * ref], s1 = S.tshade[2 * ref + 1];
+    mat = f2i(s1.x);
+    if (f2i(s1.y)) {                                           // use_geometry_normals (triangle.h:100-101)
+        n = xyz(s0);
+    } else {                                                   // triangle.h:103
+        const f3 n0 = xyz(S.tnorm[3 * ref]), n1 = xyz(S.tnorm[3 * ref + 1]), n2 = xyz(S.tnorm[3 * ref + 2]);
+        n = normalize((1.0f - u - v) * n0 + u * n1 + v * n2);
+    }
+}
+
+// pdf_direct_sampling with the record's (p, t, normal) and direction
+FRT_HD float prim_pdf(const DevScene &S, int ref, f3 rec_p, float rec_t, f3 rec_n, f3 to_light)
+{
+    if (!(ref & FRT_PRIM_SPHERE)) return S.tshade[2 * ref].w;     // inv_area (triangle.h:139-144)
+    const float4 sp = S.spheres[ref & ~FRT_PRIM_SPHERE];           // sphere.h:64-78
+    const f3 o = rec_p - rec_t * to_light;
+    const f3 dir = xyz(sp) - o;
+    const float d2 = len2(dir);
+    const float r2 = sp.w * sp.w;
+    if (d2 <= r2) return 1.0f / (4.0f * kPi * r2);
+    const float cos_max = sqrtf(1.0f - r2 / d2);
+    const float solid = 2.0f * kPi * (1.0f - cos_max);
+    return (1.0f / solid) * fabsf(dot(to_light, rec_n)) / d2;
+}
+
+// sample_direct: returns to_light (unnormalised, as the reference), light normal, material
+FRT_HD f3 prim_sample(const DevScene &S, int ref, f3 o, float u0, float u1, f3 &ln, int &lmat)
+{
+    if (ref & FRT_PRIM_SPHERE) {                                   // sphere.h:80-107
+        const int k = ref & ~FRT_PRIM_SPHERE;
+        const float4 sp = S.spheres[k];
+        const f3 c = xyz(sp);
+        lmat = S.sphere_mat[k];
+        const f3 direction = c - o;
+        const float d2 = len2(direction);
+        if (d2 <= sp.w * sp.w) {
+            const f3 p = c + sp.w * uniform_sphere(u0, u1);
+            ln = normalize(c - p);
+            return p - o;
+        }
+        const Onb uvw = onb_from_w(direction);                     // unnormalised axis, as the reference
+        const f3 p = onb_local(uvw, random_to_sphere(sp.w, d2, u0, u1));
+        ln = normalize(p);
+        return p;
+    }
+    const float4 a = S.tris[3 * ref], b = S.tris[3 * ref + 1], c = S.tris[3 * ref + 2];   // triangle.h:145-175
+    const float su0 = sqrtf(u0);
+    const float b0 = 1.0f - su0;
+    const float b1 = u1 * su0;
+    const f3 lp = xyz(a) + b0 * xyz(b) + b1 * xyz(c);            // (1-b0-b1) v0 + b0 v1 + b1 v2
+    const float4 s0 = S.tshade[2 * ref], s1 = S.tshade[2 * ref + 1];
+    lmat = f2i(s1.x);
+    if (f2i(s1.y)) {
+        ln = xyz(s0);
+    } else {
+        const f3 n0 = xyz(S.tnorm[3 * ref]), n1 = xyz(S.tnorm[3 * ref + 1]), n2 = xyz(S.tnorm[3 * ref + 2]);
+        ln = normalize((1.0f - b0 - b1) * n0 + b0 * n1 + b1 * n2);
+    }
+    return lp - o;
+}
+
+// ---------------------------------------------------------------------------
+// one path as a state machine: begin() makes the camera ray, shade() consumes
+// the hit of the ray just traced and sets up the next one (shadow first,
+// then the extension ray) or finishes the path.
+// ---------------------------------------------------------------------------
+struct PathState {
+    f3 ro, rd;            // ray to trace next
+    float rtmax;
+    bool shadow;          // any-hit query
+    f3 beta, L;           // throughput, radiance of this sample
+    f3 nee;               // NEE contribution if the shadow ray is unoccluded
+    f3 nxt_o, nxt_d;      // extension ray after the shadow ray
+    f3 prev_p;            // previous hit point (MIS distance, path.cpp:25)
+    float prev_pdf;       // bsdf pdf of the previous bounce
+    int depth;
+    RngKey key;
+};
+
+// path.cpp:129-136 + camera.h:30-35 (+ util.h:21-41 thin lens)
+FRT_HD void path_begin(PathState &P, const DevScene &S, int px, int py, int nx, int ny, uint32_t seed,
+                       uint32_t pixel, uint32_t sample)
+{
+    P.key = rng_key(seed, pixel, sample);
+    const float u = ((float)px + rng_u(P.key, 0)) / (float)nx;
+    const float v = ((float)py + rng_u(P.key, 1)) / (float)ny;
+    f3 off = mk3(0, 0, 0);
+    if (S.lens_r != 0.0f) {
+        const float a = rng_u(P.key, 2) * 2.0f - 1.0f, b = rng_u(P.key, 3) * 2.0f - 1.0f;
+        float rx = 0.0f, ry = 0.0f;
+        if (a != 0.0f || b != 0.0f) {
+            float r, phi;
+            if (a * a > b * b) { r = a; phi = (kPi / 4.0f) * (b / a); }
+            else { r = b; phi = (kPi / 2.0f) - (kPi / 4.0f) * (a / b); }
+            rx = r * cosf(phi); ry = r * sinf(phi);
+        }
+        off = (S.lens_r * rx) * S.cam_u + (S.lens_r * ry) * S.cam_vv;
+    }
+    P.ro = S.cam_o + off;
+    P.rd = ((S.cam_llc + u * S.cam_h + v * S.cam_v) - S.cam_o) - off;
+    P.rtmax = kTMaxClosest;
+    P.shadow = false;
+    P.depth = 0;
+    P.beta = mk3(1, 1, 1);
+    P.L = mk3(0, 0, 0);
+    P.prev_pdf = 0.0f;
+    P.prev_p = mk3(0, 0, 0);
+}
+
+// Returns true when the path is finished (P.L is the sample's radiance).
+FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_depth, uint32_t &n_ext, uint32_t &n_sh)
+{
+    if (P.shadow) {                                     // path.cpp:50-77
+        if (h.prim < 0) P.L = P.L + P.nee;
+        P.shadow = false;
+        P.ro = P.nxt_o; P.rd = P.nxt_d; P.rtmax = kTMaxClosest;
+        ++P.depth; ++n_ext;
+        return false;
+    }
+    if (h.prim < 0) {                                   // path.cpp:115 environment
+        P.L = P.L + P.beta * S.env;
+        return true;
+    }
+    const f3 p = P.ro + h.t * P.rd;
+    f3 n;
+    int mat;
+    prim_shade(S, h.prim, P.ro, p, h.u, h.v, n, mat);
+    const float4 m0 = S.mats[2 * mat], m1 = S.mats[2 * mat + 1];
+    const int mtype = f2i(m0.w);
+    // diffuse_light::emitted is one-sided (material.h:184-190)
+    if (mtype == FRT_MAT_DIFFUSE_LIGHT && dot(n, P.rd) < 0.0f) {
+        const f3 Le = xyz(m1);
+        if (P.depth == 0) {
+            P.L = P.L + P.beta * Le;                    // path.cpp:16-22
+        } else {                                        // path.cpp:24-31: MIS against the bsdf sample
+            const float cos_wo = dot(n, -normalize(P.rd));
+            float d2 = len2(p - P.prev_p);
+            if (d2 <= kEps) d2 = kEps;
+            const float light_pdf = prim_pdf(S, h.prim, p, h.t, n, P.rd) * d2 / fabsf(cos_wo);
+            P.L = P.L + mi_weight(P.prev_pdf, light_pdf) * (P.beta * Le);
+        }
+        return true;
+    }
+    if (mtype != FRT_MAT_LAMBERTIAN || P.depth > max_depth) return true;   // no scatter: Le (= 0)
+    const uint32_t base = dim_bounce(P.depth);
+    // bsdf sample first: a zero pdf drops this vertex's NEE too (path.cpp:96-106)
+    const Onb uvw = onb_from_w(n);
+    const f3 wo = onb_local(uvw, cosine_direction(rng_u(P.key, base + 6), rng_u(P.key, base + 7)));
+    const float cw = dot(n, normalize(wo));
+    const float pdf = fmaxf(cw, 0.0f) * kInvPi;
+    if (pdf == 0.0f) return true;
+    const f3 f = kInvPi * xyz(m0);                      // lambertian::eval_bsdf (material.h:62-65)
+    const f3 beta_next = (fabsf(cw) / pdf) * (P.beta * f);
+    P.nxt_o = p + kEps * n;
+    P.nxt_d = wo;
+    // next-event estimation (path.cpp:38-77)
+    const int nl = S.n_lights;
+    int idx = (int)(rng_u(P.key, base + 3) * (float)nl);
+    if (idx == nl) idx -= 1;
+    if (idx >= 0) {
+        const int lref = S.lights[idx];
+        f3 ln;
+        int lmat;
+        const f3 origin = p + kEps * n;
+        const f3 tl = prim_sample(S, lref, origin, rng_u(P.key, base + 4), rng_u(P.key, base + 5), ln, lmat);
+        const float dist2 = len2(tl);
+        const f3 tu = rlen(tl) * tl;
+        const float cos_wi = dot(n, tu);
+        const float cos_lo = dot(ln, -tu);
+        P.nee = mk3(0, 0, 0);
+        if (cos_lo != 0.0f) {
+            const float light_pdf = prim_pdf(S, lref, p, h.t, n, tu) * dist2 / fabsf(cos_lo);
+            const float bsdf_pdf = fmaxf(cos_wi, 0.0f) * kInvPi;
+            const float wgt = mi_weight(light_pdf, bsdf_pdf);
+            const float4 lm0 = S.mats[2 * lmat], lm1 = S.mats[2 * lmat + 1];
+            if (f2i(lm0.w) == FRT_MAT_DIFFUSE_LIGHT && dot(ln, tu) < 0.0f)
+                P.nee = (wgt / light_pdf * cos_wi) * (P.beta * (xyz(lm1) * f));
+        }
+        P.ro = origin; P.rd = tl; P.rtmax = 1.0f - kShadowEps;
+        P.shadow = true;
+        ++n_sh;
+    }
+    P.beta = beta_next;
+    P.prev_p = p;
+    P.prev_pdf = pdf;
+    if (!P.shadow) {
+        P.ro = P.nxt_o; P.rd = P.nxt_d; P.rtmax = kTMaxClosest;
+        ++P.depth; ++n_ext;
+    }
+    return false;
+}
+
+}  // namespace frt

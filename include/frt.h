@@ -161,6 +161,13 @@ int frt_write_tessellated_obj(const char *src_obj, int k, const char *dst_obj);
 /* image_pfm::save_image layout (image.h:89-118), path used as given. */
 int frt_write_pfm(const char *path, int nx, int ny, const float *rgb);
 
+/* ---- self-test hook for CPU-only unit tests: runs the megakernel's per-lane
+ *      path code (frt_path.hpp) on the host over the flattened fp32 scene for
+ *      the listed pixels (linear y*nx+x); out_rgb = per-pixel means.  Not a
+ *      render path: frt_render / frt_render_device never use it. ---- */
+int frt_selftest_path_host(const frt_scene_view *scene, const frt_render_params *p, const int32_t *pixels,
+                           int npix, float *out_rgb, frt_stats *st);
+
 #ifdef __cplusplus
 }
 #endif

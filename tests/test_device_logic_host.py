@@ -1,0 +1,45 @@
+"""The megakernel's per-lane path code (csrc/frt_path.hpp: traversal, NEE, MIS,
+bounce) compiled for the host via the frt_selftest_path_host hook, against the
+fp64 oracle on the same RNG streams.  Runs on CPU, so logic errors in the
+device code are caught before a GPU run.  Tolerance: RMSE <= 1e-3 (the gate);
+in practice fp32-vs-fp64 rounding gives ~1e-7."""
+import numpy as np
+import pytest
+
+import first_raytracer_amd as frt
+import oracle
+
+
+def run(kind, obj, nx, ny, spp, seed, pixels=None, max_depth=33):
+    hs = frt.HostScene(kind, obj, nx / ny)
+    pix = np.arange(nx * ny, dtype=np.int32) if pixels is None else pixels
+    out, st = frt.selftest_path_host(hs, frt.RenderParams.make(nx, ny, spp, seed=seed, max_depth=max_depth), pix)
+    ref, cnt = oracle.OracleScene(kind, obj, nx / ny).render(nx, ny, spp, seed=seed, pixels=pix)
+    return out, st, ref, cnt
+
+
+def test_cornell(cornell_obj):
+    out, st, ref, cnt = run("cornell_box_obj", cornell_obj, 48, 48, 16, seed=0)
+    e = float(np.sqrt(np.mean((out.astype(np.float64) - ref) ** 2)))
+    assert e < 1e-4, e
+    assert st.camera_rays == cnt.camera_rays
+    assert abs(st.rays - cnt.rays) <= 1e-3 * cnt.rays
+
+
+def test_cornell_widescreen_sampled_pixels(cornell_obj):
+    pix = np.linspace(0, 1920 * 1080 - 1, 300).astype(np.int32)
+    out, st, ref, cnt = run("cornell_box_obj", cornell_obj, 1920, 1080, 32, seed=7, pixels=pix)
+    assert float(np.sqrt(np.mean((out.astype(np.float64) - ref) ** 2))) < 1e-4
+
+
+def test_veach(veach_obj):
+    out, st, ref, cnt = run("veach_mis", veach_obj, 48, 32, 32, seed=1)
+    assert float(np.sqrt(np.mean((out.astype(np.float64) - ref) ** 2))) < 1e-3
+    assert st.rays == pytest.approx(cnt.rays, rel=1e-3)
+
+
+def test_tessellated(cornell_obj, tmp_path):
+    dst = str(tmp_path / "t.obj")
+    frt.write_tessellated_obj(cornell_obj, 6, dst)
+    out, st, ref, cnt = run("cornell_box_obj", dst, 32, 32, 8, seed=3)
+    assert float(np.sqrt(np.mean((out.astype(np.float64) - ref) ** 2))) < 1e-4
