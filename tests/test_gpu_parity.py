@@ -56,14 +56,29 @@ def test_cornell_widescreen_more_spp(ctx, cornell_obj):
     assert rmse(film, ref) <= RMSE_TOL
 
 
+def split_diverged(film, ref, thresh=1e-3):
+    """Per-pixel max-channel |diff|; pixels above `thresh` are the ones where
+    fp32 rounding sent a sample down another branch (a different primitive at
+    a silhouette).  Returns (rmse of the others, number diverged)."""
+    d = np.abs(np.asarray(film, np.float64).reshape(-1, 3) - np.asarray(ref, np.float64).reshape(-1, 3)).max(axis=1)
+    bad = d > thresh
+    good = ~bad
+    return rmse(np.asarray(film).reshape(-1, 3)[good], np.asarray(ref).reshape(-1, 3)[good]), int(bad.sum())
+
+
 def test_veach_mis_c3_geometry(ctx, veach_obj):
-    """C3 geometry: list world, 5 sphere lights (NEE contributes 0, MIS via bsdf hits)."""
-    film, st, ref, cnt = render_pair(ctx, "veach_mis", veach_obj, 96, 64, 64, seed=5)
-    e = rmse(film, ref)
-    print("veach rmse", e, "mean", film.reshape(-1, 3).mean(0), ref.mean(0))
+    """C3 geometry: list world, 5 sphere lights (NEE contributes 0, MIS via bsdf hits).
+    A diverged sample that hits the r=0.033, L=901.8 sphere is a firefly of
+    ~900/spp, so this scene is checked pixel by pixel: at most 0.1% of the
+    pixels may carry a diverged sample, and the rest must meet the RMSE gate."""
+    nx, ny, spp = 96, 64, 64
+    film, st, ref, cnt = render_pair(ctx, "veach_mis", veach_obj, nx, ny, spp, seed=5)
+    e, nbad = split_diverged(film, ref)
+    print("veach rmse(all)", rmse(film, ref), "rmse(non-diverged)", e, "diverged pixels", nbad)
     assert st.samples == cnt.samples
     assert abs(st.rays - cnt.rays) / cnt.rays < 2e-3
-    assert e <= RMSE_TOL * max(1.0, float(np.abs(ref).mean()) * 10)
+    assert nbad <= max(2, nx * ny // 1000)
+    assert e <= RMSE_TOL
 
 
 def test_tessellated_cornell(ctx, cornell_obj, tmp_path):
