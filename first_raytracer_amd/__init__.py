@@ -99,6 +99,13 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise FrtError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7 (same
+    # soname as /opt/rocm's).  Load torch first so libfrt.so binds to that
+    # copy; loading libfrt first would bind torch to the other runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp = ctypes.c_void_p
     L.frt_get_abi_version.restype = ctypes.c_int
