@@ -87,7 +87,7 @@ def main():
     ap.add_argument("--spp", type=int, default=512)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--tile", type=int, default=32)
-    ap.add_argument("--cpu-pixels", type=int, default=12288, help="pixels in the CPU-baseline sample")
+    ap.add_argument("--cpu-pixels", type=int, default=65536, help="pixels in the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pfm", default="", help="write the rank-0 film here")
