@@ -119,35 +119,13 @@ def main():
 
     params = frt.RenderParams.make(nx, ny, args.spp, seed=args.seed, tile_size=args.tile,
                                    shard_index=rank, shard_count=world)
-    slot_counts = [int(frt.lib().frt_shard_slot_count(
-        frt.RenderParams.make(nx, ny, args.spp, tile_size=args.tile, shard_index=r, shard_count=world)))
-        for r in range(world)]
-    max_slots = max(slot_counts)
-    my_slots = torch.zeros(max_slots * 3, dtype=torch.float32, device=dev)
-    gathered = torch.zeros(world * max_slots * 3, dtype=torch.float32, device=dev) if world > 1 else None
-    film = torch.zeros(nx * ny * 3, dtype=torch.float32, device=dev)
-    if rank == 0:
-        maps = []
-        for r in range(world):
-            m = frt.shard_slots(frt.RenderParams.make(nx, ny, args.spp, tile_size=args.tile, shard_index=r,
-                                                      shard_count=world))
-            pad = np.full(max_slots, -1, np.int32)
-            pad[:len(m)] = m
-            maps.append(pad)
-        slot_pix = torch.from_numpy(np.concatenate(maps).astype(np.int64)).to(dev)
-        valid = slot_pix >= 0
-        dst_idx = slot_pix[valid]
+    from first_raytracer_amd.dist import TileGather
+    tg = TileGather(nx, ny, args.tile, world, rank, dev)
     stream = torch.cuda.current_stream(dev)
 
     def step():
-        st = ctx.render_device(params, my_slots.data_ptr(), stream.cuda_stream)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, my_slots)
-            src = gathered
-        else:
-            src = my_slots
-        if rank == 0:
-            film.view(-1, 3)[dst_idx] = src.view(-1, 3)[valid]
+        st = ctx.render_device(params, tg.my_slots.data_ptr(), stream.cuda_stream)
+        tg.gather()       # RCCL all-gather of the tile slots, rank 0 scatters into its film
         return st
 
     for _ in range(args.warmup):
@@ -179,7 +157,7 @@ def main():
 
     if rank == 0:
         value = rays / elapsed / 1e6
-        film_np = film.cpu().numpy()
+        film_np = tg.film.cpu().numpy()
         key = f"{args.scene}:{nx}x{ny}"
         cpu = None
         if world == 1 and not args.no_cpu_baseline:

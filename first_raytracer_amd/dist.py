@@ -1,0 +1,51 @@
+"""Tile sharding + the one collective of the multi-GPU path.
+
+Tile t of the frame belongs to rank t mod N (frt_render_params.shard_index /
+shard_count).  Each rank renders its tiles into a slot buffer in HBM; the
+buffers (padded to the largest shard) are all-gathered with torch.distributed
+-- RCCL over xGMI with the "nccl" backend, gloo in the CPU tests -- and rank 0
+scatters the slots into the film (viewer::fout_image order, y = 0 bottom).
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import RenderParams, shard_slots
+
+
+def shard_layout(nx, ny, tile, world):
+    """(slot counts per rank, padded slot->pixel map of all ranks concatenated)."""
+    maps = [shard_slots(RenderParams.make(nx, ny, 1, tile_size=tile, shard_index=r, shard_count=world))
+            for r in range(world)]
+    max_slots = max(len(m) for m in maps)
+    padded = np.full((world, max_slots), -1, np.int64)
+    for r, m in enumerate(maps):
+        padded[r, :len(m)] = m
+    return [len(m) for m in maps], padded.reshape(-1)
+
+
+class TileGather:
+    """All-gather of per-rank slot buffers + scatter into rank 0's film."""
+
+    def __init__(self, nx, ny, tile, world, rank, device):
+        self.nx, self.ny, self.world, self.rank = nx, ny, world, rank
+        counts, slot_pix = shard_layout(nx, ny, tile, world)
+        self.max_slots = max(counts)
+        self.my_slots = torch.zeros(self.max_slots * 3, dtype=torch.float32, device=device)
+        self.gathered = (torch.zeros(world * self.max_slots * 3, dtype=torch.float32, device=device)
+                         if world > 1 else None)
+        self.film = torch.zeros(nx * ny * 3, dtype=torch.float32, device=device) if rank == 0 else None
+        if rank == 0:
+            sp = torch.from_numpy(slot_pix).to(device)
+            self.valid = sp >= 0
+            self.dst = sp[self.valid]
+
+    def gather(self):
+        """Collective: every rank calls it after rendering into self.my_slots."""
+        src = self.my_slots
+        if self.world > 1:
+            dist.all_gather_into_tensor(self.gathered, self.my_slots)
+            src = self.gathered
+        if self.rank == 0:
+            self.film.view(-1, 3)[self.dst] = src.view(-1, 3)[self.valid]
+        return self.film
