@@ -17,6 +17,7 @@ LIB_PATH = os.path.join(HERE, "libfrt.so")
 FRT_WORLD_BVH, FRT_WORLD_LIST = 0, 1
 FRT_MAT_LAMBERTIAN, FRT_MAT_DIFFUSE_LIGHT = 0, 1
 FRT_PRIM_SPHERE = 1 << 30
+FRT_FLAG_NO_LDS_SCENE = 1
 
 ERRORS = {0: "ok", -1: "invalid", -2: "hip", -3: "no scene", -4: "unsupported", -5: "io", -6: "no gfx950 device"}
 
@@ -57,9 +58,9 @@ class RenderParams(ctypes.Structure):
 
     @classmethod
     def make(cls, nx, ny, spp, seed=0, max_depth=33, tile_size=32, shard_index=0, shard_count=1,
-             samples_per_item=0):
+             samples_per_item=0, flags=0):
         return cls(nx=nx, ny=ny, spp=spp, seed=seed, max_depth=max_depth, integrator=0, tile_size=tile_size,
-                   shard_index=shard_index, shard_count=shard_count, samples_per_item=samples_per_item, flags=0)
+                   shard_index=shard_index, shard_count=shard_count, samples_per_item=samples_per_item, flags=flags)
 
 
 class Stats(ctypes.Structure):

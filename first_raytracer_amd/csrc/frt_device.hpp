@@ -68,27 +68,42 @@ FRT_HD uint32_t dim_bounce(int depth) { return 4u + 8u * (uint32_t)depth; }
 // ---------------------------------------------------------------------------
 // geometry
 // ---------------------------------------------------------------------------
-// reciprocal direction for the slab test.  Zero components are nudged to
+// fast reciprocal: v_rcp_f32 on the GPU (1 ulp), IEEE division on the host
+FRT_HD float rcp(float x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.0f / x;
+#endif
+}
+
+// Ray prepared for slab tests: t = lo * invd + oinv with oinv = -o * invd
+// (one FMA per slab plane).  Zero direction components are nudged to
 // +-1e-30 so no 0*inf NaN can arise; the reference's NaN-tolerant compare
 // (aabb.h:24-25) keeps the interval unchanged in that case, and so does this
-// (the near-parallel slab then spans +-huge).  Device boxes are padded
-// outward, so the degenerate "origin exactly on a face" case cannot cull.
-FRT_HD f3 safe_inv(f3 d)
+// (the near-parallel slab spans +-huge).  Device boxes are padded outward, so
+// neither the nudge nor the FMA rounding can cull a hit.
+struct SlabRay { f3 invd, oinv; };
+FRT_HD SlabRay slab_ray(f3 o, f3 d)
 {
     const float tiny = 1e-30f;
     const float dx = fabsf(d.x) > tiny ? d.x : copysignf(tiny, d.x);
     const float dy = fabsf(d.y) > tiny ? d.y : copysignf(tiny, d.y);
     const float dz = fabsf(d.z) > tiny ? d.z : copysignf(tiny, d.z);
-    return f3{1.0f / dx, 1.0f / dy, 1.0f / dz};
+    SlabRay r;
+    r.invd = f3{rcp(dx), rcp(dy), rcp(dz)};
+    r.oinv = f3{-o.x * r.invd.x, -o.y * r.invd.y, -o.z * r.invd.z};
+    return r;
 }
 // slab test of a box against [tmin, tmax]; returns entry distance or +inf on
 // miss (aabb.h:14-31: the reference's per-axis early exit decides the same).
-FRT_HD float slab_entry(float lox, float loy, float loz, float hix, float hiy, float hiz,
-                        f3 o, f3 invd, float tmin, float tmax)
+FRT_HD float slab_entry(float lox, float loy, float loz, float hix, float hiy, float hiz, const SlabRay &r,
+                        float tmin, float tmax)
 {
-    const float tx0 = (lox - o.x) * invd.x, tx1 = (hix - o.x) * invd.x;
-    const float ty0 = (loy - o.y) * invd.y, ty1 = (hiy - o.y) * invd.y;
-    const float tz0 = (loz - o.z) * invd.z, tz1 = (hiz - o.z) * invd.z;
+    const float tx0 = fmaf(lox, r.invd.x, r.oinv.x), tx1 = fmaf(hix, r.invd.x, r.oinv.x);
+    const float ty0 = fmaf(loy, r.invd.y, r.oinv.y), ty1 = fmaf(hiy, r.invd.y, r.oinv.y);
+    const float tz0 = fmaf(loz, r.invd.z, r.oinv.z), tz1 = fmaf(hiz, r.invd.z, r.oinv.z);
     const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
     const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
     return (tf < tn) ? __builtin_inff() : tn;
@@ -101,7 +116,7 @@ FRT_HD float tri_intersect(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float tmin, float tm
     const f3 h = cross(d, e2);
     const float a = dot(e1, h);
     if (a == 0.0f) return -1.0f;
-    const float f = 1.0f / a;
+    const float f = rcp(a);
     const f3 s = o - v0;
     u = f * dot(s, h);
     if (u < 0.0f || u > 1.0f) return -1.0f;

@@ -32,6 +32,7 @@ struct DevScene {
     const int *list;         // device prim refs (list worlds)
     int root;                // node index, or ~prim for a single-leaf world
     int n_lights, n_list, world_kind;
+    int n_nodes, n_tris, n_mats;
     float root_lo[3], root_hi[3];
     f3 cam_o, cam_llc, cam_h, cam_v, cam_u, cam_vv;
     float lens_r;
@@ -63,10 +64,10 @@ template <int STRIDE>
 FRT_HD Hit trace_bvh(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int *stk)
 {
     Hit h{-1, tmax, 0.0f, 0.0f};
-    const f3 invd = safe_inv(d);
+    const SlabRay sr = slab_ray(o, d);
     // root box with the unscaled EPSILON (parallel_bvh.h:43), then
     // t_min = EPSILON * max(1, |o|_inf) (parallel_bvh.h:46-51)
-    if (slab_entry(S.root_lo[0], S.root_lo[1], S.root_lo[2], S.root_hi[0], S.root_hi[1], S.root_hi[2], o, invd,
+    if (slab_entry(S.root_lo[0], S.root_lo[1], S.root_lo[2], S.root_hi[0], S.root_hi[1], S.root_hi[2], sr,
                    kEps, tmax) == __builtin_inff())
         return h;
     const float tmin = kEps * fmaxf(1.0f, fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z))));
@@ -76,8 +77,8 @@ FRT_HD Hit trace_bvh(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int
         while ((unsigned)node < (unsigned)kSentinel) {   // interior node
             const float4 n0 = S.nodes[4 * node], n1 = S.nodes[4 * node + 1];
             const float4 n2 = S.nodes[4 * node + 2], n3 = S.nodes[4 * node + 3];
-            const float t0 = slab_entry(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, invd, tmin, h.t);
-            const float t1 = slab_entry(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, invd, tmin, h.t);
+            const float t0 = slab_entry(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, sr, tmin, h.t);
+            const float t1 = slab_entry(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, sr, tmin, h.t);
             const int c0 = f2i(n3.x), c1 = f2i(n3.y);
             const bool h0 = t0 != __builtin_inff(), h1 = t1 != __builtin_inff();
             if (h0 && h1) {

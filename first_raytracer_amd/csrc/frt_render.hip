@@ -63,11 +63,28 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t m)
 // ------------------------------------------------------------------------
 // the persistent path megakernel
 // ------------------------------------------------------------------------
-template <int STACK, int WORLD>
-__global__ __launch_bounds__(kBlock) void path_megakernel(const DevScene S, const DevWork W)
+// LDS_SCENE: small scenes (nodes + triangles + shading records + materials,
+// <= kLdsSceneBytes) are copied into LDS once per block and traversed there
+// (ds_read_b128 instead of L1/L2 round trips).
+template <int STACK, int WORLD, bool LDS_SCENE>
+__global__ __launch_bounds__(kBlock) void path_megakernel(const DevScene S0, const DevWork W)
 {
-    extern __shared__ int lds_stack[];       // [STACK][kBlock]: one LDS column per lane
-    int *stk = lds_stack + threadIdx.x;
+    extern __shared__ __attribute__((aligned(16))) int lds_mem[];   // [STACK][kBlock] stack, then the scene
+    int *stk = lds_mem + threadIdx.x;                                 // one LDS column per lane
+    DevScene S = S0;
+    if constexpr (LDS_SCENE) {
+        float4 *l4 = reinterpret_cast<float4 *>(lds_mem + STACK * kBlock);
+        const int nn = 4 * S0.n_nodes, nt = 3 * S0.n_tris, ns = 2 * S0.n_tris, nm = 2 * S0.n_mats;
+        for (int i = threadIdx.x; i < nn; i += kBlock) l4[i] = S0.nodes[i];
+        for (int i = threadIdx.x; i < nt; i += kBlock) l4[nn + i] = S0.tris[i];
+        for (int i = threadIdx.x; i < ns; i += kBlock) l4[nn + nt + i] = S0.tshade[i];
+        for (int i = threadIdx.x; i < nm; i += kBlock) l4[nn + nt + ns + i] = S0.mats[i];
+        __syncthreads();
+        S.nodes = l4;
+        S.tris = l4 + nn;
+        S.tshade = l4 + nn + nt;
+        S.mats = l4 + nn + nt + ns;
+    }
     const int lane = threadIdx.x & 63;
     const int T2 = W.tile * W.tile;
 
@@ -190,6 +207,7 @@ struct frt_ctx {
     bool have_scene = false;
     DevScene S{};
     int world_kind = 0, stack_needed = 0;
+    size_t scene_lds_bytes = 0;
     std::vector<void *> scene_bufs;
     // workspace
     float *partial = nullptr; size_t partial_bytes = 0;
@@ -454,6 +472,9 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     S.root = (sv->world_kind == FRT_WORLD_BVH) ? ((sv->root >= 0) ? 0 : ~dev_ref(~sv->root)) : 0;
     S.n_lights = sv->n_lights;
     S.n_list = (int)F.list.size();
+    S.n_nodes = (int)(F.nodes.size() / 4);
+    S.n_tris = nt;
+    S.n_mats = nm;
     S.world_kind = sv->world_kind;
     auto f3d = [](const double *x) { return mk3((float)x[0], (float)x[1], (float)x[2]); };
     S.cam_o = f3d(sv->cam_origin); S.cam_llc = f3d(sv->cam_lower_left);
@@ -496,6 +517,7 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
         return rc;
     c->world_kind = S.world_kind;
     c->stack_needed = F.depth;
+    c->scene_lds_bytes = sizeof(float4) * (F.nodes.size() + F.tris.size() + F.tshade.size() + F.mats.size());
     c->have_scene = true;
     return FRT_OK;
 }
@@ -588,19 +610,36 @@ extern "C" int frt_shard_slots(const frt_render_params *p, int32_t *slot_pixel)
     return FRT_OK;
 }
 
-template <int STACK, int WORLD>
-static hipError_t launch_path(frt_ctx *c, const DevWork &W, int grid, hipStream_t st)
+constexpr size_t kLdsSceneBytes = 24 * 1024;   // 4 blocks/CU x (stack + scene) must fit 160 KiB
+
+struct Launcher {
+    const void *fn = nullptr;
+    size_t lds = 0;
+    int stack = 0;
+    bool lds_scene = false;
+};
+template <int STACK, int WORLD, bool LDS>
+static Launcher make_launcher(size_t scene_bytes)
 {
-    const size_t lds = (WORLD == FRT_WORLD_BVH) ? (size_t)STACK * kBlock * sizeof(int) : 0;
-    hipLaunchKernelGGL((path_megakernel<STACK, WORLD>), dim3(grid), dim3(kBlock), lds, st, c->S, W);
-    return hipGetLastError();
+    Launcher L;
+    L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS>);
+    L.lds = (WORLD == FRT_WORLD_BVH ? (size_t)STACK * kBlock * sizeof(int) : 0) + (LDS ? scene_bytes : 0);
+    L.stack = STACK;
+    L.lds_scene = LDS;
+    return L;
 }
-template <int STACK, int WORLD>
-static int occupancy(int *blocks)
+static int pick_launcher(const frt_ctx *c, int flags, Launcher &L)
 {
-    const size_t lds = (WORLD == FRT_WORLD_BVH) ? (size_t)STACK * kBlock * sizeof(int) : 0;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, path_megakernel<STACK, WORLD>, kBlock, lds) ==
-                   hipSuccess ? 0 : -1;
+    if (c->world_kind == FRT_WORLD_LIST) { L = make_launcher<16, FRT_WORLD_LIST, false>(0); return FRT_OK; }
+    const int d = c->stack_needed;
+    const size_t sb = c->scene_lds_bytes;
+    const bool lds = sb <= kLdsSceneBytes && !(flags & FRT_FLAG_NO_LDS_SCENE);
+    if (d < 8) L = lds ? make_launcher<8, FRT_WORLD_BVH, true>(sb) : make_launcher<8, FRT_WORLD_BVH, false>(0);
+    else if (d < 16) L = lds ? make_launcher<16, FRT_WORLD_BVH, true>(sb) : make_launcher<16, FRT_WORLD_BVH, false>(0);
+    else if (d < 32) L = lds ? make_launcher<32, FRT_WORLD_BVH, true>(sb) : make_launcher<32, FRT_WORLD_BVH, false>(0);
+    else if (d < 64) L = make_launcher<64, FRT_WORLD_BVH, false>(0);
+    else return FRT_E_UNSUPPORTED;
+    return FRT_OK;
 }
 
 static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots, hipStream_t st, frt_stats *stats)
@@ -613,21 +652,11 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     const int T = eff_tile(p);
     const int nmt = my_tiles(p);
     const uint32_t n_slots = (uint32_t)nmt * T * T;
-    // kernel variant by stack depth
-    int stack = 16;
-    if (c->world_kind == FRT_WORLD_BVH) {
-        if (c->stack_needed < 16) stack = 16;
-        else if (c->stack_needed < 32) stack = 32;
-        else if (c->stack_needed < 64) stack = 64;
-        else return set_err(c, FRT_E_UNSUPPORTED, "BVH deeper than 63 levels");
-    }
+    // kernel variant: stack depth, world kind, LDS-resident scene
+    Launcher L;
+    if (pick_launcher(c, p->flags, L) != FRT_OK) return set_err(c, FRT_E_UNSUPPORTED, "BVH deeper than 63 levels");
     int bpc = 0;
-    int oc;
-    if (c->world_kind == FRT_WORLD_LIST) oc = occupancy<16, FRT_WORLD_LIST>(&bpc);
-    else if (stack == 16) oc = occupancy<16, FRT_WORLD_BVH>(&bpc);
-    else if (stack == 32) oc = occupancy<32, FRT_WORLD_BVH>(&bpc);
-    else oc = occupancy<64, FRT_WORLD_BVH>(&bpc);
-    if (oc != 0 || bpc <= 0) bpc = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, L.fn, kBlock, L.lds) != hipSuccess || bpc <= 0) bpc = 1;
     const int grid = c->n_cu * bpc;
     const long long lanes = (long long)grid * kBlock;
     // work granule: aim for >= 16 items per resident lane
@@ -664,11 +693,9 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
 
     HIPCHK(c, hipMemsetAsync(c->counter, 0, 64, st));
     HIPCHK(c, hipEventRecord(c->ev0, st));
-    hipError_t le;
-    if (c->world_kind == FRT_WORLD_LIST) le = launch_path<16, FRT_WORLD_LIST>(c, W, grid, st);
-    else if (stack == 16) le = launch_path<16, FRT_WORLD_BVH>(c, W, grid, st);
-    else if (stack == 32) le = launch_path<32, FRT_WORLD_BVH>(c, W, grid, st);
-    else le = launch_path<64, FRT_WORLD_BVH>(c, W, grid, st);
+    DevScene Sarg = c->S;
+    void *args[] = {&Sarg, &W};
+    const hipError_t le = hipLaunchKernel(L.fn, dim3(grid), dim3(kBlock), args, L.lds, st);
     if (le != hipSuccess) return set_err(c, FRT_E_HIP, std::string("path_megakernel launch: ") + hipGetErrorString(le));
     HIPCHK(c, hipEventRecord(c->ev1, st));
     if (n_slots > 0) {

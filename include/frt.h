@@ -42,6 +42,7 @@ enum {
 enum { FRT_WORLD_BVH = 0, FRT_WORLD_LIST = 1 };          /* parallel_bvh_node | hitable_list */
 enum { FRT_MAT_LAMBERTIAN = 0, FRT_MAT_DIFFUSE_LIGHT = 1 }; /* material.h:50-73, 179-192 */
 enum { FRT_INTEGRATOR_PATH = 0 };                         /* path.h:8-18 */
+enum { FRT_FLAG_NO_LDS_SCENE = 1 };   /* render_params.flags: keep small scenes in HBM/L2 (A/B timing) */
 
 /* primitive reference: triangle t -> t ; sphere k -> FRT_PRIM_SPHERE | k */
 #define FRT_PRIM_SPHERE (1 << 30)
@@ -98,7 +99,7 @@ typedef struct frt_render_params {
     int32_t shard_index;     /* this call renders tiles t with t % shard_count == index    */
     int32_t shard_count;     /* 1 = whole frame                                            */
     int32_t samples_per_item;/* work granule in samples; 0 = automatic                     */
-    int32_t flags;           /* reserved, 0                                                */
+    int32_t flags;           /* FRT_FLAG_* bits, 0 = defaults                              */
 } frt_render_params;
 
 typedef struct frt_stats {
