@@ -18,6 +18,7 @@ FRT_WORLD_BVH, FRT_WORLD_LIST = 0, 1
 FRT_MAT_LAMBERTIAN, FRT_MAT_DIFFUSE_LIGHT = 0, 1
 FRT_PRIM_SPHERE = 1 << 30
 FRT_FLAG_NO_LDS_SCENE = 1
+FRT_INTEGRATOR_PATH, FRT_INTEGRATOR_PSSMLT = 0, 1
 
 ERRORS = {0: "ok", -1: "invalid", -2: "hip", -3: "no scene", -4: "unsupported", -5: "io", -6: "no gfx950 device"}
 
@@ -48,19 +49,29 @@ class SceneView(ctypes.Structure):
         ("cam_u", ctypes.c_double * 3), ("cam_v", ctypes.c_double * 3),
         ("cam_lens_radius", ctypes.c_double),
         ("env_color", ctypes.c_double * 3),
+        ("cam_w", ctypes.c_double * 3),
+        ("cam_half_height", ctypes.c_double),
     ]
 
 
 class RenderParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in ("nx", "ny", "spp")] + [("seed", ctypes.c_uint32)] + [
         (n, ctypes.c_int32) for n in ("max_depth", "integrator", "tile_size", "shard_index", "shard_count",
-                                      "samples_per_item", "flags")]
+                                      "samples_per_item", "flags", "mlt_chains", "mlt_bootstrap")]
 
     @classmethod
     def make(cls, nx, ny, spp, seed=0, max_depth=33, tile_size=32, shard_index=0, shard_count=1,
              samples_per_item=0, flags=0):
         return cls(nx=nx, ny=ny, spp=spp, seed=seed, max_depth=max_depth, integrator=0, tile_size=tile_size,
-                   shard_index=shard_index, shard_count=shard_count, samples_per_item=samples_per_item, flags=flags)
+                   shard_index=shard_index, shard_count=shard_count, samples_per_item=samples_per_item, flags=flags,
+                   mlt_chains=0, mlt_bootstrap=0)
+
+    @classmethod
+    def pssmlt(cls, nx, ny, mutations_per_pixel, chains, seed=0, bootstrap=10000, shard_index=0, shard_count=1):
+        """PSS-MLT (pssmlt.cpp): total mutations = mutations_per_pixel*nx*ny over `chains` chains."""
+        return cls(nx=nx, ny=ny, spp=mutations_per_pixel, seed=seed, max_depth=10, integrator=FRT_INTEGRATOR_PSSMLT,
+                   tile_size=32, shard_index=shard_index, shard_count=shard_count, samples_per_item=0, flags=0,
+                   mlt_chains=chains, mlt_bootstrap=bootstrap)
 
 
 class Stats(ctypes.Structure):
@@ -90,7 +101,7 @@ _lib = None
 EXPORTS = ("frt_get_abi_version", "frt_create", "frt_destroy", "frt_last_error", "frt_upload_scene",
            "frt_shard_slot_count", "frt_shard_slots", "frt_render", "frt_render_device", "frt_scene_create",
            "frt_scene_view_get", "frt_scene_info", "frt_scene_destroy", "frt_write_tessellated_obj",
-           "frt_write_pfm", "frt_selftest_path_host")
+           "frt_write_pfm", "frt_selftest_path_host", "frt_selftest_mlt_paths_host")
 
 
 def lib():
@@ -129,6 +140,8 @@ def lib():
     L.frt_write_pfm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, vp]
     L.frt_selftest_path_host.argtypes = [ctypes.POINTER(SceneView), ctypes.POINTER(RenderParams), vp,
                                          ctypes.c_int, vp, ctypes.POINTER(Stats)]
+    L.frt_selftest_mlt_paths_host.argtypes = [ctypes.POINTER(SceneView), ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
+                                              ctypes.c_int, vp]
     _lib = L
     return L
 
@@ -246,6 +259,15 @@ def selftest_path_host(scene, params, pixels):
     _check(lib().frt_selftest_path_host(ctypes.byref(view), ctypes.byref(params), pixels.ctypes.data, len(pixels),
                                         out.ctypes.data, ctypes.byref(st)), "frt_selftest_path_host")
     return out, st
+
+
+def selftest_mlt_paths_host(scene, nx, ny, seed, n):
+    """Self-test hook: n PSS-MLT bootstrap eye paths through the device code on the host."""
+    out = np.zeros((n, 6), np.float32)
+    view = scene.view()
+    _check(lib().frt_selftest_mlt_paths_host(ctypes.byref(view), nx, ny, seed, n, out.ctypes.data),
+           "frt_selftest_mlt_paths_host")
+    return out
 
 
 def write_pfm(path, film):

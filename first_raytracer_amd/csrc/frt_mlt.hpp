@@ -1,0 +1,200 @@
+// frt_mlt.hpp -- PSS-MLT (Kelemen et al.) restated from first_ray/pssmlt.cpp
+// for the GPU: one lane = one Markov chain.  __host__ __device__ like
+// frt_path.hpp (the host self-test runs the same code).
+//
+//   pssmlt::Li              pssmlt.cpp:147-277 (depth <= 10, prnd offsets, MIS t^2)
+//   GenerateEyePath         pssmlt.cpp:105-144 (pixel mapping generalised to nx, ny)
+//   perturb / mutate        pssmlt.cpp:6-17, 62-73
+//   Render (chain loop)     pssmlt.cpp:301-365, AccumulatePathContribution :19-38
+//
+// Primary samples: a chain's current state u[0..91] lives in HBM as
+// U[dim][chain] (coalesced).  A proposal is never stored: its dimension d is
+// computed when the path reads it -- a fresh uniform on a large step, else
+// perturb(U[d][c], r) -- and written back for all 92 dimensions only when the
+// proposal is accepted.  Random numbers follow DESIGN.md "PSS-MLT streams".
+#pragma once
+#include "frt_path.hpp"
+
+namespace frt {
+
+constexpr int kMltMaxPath = 10;                              // MaxPathLength (pssmlt.h:11)
+constexpr int kMltDims = 4 + (kMltMaxPath + 1) * 8;          // 92 prnds a path can read
+constexpr float kMltLargeStep = 0.3f;                        // LargeStepProb (pssmlt.h:13)
+constexpr uint32_t kMltChainSalt = 0x3C6EF372U, kMltBootSalt = 0xB5297A4DU;
+
+// perturb (pssmlt.cpp:6-17) with log(s2/s1) precomputed
+FRT_HD float mlt_perturb(float value, float s2, float log_ratio, float r)
+{
+    float result;
+    if (r < 0.5f) {
+        r = r * 2.0f;
+        result = value + s2 * expf(-log_ratio * r);
+        if (result > 1.0f) result -= 1.0f;
+    } else {
+        r = (r - 0.5f) * 2.0f;
+        result = value - s2 * expf(-log_ratio * r);
+        if (result < 0.0f) result += 1.0f;
+    }
+    return result;
+}
+
+// Source of primary samples for one eye path.
+struct PrndSource {
+    const float *U;        // chain states [dim][n_chains] (null: bootstrap / fresh)
+    uint32_t n_chains, chain;
+    RngKey key;            // step key (chain, step) or bootstrap key
+    uint32_t dim0;         // first RNG dimension holding prnd 0
+    bool fresh;            // large step / initial state / bootstrap: uniform from the key
+    float s2p, logp;       // pixel dims (0,1): s1 = 2/(nx+ny), s2 = 0.1f
+    FRT_HD float get(int d) const
+    {
+        const float r = rng_u(key, dim0 + (uint32_t)d);
+        if (fresh) return r;
+        const float cur = U[(size_t)d * n_chains + chain];
+        if (d < 2) return mlt_perturb(cur, s2p, logp, r);
+        return mlt_perturb(cur, 1.0f / 64.0f, 2.77258872223978123767f /* log(16) */, r);
+    }
+};
+
+struct MltPath {
+    PathState P;           // ro, rd, rtmax, shadow, beta, L, nee, nxt_o, nxt_d, depth (prev_p unused)
+    int off;               // PathRndsOffset
+    float x, y;            // film position of the eye ray (GenerateEyePath)
+};
+
+// GenerateEyePath, first half: camera ray from prnds 0..3 and its film position
+// (pssmlt.cpp:115-138 with PixelWidth/Height = nx/ny, dist = ny/(2 half_height)).
+FRT_HD void mlt_begin(MltPath &M, const DevScene &S, const PrndSource &src, int nx, int ny)
+{
+    const float s = src.get(0), t = src.get(1), l0 = src.get(2), l1 = src.get(3);
+    f3 off = mk3(0, 0, 0);
+    if (S.lens_r != 0.0f) {
+        const float a = l0 * 2.0f - 1.0f, b = l1 * 2.0f - 1.0f;
+        float rx = 0.0f, ry = 0.0f;
+        if (a != 0.0f || b != 0.0f) {
+            float r, phi;
+            if (a * a > b * b) { r = a; phi = (kPi / 4.0f) * (b / a); }
+            else { r = b; phi = (kPi / 2.0f) - (kPi / 4.0f) * (a / b); }
+            rx = r * cosf(phi); ry = r * sinf(phi);
+        }
+        off = (S.lens_r * rx) * S.cam_u + (S.lens_r * ry) * S.cam_vv;
+    }
+    PathState &P = M.P;
+    P.ro = S.cam_o + off;
+    P.rd = ((S.cam_llc + s * S.cam_h + t * S.cam_v) - S.cam_o) - off;
+    P.rtmax = kTMaxClosest;
+    P.shadow = false;
+    P.depth = 0;
+    P.beta = mk3(1, 1, 1);
+    P.L = mk3(0, 0, 0);
+    P.prev_pdf = 0.0f;
+    M.off = 4;
+    const f3 dir = normalize(P.rd);
+    const float dist = (float)ny / (2.0f * S.cam_half_height);
+    const f3 center = S.cam_o + dist * S.cam_w;
+    const f3 pos = (S.cam_o + (dist / dot(dir, S.cam_w)) * dir) - center;
+    M.x = -dot(S.cam_u, pos) + (float)nx * 0.5f;
+    M.y = -dot(S.cam_vv, pos) + (float)ny * 0.5f;
+}
+
+// True when the next ray would be at depth > MaxPathLength: the reference does
+// not trace it and returns the environment (pssmlt.cpp:151, :276).
+FRT_HD bool mlt_beyond(const MltPath &M) { return !M.P.shadow && M.P.depth > kMltMaxPath; }
+
+// pssmlt::Li, one hit at a time.  Returns true when the path is finished.
+FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSource &src, uint32_t &n_ext,
+                      uint32_t &n_sh)
+{
+    PathState &P = M.P;
+    if (P.shadow) {
+        if (h.prim < 0) P.L = P.L + P.nee;
+        P.shadow = false;
+        P.ro = P.nxt_o; P.rd = P.nxt_d; P.rtmax = kTMaxClosest;
+        ++P.depth;
+        if (P.depth <= kMltMaxPath) ++n_ext;
+        return false;
+    }
+    if (h.prim < 0) {
+        P.L = P.L + P.beta * S.env;
+        return true;
+    }
+    const f3 p = P.ro + h.t * P.rd;
+    f3 n;
+    int mat;
+    prim_shade(S, h.prim, P.ro, p, h.u, h.v, n, mat);
+    const float4 m0 = S.mats[2 * mat], m1 = S.mats[2 * mat + 1];
+    const int mtype = f2i(m0.w);
+    M.off += 3;                                         // scatter rnd, consumed at every hit
+    if (mtype == FRT_MAT_DIFFUSE_LIGHT && dot(n, P.rd) < 0.0f) {
+        const f3 Le = xyz(m1);
+        if (P.depth == 0) {
+            P.L = P.L + P.beta * Le;
+        } else {                                        // pssmlt.cpp:175-184: distance^2 = t^2
+            const float cos_wo = dot(n, -normalize(P.rd));
+            float d2 = h.t * h.t;
+            if (d2 <= kEps) d2 = kEps;
+            const float light_pdf = prim_pdf(S, h.prim, p, h.t, n, P.rd) * d2 / fabsf(cos_wo);
+            P.L = P.L + mi_weight(P.prev_pdf, light_pdf) * (P.beta * Le);
+        }
+        return true;
+    }
+    if (mtype != FRT_MAT_LAMBERTIAN) return true;      // diffuse_light seen from behind
+    // NEE prnds (pssmlt.cpp:190-195), then the bsdf prnds after the offset move
+    const float rnd0 = src.get(M.off), rnd1 = src.get(M.off + 1), rnd2 = src.get(M.off + 2);
+    M.off += 3;
+    const float b0 = src.get(M.off), b1 = src.get(M.off + 1);
+    M.off += 2;
+    const Onb uvw = onb_from_w(n);
+    const f3 wo = onb_local(uvw, cosine_direction(b0, b1));
+    const float cw = dot(n, normalize(wo));
+    const float pdf = fmaxf(cw, 0.0f) * kInvPi;
+    if (pdf == 0.0f) return true;                       // drops this vertex's NEE (pssmlt.cpp:261-264)
+    const f3 f = kInvPi * xyz(m0);
+    const f3 beta_next = (fabsf(cw) / pdf) * (P.beta * f);
+    const f3 origin = p + kEps * n;
+    P.nxt_o = origin;                                   // hrec.p moved off the surface (pssmlt.cpp:253)
+    P.nxt_d = wo;
+    const int nl = S.n_lights;
+    int idx = (int)(rnd0 * (float)nl);
+    if (idx == nl) idx -= 1;
+    if (idx >= 0) {
+        const int lref = S.lights[idx];
+        f3 ln;
+        int lmat;
+        const f3 tl = prim_sample(S, lref, origin, rnd1, rnd2, ln, lmat);
+        const float dist2 = len2(tl);
+        const f3 tu = rlen(tl) * tl;
+        const float cos_wi = dot(n, tu);
+        const float cos_lo = dot(ln, -tu);
+        P.nee = mk3(0, 0, 0);
+        if (cos_lo != 0.0f) {
+            const float light_pdf = prim_pdf(S, lref, p, h.t, n, tu) * dist2 / fabsf(cos_lo);
+            const float bsdf_pdf = fmaxf(cos_wi, 0.0f) * kInvPi;
+            const float wgt = mi_weight(light_pdf, bsdf_pdf);
+            const float4 lm0 = S.mats[2 * lmat], lm1 = S.mats[2 * lmat + 1];
+            if (f2i(lm0.w) == FRT_MAT_DIFFUSE_LIGHT && dot(ln, tu) < 0.0f)
+                P.nee = (wgt / light_pdf * cos_wi) * (P.beta * (xyz(lm1) * f));
+        }
+        P.ro = origin; P.rd = tl; P.rtmax = 1.0f - kShadowEps;
+        P.shadow = true;
+        ++n_sh;
+    }
+    P.beta = beta_next;
+    P.prev_pdf = pdf;
+    if (!P.shadow) {
+        P.ro = P.nxt_o; P.rd = P.nxt_d; P.rtmax = kTMaxClosest;
+        ++P.depth;
+        if (P.depth <= kMltMaxPath) ++n_ext;
+    }
+    return false;
+}
+
+// AccumulatePathContribution target pixel (pssmlt.cpp:19-31); -1 if off film
+FRT_HD int mlt_pixel(float x, float y, int nx, int ny)
+{
+    const int ix = (int)x, iy = (int)y;
+    if (ix < 0 || ix >= nx || iy < 0 || iy >= ny) return -1;
+    return iy * nx + ix;
+}
+
+}  // namespace frt

@@ -34,8 +34,8 @@ struct DevScene {
     int n_lights, n_list, world_kind;
     int n_nodes, n_tris, n_mats;
     float root_lo[3], root_hi[3];
-    f3 cam_o, cam_llc, cam_h, cam_v, cam_u, cam_vv;
-    float lens_r;
+    f3 cam_o, cam_llc, cam_h, cam_v, cam_u, cam_vv, cam_w;
+    float lens_r, cam_half_height;
     f3 env;
 };
 

@@ -28,6 +28,7 @@
 #include "frt.h"
 #include "frt_device.hpp"
 #include "frt_path.hpp"
+#include "frt_mlt.hpp"
 
 using namespace frt;
 
@@ -192,6 +193,164 @@ __global__ void film_reduce(const float *__restrict__ partial, float *__restrict
     out[3ull * s + 2] = b;
 }
 
+
+// ------------------------------------------------------------------------
+// PSS-MLT (pssmlt.cpp:301-365)
+// ------------------------------------------------------------------------
+struct MltWork {
+    int nx, ny;
+    uint32_t seed;
+    int shard_index, shard_count;
+    uint32_t n_local;                    // chains of this shard: global c = shard_index + j * shard_count
+    uint64_t steps;                      // mutations per chain
+    float b, scale, s2p, logp;           // normaliser, nx*ny/ns, pixel-dim perturb constants
+    float *U;                            // [kMltDims][n_local] current primary samples
+    float *film;                         // [nx*ny*3] splat accumulation
+    unsigned *counter;
+    unsigned long long *wave_rays;
+};
+
+template <int WORLD>
+__device__ __forceinline__ Hit trace_any(const DevScene &S, const PathState &P, int *stk)
+{
+    return trace<WORLD, kBlock>(S, P.ro, P.rd, P.rtmax, P.shadow, stk);
+}
+
+// bootstrap: sc of n_init independent eye paths (pssmlt.cpp:303-312); the host
+// sums them in a fixed order
+template <int STACK, int WORLD>
+__global__ __launch_bounds__(kBlock) void mlt_bootstrap(const DevScene S, int nx, int ny, uint32_t seed, int n_init,
+                                                        float *sc)
+{
+    extern __shared__ __attribute__((aligned(16))) int lds_mem[];
+    int *stk = lds_mem + threadIdx.x;
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n_init) return;
+    PrndSource src{nullptr, 0, 0, rng_key(seed ^ kMltBootSalt, (uint32_t)i, 0u), 0u, true, 0.0f, 0.0f};
+    MltPath M;
+    mlt_begin(M, S, src, nx, ny);
+    uint32_t ne = 0, ns = 0;
+    for (;;) {
+        if (mlt_beyond(M)) { M.P.L = M.P.L + M.P.beta * S.env; break; }
+        const Hit h = trace_any<WORLD>(S, M.P, stk);
+        if (mlt_shade(M, S, h, src, ne, ns)) break;
+    }
+    sc[i] = fmaxf(fmaxf(M.P.L.x, M.P.L.y), M.P.L.z);
+}
+
+__device__ __forceinline__ void mlt_splat(const MltWork &W, float x, float y, f3 c, float w)
+{
+    const int pix = mlt_pixel(x, y, W.nx, W.ny);
+    if (pix < 0) return;
+    const float k = W.scale * w;
+    atomicAdd(&W.film[3 * (size_t)pix + 0], k * c.x);
+    atomicAdd(&W.film[3 * (size_t)pix + 1], k * c.y);
+    atomicAdd(&W.film[3 * (size_t)pix + 2], k * c.z);
+}
+
+// one lane = one chain; every iteration traces one ray of the chain's current
+// eye path (initial state, then one proposal per mutation)
+template <int STACK, int WORLD>
+__global__ __launch_bounds__(kBlock) void mlt_megakernel(const DevScene S, const MltWork W)
+{
+    extern __shared__ __attribute__((aligned(16))) int lds_mem[];
+    int *stk = lds_mem + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    bool have = false, exhausted = false, init = false, large = false;
+    uint32_t j = 0, c = 0;
+    uint64_t t = 0;
+    float cx = 0, cy = 0, csc = 0, cw = 0;
+    f3 cc = mk3(0, 0, 0);
+    RngKey key{0, 0};
+    MltPath M;
+    uint32_t n_cam = 0, n_ext = 0, n_sh = 0, n_smp = 0;
+
+    auto source = [&]() {
+        PrndSource src{W.U, W.n_local, j, key, 2u, init || large, W.s2p, W.logp};
+        return src;
+    };
+    for (;;) {
+        // ---- chains from the queue, one atomic per wave ----
+        const bool need = !have && !exhausted;
+        const uint64_t m = __ballot(need);
+        if (m) {
+            const int leader = __ffsll((unsigned long long)m) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(W.counter, (unsigned)__popcll(m));
+            base = __shfl(base, leader);
+            if (need) {
+                const uint32_t w = base + lane_rank(m);
+                if (w >= W.n_local) {
+                    exhausted = true;
+                } else {
+                    have = true;
+                    init = true;
+                    j = w;
+                    c = (uint32_t)W.shard_index + w * (uint32_t)W.shard_count;
+                    t = 0;
+                    cw = 0.0f;
+                    key = rng_key(W.seed ^ kMltChainSalt, c, 0u);   // initial state: TMarkovChain(s)
+                    mlt_begin(M, S, source(), W.nx, W.ny);
+                    ++n_cam;
+                }
+            }
+        }
+        if (__ballot(have) == 0) {
+            if (__ballot(!exhausted) == 0) break;
+            continue;
+        }
+        if (!have) continue;
+        bool done;
+        if (mlt_beyond(M)) {
+            M.P.L = M.P.L + M.P.beta * S.env;
+            done = true;
+        } else {
+            const Hit h = trace_any<WORLD>(S, M.P, stk);
+            uint32_t ne = 0, ns = 0;
+            done = mlt_shade(M, S, h, source(), ne, ns);
+            n_ext += ne; n_sh += ns;
+        }
+        if (!done) continue;
+        const f3 L = M.P.L;
+        const float sc = fmaxf(fmaxf(L.x, L.y), L.z);
+        const PrndSource src = source();
+        if (init) {                                     // current = initial state, materialised
+            for (int d = 0; d < kMltDims; ++d) W.U[(size_t)d * W.n_local + j] = src.get(d);
+            cx = M.x; cy = M.y; cc = L; csc = sc;
+            init = false;
+        } else {                                        // pssmlt.cpp:200-209
+            float a = 1.0f;
+            if (csc > 0.0f) a = fmaxf(fminf(1.0f, sc / csc), 0.0f);
+            if (sc > 0.0f) mlt_splat(W, M.x, M.y, L, (a + (large ? 1.0f : 0.0f)) / (sc / W.b + kMltLargeStep));
+            if (csc > 0.0f) cw += (1.0f - a) / (csc / W.b + kMltLargeStep);
+            if (rng_u(key, 1) <= a) {                   // accept: splat the old state's weight, move
+                if (csc > 0.0f && cw != 0.0f) mlt_splat(W, cx, cy, cc, cw);
+                cw = 0.0f;
+                for (int d = 0; d < kMltDims; ++d) W.U[(size_t)d * W.n_local + j] = src.get(d);
+                cx = M.x; cy = M.y; cc = L; csc = sc;
+            }
+            ++t;
+            ++n_smp;
+        }
+        if (t >= W.steps) {                             // chain finished
+            if (csc > 0.0f && cw != 0.0f) mlt_splat(W, cx, cy, cc, cw);
+            have = false;
+            continue;
+        }
+        key = rng_key(W.seed ^ kMltChainSalt, c, (uint32_t)(t + 1));
+        large = rng_u(key, 0) < kMltLargeStep;          // large_step vs mutate (pssmlt.cpp:187-196)
+        mlt_begin(M, S, source(), W.nx, W.ny);
+        ++n_cam;
+    }
+    unsigned long long cnt[4] = {n_cam, n_ext, n_sh, n_smp};
+    for (int k = 0; k < 4; ++k)
+        for (int off = 32; off > 0; off >>= 1) cnt[k] += __shfl_xor(cnt[k], off);
+    if (lane == 0) {
+        const size_t wv = ((size_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+        for (int k = 0; k < 4; ++k) W.wave_rays[4 * wv + k] = cnt[k];
+    }
+}
+
 }  // namespace
 
 // ==========================================================================
@@ -208,6 +367,7 @@ struct frt_ctx {
     DevScene S{};
     int world_kind = 0, stack_needed = 0;
     size_t scene_lds_bytes = 0;
+    double last_mlt_b = 0.0;
     std::vector<void *> scene_bufs;
     // workspace
     float *partial = nullptr; size_t partial_bytes = 0;
@@ -481,6 +641,8 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     S.cam_h = f3d(sv->cam_horizontal); S.cam_v = f3d(sv->cam_vertical);
     S.cam_u = f3d(sv->cam_u); S.cam_vv = f3d(sv->cam_v);
     S.lens_r = (float)sv->cam_lens_radius;
+    S.cam_w = f3d(sv->cam_w);
+    S.cam_half_height = (float)sv->cam_half_height;
     S.env = f3d(sv->env_color);
     return FRT_OK;
 }
@@ -571,14 +733,51 @@ extern "C" int frt_selftest_path_host(const frt_scene_view *sv, const frt_render
     return FRT_OK;
 }
 
+
+// Self-test hook: n PSS-MLT bootstrap eye paths (fresh primary samples from the
+// bootstrap stream) through frt_mlt.hpp on the host; out6[i] = x, y, r, g, b, sc.
+extern "C" int frt_selftest_mlt_paths_host(const frt_scene_view *sv, int nx, int ny, uint32_t seed, int n,
+                                           float *out6)
+{
+    if (!sv || !out6 || n < 0 || nx <= 0 || ny <= 0) return FRT_E_INVALID;
+    FlatScene F;
+    std::string err;
+    const int rc = flatten_scene(sv, F, err);
+    if (rc != FRT_OK) return rc;
+    DevScene S = F.meta;
+    S.nodes = F.nodes.data(); S.tris = F.tris.data(); S.tshade = F.tshade.data(); S.tnorm = F.tnorm.data();
+    S.spheres = F.spheres.data(); S.sphere_mat = F.smat.data(); S.mats = F.mats.data();
+    S.lights = F.lights.data(); S.list = F.list.data();
+    std::vector<int> stack(std::max(F.depth + 1, 1));
+    for (int i = 0; i < n; ++i) {
+        PrndSource src{nullptr, 0, 0, rng_key(seed ^ kMltBootSalt, (uint32_t)i, 0u), 0u, true, 0.0f, 0.0f};
+        MltPath M;
+        mlt_begin(M, S, src, nx, ny);
+        uint32_t ne = 0, ns = 0;
+        for (;;) {
+            if (mlt_beyond(M)) { M.P.L = M.P.L + M.P.beta * S.env; break; }
+            const Hit h = (S.world_kind == FRT_WORLD_LIST)
+                              ? trace<FRT_WORLD_LIST, 1>(S, M.P.ro, M.P.rd, M.P.rtmax, M.P.shadow, stack.data())
+                              : trace<FRT_WORLD_BVH, 1>(S, M.P.ro, M.P.rd, M.P.rtmax, M.P.shadow, stack.data());
+            if (mlt_shade(M, S, h, src, ne, ns)) break;
+        }
+        const f3 L = M.P.L;
+        float *o = &out6[6 * (size_t)i];
+        o[0] = M.x; o[1] = M.y; o[2] = L.x; o[3] = L.y; o[4] = L.z; o[5] = fmaxf(fmaxf(L.x, L.y), L.z);
+    }
+    return FRT_OK;
+}
+
 // ---- shard geometry ----
 static int eff_tile(const frt_render_params *p) { return p->tile_size > 0 ? p->tile_size : 32; }
 static bool params_ok(const frt_render_params *p)
 {
     const int T = eff_tile(p);
-    return p && p->nx > 0 && p->ny > 0 && p->spp > 0 && (T % 8) == 0 && T <= 256 && p->shard_count >= 1 &&
-           p->shard_index >= 0 && p->shard_index < p->shard_count && p->max_depth >= -1 && p->max_depth < 100000 &&
-           p->integrator == FRT_INTEGRATOR_PATH;
+    if (!(p && p->nx > 0 && p->ny > 0 && p->spp > 0 && (T % 8) == 0 && T <= 256 && p->shard_count >= 1 &&
+          p->shard_index >= 0 && p->shard_index < p->shard_count && p->max_depth >= -1 && p->max_depth < 100000))
+        return false;
+    if (p->integrator == FRT_INTEGRATOR_PATH) return true;
+    return p->integrator == FRT_INTEGRATOR_PSSMLT && p->mlt_chains > 0 && p->mlt_bootstrap > 0;
 }
 static int my_tiles(const frt_render_params *p)
 {
@@ -590,12 +789,17 @@ static int my_tiles(const frt_render_params *p)
 extern "C" int64_t frt_shard_slot_count(const frt_render_params *p)
 {
     if (!params_ok(p)) return FRT_E_INVALID;
+    if (p->integrator == FRT_INTEGRATOR_PSSMLT) return (int64_t)p->nx * p->ny;   // whole film per shard
     const int T = eff_tile(p);
     return (int64_t)my_tiles(p) * T * T;
 }
 extern "C" int frt_shard_slots(const frt_render_params *p, int32_t *slot_pixel)
 {
     if (!params_ok(p) || !slot_pixel) return FRT_E_INVALID;
+    if (p->integrator == FRT_INTEGRATOR_PSSMLT) {
+        for (int64_t i = 0; i < (int64_t)p->nx * p->ny; ++i) slot_pixel[i] = (int32_t)i;
+        return FRT_OK;
+    }
     const int T = eff_tile(p), ntx = (p->nx + T - 1) / T;
     const int nmt = my_tiles(p);
     for (int t = 0; t < nmt; ++t) {
@@ -642,6 +846,103 @@ static int pick_launcher(const frt_ctx *c, int flags, Launcher &L)
     return FRT_OK;
 }
 
+
+// ---- PSS-MLT render: bootstrap b, then the chain megakernel splatting into dev_film ----
+template <int STACK, int WORLD>
+static void mlt_kernels(const void **boot, const void **chains)
+{
+    *boot = reinterpret_cast<const void *>(&mlt_bootstrap<STACK, WORLD>);
+    *chains = reinterpret_cast<const void *>(&mlt_megakernel<STACK, WORLD>);
+}
+
+static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, hipStream_t st, frt_stats *stats)
+{
+    const auto t_start = std::chrono::steady_clock::now();
+    int stack;
+    const void *kboot = nullptr, *kchain = nullptr;
+    if (c->world_kind == FRT_WORLD_LIST) { stack = 0; mlt_kernels<16, FRT_WORLD_LIST>(&kboot, &kchain); }
+    else if (c->stack_needed < 16) { stack = 16; mlt_kernels<16, FRT_WORLD_BVH>(&kboot, &kchain); }
+    else if (c->stack_needed < 32) { stack = 32; mlt_kernels<32, FRT_WORLD_BVH>(&kboot, &kchain); }
+    else if (c->stack_needed < 64) { stack = 64; mlt_kernels<64, FRT_WORLD_BVH>(&kboot, &kchain); }
+    else return set_err(c, FRT_E_UNSUPPORTED, "BVH deeper than 63 levels");
+    const size_t lds = (size_t)stack * kBlock * sizeof(int);
+    const uint32_t n_chains = (uint32_t)p->mlt_chains;
+    const uint32_t n_local = (n_chains > (uint32_t)p->shard_index)
+                                 ? (n_chains - 1 - (uint32_t)p->shard_index) / (uint32_t)p->shard_count + 1 : 0;
+    const uint64_t total = (uint64_t)p->spp * (uint64_t)p->nx * (uint64_t)p->ny;   // viewer ns
+    const uint64_t steps = total / n_chains;                                       // samples_per_thread
+    // bootstrap normaliser (identical on every shard: same streams, fixed-order host sum)
+    const int n_init = p->mlt_bootstrap;
+    const size_t need = std::max<size_t>((size_t)n_init * sizeof(float), (size_t)kMltDims * n_local * sizeof(float));
+    if (need > c->partial_bytes) {
+        if (c->partial) HIPCHK(c, hipFree(c->partial));
+        c->partial = nullptr;
+        HIPCHK(c, hipMalloc(&c->partial, need));
+        c->partial_bytes = need;
+    }
+    {
+        int nx = p->nx, ny = p->ny, ni = n_init;
+        uint32_t seed = p->seed;
+        float *sc = c->partial;
+        DevScene Sarg = c->S;
+        void *args[] = {&Sarg, &nx, &ny, &seed, &ni, &sc};
+        HIPCHK(c, hipLaunchKernel(kboot, dim3((n_init + kBlock - 1) / kBlock), dim3(kBlock), args, lds, st));
+    }
+    std::vector<float> sc(n_init);
+    HIPCHK(c, hipMemcpyAsync(sc.data(), c->partial, n_init * sizeof(float), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    double b = 0.0;
+    for (float v : sc) b += v;
+    b /= n_init;
+    int bpc = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kchain, kBlock, lds) != hipSuccess || bpc <= 0) bpc = 1;
+    const int grid = std::max(1, std::min<int>(c->n_cu * bpc, (int)((n_local + kBlock - 1) / kBlock)));
+    const size_t n_waves = (size_t)grid * kBlock / 64;
+    if (n_waves > c->wave_rays_n) {
+        if (c->wave_rays) HIPCHK(c, hipFree(c->wave_rays));
+        c->wave_rays = nullptr;
+        HIPCHK(c, hipMalloc(&c->wave_rays, n_waves * 4 * sizeof(unsigned long long)));
+        c->wave_rays_n = n_waves;
+    }
+    MltWork W{};
+    W.nx = p->nx; W.ny = p->ny; W.seed = p->seed;
+    W.shard_index = p->shard_index; W.shard_count = p->shard_count;
+    W.n_local = n_local; W.steps = steps;
+    W.b = (float)b;
+    W.scale = (float)((double)p->nx * p->ny / ((double)steps * (double)n_chains));   // AccumulatePathContribution
+    W.s2p = 0.1f;
+    W.logp = (float)std::log((double)0.1f / (2.0 / (double)(p->nx + p->ny)));
+    W.U = c->partial; W.film = dev_film; W.counter = c->counter; W.wave_rays = c->wave_rays;
+    HIPCHK(c, hipMemsetAsync(dev_film, 0, (size_t)p->nx * p->ny * 3 * sizeof(float), st));
+    HIPCHK(c, hipMemsetAsync(c->counter, 0, 64, st));
+    HIPCHK(c, hipEventRecord(c->ev0, st));
+    if (n_local > 0 && steps > 0) {
+        DevScene Sarg = c->S;
+        void *args[] = {&Sarg, &W};
+        HIPCHK(c, hipLaunchKernel(kchain, dim3(grid), dim3(kBlock), args, lds, st));
+    }
+    HIPCHK(c, hipEventRecord(c->ev1, st));
+    std::vector<unsigned long long> wr(n_waves * 4, 0);
+    if (n_local > 0 && steps > 0)
+        HIPCHK(c, hipMemcpyAsync(wr.data(), c->wave_rays, wr.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    float ms = 0.0f;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    if (stats) {
+        memset(stats, 0, sizeof(*stats));
+        for (size_t w = 0; w < n_waves; ++w) {
+            stats->camera_rays += wr[4 * w]; stats->extension_rays += wr[4 * w + 1];
+            stats->shadow_rays += wr[4 * w + 2]; stats->samples += wr[4 * w + 3];
+        }
+        stats->pixels = (uint64_t)p->nx * p->ny;
+        stats->work_items = n_local;
+        stats->kernel_ms = ms;
+        stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    }
+    c->last_mlt_b = b;
+    return FRT_OK;
+}
+
 static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots, hipStream_t st, frt_stats *stats)
 {
     const auto t_start = std::chrono::steady_clock::now();
@@ -649,6 +950,7 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     if (!params_ok(p)) return set_err(c, FRT_E_INVALID, "bad render params");
     if (!c->have_scene) return set_err(c, FRT_E_NO_SCENE, "no scene uploaded");
     HIPCHK(c, hipSetDevice(c->device));
+    if (p->integrator == FRT_INTEGRATOR_PSSMLT) return render_mlt(c, p, dev_slots, st, stats);
     const int T = eff_tile(p);
     const int nmt = my_tiles(p);
     const uint32_t n_slots = (uint32_t)nmt * T * T;
@@ -752,6 +1054,10 @@ extern "C" int frt_render(frt_ctx *c, const frt_render_params *p, float *film_rg
     std::vector<float> host((size_t)ns * 3);
     std::vector<int32_t> map((size_t)ns);
     HIPCHK(c, hipMemcpy(host.data(), c->slots_out, host.size() * sizeof(float), hipMemcpyDeviceToHost));
+    if (p->integrator == FRT_INTEGRATOR_PSSMLT) {   // splat film of this shard: accumulate
+        for (size_t i = 0; i < host.size(); ++i) film_rgb[i] += host[i];
+        return FRT_OK;
+    }
     frt_shard_slots(p, map.data());
     for (int64_t s = 0; s < ns; ++s) {
         const int32_t px = map[s];

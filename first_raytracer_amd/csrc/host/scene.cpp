@@ -394,8 +394,8 @@ struct frt_host_scene {
     int32_t root = 0;
     int32_t world_kind = FRT_WORLD_BVH;
     std::vector<int32_t> list, lights;
-    double cam[6][3] = {};
-    double lens_radius = 0;
+    double cam[7][3] = {};   // origin, llc, horizontal, vertical, u, v, w
+    double lens_radius = 0, half_height = 0;
     double env[3] = {0, 0, 0};
     int bvh_depth = 0;
     double load_ms = 0, build_ms = 0;
@@ -428,8 +428,9 @@ struct frt_host_scene {
         const V3 llc = ((lookfrom - (hw * focus) * u) - (hh * focus) * v) - focus * w;
         const V3 h = (2 * hw * focus) * u;
         const V3 vv = (2 * hh * focus) * v;
-        const V3 all[6] = {lookfrom, llc, h, vv, u, v};
-        for (int i = 0; i < 6; ++i) { cam[i][0] = all[i].x; cam[i][1] = all[i].y; cam[i][2] = all[i].z; }
+        const V3 all[7] = {lookfrom, llc, h, vv, u, v, w};
+        for (int i = 0; i < 7; ++i) { cam[i][0] = all[i].x; cam[i][1] = all[i].y; cam[i][2] = all[i].z; }
+        half_height = hh;
     }
 };
 
@@ -707,9 +708,11 @@ extern "C" int frt_scene_view_get(const frt_host_scene *s, frt_scene_view *v)
         v->cam_vertical[k] = s->cam[3][k];
         v->cam_u[k] = s->cam[4][k];
         v->cam_v[k] = s->cam[5][k];
+        v->cam_w[k] = s->cam[6][k];
         v->env_color[k] = s->env[k];
     }
     v->cam_lens_radius = s->lens_radius;
+    v->cam_half_height = s->half_height;
     return FRT_OK;
 }
 

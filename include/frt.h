@@ -41,7 +41,7 @@ enum {
 
 enum { FRT_WORLD_BVH = 0, FRT_WORLD_LIST = 1 };          /* parallel_bvh_node | hitable_list */
 enum { FRT_MAT_LAMBERTIAN = 0, FRT_MAT_DIFFUSE_LIGHT = 1 }; /* material.h:50-73, 179-192 */
-enum { FRT_INTEGRATOR_PATH = 0 };                         /* path.h:8-18 */
+enum { FRT_INTEGRATOR_PATH = 0, FRT_INTEGRATOR_PSSMLT = 1 };  /* path.h:8-18, pssmlt.h:29-76 */
 enum { FRT_FLAG_NO_LDS_SCENE = 1 };   /* render_params.flags: keep small scenes in HBM/L2 (A/B timing) */
 
 /* primitive reference: triangle t -> t ; sphere k -> FRT_PRIM_SPHERE | k */
@@ -87,6 +87,10 @@ typedef struct frt_scene_view {
     double cam_lens_radius;
     /* environment_map with a constant texture (material.h:206-232) */
     double env_color[3];
+    /* camera w axis and half_height (camera.h:18-26): PSS-MLT's screen mapping
+     * (pssmlt.cpp:134-138) needs them; half_height = 256 / camera::dist */
+    double cam_w[3];
+    double cam_half_height;
 } frt_scene_view;
 
 typedef struct frt_render_params {
@@ -94,12 +98,17 @@ typedef struct frt_render_params {
     int32_t spp;             /* samples per pixel (viewer ns)                              */
     uint32_t seed;           /* frame seed of the counter RNG (DESIGN.md "RNG stream spec") */
     int32_t max_depth;       /* scatter while depth <= max_depth; reference: 33 (path.cpp:36) */
-    int32_t integrator;      /* FRT_INTEGRATOR_PATH                                        */
+    int32_t integrator;      /* FRT_INTEGRATOR_PATH or FRT_INTEGRATOR_PSSMLT                */
     int32_t tile_size;       /* square tiles, multiple of 8; 0 = 32                        */
     int32_t shard_index;     /* this call renders tiles t with t % shard_count == index    */
     int32_t shard_count;     /* 1 = whole frame                                            */
     int32_t samples_per_item;/* work granule in samples; 0 = automatic                     */
     int32_t flags;           /* FRT_FLAG_* bits, 0 = defaults                              */
+    /* PSS-MLT only: spp = mutations per pixel (total = spp*nx*ny, the reference's
+     * ns), split over mlt_chains chains (chain c runs in shard c % shard_count);
+     * mlt_bootstrap = paths for the normaliser b (pssmlt.h:12 N_Init = 10000). */
+    int32_t mlt_chains;
+    int32_t mlt_bootstrap;
 } frt_render_params;
 
 typedef struct frt_stats {
@@ -132,12 +141,17 @@ int frt_shard_slots(const frt_render_params *p, int32_t *slot_pixel);
 
 /* Render this shard.  `film_rgb` is the caller's full film (nx*ny*3 floats,
  * index (y*nx+x)*3, y = 0 bottom row, as viewer::fout_image); only this
- * shard's pixels are written, with the mean radiance (viewer.cpp:111). */
+ * shard's pixels are written, with the mean radiance (viewer.cpp:111).
+ * PSS-MLT: every chain splats anywhere, so the shard's splat film is ADDED to
+ * film_rgb (zero it first; summing all shards gives the image,
+ * AccumulatePathContribution pssmlt.cpp:19-38). */
 int frt_render(frt_ctx *ctx, const frt_render_params *p, float *film_rgb, frt_stats *st);
 
 /* Device variant: writes the shard's slots (frt_shard_slot_count * 3 floats,
  * slot order) into device memory `slots_rgb` on `hip_stream` (NULL = the
- * context's stream) and returns after the work has completed. */
+ * context's stream) and returns after the work has completed.  PSS-MLT: the
+ * slots are the whole film (nx*ny, natural order) holding this shard's splats;
+ * shards are combined with a sum (RCCL reduce / all-reduce). */
 int frt_render_device(frt_ctx *ctx, const frt_render_params *p, float *slots_rgb, void *hip_stream,
                       frt_stats *st);
 
@@ -168,6 +182,9 @@ int frt_write_pfm(const char *path, int nx, int ny, const float *rgb);
  *      render path: frt_render / frt_render_device never use it. ---- */
 int frt_selftest_path_host(const frt_scene_view *scene, const frt_render_params *p, const int32_t *pixels,
                            int npix, float *out_rgb, frt_stats *st);
+/* Same for PSS-MLT: n bootstrap-stream eye paths (frt_mlt.hpp) on the host;
+ * out6 per path = film x, film y, r, g, b, scalar contribution. */
+int frt_selftest_mlt_paths_host(const frt_scene_view *scene, int nx, int ny, uint32_t seed, int n, float *out6);
 
 #ifdef __cplusplus
 }

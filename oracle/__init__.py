@@ -73,6 +73,13 @@ def lib():
         L.ora_kat_pick.argtypes = [ctypes.c_double, ctypes.c_int]
         L.ora_kat_sort.argtypes = [dp, ctypes.c_int, ctypes.c_void_p]
         L.ora_kat_list_hit.argtypes = [ctypes.c_int, ctypes.c_int, dp, dp, dp, dp]
+        L.ora_mlt_bootstrap.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_int]
+        L.ora_mlt_bootstrap.restype = ctypes.c_double
+        L.ora_mlt_render.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_longlong, ctypes.c_int, ctypes.c_void_p,
+                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(Counters)]
+        L.ora_mlt_eye_path.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, dp, dp]
+        L.ora_mlt_eye_path.restype = None
         L.ora_write_pfm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, dp]
         _lib = L
     return _lib
@@ -142,6 +149,21 @@ class OracleScene:
         if rc != 0:
             raise RuntimeError(f"ora_render failed: {rc}")
         return out, cnt
+
+    def mlt_render(self, nx, ny, n_chains, steps, seed=0, n_init=10000, nthreads=None):
+        """PSS-MLT film (pssmlt.cpp:301-365), mean-radiance scale; returns (film, b, counters)."""
+        film = np.zeros((ny, nx, 3))
+        b = ctypes.c_double()
+        cnt = Counters()
+        nthreads = nthreads or min(16, os.cpu_count() or 1)
+        rc = lib().ora_mlt_render(self.ptr, nx, ny, seed, n_init, n_chains, steps, nthreads, film.ctypes.data,
+                                  ctypes.byref(b), ctypes.byref(cnt))
+        if rc != 0:
+            raise RuntimeError(f"ora_mlt_render failed: {rc}")
+        return film, b.value, cnt
+
+    def mlt_bootstrap(self, nx, ny, seed=0, n_init=10000):
+        return lib().ora_mlt_bootstrap(self.ptr, nx, ny, seed, n_init)
 
     def world_hit(self, o, d, tmin, tmax):
         oa, op = darr(o); da, dptr = darr(d)

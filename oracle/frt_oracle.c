@@ -219,7 +219,7 @@ static inline void random_in_unit_disk(double s0, double s1, double *ox, double 
 /* ------------------------------------------------------------------------ */
 /* camera (camera.h:10-35)                                                  */
 /* ------------------------------------------------------------------------ */
-typedef struct { v3 origin, llc, horizontal, vertical, u, v, w; double lens_radius; } camera;
+typedef struct { v3 origin, llc, horizontal, vertical, u, v, w; double lens_radius, half_height; } camera;
 static camera camera_mk(v3 lookfrom, v3 lookat, v3 vup, double vfov, double aspect, double aperture, double focus_dist)
 {
     camera c;
@@ -227,6 +227,7 @@ static camera camera_mk(v3 lookfrom, v3 lookat, v3 vup, double vfov, double aspe
     double theta = vfov * (double)M_PI / 180.0;
     double half_height = tan(theta / 2);
     double half_width = aspect * half_height;
+    c.half_height = half_height;
     c.origin = lookfrom;
     c.w = unit(vsub(lookfrom, lookat));
     c.u = unit(cross(vup, c.w));
@@ -626,6 +627,232 @@ int ora_world_hit(const ora_scene *s, const double *o, const double *d, double t
     int ok = world_hit(s, &r, tmin, tmax, &h, cnt ? cnt : &local);
     if (ok) { *t_out = h.t; *prim_out = h.obj; } else { *t_out = 0; *prim_out = -1; }
     return ok;
+}
+
+
+/* ------------------------------------------------------------------------ */
+/* PSS-MLT (pssmlt.cpp:6-365, pssmlt.h:9-18), Kelemen et al.; chains and the */
+/* bootstrap draw from the counter RNG (DESIGN.md "PSS-MLT streams").        */
+/* ------------------------------------------------------------------------ */
+#define MLT_MAX_PATH 10                       /* MaxPathLength */
+#define MLT_DIMS (4 + (MLT_MAX_PATH + 1) * 8) /* prnds a path can read: 92 */
+static const double MLT_LARGE_STEP_PROB = (double)0.3f;
+
+typedef struct { double x, y; v3 c; double sc; } mlt_contrib;   /* PathContribution */
+
+typedef struct { const double *prnds; int off; int depth; hit_record prev; double prev_pdf; ora_counters *cnt; } mlt_state;
+
+/* pssmlt::Li (pssmlt.cpp:147-277) */
+static v3 mlt_Li(const ora_scene *s, const ray *r, mlt_state *st)
+{
+    hit_record hrec;
+    if (st->depth == 0) st->cnt->camera_rays++; else if (st->depth <= MLT_MAX_PATH) st->cnt->extension_rays++;
+    if (st->depth <= MLT_MAX_PATH && world_hit(s, r, EPSILON, FLT_MAX, &hrec, st->cnt)) {
+        v3 Le = mat_emitted(s, hrec.mat, r->d, hrec.normal);
+        st->off += 3;                                          /* scatter rnd (unused by lambertian) */
+        if ((Le.e[0] != 0.0) || (Le.e[1] != 0.0) || (Le.e[2] != 0.0)) {
+            if (st->depth == 0 || s->mats[st->prev.mat].type == MAT_PHONG || s->mats[st->prev.mat].type == MAT_DIELECTRIC)
+                return Le;
+            const double cos_wo = dot(hrec.normal, vneg(unit(r->d)));
+            double distance_squared = hrec.t * hrec.t;
+            if (distance_squared <= EPSILON) distance_squared = EPSILON;
+            const double light_pdf = prim_pdf_direct(s, hrec.obj, &hrec, r->d) * distance_squared / fabs(cos_wo);
+            const double weight = miWeight(st->prev_pdf, light_pdf);
+            return smul(weight, Le);
+        }
+        const material *m = &s->mats[hrec.mat];
+        if (m->type == MAT_LAMBERT) {
+            const double rnd0 = st->prnds[st->off + 0], rnd1 = st->prnds[st->off + 1], rnd2 = st->prnds[st->off + 2];
+            st->off += 3;
+            const int index = pick_sample(rnd0, s->nlights);
+            if (index >= 0) {
+                hit_record lrec;
+                v3 offset_origin = vadd(hrec.p, smul(EPSILON, hrec.normal));
+                v3 to_light = prim_sample_direct(s, s->lights[index], &lrec, offset_origin, rnd1, rnd2);
+                const double dist_to_light = vlen(to_light);
+                ray shadow; shadow.o = offset_origin; shadow.d = to_light;
+                st->cnt->shadow_rays++;
+                if (!world_hit(s, &shadow, EPSILON, 1 - SHADOW_EPSILON, &lrec, st->cnt)) {
+                    to_light = make_unit(to_light);
+                    shadow.d = to_light;
+                    v3 surface_bsdf = sdiv(m->albedo, M_PI);
+                    const double cos_wi = dot(hrec.normal, unit(to_light));
+                    const double cos_wo = dot(lrec.normal, vneg(unit(to_light)));
+                    if (cos_wo != 0) {
+                        double distance_squared = dist_to_light * dist_to_light;
+                        surface_bsdf = vscale_inplace(surface_bsdf, cos_wi);
+                        const double light_pdf = prim_pdf_direct(s, s->lights[index], &hrec, to_light)
+                                                 * distance_squared / fabs(cos_wo);
+                        const double surface_bsdf_pdf = cosine_pdf_value(hrec.normal, to_light);
+                        const double weight = miWeight(light_pdf, surface_bsdf_pdf);
+                        v3 em = mat_emitted(s, lrec.mat, shadow.d, lrec.normal);
+                        Le = vadd(Le, sdiv(smul(weight, vmul(em, surface_bsdf)), light_pdf));
+                    }
+                }
+            }
+            /* diffuse bounce: hrec.p is moved off the surface first (pssmlt.cpp:253) */
+            hrec.p = vadd(hrec.p, smul(EPSILON, hrec.normal));
+            const double r0 = st->prnds[st->off + 0], r1 = st->prnds[st->off + 1];
+            st->off += 2;
+            onb uvw = onb_from_w(hrec.normal);
+            ray wo; wo.o = hrec.p;
+            wo.d = onb_from_local(&uvw, hemisphere_to_cosine_direction(r0, r1));
+            const double surface_bsdf_pdf = cosine_pdf_value(hrec.normal, wo.d);
+            const v3 surface_bsdf = sdiv(m->albedo, M_PI);
+            if (surface_bsdf_pdf == 0) return mk(0, 0, 0);
+            const double cos_wo = fabs(dot(hrec.normal, unit(wo.d)));
+            st->depth += 1;
+            st->prev_pdf = surface_bsdf_pdf;
+            st->prev = hrec;
+            v3 li = mlt_Li(s, &wo, st);
+            return vadd(Le, sdiv(smul(cos_wo, vmul(surface_bsdf, li)), surface_bsdf_pdf));
+        }
+        return Le;
+    }
+    return s->env;
+}
+
+/* GenerateEyePath (pssmlt.cpp:105-144) with PixelWidth/Height and
+ * camera::dist = PixelHeight/(2 half_height) generalised to the film size. */
+static mlt_contrib mlt_eye_path(const ora_scene *s, const double *prnds, int nx, int ny, ora_counters *cnt)
+{
+    const camera *cam = &s->cam;
+    ray r = camera_get_ray(cam, prnds[0], prnds[1], prnds[2], prnds[3]);
+    const v3 dir = unit(r.d);
+    mlt_state st; memset(&st, 0, sizeof st);
+    st.prnds = prnds; st.off = 4; st.depth = 0; st.prev_pdf = 0.0; st.cnt = cnt;
+    mlt_contrib pc;
+    pc.c = mlt_Li(s, &r, &st);
+    pc.sc = std_max(std_max(pc.c.e[0], pc.c.e[1]), pc.c.e[2]);
+    const double dist = (double)ny / (2 * cam->half_height);
+    const v3 center = vadd(cam->origin, smul(dist, cam->w));
+    const v3 pos = vsub(vadd(cam->origin, smul(dist / dot(dir, cam->w), dir)), center);
+    pc.x = -dot(cam->u, pos) + (nx * 0.5);
+    pc.y = -dot(cam->v, pos) + (ny * 0.5);
+    return pc;
+}
+
+/* perturb (pssmlt.cpp:6-17) */
+static inline double mlt_perturb(double value, double s1, double s2, double r)
+{
+    double result;
+    if (r < 0.5) {
+        r = r * 2.0;
+        result = value + s2 * exp(-log(s2 / s1) * r); if (result > 1.0) result -= 1.0;
+    } else {
+        r = (r - 0.5) * 2.0;
+        result = value - s2 * exp(-log(s2 / s1) * r); if (result < 0.0) result += 1.0;
+    }
+    return result;
+}
+
+typedef struct {
+    const ora_scene *s; int nx, ny; uint32_t seed; double b, scale;
+    int c0, c1; long long steps;
+    double *film; ora_counters cnt; pthread_mutex_t *mu;
+} mlt_job;
+
+static void mlt_splat(double *film, int nx, int ny, const mlt_contrib *pc, double w, double scale)
+{
+    if (pc->sc == 0) return;                                   /* AccumulatePathContribution */
+    const int ix = (int)pc->x, iy = (int)pc->y;
+    if (ix < 0 || ix >= nx || iy < 0 || iy >= ny) return;
+    const v3 c = smul(w, pc->c);
+    for (int k = 0; k < 3; ++k) film[((size_t)ix + (size_t)iy * nx) * 3 + k] += scale * c.e[k];
+}
+
+static void *mlt_worker(void *arg)
+{
+    mlt_job *j = (mlt_job *)arg;
+    double cur[MLT_DIMS], prop[MLT_DIMS];
+    const double s1p = 2.0 / (double)(j->nx + j->ny), s2p = (double)0.1f;
+    memset(&j->cnt, 0, sizeof j->cnt);
+    for (int c = j->c0; c < j->c1; ++c) {
+        rng_key k0 = rng_make(j->seed ^ 0x3C6EF372U, (uint32_t)c, 0u);
+        for (int d = 0; d < MLT_DIMS; ++d) cur[d] = rng_u(k0, (uint32_t)(2 + d));
+        mlt_contrib C = mlt_eye_path(j->s, cur, j->nx, j->ny, &j->cnt);
+        for (long long t = 0; t < j->steps; ++t) {
+            rng_key k = rng_make(j->seed ^ 0x3C6EF372U, (uint32_t)c, (uint32_t)(t + 1));
+            double large;
+            if (rng_u(k, 0) < MLT_LARGE_STEP_PROB) {
+                for (int d = 0; d < MLT_DIMS; ++d) prop[d] = rng_u(k, (uint32_t)(2 + d));
+                large = 1.0;
+            } else {
+                prop[0] = mlt_perturb(cur[0], s1p, s2p, rng_u(k, 2));
+                prop[1] = mlt_perturb(cur[1], s1p, s2p, rng_u(k, 3));
+                for (int d = 2; d < MLT_DIMS; ++d) prop[d] = mlt_perturb(cur[d], 1.0 / 1024.0, 1.0 / 64.0, rng_u(k, (uint32_t)(2 + d)));
+                large = 0.0;
+            }
+            mlt_contrib P = mlt_eye_path(j->s, prop, j->nx, j->ny, &j->cnt);
+            j->cnt.samples++;
+            double a = 1.0;
+            if (C.sc > 0.0) { a = P.sc / C.sc; a = a < 1.0 ? a : 1.0; a = a > 0.0 ? a : 0.0; }
+            if (P.sc > 0.0) mlt_splat(j->film, j->nx, j->ny, &P, (a + large) / (P.sc / j->b + MLT_LARGE_STEP_PROB), j->scale);
+            if (C.sc > 0.0) mlt_splat(j->film, j->nx, j->ny, &C, (1.0 - a) / (C.sc / j->b + MLT_LARGE_STEP_PROB), j->scale);
+            if (rng_u(k, 1) <= a) { memcpy(cur, prop, sizeof cur); C = P; }
+        }
+    }
+    return NULL;
+}
+
+/* bootstrap normaliser b (pssmlt.cpp:303-312): mean scalar contribution of
+ * n_init independent paths */
+double ora_mlt_bootstrap(const ora_scene *s, int nx, int ny, uint32_t seed, int n_init)
+{
+    double prnds[MLT_DIMS];
+    ora_counters cnt; memset(&cnt, 0, sizeof cnt);
+    double b = 0.0;
+    for (int i = 0; i < n_init; ++i) {
+        rng_key k = rng_make(seed ^ 0xB5297A4DU, (uint32_t)i, 0u);
+        for (int d = 0; d < MLT_DIMS; ++d) prnds[d] = rng_u(k, (uint32_t)d);
+        b += mlt_eye_path(s, prnds, nx, ny, &cnt).sc;
+    }
+    return b / n_init;
+}
+
+/* pssmlt::Render (pssmlt.cpp:301-365): n_chains chains of `steps` mutations
+ * each; film (nx*ny*3, zeroed by the caller) receives the splats scaled by
+ * nx*ny/(n_chains*steps) as AccumulatePathContribution does with ns. */
+int ora_mlt_render(const ora_scene *s, int nx, int ny, uint32_t seed, int n_init, int n_chains, long long steps,
+                   int nthreads, double *film, double *b_out, ora_counters *cnt)
+{
+    if (!s || nx <= 0 || ny <= 0 || n_chains <= 0 || steps <= 0 || n_init <= 0) return -1;
+    const double b = ora_mlt_bootstrap(s, nx, ny, seed, n_init);
+    if (b_out) *b_out = b;
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > n_chains) nthreads = n_chains;
+    mlt_job *jobs = (mlt_job *)calloc((size_t)nthreads, sizeof(mlt_job));
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    double **films = (double **)calloc((size_t)nthreads, sizeof(double *));
+    const double scale = (double)nx * ny / ((double)n_chains * (double)steps);
+    for (int t = 0; t < nthreads; ++t) {
+        films[t] = (double *)calloc((size_t)nx * ny * 3, sizeof(double));
+        jobs[t].s = s; jobs[t].nx = nx; jobs[t].ny = ny; jobs[t].seed = seed; jobs[t].b = b; jobs[t].scale = scale;
+        jobs[t].c0 = (int)((long long)n_chains * t / nthreads); jobs[t].c1 = (int)((long long)n_chains * (t + 1) / nthreads);
+        jobs[t].steps = steps; jobs[t].film = films[t];
+        pthread_create(&th[t], NULL, mlt_worker, &jobs[t]);
+    }
+    ora_counters tot; memset(&tot, 0, sizeof tot);
+    for (int t = 0; t < nthreads; ++t) {
+        pthread_join(th[t], NULL);
+        for (size_t i = 0; i < (size_t)nx * ny * 3; ++i) film[i] += films[t][i];
+        free(films[t]);
+        tot.node_visits += jobs[t].cnt.node_visits; tot.tri_tests += jobs[t].cnt.tri_tests;
+        tot.sphere_tests += jobs[t].cnt.sphere_tests; tot.camera_rays += jobs[t].cnt.camera_rays;
+        tot.extension_rays += jobs[t].cnt.extension_rays; tot.shadow_rays += jobs[t].cnt.shadow_rays;
+        tot.samples += jobs[t].cnt.samples; tot.box_passes += jobs[t].cnt.box_passes;
+    }
+    if (cnt) *cnt = tot;
+    free(jobs); free(th); free(films);
+    return 0;
+}
+
+/* one PSS-MLT eye path for given primary samples (92 doubles): out x, y, r, g, b, sc */
+void ora_mlt_eye_path(const ora_scene *s, int nx, int ny, const double *prnds, double *out6)
+{
+    ora_counters cnt; memset(&cnt, 0, sizeof cnt);
+    mlt_contrib pc = mlt_eye_path(s, prnds, nx, ny, &cnt);
+    out6[0] = pc.x; out6[1] = pc.y; vstore(out6 + 2, pc.c); out6[5] = pc.sc;
 }
 
 /* ------------------------------------------------------------------------ */

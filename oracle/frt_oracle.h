@@ -72,6 +72,13 @@ int  ora_render(const ora_scene *s, int nx, int ny, int spp, uint32_t seed,
                 const int32_t *pixels, int npix, int nthreads,
                 double *out_rgb, ora_counters *cnt);
 
+/* PSS-MLT (pssmlt.cpp): bootstrap b, full render (splat film, caller-zeroed),
+ * and a single eye path for given primary samples (92 doubles -> x, y, rgb, sc). */
+double ora_mlt_bootstrap(const ora_scene *s, int nx, int ny, uint32_t seed, int n_init);
+int  ora_mlt_render(const ora_scene *s, int nx, int ny, uint32_t seed, int n_init, int n_chains, long long steps,
+                    int nthreads, double *film, double *b_out, ora_counters *cnt);
+void ora_mlt_eye_path(const ora_scene *s, int nx, int ny, const double *prnds, double *out6);
+
 /* Single query of the world (closest or any hit) with reference counters. */
 int  ora_world_hit(const ora_scene *s, const double *o, const double *d, double tmin, double tmax,
                    double *t_out, int32_t *prim_out, ora_counters *cnt);

@@ -43,3 +43,24 @@ def test_tessellated(cornell_obj, tmp_path):
     frt.write_tessellated_obj(cornell_obj, 6, dst)
     out, st, ref, cnt = run("cornell_box_obj", dst, 32, 32, 8, seed=3)
     assert float(np.sqrt(np.mean((out.astype(np.float64) - ref) ** 2))) < 1e-4
+
+
+@pytest.mark.parametrize("kind,objfix", [("cornell_box_obj", "cornell_obj"), ("veach_mis", "veach_obj")])
+def test_pssmlt_eye_paths(kind, objfix, request):
+    """PSS-MLT eye paths (frt_mlt.hpp, pssmlt.cpp:105-277) vs the oracle on the
+    bootstrap primary-sample stream: film position and contribution."""
+    obj = request.getfixturevalue(objfix)
+    nx, ny, seed, n = 96, 64, 3, 400
+    hs = frt.HostScene(kind, obj, nx / ny)
+    got = frt.selftest_mlt_paths_host(hs, nx, ny, seed, n)
+    osc = oracle.OracleScene(kind, obj, nx / ny)
+    ref = np.zeros((n, 6))
+    for i in range(n):
+        pr = oracle.darr([oracle.rng_uniform(seed ^ 0xB5297A4D, i, 0, d) for d in range(92)])
+        out = oracle.darr(np.zeros(6))
+        oracle.lib().ora_mlt_eye_path(osc.ptr, nx, ny, pr[1], out[1])
+        ref[i] = out[0]
+    assert np.abs(got[:, :2] - ref[:, :2]).max() < 1e-3                      # film position (pixels)
+    rel = np.abs(got[:, 2:] - ref[:, 2:]).max(axis=1) / (np.abs(ref[:, 2:]).max(axis=1) + 1e-6)
+    assert (rel > 1e-3).sum() <= 1
+    assert got[:, 5].mean() == pytest.approx(osc.mlt_bootstrap(nx, ny, seed, n), rel=1e-5)

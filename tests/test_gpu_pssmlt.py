@@ -1,0 +1,67 @@
+"""PSS-MLT on the GPU (one lane per Markov chain) against the oracle's
+restatement of pssmlt.cpp on the same chain streams.  Short chains are
+path-exact (an accept decision flips only if u lands within fp32 rounding of
+the acceptance ratio), so the splat films agree to fp32 accumulation noise;
+long runs are checked statistically against the path tracer."""
+import numpy as np
+import pytest
+
+import first_raytracer_amd as frt
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = frt.Context(0)
+    yield c
+    c.close()
+
+
+def rmse(a, b):
+    return float(np.sqrt(np.mean((np.asarray(a, np.float64) - np.asarray(b, np.float64)) ** 2)))
+
+
+@pytest.mark.parametrize("kind,objfix", [("cornell_box_obj", "cornell_obj"), ("veach_mis", "veach_obj")])
+def test_short_chains_match_oracle(ctx, kind, objfix, request):
+    obj = request.getfixturevalue(objfix)
+    nx, ny, mpp, chains = 64, 48, 4, 3072          # 4 mutations/pixel -> 4 steps per chain
+    hs = frt.HostScene(kind, obj, nx / ny)
+    ctx.upload(hs)
+    film = np.zeros((ny, nx, 3), np.float32)
+    film, st = ctx.render(frt.RenderParams.pssmlt(nx, ny, mpp, chains, seed=7, bootstrap=2000), film)
+    steps = mpp * nx * ny // chains
+    ref, b, cnt = oracle.OracleScene(kind, obj, nx / ny).mlt_render(nx, ny, chains, steps, seed=7, n_init=2000)
+    e = rmse(film, ref)
+    print(kind, "mlt rmse", e, "mean", film.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0), "b", b)
+    assert st.samples == chains * steps == cnt.samples
+    assert abs(st.rays - cnt.rays) / cnt.rays < 2e-3
+    scale = max(1.0, float(np.abs(ref).max()))
+    assert e <= 1e-3 * scale
+
+
+def test_sharded_chains_sum_to_single(ctx, cornell_obj):
+    nx, ny = 32, 32
+    ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, 1.0))
+    one = np.zeros((ny, nx, 3), np.float32)
+    ctx.render(frt.RenderParams.pssmlt(nx, ny, 8, 1024, seed=2, bootstrap=1000), one)
+    two = np.zeros((ny, nx, 3), np.float32)
+    for r in range(2):
+        ctx.render(frt.RenderParams.pssmlt(nx, ny, 8, 1024, seed=2, bootstrap=1000, shard_index=r, shard_count=2), two)
+    assert np.allclose(one, two, rtol=1e-4, atol=1e-5)
+
+
+def test_converges_to_path_tracer(ctx, cornell_obj):
+    """Unbiased estimator of the same image (depth <= 10): 8x8-block means agree."""
+    nx, ny = 64, 64
+    ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, 1.0))
+    film = np.zeros((ny, nx, 3), np.float32)
+    film, st = ctx.render(frt.RenderParams.pssmlt(nx, ny, 2048, 1 << 14, seed=1), film)
+    ref, _ = ctx.render(frt.RenderParams.make(nx, ny, 2048, seed=1, max_depth=10))
+    fb = film.reshape(8, 8, 8, 8, 3).mean(axis=(1, 3))
+    rb = ref.reshape(8, 8, 8, 8, 3).mean(axis=(1, 3))
+    rel = np.abs(fb - rb) / (rb + 1e-2)
+    print("mlt vs path block rel: median", np.median(rel), "max", rel.max(), "means", film.mean((0, 1)), ref.mean((0, 1)))
+    assert np.median(rel) < 0.05
+    assert abs(film.mean() - ref.mean()) / ref.mean() < 0.03
