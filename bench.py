@@ -77,6 +77,20 @@ def cpu_baseline(kind, obj, nx, ny, spp, seed, npix, threads, film):
     }
 
 
+def cpu_baseline_mlt(kind, obj, nx, ny, seed, threads):
+    """The oracle's PSS-MLT on a bounded sample: 4096 chains x 512 mutations of
+    the same frame (2.1M mutations)."""
+    import oracle
+    sc = oracle.OracleScene(kind, obj, nx / ny)
+    chains, steps = 4096, 512
+    t0 = time.perf_counter()
+    _, _, cnt = sc.mlt_render(nx, ny, chains, steps, seed=seed, n_init=10000, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"mrays": cnt.rays / dt / 1e6, "seconds": dt, "rays": cnt.rays, "npix": 0,
+            "V": cnt.node_visits / cnt.rays, "T": (cnt.tri_tests + cnt.sphere_tests) / cnt.rays,
+            "rmse": None, "sample": f"{chains} chains x {steps} mutations"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -91,6 +105,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pfm", default="", help="write the rank-0 film here")
+    ap.add_argument("--integrator", default="path", choices=["path", "pssmlt"],
+                    help="pssmlt: C5 config, --spp = mutations per pixel")
+    ap.add_argument("--chains", type=int, default=1 << 18, help="PSS-MLT chains (all ranks)")
     args = ap.parse_args()
     nx, ny = (int(x) for x in args.res.lower().split("x"))
 
@@ -117,13 +134,28 @@ def main():
     ctx.upload(hs)
     setup_s = time.perf_counter() - t0
 
-    params = frt.RenderParams.make(nx, ny, args.spp, seed=args.seed, tile_size=args.tile,
-                                   shard_index=rank, shard_count=world)
-    from first_raytracer_amd.dist import TileGather
-    tg = TileGather(nx, ny, args.tile, world, rank, dev)
+    if args.integrator == "pssmlt":
+        # chains shard over ranks (chain c -> rank c mod N); splat films are summed
+        params = frt.RenderParams.pssmlt(nx, ny, args.spp, args.chains, seed=args.seed,
+                                         shard_index=rank, shard_count=world)
+        mlt_film = torch.zeros(nx * ny * 3, dtype=torch.float32, device=dev)
+
+        class _Film:
+            film = mlt_film
+        tg = _Film()
+    else:
+        params = frt.RenderParams.make(nx, ny, args.spp, seed=args.seed, tile_size=args.tile,
+                                       shard_index=rank, shard_count=world)
+        from first_raytracer_amd.dist import TileGather
+        tg = TileGather(nx, ny, args.tile, world, rank, dev)
     stream = torch.cuda.current_stream(dev)
 
     def step():
+        if args.integrator == "pssmlt":
+            st = ctx.render_device(params, mlt_film.data_ptr(), stream.cuda_stream)
+            if world > 1:
+                dist.all_reduce(mlt_film)   # RCCL sum of the per-rank splat films
+            return st
         st = ctx.render_device(params, tg.my_slots.data_ptr(), stream.cuda_stream)
         tg.gather()       # RCCL all-gather of the tile slots, rank 0 scatters into its film
         return st
@@ -162,7 +194,10 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            cpu = cpu_baseline(kind, obj, nx, ny, args.spp, args.seed, args.cpu_pixels, threads, film_np)
+            if args.integrator == "pssmlt":
+                cpu = cpu_baseline_mlt(kind, obj, nx, ny, args.seed, threads)
+            else:
+                cpu = cpu_baseline(kind, obj, nx, ny, args.spp, args.seed, args.cpu_pixels, threads, film_np)
             cpu["threads"] = threads
         ts = load_traversal_stats(key)
         if cpu is not None:
@@ -191,18 +226,25 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": f"{scene_name} {nx}x{ny} {args.spp}spp path+NEE+MIS", "scene": args.scene,
+            "config": {"workload": (f"{scene_name} {nx}x{ny} {args.spp}spp path+NEE+MIS" if args.integrator == "path"
+                                    else f"{scene_name} {nx}x{ny} PSS-MLT {args.spp} mutations/pixel, "
+                                         f"{args.chains} chains"),
+                       "integrator": args.integrator, "scene": args.scene,
                        "nx": nx, "ny": ny, "spp": args.spp, "seed": args.seed, "tile": args.tile,
                        "parallelism": f"tiles-interleaved x{world} + rccl all-gather"},
             "rmse": None if cpu is None else cpu["rmse"],
+            "mutations_per_step": int(last.samples) if args.integrator == "pssmlt" else None,
             "rays_per_step": int(rays // args.steps),
             "setup_s": round(setup_s, 2),
             "image_mean": [round(float(x), 6) for x in film_np.reshape(-1, 3).mean(0)],
             "roofline": roofline,
             "cpu_baseline": None if cpu is None else {
                 "value": round(cpu["mrays"], 3), "unit": "Mrays/s", "cores": cpu["threads"], "kind": "port",
-                "sample": f"{cpu['npix']} evenly spaced pixels of the same {nx}x{ny} frame at {args.spp} spp "
-                          f"({cpu['rays']} rays, {cpu['seconds']:.1f} s); fp64 C restatement of path::Li"},
+                "sample": (f"{cpu['npix']} evenly spaced pixels of the same {nx}x{ny} frame at {args.spp} spp "
+                           f"({cpu['rays']} rays, {cpu['seconds']:.1f} s); fp64 C restatement of path::Li")
+                if args.integrator == "path" else
+                          (f"PSS-MLT {cpu['sample']} on the same {nx}x{ny} frame ({cpu['rays']} rays, "
+                           f"{cpu['seconds']:.1f} s); fp64 C restatement of pssmlt.cpp")},
         }
         if args.pfm:
             frt.write_pfm(args.pfm, film_np.reshape(ny, nx, 3))
