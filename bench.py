@@ -216,10 +216,11 @@ def main():
             pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
             if os.path.exists(pmc):
                 with open(pmc) as f:
-                    traffic = json.load(f).get(f"{key}:n{world}")
+                    traffic = json.load(f).get(f"{args.integrator}:{key}:n{world}")
             roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "kernel": "path_megakernel", "bytes_per_ray": round(b_ray, 1),
+                        "kernel": "path_megakernel" if args.integrator == "path" else "mlt_megakernel",
+                        "bytes_per_ray": round(b_ray, 1),
                         "V_node": round(V, 3), "T_tri": round(T, 3), "rays_per_launch": int(rays_per_launch),
                         "avg_launch_ms": round(avg_kernel_s * 1e3, 3)}
         line = {
@@ -231,7 +232,8 @@ def main():
                                          f"{args.chains} chains"),
                        "integrator": args.integrator, "scene": args.scene,
                        "nx": nx, "ny": ny, "spp": args.spp, "seed": args.seed, "tile": args.tile,
-                       "parallelism": f"tiles-interleaved x{world} + rccl all-gather"},
+                       "parallelism": (f"tiles-interleaved x{world} + rccl all-gather" if args.integrator == "path"
+                                       else f"chains-interleaved x{world} + rccl all-reduce")},
             "rmse": None if cpu is None else cpu["rmse"],
             "mutations_per_step": int(last.samples) if args.integrator == "pssmlt" else None,
             "rays_per_step": int(rays // args.steps),
