@@ -33,6 +33,10 @@ struct DevScene {
     int root;                // node index, or ~prim for a single-leaf world
     int n_lights, n_list, world_kind;
     int n_nodes, n_tris, n_mats;
+    // element i, part k of nodes / tris / tshade lives at [i * es + k * ps]:
+    // interleaved in HBM (es = parts, ps = 1), planar in LDS (es = 1, ps = count)
+    // so that lanes reading distinct elements hit distinct LDS bank slots
+    int node_es, node_ps, tri_es, tri_ps, sh_es, sh_ps;
     float root_lo[3], root_hi[3];
     f3 cam_o, cam_llc, cam_h, cam_v, cam_u, cam_vv, cam_w;
     float lens_r, cam_half_height;
@@ -44,6 +48,10 @@ struct Hit {
     float t, u, v;
 };
 
+FRT_HD float4 node_part(const DevScene &S, int i, int k) { return S.nodes[i * S.node_es + k * S.node_ps]; }
+FRT_HD float4 tri_part(const DevScene &S, int i, int k) { return S.tris[i * S.tri_es + k * S.tri_ps]; }
+FRT_HD float4 shade_part(const DevScene &S, int i, int k) { return S.tshade[i * S.sh_es + k * S.sh_ps]; }
+
 FRT_HD float prim_t(const DevScene &S, int ref, f3 o, f3 d, float tmin, float tmax, float &u, float &v)
 {
     if (ref & FRT_PRIM_SPHERE) {
@@ -51,7 +59,7 @@ FRT_HD float prim_t(const DevScene &S, int ref, f3 o, f3 d, float tmin, float tm
         u = v = 0.0f;
         return sphere_intersect(o, d, xyz(sp), sp.w, tmin, tmax);
     }
-    const float4 a = S.tris[3 * ref], b = S.tris[3 * ref + 1], c = S.tris[3 * ref + 2];
+    const float4 a = tri_part(S, ref, 0), b = tri_part(S, ref, 1), c = tri_part(S, ref, 2);
     return tri_intersect(o, d, xyz(a), xyz(b), xyz(c), tmin, tmax, u, v);
 }
 
@@ -75,8 +83,8 @@ FRT_HD Hit trace_bvh(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int
     int sp = 0;
     for (;;) {
         while ((unsigned)node < (unsigned)kSentinel) {   // interior node
-            const float4 n0 = S.nodes[4 * node], n1 = S.nodes[4 * node + 1];
-            const float4 n2 = S.nodes[4 * node + 2], n3 = S.nodes[4 * node + 3];
+            const float4 n0 = node_part(S, node, 0), n1 = node_part(S, node, 1);
+            const float4 n2 = node_part(S, node, 2), n3 = node_part(S, node, 3);
             const float t0 = slab_entry(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, sr, tmin, h.t);
             const float t1 = slab_entry(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, sr, tmin, h.t);
             const int c0 = f2i(n3.x), c1 = f2i(n3.y);
@@ -146,7 +154,7 @@ FRT_HD void prim_shade(const DevScene &S, int ref, f3 ro, f3 p, float u, float v
         mat = S.sphere_mat[k];
         return;
     }
-    const float4 s0 = S.tshade[2 * ref], s1 = S.tshade[2 * ref + 1];
+    const float4 s0 = shade_part(S, ref, 0), s1 = shade_part(S, ref, 1);
     mat = f2i(s1.x);
     if (f2i(s1.y)) {                                           // use_geometry_normals (triangle.h:100-101)
         n = xyz(s0);
@@ -159,7 +167,7 @@ FRT_HD void prim_shade(const DevScene &S, int ref, f3 ro, f3 p, float u, float v
 // pdf_direct_sampling with the record's (p, t, normal) and direction
 FRT_HD float prim_pdf(const DevScene &S, int ref, f3 rec_p, float rec_t, f3 rec_n, f3 to_light)
 {
-    if (!(ref & FRT_PRIM_SPHERE)) return S.tshade[2 * ref].w;     // inv_area (triangle.h:139-144)
+    if (!(ref & FRT_PRIM_SPHERE)) return shade_part(S, ref, 0).w;  // inv_area (triangle.h:139-144)
     const float4 sp = S.spheres[ref & ~FRT_PRIM_SPHERE];           // sphere.h:64-78
     const f3 o = rec_p - rec_t * to_light;
     const f3 dir = xyz(sp) - o;
@@ -191,12 +199,12 @@ FRT_HD f3 prim_sample(const DevScene &S, int ref, f3 o, float u0, float u1, f3 &
         ln = normalize(p);
         return p;
     }
-    const float4 a = S.tris[3 * ref], b = S.tris[3 * ref + 1], c = S.tris[3 * ref + 2];   // triangle.h:145-175
+    const float4 a = tri_part(S, ref, 0), b = tri_part(S, ref, 1), c = tri_part(S, ref, 2);   // triangle.h:145-175
     const float su0 = sqrtf(u0);
     const float b0 = 1.0f - su0;
     const float b1 = u1 * su0;
     const f3 lp = xyz(a) + b0 * xyz(b) + b1 * xyz(c);            // (1-b0-b1) v0 + b0 v1 + b1 v2
-    const float4 s0 = S.tshade[2 * ref], s1 = S.tshade[2 * ref + 1];
+    const float4 s0 = shade_part(S, ref, 0), s1 = shade_part(S, ref, 1);
     lmat = f2i(s1.x);
     if (f2i(s1.y)) {
         ln = xyz(s0);

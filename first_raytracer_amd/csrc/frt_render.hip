@@ -67,8 +67,9 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t m)
 // LDS_SCENE: small scenes (nodes + triangles + shading records + materials,
 // <= kLdsSceneBytes) are copied into LDS once per block and traversed there
 // (ds_read_b128 instead of L1/L2 round trips).
-template <int STACK, int WORLD, bool LDS_SCENE>
-__global__ __launch_bounds__(kBlock) void path_megakernel(const DevScene S0, const DevWork W)
+template <int STACK, int WORLD, bool LDS_SCENE, int WAVES = 1>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void path_megakernel(
+    const DevScene S0, const DevWork W)
 {
     extern __shared__ __attribute__((aligned(16))) int lds_mem[];   // [STACK][kBlock] stack, then the scene
     int *stk = lds_mem + threadIdx.x;                                 // one LDS column per lane
@@ -76,15 +77,19 @@ __global__ __launch_bounds__(kBlock) void path_megakernel(const DevScene S0, con
     if constexpr (LDS_SCENE) {
         float4 *l4 = reinterpret_cast<float4 *>(lds_mem + STACK * kBlock);
         const int nn = 4 * S0.n_nodes, nt = 3 * S0.n_tris, ns = 2 * S0.n_tris, nm = 2 * S0.n_mats;
-        for (int i = threadIdx.x; i < nn; i += kBlock) l4[i] = S0.nodes[i];
-        for (int i = threadIdx.x; i < nt; i += kBlock) l4[nn + i] = S0.tris[i];
-        for (int i = threadIdx.x; i < ns; i += kBlock) l4[nn + nt + i] = S0.tshade[i];
+        // planar copies: part k of element i at [k * count + i] (conflict-free ds_read_b128)
+        for (int i = threadIdx.x; i < nn; i += kBlock) l4[(i & 3) * S0.n_nodes + (i >> 2)] = S0.nodes[i];
+        for (int i = threadIdx.x; i < nt; i += kBlock) l4[nn + (i % 3) * S0.n_tris + i / 3] = S0.tris[i];
+        for (int i = threadIdx.x; i < ns; i += kBlock) l4[nn + nt + (i & 1) * S0.n_tris + (i >> 1)] = S0.tshade[i];
         for (int i = threadIdx.x; i < nm; i += kBlock) l4[nn + nt + ns + i] = S0.mats[i];
         __syncthreads();
         S.nodes = l4;
         S.tris = l4 + nn;
         S.tshade = l4 + nn + nt;
         S.mats = l4 + nn + nt + ns;
+        S.node_es = 1; S.node_ps = S0.n_nodes;
+        S.tri_es = 1; S.tri_ps = S0.n_tris;
+        S.sh_es = 1; S.sh_ps = S0.n_tris;
     }
     const int lane = threadIdx.x & 63;
     const int T2 = W.tile * W.tile;
@@ -96,7 +101,8 @@ __global__ __launch_bounds__(kBlock) void path_megakernel(const DevScene S0, con
     int px = 0, py = 0;
     f3 acc = mk3(0, 0, 0);
     PathState P;
-    uint32_t n_cam = 0, n_ext = 0, n_sh = 0, n_smp = 0;
+    // ray counters are wave-uniform (SGPRs): popcounts of per-iteration ballots
+    unsigned long long n_cam = 0, n_ext = 0, n_sh = 0, n_smp = 0;
 
     for (;;) {
         // ---- retire a finished item: its chunk sum goes to its own slot ----
@@ -139,28 +145,33 @@ __global__ __launch_bounds__(kBlock) void path_megakernel(const DevScene S0, con
             }
         }
         // ---- next camera sample of the item ----
-        if (!active && have_item && s_cur < s_end) {
+        const bool start = !active && have_item && s_cur < s_end;
+        if (start) {
             path_begin(P, S, px, py, W.nx, W.ny, W.seed, pix, (uint32_t)s_cur);
             ++s_cur;
             active = true;
-            ++n_cam; ++n_smp;
         }
+        const unsigned long long started = __popcll(__ballot(start));
+        n_cam += started;
+        n_smp += started;
         if (__ballot(active) == 0) {
             if (__ballot(!exhausted) == 0) break;
             continue;
         }
-        if (!active) continue;
         // ---- one ray, then shade ----
-        const Hit h = trace<WORLD, kBlock>(S, P.ro, P.rd, P.rtmax, P.shadow, stk);
-        if (path_shade(P, S, h, W.max_depth, n_ext, n_sh)) {
-            acc = acc + P.L;
-            active = false;
+        uint32_t ne = 0, ns = 0;
+        if (active) {
+            const Hit h = trace<WORLD, kBlock>(S, P.ro, P.rd, P.rtmax, P.shadow, stk);
+            if (path_shade(P, S, h, W.max_depth, ne, ns)) {
+                acc = acc + P.L;
+                active = false;
+            }
         }
+        n_ext += __popcll(__ballot(ne != 0));
+        n_sh += __popcll(__ballot(ns != 0));
     }
     // per-wave ray counters, no atomics: lane 0 writes the wave's sums
-    unsigned long long c[4] = {n_cam, n_ext, n_sh, n_smp};
-    for (int k = 0; k < 4; ++k)
-        for (int off = 32; off > 0; off >>= 1) c[k] += __shfl_xor(c[k], off);
+    const unsigned long long c[4] = {n_cam, n_ext, n_sh, n_smp};
     if (lane == 0) {
         const size_t wv = ((size_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
         for (int k = 0; k < 4; ++k) W.wave_rays[4 * wv + k] = c[k];
@@ -635,6 +646,9 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     S.n_nodes = (int)(F.nodes.size() / 4);
     S.n_tris = nt;
     S.n_mats = nm;
+    S.node_es = 4; S.node_ps = 1;
+    S.tri_es = 3; S.tri_ps = 1;
+    S.sh_es = 2; S.sh_ps = 1;
     S.world_kind = sv->world_kind;
     auto f3d = [](const double *x) { return mk3((float)x[0], (float)x[1], (float)x[2]); };
     S.cam_o = f3d(sv->cam_origin); S.cam_llc = f3d(sv->cam_lower_left);
@@ -822,11 +836,11 @@ struct Launcher {
     int stack = 0;
     bool lds_scene = false;
 };
-template <int STACK, int WORLD, bool LDS>
+template <int STACK, int WORLD, bool LDS, int WAVES = 1>
 static Launcher make_launcher(size_t scene_bytes)
 {
     Launcher L;
-    L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS>);
+    L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES>);
     L.lds = (WORLD == FRT_WORLD_BVH ? (size_t)STACK * kBlock * sizeof(int) : 0) + (LDS ? scene_bytes : 0);
     L.stack = STACK;
     L.lds_scene = LDS;
@@ -838,7 +852,8 @@ static int pick_launcher(const frt_ctx *c, int flags, Launcher &L)
     const int d = c->stack_needed;
     const size_t sb = c->scene_lds_bytes;
     const bool lds = sb <= kLdsSceneBytes && !(flags & FRT_FLAG_NO_LDS_SCENE);
-    if (d < 8) L = lds ? make_launcher<8, FRT_WORLD_BVH, true>(sb) : make_launcher<8, FRT_WORLD_BVH, false>(0);
+    if (d < 8 && lds && (flags & FRT_FLAG_WAVES5)) L = make_launcher<8, FRT_WORLD_BVH, true, 5>(sb);
+    else if (d < 8) L = lds ? make_launcher<8, FRT_WORLD_BVH, true>(sb) : make_launcher<8, FRT_WORLD_BVH, false>(0);
     else if (d < 16) L = lds ? make_launcher<16, FRT_WORLD_BVH, true>(sb) : make_launcher<16, FRT_WORLD_BVH, false>(0);
     else if (d < 32) L = lds ? make_launcher<32, FRT_WORLD_BVH, true>(sb) : make_launcher<32, FRT_WORLD_BVH, false>(0);
     else if (d < 64) L = make_launcher<64, FRT_WORLD_BVH, false>(0);

@@ -31,7 +31,7 @@ def main():
     kind, obj, name = scene_spec(args.scene, "/tmp")
     ctx = frt.Context(0)
     ctx.upload(frt.HostScene(kind, obj, nx / ny))
-    variants = {"default": 0, "no_lds": frt.FRT_FLAG_NO_LDS_SCENE}
+    variants = {"default": 0, "no_lds": frt.FRT_FLAG_NO_LDS_SCENE, "waves5": frt.FRT_FLAG_WAVES5}
     chosen = [v for v in args.variants.split(",") if v in variants]
     res = {v: [] for v in chosen}
     rays = {}
