@@ -48,6 +48,10 @@ struct Hit {
     float t, u, v;
 };
 
+// BVH leaf ref ~x: x = FRT_PRIM_SPHERE | k, or first triangle | (count - 1) << kLeafCountShift
+constexpr int kLeafCountShift = 28, kLeafIndexMask = (1 << kLeafCountShift) - 1, kLeafIndexLimit = 1 << kLeafCountShift;
+constexpr int kLeafMax = 4, kLeafDefault = 4;
+
 FRT_HD float4 node_part(const DevScene &S, int i, int k) { return S.nodes[i * S.node_es + k * S.node_ps]; }
 FRT_HD float4 tri_part(const DevScene &S, int i, int k) { return S.tris[i * S.tri_es + k * S.tri_ps]; }
 FRT_HD float4 shade_part(const DevScene &S, int i, int k) { return S.tshade[i * S.sh_es + k * S.sh_ps]; }
@@ -103,15 +107,22 @@ FRT_HD Hit trace_bvh(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int
             }
         }
         if (node == kSentinel) break;
-        // leaf: one primitive (single-prim leaves, parallel_bvh.h:129-149)
-        const int ref = ~node;
-        float u, v;
-        const float t = prim_t(S, ref, o, d, tmin, h.t, u, v);
-        if (t > 0.0f) {
-            const bool better = (t < h.t) || (h.prim >= 0 && ((ref & FRT_PRIM_SPHERE) || ref < h.prim));
-            if (better) {
-                h.prim = ref; h.t = t; h.u = u; h.v = v;
-                if (anyhit) return h;
+        // leaf: one sphere, or triangles [first, first + count) (collapse_leaves;
+        // the reference's leaves hold one prim, parallel_bvh.h:129-149)
+        const int lref = ~node;
+        const bool is_sph = (lref & FRT_PRIM_SPHERE) != 0;
+        const int first = is_sph ? lref : (lref & kLeafIndexMask);
+        const int count = is_sph ? 1 : (lref >> kLeafCountShift) + 1;
+        for (int k = 0; k < count; ++k) {
+            const int ref = first + k;
+            float u, v;
+            const float t = prim_t(S, ref, o, d, tmin, h.t, u, v);
+            if (t > 0.0f) {
+                const bool better = (t < h.t) || (h.prim >= 0 && (is_sph || ref < h.prim));
+                if (better) {
+                    h.prim = ref; h.t = t; h.u = u; h.v = v;
+                    if (anyhit) return h;
+                }
             }
         }
         node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel;

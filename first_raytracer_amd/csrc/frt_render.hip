@@ -477,6 +477,72 @@ struct FlatScene {
     int depth = 0;
 };
 
+// Triangles per leaf (FRT_LEAF_SIZE overrides, 1 = the reference's one-prim
+// leaves).  A tuning knob of this library, not part of the C-ABI.
+static int leaf_size()
+{
+    const char *e = std::getenv("FRT_LEAF_SIZE");
+    const int v = e ? std::atoi(e) : kLeafDefault;
+    return std::min(std::max(v, 1), kLeafMax);
+}
+
+// Multi-triangle leaves: every subtree of the DFS-ordered binary tree holding
+// only triangles, at most `leaf_max` of them, becomes one leaf.  Its triangles
+// are the contiguous device ids [first, first + count) (device id = DFS rank).
+// The closest hit over triangles is the lexicographic minimum of (t, DFS rank)
+// whatever the visit order (the tie rule in trace_bvh), and the parent's box
+// already bounds the subtree, so hits are unchanged -- only node visits drop.
+static void collapse_leaves(FlatScene &F, int leaf_max)
+{
+    const int nn = (int)(F.nodes.size() / 4);
+    if (leaf_max <= 1 || nn == 0) return;
+    auto child = [&](int i, int side) { return f2i(side ? F.nodes[4 * i + 3].y : F.nodes[4 * i + 3].x); };
+    // subtree triangle count / first device id / holds a sphere; children follow parents in pre-order
+    std::vector<int> cnt(nn, 0), first(nn, INT32_MAX);
+    std::vector<char> sph(nn, 0);
+    for (int i = nn - 1; i >= 0; --i)
+        for (int side = 0; side < 2; ++side) {
+            const int c = child(i, side);
+            if (c >= 0) {
+                cnt[i] += cnt[c]; first[i] = std::min(first[i], first[c]); sph[i] |= sph[c];
+            } else if (~c & FRT_PRIM_SPHERE) {
+                sph[i] = 1;
+            } else {
+                cnt[i] += 1; first[i] = std::min(first[i], ~c);
+            }
+        }
+    std::vector<float4> out;
+    out.reserve(F.nodes.size());
+    int depth = 0;
+    // pre-order rebuild; (old node, slot in `out` of the parent's child ref or -1, level)
+    struct Item { int old, parent_slot, side, lvl; };
+    std::vector<Item> st{{0, -1, 0, 1}};
+    while (!st.empty()) {
+        const Item it = st.back();
+        st.pop_back();
+        const int me = (int)(out.size() / 4);
+        if (it.parent_slot >= 0) {
+            float4 &r = out[it.parent_slot];
+            (it.side ? r.y : r.x) = i2f(me);
+        }
+        depth = std::max(depth, it.lvl);
+        for (int k = 0; k < 4; ++k) out.push_back(F.nodes[4 * it.old + k]);
+        const int slot = 4 * me + 3;
+        for (int side = 1; side >= 0; --side) {
+            const int c = child(it.old, side);
+            if (c < 0) continue;                                  // leaf ref kept as is
+            if (!sph[c] && cnt[c] <= leaf_max) {
+                float4 &r = out[slot];
+                (side ? r.y : r.x) = i2f(~(first[c] | ((cnt[c] - 1) << kLeafCountShift)));
+            } else {
+                st.push_back({c, slot, side, it.lvl + 1});
+            }
+        }
+    }
+    F.nodes.swap(out);
+    F.depth = depth;
+}
+
 static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &err)
 {
     auto fail = [&](int code, const std::string &m) { err = m; return code; };
@@ -576,6 +642,8 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
             F.nodes[4 * i + 2] = make_float4(cb[1][2], cb[1][3], cb[1][4], cb[1][5]);
             F.nodes[4 * i + 3] = make_float4(i2f(cref[0]), i2f(cref[1]), 0.0f, 0.0f);
         }
+        if (nt >= kLeafIndexLimit) return fail(FRT_E_INVALID, "scene view: too many triangles");
+        collapse_leaves(F, leaf_size());
         for (int i = 0; i < nt; ++i)   // triangles outside the tree: trailing ids, never intersected
             if (tri_dev[i] < 0) { tri_dev[i] = (int)tri_order.size(); tri_order.push_back(i); }
     } else if (sv->world_kind == FRT_WORLD_LIST) {

@@ -64,3 +64,29 @@ def test_pssmlt_eye_paths(kind, objfix, request):
     rel = np.abs(got[:, 2:] - ref[:, 2:]).max(axis=1) / (np.abs(ref[:, 2:]).max(axis=1) + 1e-6)
     assert (rel > 1e-3).sum() <= 1
     assert got[:, 5].mean() == pytest.approx(osc.mlt_bootstrap(nx, ny, seed, n), rel=1e-5)
+
+
+@pytest.mark.parametrize("kind,objfix,tess", [("cornell_box_obj", "cornell_obj", 0),
+                                              ("cornell_box_obj", "cornell_obj", 5),
+                                              ("veach_mis", "veach_obj", 0)])
+def test_leaf_size_invariance(kind, objfix, tess, request, tmp_path, monkeypatch):
+    """Multi-triangle leaves (collapse_leaves) change node visits, never hits:
+    the closest hit is the (t, DFS rank) minimum in any visit order, so leaf
+    sizes 1 (the reference's one-prim leaves), 2 and 4 give bit-identical
+    samples and identical ray counts."""
+    obj = request.getfixturevalue(objfix)
+    if tess:
+        obj2 = str(tmp_path / "t.obj")
+        frt.write_tessellated_obj(obj, tess, obj2)
+        obj = obj2
+    nx, ny = 40, 30
+    hs = frt.HostScene(kind, obj, nx / ny)
+    pix = np.arange(nx * ny, dtype=np.int32)
+    res = {}
+    for leaf in (1, 2, 4):
+        monkeypatch.setenv("FRT_LEAF_SIZE", str(leaf))
+        out, st = frt.selftest_path_host(hs, frt.RenderParams.make(nx, ny, 8, seed=11), pix)
+        res[leaf] = (out, st.rays)
+    for leaf in (2, 4):
+        assert np.array_equal(res[leaf][0], res[1][0])
+        assert res[leaf][1] == res[1][1]

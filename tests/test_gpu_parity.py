@@ -88,6 +88,24 @@ def test_tessellated_cornell(ctx, cornell_obj, tmp_path):
     assert rmse(film, ref) <= RMSE_TOL
 
 
+@pytest.mark.parametrize("flags", [0, frt.FRT_FLAG_NO_LDS_SCENE])
+def test_leaf_size_invariance(ctx, cornell_obj, tmp_path, monkeypatch, flags):
+    """Multi-triangle leaves change node visits only: bit-identical films to the
+    reference's one-prim leaves (FRT_LEAF_SIZE=1), LDS and HBM scene paths."""
+    dst = str(tmp_path / "tess.obj")
+    frt.write_tessellated_obj(cornell_obj, 10, dst)
+    nx, ny, spp = 64, 48, 8
+    hs = frt.HostScene("cornell_box_obj", dst, nx / ny)
+    films = []
+    for leaf in ("1", "4"):
+        monkeypatch.setenv("FRT_LEAF_SIZE", leaf)
+        ctx.upload(hs)
+        f, st = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=5, flags=flags))
+        films.append((f, st.rays))
+    assert np.array_equal(films[0][0], films[1][0])
+    assert films[0][1] == films[1][1]
+
+
 def test_deterministic_and_shard_invariant(ctx, cornell_obj):
     nx, ny, spp = 100, 70, 8
     ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, nx / ny))

@@ -4,6 +4,10 @@
 kernel ms and Grays/s as JSON lines.
 
   python tools/perf_ab.py [--scene cornell|cornell_1m|veach] [--spp 64] [--rounds 5]
+                          [--variants default,waves5,default/leaf1]
+
+A variant is FLAG[/leafN]: a render flag set, on a scene uploaded with
+FRT_LEAF_SIZE=N (one context per leaf size; default = the library default).
 """
 import argparse
 import json
@@ -29,16 +33,28 @@ def main():
     from bench import scene_spec
     nx, ny = (int(v) for v in args.res.split("x"))
     kind, obj, name = scene_spec(args.scene, "/tmp")
-    ctx = frt.Context(0)
-    ctx.upload(frt.HostScene(kind, obj, nx / ny))
-    variants = {"default": 0, "no_lds": frt.FRT_FLAG_NO_LDS_SCENE, "waves5": frt.FRT_FLAG_WAVES5}
-    chosen = [v for v in args.variants.split(",") if v in variants]
+    flags = {"default": 0, "no_lds": frt.FRT_FLAG_NO_LDS_SCENE, "waves5": frt.FRT_FLAG_WAVES5}
+    chosen = [v for v in args.variants.split(",") if v.split("/")[0] in flags]
+    hs = frt.HostScene(kind, obj, nx / ny)
+    ctxs = {}
+    for v in chosen:
+        leaf = v.split("/")[1][4:] if "/" in v else ""
+        if leaf not in ctxs:
+            if leaf:
+                os.environ["FRT_LEAF_SIZE"] = leaf
+            else:
+                os.environ.pop("FRT_LEAF_SIZE", None)
+            ctxs[leaf] = frt.Context(0)
+            ctxs[leaf].upload(hs)
+    os.environ.pop("FRT_LEAF_SIZE", None)
     res = {v: [] for v in chosen}
     rays = {}
-    film = None
+    films = {}
     for r in range(args.rounds + 1):
         for v in chosen:
-            film, st = ctx.render(frt.RenderParams.make(nx, ny, args.spp, seed=0, flags=variants[v]), film)
+            leaf = v.split("/")[1][4:] if "/" in v else ""
+            p = frt.RenderParams.make(nx, ny, args.spp, seed=0, flags=flags[v.split("/")[0]])
+            films[leaf], st = ctxs[leaf].render(p, films.get(leaf))
             if r > 0:
                 res[v].append(st.kernel_ms)
             rays[v] = st.rays
@@ -47,7 +63,8 @@ def main():
         print(json.dumps({"scene": args.scene, "variant": v, "spp": args.spp, "median_ms": statistics.median(ms),
                           "min_ms": min(ms), "grays_per_s": rays[v] / (statistics.median(ms) * 1e-3) / 1e9,
                           "rays": rays[v]}), flush=True)
-    ctx.close()
+    for c in ctxs.values():
+        c.close()
 
 
 if __name__ == "__main__":
