@@ -57,7 +57,7 @@ struct PrndSource {
 };
 
 struct MltPath {
-    PathState P;           // ro, rd, rtmax, shadow, beta, L, nee, nxt_o, nxt_d, depth (prev_p unused)
+    PathState P;           // ro, rd, rtmax, shadow, beta, L, nee, nxt_d, depth (prev_p unused)
     int off;               // PathRndsOffset
     float x, y;            // film position of the eye ray (GenerateEyePath)
 };
@@ -109,7 +109,7 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
     if (P.shadow) {
         if (h.prim < 0) P.L = P.L + P.nee;
         P.shadow = false;
-        P.ro = P.nxt_o; P.rd = P.nxt_d; P.rtmax = kTMaxClosest;
+        P.rd = P.nxt_d; P.rtmax = kTMaxClosest;            // P.ro is already the extension origin
         ++P.depth;
         if (P.depth <= kMltMaxPath) ++n_ext;
         return false;
@@ -152,7 +152,6 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
     const f3 f = kInvPi * xyz(m0);
     const f3 beta_next = (fabsf(cw) / pdf) * (P.beta * f);
     const f3 origin = p + kEps * n;
-    P.nxt_o = origin;                                   // hrec.p moved off the surface (pssmlt.cpp:253)
     P.nxt_d = wo;
     const int nl = S.n_lights;
     int idx = (int)(rnd0 * (float)nl);
@@ -182,7 +181,7 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
     P.beta = beta_next;
     P.prev_pdf = pdf;
     if (!P.shadow) {
-        P.ro = P.nxt_o; P.rd = P.nxt_d; P.rtmax = kTMaxClosest;
+        P.ro = origin; P.rd = wo; P.rtmax = kTMaxClosest;   // hrec.p moved off the surface (pssmlt.cpp:253)
         ++P.depth;
         if (P.depth <= kMltMaxPath) ++n_ext;
     }

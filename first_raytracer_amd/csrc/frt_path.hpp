@@ -237,7 +237,7 @@ struct PathState {
     bool shadow;          // any-hit query
     f3 beta, L;           // throughput, radiance of this sample
     f3 nee;               // NEE contribution if the shadow ray is unoccluded
-    f3 nxt_o, nxt_d;      // extension ray after the shadow ray
+    f3 nxt_d;             // extension direction after the shadow ray (its origin is the shadow ray's)
     f3 prev_p;            // previous hit point (MIS distance, path.cpp:25)
     float prev_pdf;       // bsdf pdf of the previous bounce
     int depth;
@@ -280,7 +280,7 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
     if (P.shadow) {                                     // path.cpp:50-77
         if (h.prim < 0) P.L = P.L + P.nee;
         P.shadow = false;
-        P.ro = P.nxt_o; P.rd = P.nxt_d; P.rtmax = kTMaxClosest;
+        P.rd = P.nxt_d; P.rtmax = kTMaxClosest;            // P.ro is already the extension origin
         ++P.depth; ++n_ext;
         return false;
     }
@@ -318,7 +318,7 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
     if (pdf == 0.0f) return true;
     const f3 f = kInvPi * xyz(m0);                      // lambertian::eval_bsdf (material.h:62-65)
     const f3 beta_next = (fabsf(cw) / pdf) * (P.beta * f);
-    P.nxt_o = p + kEps * n;
+    const f3 origin = p + kEps * n;
     P.nxt_d = wo;
     // next-event estimation (path.cpp:38-77)
     const int nl = S.n_lights;
@@ -328,7 +328,6 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
         const int lref = S.lights[idx];
         f3 ln;
         int lmat;
-        const f3 origin = p + kEps * n;
         const f3 tl = prim_sample(S, lref, origin, rng_u(P.key, base + 4), rng_u(P.key, base + 5), ln, lmat);
         const float dist2 = len2(tl);
         const f3 tu = rlen(tl) * tl;
@@ -351,7 +350,7 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
     P.prev_p = p;
     P.prev_pdf = pdf;
     if (!P.shadow) {
-        P.ro = P.nxt_o; P.rd = P.nxt_d; P.rtmax = kTMaxClosest;
+        P.ro = origin; P.rd = wo; P.rtmax = kTMaxClosest;
         ++P.depth; ++n_ext;
     }
     return false;

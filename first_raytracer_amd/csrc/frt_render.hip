@@ -896,7 +896,8 @@ extern "C" int frt_shard_slots(const frt_render_params *p, int32_t *slot_pixel)
     return FRT_OK;
 }
 
-constexpr size_t kLdsSceneBytes = 24 * 1024;   // 4 blocks/CU x (stack + scene) must fit 160 KiB
+constexpr size_t kLdsSceneBytes = 16 * 1024;   // 5-6 blocks/CU x (stack + scene) must fit 160 KiB
+constexpr int kDefaultWaves = 0;               // 0: the compiler's own register allocation
 
 struct Launcher {
     const void *fn = nullptr;
@@ -914,16 +915,26 @@ static Launcher make_launcher(size_t scene_bytes)
     L.lds_scene = LDS;
     return L;
 }
+template <int STACK>
+static Launcher bvh_launcher(bool lds, int waves, size_t sb)
+{
+    if (waves == 6) return lds ? make_launcher<STACK, FRT_WORLD_BVH, true, 6>(sb) : make_launcher<STACK, FRT_WORLD_BVH, false, 6>(0);
+    if (waves == 5) return lds ? make_launcher<STACK, FRT_WORLD_BVH, true, 5>(sb) : make_launcher<STACK, FRT_WORLD_BVH, false, 5>(0);
+    return lds ? make_launcher<STACK, FRT_WORLD_BVH, true>(sb) : make_launcher<STACK, FRT_WORLD_BVH, false>(0);
+}
 static int pick_launcher(const frt_ctx *c, int flags, Launcher &L)
 {
     if (c->world_kind == FRT_WORLD_LIST) { L = make_launcher<16, FRT_WORLD_LIST, false>(0); return FRT_OK; }
     const int d = c->stack_needed;
     const size_t sb = c->scene_lds_bytes;
     const bool lds = sb <= kLdsSceneBytes && !(flags & FRT_FLAG_NO_LDS_SCENE);
-    if (d < 8 && lds && (flags & FRT_FLAG_WAVES5)) L = make_launcher<8, FRT_WORLD_BVH, true, 5>(sb);
-    else if (d < 8) L = lds ? make_launcher<8, FRT_WORLD_BVH, true>(sb) : make_launcher<8, FRT_WORLD_BVH, false>(0);
-    else if (d < 16) L = lds ? make_launcher<16, FRT_WORLD_BVH, true>(sb) : make_launcher<16, FRT_WORLD_BVH, false>(0);
-    else if (d < 32) L = lds ? make_launcher<32, FRT_WORLD_BVH, true>(sb) : make_launcher<32, FRT_WORLD_BVH, false>(0);
+    // register cap: waves/SIMD the compiler must fit (spills land in the shading code)
+    const int waves = (flags & FRT_FLAG_WAVES6) ? 6 : (flags & FRT_FLAG_WAVES5) ? 5 : (flags & FRT_FLAG_WAVES4) ? 0
+                                                                                                            : kDefaultWaves;
+    if (d < 8) L = bvh_launcher<8>(lds, waves, sb);
+    else if (d < 16) L = bvh_launcher<16>(lds, waves, sb);
+    else if (d < 24) L = bvh_launcher<24>(false, waves, sb);
+    else if (d < 32) L = bvh_launcher<32>(false, waves, sb);
     else if (d < 64) L = make_launcher<64, FRT_WORLD_BVH, false>(0);
     else return FRT_E_UNSUPPORTED;
     return FRT_OK;

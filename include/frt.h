@@ -43,7 +43,9 @@ enum { FRT_WORLD_BVH = 0, FRT_WORLD_LIST = 1 };          /* parallel_bvh_node | 
 enum { FRT_MAT_LAMBERTIAN = 0, FRT_MAT_DIFFUSE_LIGHT = 1 }; /* material.h:50-73, 179-192 */
 enum { FRT_INTEGRATOR_PATH = 0, FRT_INTEGRATOR_PSSMLT = 1 };  /* path.h:8-18, pssmlt.h:29-76 */
 enum { FRT_FLAG_NO_LDS_SCENE = 1,      /* render_params.flags: keep small scenes in HBM/L2 (A/B timing)  */
-       FRT_FLAG_WAVES5 = 2 };          /* experimental: cap registers for 5 waves/SIMD (A/B timing)      */
+       FRT_FLAG_WAVES5 = 2,            /* register cap for 5 waves/SIMD (A/B timing)                     */
+       FRT_FLAG_WAVES6 = 4,            /* register cap for 6 waves/SIMD (A/B timing)                     */
+       FRT_FLAG_WAVES4 = 8 };          /* the compiler's own allocation, ~4 waves/SIMD (A/B timing)      */
 
 /* primitive reference: triangle t -> t ; sphere k -> FRT_PRIM_SPHERE | k */
 #define FRT_PRIM_SPHERE (1 << 30)

@@ -33,7 +33,8 @@ def main():
     from bench import scene_spec
     nx, ny = (int(v) for v in args.res.split("x"))
     kind, obj, name = scene_spec(args.scene, "/tmp")
-    flags = {"default": 0, "no_lds": frt.FRT_FLAG_NO_LDS_SCENE, "waves5": frt.FRT_FLAG_WAVES5}
+    flags = {"default": 0, "no_lds": frt.FRT_FLAG_NO_LDS_SCENE, "waves4": frt.FRT_FLAG_WAVES4,
+             "waves5": frt.FRT_FLAG_WAVES5, "waves6": frt.FRT_FLAG_WAVES6}
     chosen = [v for v in args.variants.split(",") if v.split("/")[0] in flags]
     hs = frt.HostScene(kind, obj, nx / ny)
     ctxs = {}
