@@ -61,12 +61,33 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t m)
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// Small scenes (nodes + triangles + shading records + materials, <=
+// kLdsSceneBytes) are copied into LDS once per block and traversed there
+// (ds_read_b128 instead of L1/L2 round trips).  Planar copies: part k of
+// element i at [k * count + i], so lanes reading different elements of the
+// same part hit different banks.
+__device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
+{
+    float4 *l4 = reinterpret_cast<float4 *>(lds_base);
+    const DevScene S0 = S;
+    const int nn = 4 * S0.n_nodes, nt = 3 * S0.n_tris, ns = 2 * S0.n_tris, nm = 2 * S0.n_mats;
+    for (int i = threadIdx.x; i < nn; i += kBlock) l4[(i & 3) * S0.n_nodes + (i >> 2)] = S0.nodes[i];
+    for (int i = threadIdx.x; i < nt; i += kBlock) l4[nn + (i % 3) * S0.n_tris + i / 3] = S0.tris[i];
+    for (int i = threadIdx.x; i < ns; i += kBlock) l4[nn + nt + (i & 1) * S0.n_tris + (i >> 1)] = S0.tshade[i];
+    for (int i = threadIdx.x; i < nm; i += kBlock) l4[nn + nt + ns + i] = S0.mats[i];
+    __syncthreads();
+    S.nodes = l4;
+    S.tris = l4 + nn;
+    S.tshade = l4 + nn + nt;
+    S.mats = l4 + nn + nt + ns;
+    S.node_es = 1; S.node_ps = S0.n_nodes;
+    S.tri_es = 1; S.tri_ps = S0.n_tris;
+    S.sh_es = 1; S.sh_ps = S0.n_tris;
+}
+
 // ------------------------------------------------------------------------
 // the persistent path megakernel
 // ------------------------------------------------------------------------
-// LDS_SCENE: small scenes (nodes + triangles + shading records + materials,
-// <= kLdsSceneBytes) are copied into LDS once per block and traversed there
-// (ds_read_b128 instead of L1/L2 round trips).
 template <int STACK, int WORLD, bool LDS_SCENE, int WAVES = 1>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void path_megakernel(
     const DevScene S0, const DevWork W)
@@ -74,23 +95,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     extern __shared__ __attribute__((aligned(16))) int lds_mem[];   // [STACK][kBlock] stack, then the scene
     int *stk = lds_mem + threadIdx.x;                                 // one LDS column per lane
     DevScene S = S0;
-    if constexpr (LDS_SCENE) {
-        float4 *l4 = reinterpret_cast<float4 *>(lds_mem + STACK * kBlock);
-        const int nn = 4 * S0.n_nodes, nt = 3 * S0.n_tris, ns = 2 * S0.n_tris, nm = 2 * S0.n_mats;
-        // planar copies: part k of element i at [k * count + i] (conflict-free ds_read_b128)
-        for (int i = threadIdx.x; i < nn; i += kBlock) l4[(i & 3) * S0.n_nodes + (i >> 2)] = S0.nodes[i];
-        for (int i = threadIdx.x; i < nt; i += kBlock) l4[nn + (i % 3) * S0.n_tris + i / 3] = S0.tris[i];
-        for (int i = threadIdx.x; i < ns; i += kBlock) l4[nn + nt + (i & 1) * S0.n_tris + (i >> 1)] = S0.tshade[i];
-        for (int i = threadIdx.x; i < nm; i += kBlock) l4[nn + nt + ns + i] = S0.mats[i];
-        __syncthreads();
-        S.nodes = l4;
-        S.tris = l4 + nn;
-        S.tshade = l4 + nn + nt;
-        S.mats = l4 + nn + nt + ns;
-        S.node_es = 1; S.node_ps = S0.n_nodes;
-        S.tri_es = 1; S.tri_ps = S0.n_tris;
-        S.sh_es = 1; S.sh_ps = S0.n_tris;
-    }
+    if constexpr (LDS_SCENE) scene_to_lds(S, lds_mem + STACK * kBlock);
     const int lane = threadIdx.x & 63;
     const int T2 = W.tile * W.tile;
 
@@ -261,11 +266,13 @@ __device__ __forceinline__ void mlt_splat(const MltWork &W, float x, float y, f3
 
 // one lane = one chain; every iteration traces one ray of the chain's current
 // eye path (initial state, then one proposal per mutation)
-template <int STACK, int WORLD>
-__global__ __launch_bounds__(kBlock) void mlt_megakernel(const DevScene S, const MltWork W)
+template <int STACK, int WORLD, bool LDS_SCENE>
+__global__ __launch_bounds__(kBlock) void mlt_megakernel(const DevScene S0, const MltWork W)
 {
     extern __shared__ __attribute__((aligned(16))) int lds_mem[];
     int *stk = lds_mem + threadIdx.x;
+    DevScene S = S0;
+    if constexpr (LDS_SCENE) scene_to_lds(S, lds_mem + STACK * kBlock);
     const int lane = threadIdx.x & 63;
     bool have = false, exhausted = false, init = false, large = false;
     uint32_t j = 0, c = 0;
@@ -897,7 +904,6 @@ extern "C" int frt_shard_slots(const frt_render_params *p, int32_t *slot_pixel)
 }
 
 constexpr size_t kLdsSceneBytes = 16 * 1024;   // 5-6 blocks/CU x (stack + scene) must fit 160 KiB
-constexpr int kDefaultWaves = 0;               // 0: the compiler's own register allocation
 
 struct Launcher {
     const void *fn = nullptr;
@@ -915,26 +921,30 @@ static Launcher make_launcher(size_t scene_bytes)
     L.lds_scene = LDS;
     return L;
 }
-template <int STACK>
-static Launcher bvh_launcher(bool lds, int waves, size_t sb)
+template <int STACK, bool LDS>
+static Launcher bvh_launcher(int waves, size_t sb)
 {
-    if (waves == 6) return lds ? make_launcher<STACK, FRT_WORLD_BVH, true, 6>(sb) : make_launcher<STACK, FRT_WORLD_BVH, false, 6>(0);
-    if (waves == 5) return lds ? make_launcher<STACK, FRT_WORLD_BVH, true, 5>(sb) : make_launcher<STACK, FRT_WORLD_BVH, false, 5>(0);
-    return lds ? make_launcher<STACK, FRT_WORLD_BVH, true>(sb) : make_launcher<STACK, FRT_WORLD_BVH, false>(0);
+    if (waves == 6) return make_launcher<STACK, FRT_WORLD_BVH, LDS, 6>(sb);
+    if (waves == 5) return make_launcher<STACK, FRT_WORLD_BVH, LDS, 5>(sb);
+    return make_launcher<STACK, FRT_WORLD_BVH, LDS>(sb);
 }
 static int pick_launcher(const frt_ctx *c, int flags, Launcher &L)
 {
     if (c->world_kind == FRT_WORLD_LIST) { L = make_launcher<16, FRT_WORLD_LIST, false>(0); return FRT_OK; }
     const int d = c->stack_needed;
     const size_t sb = c->scene_lds_bytes;
-    const bool lds = sb <= kLdsSceneBytes && !(flags & FRT_FLAG_NO_LDS_SCENE);
-    // register cap: waves/SIMD the compiler must fit (spills land in the shading code)
-    const int waves = (flags & FRT_FLAG_WAVES6) ? 6 : (flags & FRT_FLAG_WAVES5) ? 5 : (flags & FRT_FLAG_WAVES4) ? 0
-                                                                                                            : kDefaultWaves;
-    if (d < 8) L = bvh_launcher<8>(lds, waves, sb);
-    else if (d < 16) L = bvh_launcher<16>(lds, waves, sb);
-    else if (d < 24) L = bvh_launcher<24>(false, waves, sb);
-    else if (d < 32) L = bvh_launcher<32>(false, waves, sb);
+    const bool lds = d < 16 && sb <= kLdsSceneBytes && !(flags & FRT_FLAG_NO_LDS_SCENE);
+    // register cap: waves/SIMD the compiler must fit (its spills land in the
+    // shading code, not the traversal loops).  Measured (profiles/r01_ab_perf3.jsonl):
+    // 5 waves best for LDS-resident scenes, 6 for HBM-resident ones.
+    int waves = lds ? 5 : 6;
+    if (flags & FRT_FLAG_WAVES4) waves = 0;   // the compiler's own allocation (~120 VGPRs, 4 waves)
+    if (flags & FRT_FLAG_WAVES5) waves = 5;
+    if (flags & FRT_FLAG_WAVES6) waves = 6;
+    if (d < 8) L = lds ? bvh_launcher<8, true>(waves, sb) : bvh_launcher<8, false>(waves, 0);
+    else if (d < 16) L = lds ? bvh_launcher<16, true>(waves, sb) : bvh_launcher<16, false>(waves, 0);
+    else if (d < 24) L = bvh_launcher<24, false>(waves, 0);
+    else if (d < 32) L = bvh_launcher<32, false>(waves, 0);
     else if (d < 64) L = make_launcher<64, FRT_WORLD_BVH, false>(0);
     else return FRT_E_UNSUPPORTED;
     return FRT_OK;
@@ -942,11 +952,11 @@ static int pick_launcher(const frt_ctx *c, int flags, Launcher &L)
 
 
 // ---- PSS-MLT render: bootstrap b, then the chain megakernel splatting into dev_film ----
-template <int STACK, int WORLD>
+template <int STACK, int WORLD, bool LDS = false>
 static void mlt_kernels(const void **boot, const void **chains)
 {
     *boot = reinterpret_cast<const void *>(&mlt_bootstrap<STACK, WORLD>);
-    *chains = reinterpret_cast<const void *>(&mlt_megakernel<STACK, WORLD>);
+    *chains = reinterpret_cast<const void *>(&mlt_megakernel<STACK, WORLD, LDS>);
 }
 
 static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, hipStream_t st, frt_stats *stats)
@@ -954,12 +964,18 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
     const auto t_start = std::chrono::steady_clock::now();
     int stack;
     const void *kboot = nullptr, *kchain = nullptr;
+    const int d = c->stack_needed;
+    const bool lds_scene = c->world_kind == FRT_WORLD_BVH && d < 16 && c->scene_lds_bytes <= kLdsSceneBytes &&
+                           !(p->flags & FRT_FLAG_NO_LDS_SCENE);
     if (c->world_kind == FRT_WORLD_LIST) { stack = 0; mlt_kernels<16, FRT_WORLD_LIST>(&kboot, &kchain); }
-    else if (c->stack_needed < 16) { stack = 16; mlt_kernels<16, FRT_WORLD_BVH>(&kboot, &kchain); }
-    else if (c->stack_needed < 32) { stack = 32; mlt_kernels<32, FRT_WORLD_BVH>(&kboot, &kchain); }
-    else if (c->stack_needed < 64) { stack = 64; mlt_kernels<64, FRT_WORLD_BVH>(&kboot, &kchain); }
+    else if (lds_scene && d < 8) { stack = 8; mlt_kernels<8, FRT_WORLD_BVH, true>(&kboot, &kchain); }
+    else if (lds_scene) { stack = 16; mlt_kernels<16, FRT_WORLD_BVH, true>(&kboot, &kchain); }
+    else if (d < 16) { stack = 16; mlt_kernels<16, FRT_WORLD_BVH>(&kboot, &kchain); }
+    else if (d < 32) { stack = 32; mlt_kernels<32, FRT_WORLD_BVH>(&kboot, &kchain); }
+    else if (d < 64) { stack = 64; mlt_kernels<64, FRT_WORLD_BVH>(&kboot, &kchain); }
     else return set_err(c, FRT_E_UNSUPPORTED, "BVH deeper than 63 levels");
-    const size_t lds = (size_t)stack * kBlock * sizeof(int);
+    const size_t lds_boot = (size_t)stack * kBlock * sizeof(int);
+    const size_t lds = lds_boot + (lds_scene ? c->scene_lds_bytes : 0);
     const uint32_t n_chains = (uint32_t)p->mlt_chains;
     const uint32_t n_local = (n_chains > (uint32_t)p->shard_index)
                                  ? (n_chains - 1 - (uint32_t)p->shard_index) / (uint32_t)p->shard_count + 1 : 0;
@@ -980,7 +996,7 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
         float *sc = c->partial;
         DevScene Sarg = c->S;
         void *args[] = {&Sarg, &nx, &ny, &seed, &ni, &sc};
-        HIPCHK(c, hipLaunchKernel(kboot, dim3((n_init + kBlock - 1) / kBlock), dim3(kBlock), args, lds, st));
+        HIPCHK(c, hipLaunchKernel(kboot, dim3((n_init + kBlock - 1) / kBlock), dim3(kBlock), args, lds_boot, st));
     }
     std::vector<float> sc(n_init);
     HIPCHK(c, hipMemcpyAsync(sc.data(), c->partial, n_init * sizeof(float), hipMemcpyDeviceToHost, st));
