@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mrays/sec + RMSE vs CPU ref, CornellBox 1080p 512spp, 1/2/4/8 MI355X"
 SCENES = os.path.join(ROOT, "tests", "golden", "scenes")
+LDS_PEAK_GBS = 150000.0   # ds_read_b128 aggregate, MI355X_MICROARCH.md §LDS
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 NODE_BYTES, TRI_BYTES, RAY_BYTES = 32, 48, 32   # B_ray = 32 V + 48 T + 32
 
@@ -57,16 +58,24 @@ def load_traversal_stats(key):
     return None
 
 
-def cpu_baseline(kind, obj, nx, ny, spp, seed, npix, threads, film):
+def cpu_baseline(kind, obj, nx, ny, spp, seed, npix, threads, film, seconds):
     """The oracle (fp64 C restatement) on a bounded pixel sample of the same
     frame and RNG streams: CPU Mrays/s, reference traversal counters (for
-    B_ray) and the RMSE of the GPU film on those pixels."""
+    B_ray) and the RMSE of the GPU film on those pixels.  npix = 0: calibrate
+    on 512 pixels, then size the sample to about `seconds` of CPU work."""
     import oracle
     sc = oracle.OracleScene(kind, obj, nx / ny)
-    pix = np.unique(np.linspace(0, nx * ny - 1, npix).astype(np.int32))
-    t0 = time.perf_counter()
-    out, cnt = sc.render(nx, ny, spp, seed=seed, pixels=pix, nthreads=threads)
-    dt = time.perf_counter() - t0
+
+    def run(n):
+        pix = np.unique(np.linspace(0, nx * ny - 1, n).astype(np.int32))
+        t0 = time.perf_counter()
+        out, cnt = sc.render(nx, ny, spp, seed=seed, pixels=pix, nthreads=threads)
+        return pix, out, cnt, time.perf_counter() - t0
+
+    if npix <= 0:
+        _, _, _, dt = run(512)
+        npix = int(min(nx * ny, max(512, 512 * seconds / max(dt, 1e-3))))
+    pix, out, cnt, dt = run(npix)
     rays = cnt.rays
     gpu = film.reshape(-1, 3)[pix].astype(np.float64)
     rmse = float(np.sqrt(np.mean((gpu - out) ** 2)))
@@ -77,15 +86,22 @@ def cpu_baseline(kind, obj, nx, ny, spp, seed, npix, threads, film):
     }
 
 
-def cpu_baseline_mlt(kind, obj, nx, ny, seed, threads):
-    """The oracle's PSS-MLT on a bounded sample: 4096 chains x 512 mutations of
-    the same frame (2.1M mutations)."""
+def cpu_baseline_mlt(kind, obj, nx, ny, seed, threads, seconds):
+    """The oracle's PSS-MLT on a bounded sample of the same frame: chains x 512
+    mutations, the chain count calibrated (256 chains first) to about
+    `seconds` of CPU work."""
     import oracle
     sc = oracle.OracleScene(kind, obj, nx / ny)
-    chains, steps = 4096, 512
-    t0 = time.perf_counter()
-    _, _, cnt = sc.mlt_render(nx, ny, chains, steps, seed=seed, n_init=10000, nthreads=threads)
-    dt = time.perf_counter() - t0
+    steps = 512
+
+    def run(chains):
+        t0 = time.perf_counter()
+        _, _, cnt = sc.mlt_render(nx, ny, chains, steps, seed=seed, n_init=10000, nthreads=threads)
+        return cnt, time.perf_counter() - t0
+
+    _, dt = run(256)
+    chains = int(min(1 << 20, max(256, 256 * seconds / max(dt, 1e-3))))
+    cnt, dt = run(chains)
     return {"mrays": cnt.rays / dt / 1e6, "seconds": dt, "rays": cnt.rays, "npix": 0,
             "V": cnt.node_visits / cnt.rays, "T": (cnt.tri_tests + cnt.sphere_tests) / cnt.rays,
             "rmse": None, "sample": f"{chains} chains x {steps} mutations"}
@@ -101,7 +117,8 @@ def main():
     ap.add_argument("--spp", type=int, default=512)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--tile", type=int, default=32)
-    ap.add_argument("--cpu-pixels", type=int, default=65536, help="pixels in the CPU-baseline sample")
+    ap.add_argument("--cpu-pixels", type=int, default=0, help="pixels in the CPU-baseline sample (0: calibrated)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline duration when calibrated")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pfm", default="", help="write the rank-0 film here")
@@ -195,9 +212,10 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
             if args.integrator == "pssmlt":
-                cpu = cpu_baseline_mlt(kind, obj, nx, ny, args.seed, threads)
+                cpu = cpu_baseline_mlt(kind, obj, nx, ny, args.seed, threads, args.cpu_seconds)
             else:
-                cpu = cpu_baseline(kind, obj, nx, ny, args.spp, args.seed, args.cpu_pixels, threads, film_np)
+                cpu = cpu_baseline(kind, obj, nx, ny, args.spp, args.seed, args.cpu_pixels, threads, film_np,
+                                   args.cpu_seconds)
             cpu["threads"] = threads
         ts = load_traversal_stats(key)
         if cpu is not None:
@@ -222,7 +240,14 @@ def main():
                         "kernel": "path_megakernel" if args.integrator == "path" else "mlt_megakernel",
                         "bytes_per_ray": round(b_ray, 1),
                         "V_node": round(V, 3), "T_tri": round(T, 3), "rays_per_launch": int(rays_per_launch),
-                        "avg_launch_ms": round(avg_kernel_s * 1e3, 3)}
+                        "avg_launch_ms": round(avg_kernel_s * 1e3, 3),
+                        # where the algorithmic bytes are served from: an LDS-resident scene is not
+                        # HBM-bound (frac can exceed 1); its LDS-read peak is ~150 TB/s (MI355X_MICROARCH.md §LDS)
+                        "scene_residency": "lds" if last.scene_in_lds else "hbm",
+                        "scene_bytes": int(last.scene_bytes),
+                        "lds_frac": round(achieved / LDS_PEAK_GBS, 4) if last.scene_in_lds else None,
+                        "launch": {"waves_cap": int(last.waves_cap), "stack": int(last.stack_entries),
+                                   "bvh_depth": int(last.bvh_depth)}}
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),

@@ -17,6 +17,7 @@ LIB_PATH = os.path.join(HERE, "libfrt.so")
 FRT_WORLD_BVH, FRT_WORLD_LIST = 0, 1
 FRT_MAT_LAMBERTIAN, FRT_MAT_DIFFUSE_LIGHT = 0, 1
 FRT_PRIM_SPHERE = 1 << 30
+ABI_VERSION = 2                 # include/frt.h FRT_ABI_VERSION (frt_stats layout)
 FRT_FLAG_NO_LDS_SCENE = 1
 FRT_FLAG_WAVES5 = 2
 FRT_FLAG_WAVES6 = 4
@@ -80,7 +81,9 @@ class RenderParams(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in ("camera_rays", "extension_rays", "shadow_rays", "samples",
                                                "pixels", "work_items")] + [
-        ("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double)]
+        ("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double)] + [
+        (n, ctypes.c_uint32) for n in ("scene_in_lds", "waves_cap", "stack_entries", "bvh_depth")] + [
+        ("scene_bytes", ctypes.c_uint64)]
 
     @property
     def rays(self):
@@ -124,6 +127,8 @@ def lib():
     L = ctypes.CDLL(LIB_PATH)
     vp = ctypes.c_void_p
     L.frt_get_abi_version.restype = ctypes.c_int
+    if L.frt_get_abi_version() != ABI_VERSION:
+        raise FrtError(f"{LIB_PATH}: ABI version {L.frt_get_abi_version()}, binding expects {ABI_VERSION}; rebuild")
     L.frt_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
     L.frt_destroy.argtypes = [vp]
     L.frt_last_error.argtypes = [vp]

@@ -909,6 +909,7 @@ struct Launcher {
     const void *fn = nullptr;
     size_t lds = 0;
     int stack = 0;
+    int waves = 0;
     bool lds_scene = false;
 };
 template <int STACK, int WORLD, bool LDS, int WAVES = 1>
@@ -918,6 +919,7 @@ static Launcher make_launcher(size_t scene_bytes)
     L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES>);
     L.lds = (WORLD == FRT_WORLD_BVH ? (size_t)STACK * kBlock * sizeof(int) : 0) + (LDS ? scene_bytes : 0);
     L.stack = STACK;
+    L.waves = WAVES > 1 ? WAVES : 0;
     L.lds_scene = LDS;
     return L;
 }
@@ -1046,6 +1048,10 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
         }
         stats->pixels = (uint64_t)p->nx * p->ny;
         stats->work_items = n_local;
+        stats->scene_in_lds = lds_scene ? 1u : 0u;
+        stats->stack_entries = (uint32_t)stack;
+        stats->bvh_depth = (uint32_t)c->stack_needed;
+        stats->scene_bytes = c->scene_lds_bytes;
         stats->kernel_ms = ms;
         stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     }
@@ -1134,6 +1140,11 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
         }
         stats->pixels = px;
         stats->work_items = n_items;
+        stats->scene_in_lds = L.lds_scene ? 1u : 0u;
+        stats->waves_cap = (uint32_t)L.waves;
+        stats->stack_entries = (uint32_t)L.stack;
+        stats->bvh_depth = (uint32_t)c->stack_needed;
+        stats->scene_bytes = c->scene_lds_bytes;
         stats->kernel_ms = ms;
         stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     }

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FRT_ABI_VERSION 1
+#define FRT_ABI_VERSION 2
 
 enum {
     FRT_OK = 0,
@@ -123,6 +123,12 @@ typedef struct frt_stats {
     uint64_t work_items;
     double kernel_ms;        /* path megakernel, HIP events on its stream       */
     double total_ms;         /* whole call                                      */
+    /* launch configuration of the megakernel (measurement reporting) */
+    uint32_t scene_in_lds;   /* 1: nodes/triangles/materials were read from LDS */
+    uint32_t waves_cap;      /* register cap in waves/SIMD, 0 = compiler's own  */
+    uint32_t stack_entries;  /* per-lane LDS traversal stack                    */
+    uint32_t bvh_depth;      /* levels of the device BVH (after leaf collapse)  */
+    uint64_t scene_bytes;    /* nodes + triangles + shading records + materials */
 } frt_stats;
 
 int frt_get_abi_version(void);
