@@ -16,8 +16,12 @@ namespace frt {
 
 FRT_HD int f2i(float f) { return __builtin_bit_cast(int, f); }
 FRT_HD float i2f(int i) { return __builtin_bit_cast(float, i); }
+FRT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
 
 constexpr int kSentinel = 0x7fffffff;   // "stack empty"; never a node index
+constexpr int kEmptyChild = kSentinel;  // unused slot of a 4-wide node (never pushed)
+constexpr int kWorldBvh4 = 2;           // internal world kind: 4-wide quantized BVH
+constexpr int kBvh4Overflow = 40;       // private stack entries after the LDS ones
 
 // device scene (fp32, HBM-resident; DESIGN.md "Data layout")
 struct DevScene {
@@ -30,7 +34,9 @@ struct DevScene {
     const float4 *mats;      // 2 x float4 per material: (albedo, type) | (emit, -)
     const int *lights;       // device prim refs
     const int *list;         // device prim refs (list worlds)
+    const uint4 *nodes4;     // 4 x uint4 per 4-wide node (HBM-resident scenes; DESIGN.md "BVH4Q")
     int root;                // node index, or ~prim for a single-leaf world
+    int root4;               // 4-wide root node, or the same leaf ref as root
     int n_lights, n_list, world_kind;
     int n_nodes, n_tris, n_mats;
     // element i, part k of nodes / tris / tshade lives at [i * es + k * ps]:
@@ -65,6 +71,29 @@ FRT_HD float prim_t(const DevScene &S, int ref, f3 o, f3 d, float tmin, float tm
     }
     const float4 a = tri_part(S, ref, 0), b = tri_part(S, ref, 1), c = tri_part(S, ref, 2);
     return tri_intersect(o, d, xyz(a), xyz(b), xyz(c), tmin, tmax, u, v);
+}
+
+// Leaf ~node: one sphere, or triangles [first, first + count) (collapse_leaves;
+// the reference's leaves hold one prim, parallel_bvh.h:129-149).  Updates the
+// closest hit with the DFS-rank tie rule; true = any-hit query satisfied.
+FRT_HD bool leaf_hit(const DevScene &S, int lref, f3 o, f3 d, float tmin, bool anyhit, Hit &h)
+{
+    const bool is_sph = (lref & FRT_PRIM_SPHERE) != 0;
+    const int first = is_sph ? lref : (lref & kLeafIndexMask);
+    const int count = is_sph ? 1 : (lref >> kLeafCountShift) + 1;
+    for (int k = 0; k < count; ++k) {
+        const int ref = first + k;
+        float u, v;
+        const float t = prim_t(S, ref, o, d, tmin, h.t, u, v);
+        if (t > 0.0f) {
+            const bool better = (t < h.t) || (h.prim >= 0 && (is_sph || ref < h.prim));
+            if (better) {
+                h.prim = ref; h.t = t; h.u = u; h.v = v;
+                if (anyhit) return true;
+            }
+        }
+    }
+    return false;
 }
 
 // parallel_bvh_node::hit as an ordered stack traversal.  Closest hit keeps the
@@ -107,25 +136,79 @@ FRT_HD Hit trace_bvh(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int
             }
         }
         if (node == kSentinel) break;
-        // leaf: one sphere, or triangles [first, first + count) (collapse_leaves;
-        // the reference's leaves hold one prim, parallel_bvh.h:129-149)
-        const int lref = ~node;
-        const bool is_sph = (lref & FRT_PRIM_SPHERE) != 0;
-        const int first = is_sph ? lref : (lref & kLeafIndexMask);
-        const int count = is_sph ? 1 : (lref >> kLeafCountShift) + 1;
-        for (int k = 0; k < count; ++k) {
-            const int ref = first + k;
-            float u, v;
-            const float t = prim_t(S, ref, o, d, tmin, h.t, u, v);
-            if (t > 0.0f) {
-                const bool better = (t < h.t) || (h.prim >= 0 && (is_sph || ref < h.prim));
-                if (better) {
-                    h.prim = ref; h.t = t; h.u = u; h.v = v;
-                    if (anyhit) return h;
-                }
-            }
-        }
+        if (leaf_hit(S, ~node, o, d, tmin, anyhit, h)) return h;
         node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel;
+        if (node == kSentinel) break;
+    }
+    return h;
+}
+
+// The same query over the 4-wide quantized BVH (flatten_scene's build_bvh4):
+// node = 64 B: (frame origin xyz, exponent bytes) | 4 child refs |
+// 8-bit child box planes lo_x hi_x lo_y hi_y | lo_z hi_z.  A child plane is
+// origin + q * 2^e; the slab test runs on the ray transformed per node
+// (t = q * (2^e / d) + (origin - o) / d), so a plane costs one convert and
+// one FMA.  Quantised planes round outward and the boxes keep their padding,
+// so culling stays conservative and the hit equals trace_bvh's bit for bit
+// (the (t, DFS rank) minimum does not depend on visit order).  Stack: LSTACK
+// entries in the LDS column, then OVF private (scratch) entries.
+template <int STRIDE, int LSTACK, int OVF>
+FRT_HD Hit trace_bvh4(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int *stk)
+{
+    Hit h{-1, tmax, 0.0f, 0.0f};
+    const SlabRay sr = slab_ray(o, d);
+    if (slab_entry(S.root_lo[0], S.root_lo[1], S.root_lo[2], S.root_hi[0], S.root_hi[1], S.root_hi[2], sr,
+                   kEps, tmax) == __builtin_inff())
+        return h;
+    const float tmin = kEps * fmaxf(1.0f, fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z))));
+    int ovf[OVF];
+    int sp = 0;
+    auto push = [&](int v) {
+        if (sp < LSTACK) stk[sp * STRIDE] = v;
+        else ovf[sp - LSTACK] = v;
+        ++sp;
+    };
+    auto pop = [&]() -> int {
+        if (sp == 0) return kSentinel;
+        --sp;
+        return sp < LSTACK ? stk[sp * STRIDE] : ovf[sp - LSTACK];
+    };
+    int node = S.root4;
+    for (;;) {
+        while ((unsigned)node < (unsigned)kSentinel) {
+            const uint4 w0 = S.nodes4[4 * node], w1 = S.nodes4[4 * node + 1];
+            const uint4 w2 = S.nodes4[4 * node + 2], w3 = S.nodes4[4 * node + 3];
+            const float ax = u2f((w0.w & 0xffu) << 23) * sr.invd.x, bx = fmaf(u2f(w0.x), sr.invd.x, sr.oinv.x);
+            const float ay = u2f(((w0.w >> 8) & 0xffu) << 23) * sr.invd.y, by = fmaf(u2f(w0.y), sr.invd.y, sr.oinv.y);
+            const float az = u2f(((w0.w >> 16) & 0xffu) << 23) * sr.invd.z, bz = fmaf(u2f(w0.z), sr.invd.z, sr.oinv.z);
+            float t[4];
+            int c[4] = {(int)w1.x, (int)w1.y, (int)w1.z, (int)w1.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int sh = 8 * i;
+                const float tx0 = fmaf((float)((w2.x >> sh) & 0xffu), ax, bx), tx1 = fmaf((float)((w2.y >> sh) & 0xffu), ax, bx);
+                const float ty0 = fmaf((float)((w2.z >> sh) & 0xffu), ay, by), ty1 = fmaf((float)((w2.w >> sh) & 0xffu), ay, by);
+                const float tz0 = fmaf((float)((w3.x >> sh) & 0xffu), az, bz), tz1 = fmaf((float)((w3.y >> sh) & 0xffu), az, bz);
+                const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
+                const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), h.t));
+                t[i] = (tf < tn || c[i] == kEmptyChild) ? __builtin_inff() : tn;
+            }
+            // nearest first: sorting network on (t, child)
+            auto cx = [&](int i, int j) {
+                if (t[j] < t[i]) {
+                    const float tt = t[i]; t[i] = t[j]; t[j] = tt;
+                    const int cc = c[i]; c[i] = c[j]; c[j] = cc;
+                }
+            };
+            cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
+            if (t[3] != __builtin_inff()) push(c[3]);
+            if (t[2] != __builtin_inff()) push(c[2]);
+            if (t[1] != __builtin_inff()) push(c[1]);
+            node = (t[0] != __builtin_inff()) ? c[0] : pop();
+        }
+        if (node == kSentinel) break;
+        if (leaf_hit(S, ~node, o, d, tmin, anyhit, h)) return h;
+        node = pop();
         if (node == kSentinel) break;
     }
     return h;
@@ -147,10 +230,11 @@ FRT_HD Hit trace_list(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit)
     return h;
 }
 
-template <int WORLD, int STRIDE>
+template <int WORLD, int STRIDE, int STACK = 0>
 FRT_HD Hit trace(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int *stk)
 {
     if constexpr (WORLD == FRT_WORLD_LIST) return trace_list(S, o, d, tmax, anyhit);
+    else if constexpr (WORLD == kWorldBvh4) return trace_bvh4<STRIDE, STACK, kBvh4Overflow>(S, o, d, tmax, anyhit, stk);
     else return trace_bvh<STRIDE>(S, o, d, tmax, anyhit, stk);
 }
 

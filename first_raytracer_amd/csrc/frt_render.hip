@@ -166,7 +166,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         // ---- one ray, then shade ----
         uint32_t ne = 0, ns = 0;
         if (active) {
-            const Hit h = trace<WORLD, kBlock>(S, P.ro, P.rd, P.rtmax, P.shadow, stk);
+            const Hit h = trace<WORLD, kBlock, STACK>(S, P.ro, P.rd, P.rtmax, P.shadow, stk);
             if (path_shade(P, S, h, W.max_depth, ne, ns)) {
                 acc = acc + P.L;
                 active = false;
@@ -384,6 +384,8 @@ struct frt_ctx {
     bool have_scene = false;
     DevScene S{};
     int world_kind = 0, stack_needed = 0;
+    bool has_bvh4 = false;
+    int depth4 = 0;
     size_t scene_lds_bytes = 0;
     double last_mlt_b = 0.0;
     std::vector<void *> scene_bufs;
@@ -479,6 +481,9 @@ static inline float round_up(double x)
 // host image of the device scene (DESIGN.md "Data layout")
 struct FlatScene {
     std::vector<float4> nodes, tris, tshade, tnorm, spheres, mats;
+    std::vector<uint4> nodes4;   // 4-wide quantized BVH
+    bool has4 = false;           // nodes4 / root4 usable
+    int root4 = 0, depth4 = 0;
     std::vector<int> smat, lights, list;
     DevScene meta{};     // scalars + camera; pointers filled by the consumer
     int depth = 0;
@@ -548,6 +553,102 @@ static void collapse_leaves(FlatScene &F, int leaf_max)
     }
     F.nodes.swap(out);
     F.depth = depth;
+}
+
+// 4-wide quantized BVH (DESIGN.md "BVH4Q") from the binary tree after
+// collapse_leaves: each 4-wide node takes its binary node's two children and
+// repeatedly opens the interior child of largest surface area until it holds
+// four.  Child boxes are the binary tree's padded fp32 boxes quantized to 8
+// bits per plane on a per-node power-of-two grid, rounded outward.  Nodes in
+// pre-order.  Returns false (no BVH4; the binary tree is used) when a node's
+// grid would overflow the slab arithmetic.
+static bool build_bvh4(FlatScene &F, int root_ref)
+{
+    F.nodes4.clear();
+    F.depth4 = 0;
+    F.root4 = root_ref;
+    const int nn = (int)(F.nodes.size() / 4);
+    if (nn == 0 || root_ref < 0) return true;
+    struct Child { float lo[3], hi[3]; int ref; };
+    auto kids = [&](int i, Child *out) {
+        const float4 a = F.nodes[4 * i], b = F.nodes[4 * i + 1], c = F.nodes[4 * i + 2], r = F.nodes[4 * i + 3];
+        out[0] = Child{{a.x, a.y, a.z}, {a.w, b.x, b.y}, f2i(r.x)};
+        out[1] = Child{{b.z, b.w, c.x}, {c.y, c.z, c.w}, f2i(r.y)};
+    };
+    auto area = [](const Child &c) {
+        const double dx = (double)c.hi[0] - c.lo[0], dy = (double)c.hi[1] - c.lo[1], dz = (double)c.hi[2] - c.lo[2];
+        return dx * dy + dy * dz + dz * dx;
+    };
+    struct Item { int bin, parent, slot, lvl; };   // binary node, 4-wide parent (-1 root), child slot, level
+    std::vector<Item> st{{root_ref, -1, 0, 1}};
+    while (!st.empty()) {
+        const Item it = st.back();
+        st.pop_back();
+        const int me = (int)(F.nodes4.size() / 4);
+        if (it.parent >= 0) {
+            uint4 &r = F.nodes4[4 * it.parent + 1];
+            (it.slot == 0 ? r.x : it.slot == 1 ? r.y : it.slot == 2 ? r.z : r.w) = (uint32_t)me;
+        }
+        F.depth4 = std::max(F.depth4, it.lvl);
+        Child ch[4];
+        int n = 2;
+        kids(it.bin, ch);
+        while (n < 4) {
+            int best = -1;
+            double best_a = -1.0;
+            for (int k = 0; k < n; ++k)
+                if (ch[k].ref >= 0 && area(ch[k]) > best_a) { best = k; best_a = area(ch[k]); }
+            if (best < 0) break;
+            Child two[2];
+            kids(ch[best].ref, two);
+            for (int k = n; k > best + 1; --k) ch[k] = ch[k - 1];   // keep left-to-right order
+            ch[best] = two[0];
+            ch[best + 1] = two[1];
+            ++n;
+        }
+        // per-axis grid: origin = min child lo, step 2^e with every plane within 255 steps
+        float org[3];
+        int ex[3];
+        uint32_t qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
+        for (int a = 0; a < 3; ++a) {
+            float lo = ch[0].lo[a], hi = ch[0].hi[a];
+            for (int k = 1; k < n; ++k) { lo = std::min(lo, ch[k].lo[a]); hi = std::max(hi, ch[k].hi[a]); }
+            org[a] = lo;
+            const double ext = (double)hi - (double)lo;
+            int e = -126;
+            if (ext > 0.0) {
+                std::frexp(ext / 255.0, &e);            // ext / 255 <= 2^e
+                e = std::max(e, -126);
+                while (e > -126 && std::ldexp(255.0, e - 1) >= ext) --e;
+            }
+            if (e > 20) return false;                  // 2^e / |d| must stay finite (|1/d| <= 1e30)
+            ex[a] = e;
+            for (int k = 0; k < n; ++k) {
+                double ql = std::floor(((double)ch[k].lo[a] - lo) / std::ldexp(1.0, e));
+                double qh = std::ceil(((double)ch[k].hi[a] - lo) / std::ldexp(1.0, e));
+                ql = std::min(std::max(ql, 0.0), 255.0);
+                qh = std::min(std::max(qh, 0.0), 255.0);
+                // outward: the decoded plane must enclose the fp32 box (exact in double)
+                while (ql > 0.0 && (double)lo + ql * std::ldexp(1.0, e) > (double)ch[k].lo[a]) ql -= 1.0;
+                while (qh < 255.0 && (double)lo + qh * std::ldexp(1.0, e) < (double)ch[k].hi[a]) qh += 1.0;
+                qlo[a] |= (uint32_t)ql << (8 * k);
+                qhi[a] |= (uint32_t)qh << (8 * k);
+            }
+        }
+        uint4 w0, w1, w2, w3;
+        w0.x = (uint32_t)f2i(org[0]); w0.y = (uint32_t)f2i(org[1]); w0.z = (uint32_t)f2i(org[2]);
+        w0.w = (uint32_t)(ex[0] + 127) | ((uint32_t)(ex[1] + 127) << 8) | ((uint32_t)(ex[2] + 127) << 16);
+        uint32_t refs[4];
+        for (int k = 0; k < 4; ++k) refs[k] = (uint32_t)(k < n ? ch[k].ref : kEmptyChild);
+        w1.x = refs[0]; w1.y = refs[1]; w1.z = refs[2]; w1.w = refs[3];
+        w2.x = qlo[0]; w2.y = qhi[0]; w2.z = qlo[1]; w2.w = qhi[1];
+        w3.x = qlo[2]; w3.y = qhi[2]; w3.z = 0; w3.w = 0;
+        F.nodes4.push_back(w0); F.nodes4.push_back(w1); F.nodes4.push_back(w2); F.nodes4.push_back(w3);
+        for (int k = n - 1; k >= 0; --k)                // interior children, pre-order (first child next)
+            if (ch[k].ref >= 0) st.push_back({ch[k].ref, me, k, it.lvl + 1});
+    }
+    F.root4 = 0;
+    return true;
 }
 
 static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &err)
@@ -716,6 +817,9 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     for (size_t i = 0; i < F.list.size(); ++i) F.list[i] = dev_ref(sv->list[i]);
 
     S.root = (sv->world_kind == FRT_WORLD_BVH) ? ((sv->root >= 0) ? 0 : ~dev_ref(~sv->root)) : 0;
+    F.has4 = sv->world_kind == FRT_WORLD_BVH && build_bvh4(F, S.root);
+    if (!F.has4) F.nodes4.clear();
+    S.root4 = F.has4 ? F.root4 : S.root;
     S.n_lights = sv->n_lights;
     S.n_list = (int)F.list.size();
     S.n_nodes = (int)(F.nodes.size() / 4);
@@ -760,7 +864,8 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
     c->S = F.meta;
     DevScene &S = c->S;
     int rc;
-    if ((rc = upload_vec(c, F.nodes, &S.nodes)) || (rc = upload_vec(c, F.tris, &S.tris)) ||
+    if ((rc = upload_vec(c, F.nodes, &S.nodes)) || (rc = upload_vec(c, F.nodes4, &S.nodes4)) ||
+        (rc = upload_vec(c, F.tris, &S.tris)) ||
         (rc = upload_vec(c, F.tshade, &S.tshade)) || (rc = upload_vec(c, F.tnorm, &S.tnorm)) ||
         (rc = upload_vec(c, F.spheres, &S.spheres)) || (rc = upload_vec(c, F.smat, &S.sphere_mat)) ||
         (rc = upload_vec(c, F.mats, &S.mats)) || (rc = upload_vec(c, F.lights, &S.lights)) ||
@@ -768,10 +873,16 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
         return rc;
     c->world_kind = S.world_kind;
     c->stack_needed = F.depth;
+    c->has_bvh4 = F.has4;
+    c->depth4 = F.depth4;
     c->scene_lds_bytes = sizeof(float4) * (F.nodes.size() + F.tris.size() + F.tshade.size() + F.mats.size());
     c->have_scene = true;
     return FRT_OK;
 }
+
+// 4-wide traversal holds at most 3 pending siblings per level of the path
+static bool bvh4_stack_fits(int depth4, int lds_entries) { return 3 * depth4 <= lds_entries + kBvh4Overflow; }
+constexpr int kSelftestStack = 8;   // small, so the host self-test exercises the overflow entries
 
 // Self-test hook (CPU-only unit tests): runs frt_path.hpp -- the code the
 // megakernel runs per lane -- on the host over the flattened scene.  Not a
@@ -785,10 +896,12 @@ extern "C" int frt_selftest_path_host(const frt_scene_view *sv, const frt_render
     const int rc = flatten_scene(sv, F, err);
     if (rc != FRT_OK) return rc;
     DevScene S = F.meta;
-    S.nodes = F.nodes.data(); S.tris = F.tris.data(); S.tshade = F.tshade.data(); S.tnorm = F.tnorm.data();
+    S.nodes = F.nodes.data(); S.nodes4 = F.nodes4.data(); S.tris = F.tris.data(); S.tshade = F.tshade.data(); S.tnorm = F.tnorm.data();
     S.spheres = F.spheres.data(); S.sphere_mat = F.smat.data(); S.mats = F.mats.data();
     S.lights = F.lights.data(); S.list = F.list.data();
-    std::vector<int> stack(std::max(F.depth + 1, 1));
+    std::vector<int> stack(std::max(F.depth + 1, kSelftestStack));
+    const bool wide = S.world_kind == FRT_WORLD_BVH && F.has4 && !(p->flags & FRT_FLAG_BVH2) &&
+                      bvh4_stack_fits(F.depth4, kSelftestStack);
     uint32_t n_ext = 0, n_sh = 0;
     uint64_t n_cam = 0, ext = 0, sh = 0;
     for (int i = 0; i < npix; ++i) {
@@ -803,7 +916,8 @@ extern "C" int frt_selftest_path_host(const frt_scene_view *sv, const frt_render
             for (;;) {
                 const Hit h = (S.world_kind == FRT_WORLD_LIST)
                                   ? trace<FRT_WORLD_LIST, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data())
-                                  : trace<FRT_WORLD_BVH, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data());
+                              : wide ? trace<kWorldBvh4, 1, kSelftestStack>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data())
+                                     : trace<FRT_WORLD_BVH, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data());
                 n_ext = n_sh = 0;
                 const bool done = path_shade(P, S, h, p->max_depth, n_ext, n_sh);
                 ext += n_ext; sh += n_sh;
@@ -818,6 +932,8 @@ extern "C" int frt_selftest_path_host(const frt_scene_view *sv, const frt_render
         memset(st, 0, sizeof(*st));
         st->camera_rays = n_cam; st->extension_rays = ext; st->shadow_rays = sh;
         st->samples = n_cam; st->pixels = (uint64_t)npix;
+        st->stack_entries = wide ? (uint32_t)kSelftestStack : (uint32_t)stack.size();
+        st->bvh_depth = (uint32_t)(wide ? F.depth4 : F.depth);   // which tree was traversed
     }
     return FRT_OK;
 }
@@ -834,7 +950,7 @@ extern "C" int frt_selftest_mlt_paths_host(const frt_scene_view *sv, int nx, int
     const int rc = flatten_scene(sv, F, err);
     if (rc != FRT_OK) return rc;
     DevScene S = F.meta;
-    S.nodes = F.nodes.data(); S.tris = F.tris.data(); S.tshade = F.tshade.data(); S.tnorm = F.tnorm.data();
+    S.nodes = F.nodes.data(); S.nodes4 = F.nodes4.data(); S.tris = F.tris.data(); S.tshade = F.tshade.data(); S.tnorm = F.tnorm.data();
     S.spheres = F.spheres.data(); S.sphere_mat = F.smat.data(); S.mats = F.mats.data();
     S.lights = F.lights.data(); S.list = F.list.data();
     std::vector<int> stack(std::max(F.depth + 1, 1));
@@ -917,19 +1033,20 @@ static Launcher make_launcher(size_t scene_bytes)
 {
     Launcher L;
     L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES>);
-    L.lds = (WORLD == FRT_WORLD_BVH ? (size_t)STACK * kBlock * sizeof(int) : 0) + (LDS ? scene_bytes : 0);
+    L.lds = (WORLD != FRT_WORLD_LIST ? (size_t)STACK * kBlock * sizeof(int) : 0) + (LDS ? scene_bytes : 0);
     L.stack = STACK;
     L.waves = WAVES > 1 ? WAVES : 0;
     L.lds_scene = LDS;
     return L;
 }
-template <int STACK, bool LDS>
+template <int STACK, bool LDS, int WORLD = FRT_WORLD_BVH>
 static Launcher bvh_launcher(int waves, size_t sb)
 {
-    if (waves == 6) return make_launcher<STACK, FRT_WORLD_BVH, LDS, 6>(sb);
-    if (waves == 5) return make_launcher<STACK, FRT_WORLD_BVH, LDS, 5>(sb);
-    return make_launcher<STACK, FRT_WORLD_BVH, LDS>(sb);
+    if (waves == 6) return make_launcher<STACK, WORLD, LDS, 6>(sb);
+    if (waves == 5) return make_launcher<STACK, WORLD, LDS, 5>(sb);
+    return make_launcher<STACK, WORLD, LDS>(sb);
 }
+constexpr int kBvh4LdsStack = 16;   // 16 KiB of LDS per block; deeper entries go to scratch
 static int pick_launcher(const frt_ctx *c, int flags, Launcher &L)
 {
     if (c->world_kind == FRT_WORLD_LIST) { L = make_launcher<16, FRT_WORLD_LIST, false>(0); return FRT_OK; }
@@ -943,10 +1060,11 @@ static int pick_launcher(const frt_ctx *c, int flags, Launcher &L)
     if (flags & FRT_FLAG_WAVES4) waves = 0;   // the compiler's own allocation (~120 VGPRs, 4 waves)
     if (flags & FRT_FLAG_WAVES5) waves = 5;
     if (flags & FRT_FLAG_WAVES6) waves = 6;
-    if (d < 8) L = lds ? bvh_launcher<8, true>(waves, sb) : bvh_launcher<8, false>(waves, 0);
-    else if (d < 16) L = lds ? bvh_launcher<16, true>(waves, sb) : bvh_launcher<16, false>(waves, 0);
-    else if (d < 24) L = bvh_launcher<24, false>(waves, 0);
-    else if (d < 32) L = bvh_launcher<32, false>(waves, 0);
+    // HBM-resident scenes: the 4-wide quantized BVH (half the bytes per box test)
+    if (!lds && c->has_bvh4 && !(flags & FRT_FLAG_BVH2) && bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
+        L = bvh_launcher<kBvh4LdsStack, false, kWorldBvh4>(waves, 0);
+        return FRT_OK;
+    }
     else if (d < 64) L = make_launcher<64, FRT_WORLD_BVH, false>(0);
     else return FRT_E_UNSUPPORTED;
     return FRT_OK;

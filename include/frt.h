@@ -45,7 +45,8 @@ enum { FRT_INTEGRATOR_PATH = 0, FRT_INTEGRATOR_PSSMLT = 1 };  /* path.h:8-18, ps
 enum { FRT_FLAG_NO_LDS_SCENE = 1,      /* render_params.flags: keep small scenes in HBM/L2 (A/B timing)  */
        FRT_FLAG_WAVES5 = 2,            /* register cap for 5 waves/SIMD (A/B timing)                     */
        FRT_FLAG_WAVES6 = 4,            /* register cap for 6 waves/SIMD (A/B timing)                     */
-       FRT_FLAG_WAVES4 = 8 };          /* the compiler's own allocation, ~4 waves/SIMD (A/B timing)      */
+       FRT_FLAG_WAVES4 = 8,            /* the compiler's own allocation, ~4 waves/SIMD (A/B timing)      */
+       FRT_FLAG_BVH2 = 16 };           /* binary nodes for HBM-resident scenes (A/B timing, self-test)   */
 
 /* primitive reference: triangle t -> t ; sphere k -> FRT_PRIM_SPHERE | k */
 #define FRT_PRIM_SPHERE (1 << 30)

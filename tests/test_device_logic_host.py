@@ -90,3 +90,25 @@ def test_leaf_size_invariance(kind, objfix, tess, request, tmp_path, monkeypatch
     for leaf in (2, 4):
         assert np.array_equal(res[leaf][0], res[1][0])
         assert res[leaf][1] == res[1][1]
+
+
+@pytest.mark.parametrize("kind,objfix,tess", [("cornell_box_obj", "cornell_obj", 0),
+                                              ("cornell_box_obj", "cornell_obj", 12),
+                                              ("obj_smooth", "cornell_obj", 5)])
+def test_bvh4_matches_binary(kind, objfix, tess, request, tmp_path):
+    """The 4-wide quantized BVH (trace_bvh4, with an 8-entry stack so the
+    private overflow entries are used) returns the binary traversal's hits bit
+    for bit: identical samples and ray counts."""
+    obj = request.getfixturevalue(objfix)
+    if tess:
+        obj2 = str(tmp_path / "t.obj")
+        frt.write_tessellated_obj(obj, tess, obj2)
+        obj = obj2
+    nx, ny = 40, 30
+    hs = frt.HostScene(kind, obj, nx / ny)
+    pix = np.arange(nx * ny, dtype=np.int32)
+    wide, st4 = frt.selftest_path_host(hs, frt.RenderParams.make(nx, ny, 8, seed=13), pix)
+    bin2, st2 = frt.selftest_path_host(hs, frt.RenderParams.make(nx, ny, 8, seed=13, flags=frt.FRT_FLAG_BVH2), pix)
+    assert np.array_equal(wide, bin2)
+    assert st4.rays == st2.rays
+    assert st4.stack_entries == 8 and 0 < st4.bvh_depth < st2.bvh_depth   # the wide tree was traversed

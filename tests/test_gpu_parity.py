@@ -106,6 +106,21 @@ def test_leaf_size_invariance(ctx, cornell_obj, tmp_path, monkeypatch, flags):
     assert films[0][1] == films[1][1]
 
 
+def test_bvh4_matches_binary(ctx, cornell_obj, tmp_path):
+    """HBM-resident scenes traverse the 4-wide quantized BVH; its films equal
+    the binary BVH's bit for bit (hits do not depend on the tree's shape)."""
+    dst = str(tmp_path / "tess.obj")
+    frt.write_tessellated_obj(cornell_obj, 16, dst)
+    nx, ny, spp = 64, 48, 8
+    ctx.upload(frt.HostScene("cornell_box_obj", dst, nx / ny))
+    wide, st4 = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21, flags=frt.FRT_FLAG_NO_LDS_SCENE))
+    bin2, st2 = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21,
+                                                 flags=frt.FRT_FLAG_NO_LDS_SCENE | frt.FRT_FLAG_BVH2))
+    assert st4.scene_in_lds == 0 and st4.bvh_depth < st2.bvh_depth
+    assert np.array_equal(wide, bin2)
+    assert st4.rays == st2.rays
+
+
 def test_deterministic_and_shard_invariant(ctx, cornell_obj):
     nx, ny, spp = 100, 70, 8
     ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, nx / ny))

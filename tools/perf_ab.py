@@ -6,7 +6,7 @@ kernel ms and Grays/s as JSON lines.
   python tools/perf_ab.py [--scene cornell|cornell_1m|veach] [--spp 64] [--rounds 5]
                           [--variants default,waves5,default/leaf1]
 
-A variant is FLAG[/leafN]: a render flag set, on a scene uploaded with
+A variant is FLAG[+FLAG...][/leafN]: render flags, on a scene uploaded with
 FRT_LEAF_SIZE=N (one context per leaf size; default = the library default).
 """
 import argparse
@@ -33,8 +33,13 @@ def main():
     from bench import scene_spec
     nx, ny = (int(v) for v in args.res.split("x"))
     kind, obj, name = scene_spec(args.scene, "/tmp")
-    flags = {"default": 0, "no_lds": frt.FRT_FLAG_NO_LDS_SCENE, "waves4": frt.FRT_FLAG_WAVES4,
-             "waves5": frt.FRT_FLAG_WAVES5, "waves6": frt.FRT_FLAG_WAVES6}
+    names = {"default": 0, "no_lds": frt.FRT_FLAG_NO_LDS_SCENE, "waves4": frt.FRT_FLAG_WAVES4,
+             "waves5": frt.FRT_FLAG_WAVES5, "waves6": frt.FRT_FLAG_WAVES6, "bvh2": frt.FRT_FLAG_BVH2}
+    flags = {}
+    for v in args.variants.split(","):
+        parts = v.split("/")[0].split("+")
+        if all(p in names for p in parts):
+            flags[v.split("/")[0]] = sum(names[p] for p in parts)
     chosen = [v for v in args.variants.split(",") if v.split("/")[0] in flags]
     hs = frt.HostScene(kind, obj, nx / ny)
     ctxs = {}
