@@ -1027,6 +1027,7 @@ struct Launcher {
     int stack = 0;
     int waves = 0;
     bool lds_scene = false;
+    bool wide = false;      // 4-wide quantized BVH
 };
 template <int STACK, int WORLD, bool LDS, int WAVES = 1>
 static Launcher make_launcher(size_t scene_bytes)
@@ -1037,6 +1038,7 @@ static Launcher make_launcher(size_t scene_bytes)
     L.stack = STACK;
     L.waves = WAVES > 1 ? WAVES : 0;
     L.lds_scene = LDS;
+    L.wide = WORLD == kWorldBvh4;
     return L;
 }
 template <int STACK, bool LDS, int WORLD = FRT_WORLD_BVH>
@@ -1168,7 +1170,7 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
         stats->work_items = n_local;
         stats->scene_in_lds = lds_scene ? 1u : 0u;
         stats->stack_entries = (uint32_t)stack;
-        stats->bvh_depth = (uint32_t)c->stack_needed;
+        stats->bvh_depth = (uint32_t)(L.wide ? c->depth4 : c->stack_needed);
         stats->scene_bytes = c->scene_lds_bytes;
         stats->kernel_ms = ms;
         stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
