@@ -1170,7 +1170,7 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
         stats->work_items = n_local;
         stats->scene_in_lds = lds_scene ? 1u : 0u;
         stats->stack_entries = (uint32_t)stack;
-        stats->bvh_depth = (uint32_t)(L.wide ? c->depth4 : c->stack_needed);
+        stats->bvh_depth = (uint32_t)c->stack_needed;
         stats->scene_bytes = c->scene_lds_bytes;
         stats->kernel_ms = ms;
         stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
@@ -1263,7 +1263,7 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
         stats->scene_in_lds = L.lds_scene ? 1u : 0u;
         stats->waves_cap = (uint32_t)L.waves;
         stats->stack_entries = (uint32_t)L.stack;
-        stats->bvh_depth = (uint32_t)c->stack_needed;
+        stats->bvh_depth = (uint32_t)(L.wide ? c->depth4 : c->stack_needed);
         stats->scene_bytes = c->scene_lds_bytes;
         stats->kernel_ms = ms;
         stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
