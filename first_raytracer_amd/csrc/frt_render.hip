@@ -1067,6 +1067,10 @@ static int pick_launcher(const frt_ctx *c, int flags, Launcher &L)
         L = bvh_launcher<kBvh4LdsStack, false, kWorldBvh4>(waves, 0);
         return FRT_OK;
     }
+    if (d < 8) L = lds ? bvh_launcher<8, true>(waves, sb) : bvh_launcher<8, false>(waves, 0);
+    else if (d < 16) L = lds ? bvh_launcher<16, true>(waves, sb) : bvh_launcher<16, false>(waves, 0);
+    else if (d < 24) L = bvh_launcher<24, false>(waves, 0);
+    else if (d < 32) L = bvh_launcher<32, false>(waves, 0);
     else if (d < 64) L = make_launcher<64, FRT_WORLD_BVH, false>(0);
     else return FRT_E_UNSUPPORTED;
     return FRT_OK;

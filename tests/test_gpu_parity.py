@@ -121,6 +121,24 @@ def test_bvh4_matches_binary(ctx, cornell_obj, tmp_path):
     assert st4.rays == st2.rays
 
 
+def test_launch_plan(ctx, cornell_obj, tmp_path):
+    """The launcher picks the planned kernel: small scenes from LDS with the
+    binary BVH at 5 waves/SIMD, HBM-resident scenes on the 4-wide BVH at 6."""
+    ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, 1.0))
+    _, st = ctx.render(frt.RenderParams.make(16, 16, 1))
+    assert (st.scene_in_lds, st.waves_cap, st.stack_entries) == (1, 5, 8)
+    _, st = ctx.render(frt.RenderParams.make(16, 16, 1, flags=frt.FRT_FLAG_NO_LDS_SCENE))
+    assert (st.scene_in_lds, st.waves_cap, st.stack_entries) == (0, 6, 16)
+    _, st = ctx.render(frt.RenderParams.make(16, 16, 1, flags=frt.FRT_FLAG_NO_LDS_SCENE | frt.FRT_FLAG_BVH2))
+    assert (st.scene_in_lds, st.waves_cap, st.stack_entries) == (0, 6, 8)
+    dst = str(tmp_path / "tess.obj")
+    frt.write_tessellated_obj(cornell_obj, 60, dst)            # ~40k triangles: no longer fits LDS
+    ctx.upload(frt.HostScene("cornell_box_obj", dst, 1.0))
+    _, st = ctx.render(frt.RenderParams.make(16, 16, 1))
+    assert (st.scene_in_lds, st.waves_cap, st.stack_entries) == (0, 6, 16)
+    assert st.scene_bytes > 16 * 1024
+
+
 def test_deterministic_and_shard_invariant(ctx, cornell_obj):
     nx, ny, spp = 100, 70, 8
     ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, nx / ny))
