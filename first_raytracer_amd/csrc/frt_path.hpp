@@ -57,6 +57,7 @@ struct Hit {
 // BVH leaf ref ~x: x = FRT_PRIM_SPHERE | k, or first triangle | (count - 1) << kLeafCountShift
 constexpr int kLeafCountShift = 28, kLeafIndexMask = (1 << kLeafCountShift) - 1, kLeafIndexLimit = 1 << kLeafCountShift;
 constexpr int kLeafMax = 4, kLeafDefault = 4;
+constexpr int kTravMinDefault = 16;      // path_megakernel: see trav_min()
 
 FRT_HD float4 node_part(const DevScene &S, int i, int k) { return S.nodes[i * S.node_es + k * S.node_ps]; }
 FRT_HD float4 tri_part(const DevScene &S, int i, int k) { return S.tris[i * S.tri_es + k * S.tri_ps]; }
@@ -99,48 +100,69 @@ FRT_HD bool leaf_hit(const DevScene &S, int lref, f3 o, f3 d, float tmin, bool a
 // parallel_bvh_node::hit as an ordered stack traversal.  Closest hit keeps the
 // reference's answer: minimum t, exact ties to the leaf that comes first in
 // the left-first DFS (device triangle ids ARE that order).  Boxes are padded
-// outward, so culling never removes a hit.  `stk` entry k lives at
-// stk[k * STRIDE] (LDS column per lane on the GPU, a plain array on the host).
-template <int STRIDE>
-FRT_HD Hit trace_bvh(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int *stk)
+// outward, so culling never removes a hit.
+//
+// The traversal is resumable: Trav holds a ray's whole traversal state, and
+// one bvh*_step call descends to the next leaf and tests it.  The megakernel
+// interleaves steps of many rays with shading (path_megakernel); trace_bvh /
+// trace_bvh4 run the steps back to back.  Stack entry k lives at
+// stk[k * STRIDE] (LDS column per lane on the GPU, a plain array on the
+// host); the 4-wide traversal continues in `ovf` (private / scratch) after
+// LSTACK entries.
+struct Trav {
+    SlabRay sr;
+    float tmin;
+    int node, sp;
+    Hit h;
+};
+
+// Root box with the unscaled EPSILON (parallel_bvh.h:43), then
+// t_min = EPSILON * max(1, |o|_inf) (parallel_bvh.h:46-51).  False: the ray
+// misses the scene (T.h is the miss record).
+FRT_HD bool trav_begin(Trav &T, const DevScene &S, int root, f3 o, f3 d, float tmax)
 {
-    Hit h{-1, tmax, 0.0f, 0.0f};
-    const SlabRay sr = slab_ray(o, d);
-    // root box with the unscaled EPSILON (parallel_bvh.h:43), then
-    // t_min = EPSILON * max(1, |o|_inf) (parallel_bvh.h:46-51)
-    if (slab_entry(S.root_lo[0], S.root_lo[1], S.root_lo[2], S.root_hi[0], S.root_hi[1], S.root_hi[2], sr,
-                   kEps, tmax) == __builtin_inff())
-        return h;
-    const float tmin = kEps * fmaxf(1.0f, fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z))));
-    int node = S.root;
-    int sp = 0;
-    for (;;) {
-        while ((unsigned)node < (unsigned)kSentinel) {   // interior node
-            const float4 n0 = node_part(S, node, 0), n1 = node_part(S, node, 1);
-            const float4 n2 = node_part(S, node, 2), n3 = node_part(S, node, 3);
-            const float t0 = slab_entry(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, sr, tmin, h.t);
-            const float t1 = slab_entry(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, sr, tmin, h.t);
-            const int c0 = f2i(n3.x), c1 = f2i(n3.y);
-            const bool h0 = t0 != __builtin_inff(), h1 = t1 != __builtin_inff();
-            if (h0 && h1) {
-                const bool first0 = t0 <= t1;
-                stk[sp * STRIDE] = first0 ? c1 : c0;
-                ++sp;
-                node = first0 ? c0 : c1;
-            } else if (h0) {
-                node = c0;
-            } else if (h1) {
-                node = c1;
-            } else {
-                node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel;
-            }
+    T.h = Hit{-1, tmax, 0.0f, 0.0f};
+    T.sp = 0;
+    T.node = root;
+    T.sr = slab_ray(o, d);
+    T.tmin = kEps * fmaxf(1.0f, fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z))));
+    return slab_entry(S.root_lo[0], S.root_lo[1], S.root_lo[2], S.root_hi[0], S.root_hi[1], S.root_hi[2], T.sr,
+                      kEps, tmax) != __builtin_inff();
+}
+
+// binary nodes: descend to a leaf, test it.  True when the query is finished.
+template <int STRIDE>
+FRT_HD bool bvh2_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk)
+{
+    int node = T.node, sp = T.sp;
+    while ((unsigned)node < (unsigned)kSentinel) {   // interior node
+        const float4 n0 = node_part(S, node, 0), n1 = node_part(S, node, 1);
+        const float4 n2 = node_part(S, node, 2), n3 = node_part(S, node, 3);
+        const float t0 = slab_entry(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, T.tmin, T.h.t);
+        const float t1 = slab_entry(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, T.sr, T.tmin, T.h.t);
+        const int c0 = f2i(n3.x), c1 = f2i(n3.y);
+        const bool h0 = t0 != __builtin_inff(), h1 = t1 != __builtin_inff();
+        if (h0 && h1) {
+            const bool first0 = t0 <= t1;
+            stk[sp * STRIDE] = first0 ? c1 : c0;
+            ++sp;
+            node = first0 ? c0 : c1;
+        } else if (h0) {
+            node = c0;
+        } else if (h1) {
+            node = c1;
+        } else {
+            node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel;
         }
-        if (node == kSentinel) break;
-        if (leaf_hit(S, ~node, o, d, tmin, anyhit, h)) return h;
-        node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel;
-        if (node == kSentinel) break;
     }
-    return h;
+    bool done = node == kSentinel || leaf_hit(S, ~node, o, d, T.tmin, anyhit, T.h);
+    if (!done) {
+        node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel;
+        done = node == kSentinel;
+    }
+    T.node = node;
+    T.sp = sp;
+    return done;
 }
 
 // The same query over the 4-wide quantized BVH (flatten_scene's build_bvh4):
@@ -149,20 +171,12 @@ FRT_HD Hit trace_bvh(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int
 // origin + q * 2^e; the slab test runs on the ray transformed per node
 // (t = q * (2^e / d) + (origin - o) / d), so a plane costs one convert and
 // one FMA.  Quantised planes round outward and the boxes keep their padding,
-// so culling stays conservative and the hit equals trace_bvh's bit for bit
-// (the (t, DFS rank) minimum does not depend on visit order).  Stack: LSTACK
-// entries in the LDS column, then OVF private (scratch) entries.
-template <int STRIDE, int LSTACK, int OVF>
-FRT_HD Hit trace_bvh4(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int *stk)
+// so culling stays conservative and the hit equals the binary traversal's
+// bit for bit (the (t, DFS rank) minimum does not depend on visit order).
+template <int STRIDE, int LSTACK>
+FRT_HD bool bvh4_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int *ovf)
 {
-    Hit h{-1, tmax, 0.0f, 0.0f};
-    const SlabRay sr = slab_ray(o, d);
-    if (slab_entry(S.root_lo[0], S.root_lo[1], S.root_lo[2], S.root_hi[0], S.root_hi[1], S.root_hi[2], sr,
-                   kEps, tmax) == __builtin_inff())
-        return h;
-    const float tmin = kEps * fmaxf(1.0f, fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z))));
-    int ovf[OVF];
-    int sp = 0;
+    int node = T.node, sp = T.sp;
     auto push = [&](int v) {
         if (sp < LSTACK) stk[sp * STRIDE] = v;
         else ovf[sp - LSTACK] = v;
@@ -173,45 +187,65 @@ FRT_HD Hit trace_bvh4(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, in
         --sp;
         return sp < LSTACK ? stk[sp * STRIDE] : ovf[sp - LSTACK];
     };
-    int node = S.root4;
-    for (;;) {
-        while ((unsigned)node < (unsigned)kSentinel) {
-            const uint4 w0 = S.nodes4[4 * node], w1 = S.nodes4[4 * node + 1];
-            const uint4 w2 = S.nodes4[4 * node + 2], w3 = S.nodes4[4 * node + 3];
-            const float ax = u2f((w0.w & 0xffu) << 23) * sr.invd.x, bx = fmaf(u2f(w0.x), sr.invd.x, sr.oinv.x);
-            const float ay = u2f(((w0.w >> 8) & 0xffu) << 23) * sr.invd.y, by = fmaf(u2f(w0.y), sr.invd.y, sr.oinv.y);
-            const float az = u2f(((w0.w >> 16) & 0xffu) << 23) * sr.invd.z, bz = fmaf(u2f(w0.z), sr.invd.z, sr.oinv.z);
-            float t[4];
-            int c[4] = {(int)w1.x, (int)w1.y, (int)w1.z, (int)w1.w};
+    while ((unsigned)node < (unsigned)kSentinel) {
+        const uint4 w0 = S.nodes4[4 * node], w1 = S.nodes4[4 * node + 1];
+        const uint4 w2 = S.nodes4[4 * node + 2], w3 = S.nodes4[4 * node + 3];
+        const SlabRay &sr = T.sr;
+        const float ax = u2f((w0.w & 0xffu) << 23) * sr.invd.x, bx = fmaf(u2f(w0.x), sr.invd.x, sr.oinv.x);
+        const float ay = u2f(((w0.w >> 8) & 0xffu) << 23) * sr.invd.y, by = fmaf(u2f(w0.y), sr.invd.y, sr.oinv.y);
+        const float az = u2f(((w0.w >> 16) & 0xffu) << 23) * sr.invd.z, bz = fmaf(u2f(w0.z), sr.invd.z, sr.oinv.z);
+        float t[4];
+        int c[4] = {(int)w1.x, (int)w1.y, (int)w1.z, (int)w1.w};
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int sh = 8 * i;
-                const float tx0 = fmaf((float)((w2.x >> sh) & 0xffu), ax, bx), tx1 = fmaf((float)((w2.y >> sh) & 0xffu), ax, bx);
-                const float ty0 = fmaf((float)((w2.z >> sh) & 0xffu), ay, by), ty1 = fmaf((float)((w2.w >> sh) & 0xffu), ay, by);
-                const float tz0 = fmaf((float)((w3.x >> sh) & 0xffu), az, bz), tz1 = fmaf((float)((w3.y >> sh) & 0xffu), az, bz);
-                const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
-                const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), h.t));
-                t[i] = (tf < tn || c[i] == kEmptyChild) ? __builtin_inff() : tn;
-            }
-            // nearest first: sorting network on (t, child)
-            auto cx = [&](int i, int j) {
-                if (t[j] < t[i]) {
-                    const float tt = t[i]; t[i] = t[j]; t[j] = tt;
-                    const int cc = c[i]; c[i] = c[j]; c[j] = cc;
-                }
-            };
-            cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
-            if (t[3] != __builtin_inff()) push(c[3]);
-            if (t[2] != __builtin_inff()) push(c[2]);
-            if (t[1] != __builtin_inff()) push(c[1]);
-            node = (t[0] != __builtin_inff()) ? c[0] : pop();
+        for (int i = 0; i < 4; ++i) {
+            const int sh = 8 * i;
+            const float tx0 = fmaf((float)((w2.x >> sh) & 0xffu), ax, bx), tx1 = fmaf((float)((w2.y >> sh) & 0xffu), ax, bx);
+            const float ty0 = fmaf((float)((w2.z >> sh) & 0xffu), ay, by), ty1 = fmaf((float)((w2.w >> sh) & 0xffu), ay, by);
+            const float tz0 = fmaf((float)((w3.x >> sh) & 0xffu), az, bz), tz1 = fmaf((float)((w3.y >> sh) & 0xffu), az, bz);
+            const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), T.tmin));
+            const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), T.h.t));
+            t[i] = (tf < tn || c[i] == kEmptyChild) ? __builtin_inff() : tn;
         }
-        if (node == kSentinel) break;
-        if (leaf_hit(S, ~node, o, d, tmin, anyhit, h)) return h;
-        node = pop();
-        if (node == kSentinel) break;
+        // nearest first: sorting network on (t, child)
+        auto cx = [&](int i, int j) {
+            if (t[j] < t[i]) {
+                const float tt = t[i]; t[i] = t[j]; t[j] = tt;
+                const int cc = c[i]; c[i] = c[j]; c[j] = cc;
+            }
+        };
+        cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
+        if (t[3] != __builtin_inff()) push(c[3]);
+        if (t[2] != __builtin_inff()) push(c[2]);
+        if (t[1] != __builtin_inff()) push(c[1]);
+        node = (t[0] != __builtin_inff()) ? c[0] : pop();
     }
-    return h;
+    bool done = node == kSentinel || leaf_hit(S, ~node, o, d, T.tmin, anyhit, T.h);
+    if (!done) {
+        node = pop();
+        done = node == kSentinel;
+    }
+    T.node = node;
+    T.sp = sp;
+    return done;
+}
+
+template <int STRIDE>
+FRT_HD Hit trace_bvh(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int *stk)
+{
+    Trav T;
+    if (trav_begin(T, S, S.root, o, d, tmax))
+        while (!bvh2_step<STRIDE>(T, S, o, d, anyhit, stk)) {}
+    return T.h;
+}
+
+template <int STRIDE, int LSTACK, int OVF>
+FRT_HD Hit trace_bvh4(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int *stk)
+{
+    Trav T;
+    int ovf[OVF];
+    if (trav_begin(T, S, S.root4, o, d, tmax))
+        while (!bvh4_step<STRIDE, LSTACK>(T, S, o, d, anyhit, stk, ovf)) {}
+    return T.h;
 }
 
 // hitable_list::hit: in list order, triangles strict '<', spheres inclusive (sphere.h:34)
@@ -236,6 +270,30 @@ FRT_HD Hit trace(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int *st
     if constexpr (WORLD == FRT_WORLD_LIST) return trace_list(S, o, d, tmax, anyhit);
     else if constexpr (WORLD == kWorldBvh4) return trace_bvh4<STRIDE, STACK, kBvh4Overflow>(S, o, d, tmax, anyhit, stk);
     else return trace_bvh<STRIDE>(S, o, d, tmax, anyhit, stk);
+}
+
+// resumable form of trace<> (path_megakernel): begin, then steps until true
+template <int WORLD>
+FRT_HD bool trav_begin_world(Trav &T, const DevScene &S, f3 o, f3 d, float tmax)
+{
+    if constexpr (WORLD == FRT_WORLD_LIST) {
+        T.h = Hit{-1, tmax, 0.0f, 0.0f};
+        return true;
+    } else {
+        return trav_begin(T, S, WORLD == kWorldBvh4 ? S.root4 : S.root, o, d, tmax);
+    }
+}
+template <int WORLD, int STRIDE, int STACK>
+FRT_HD bool trav_step_world(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int *ovf)
+{
+    if constexpr (WORLD == FRT_WORLD_LIST) {
+        T.h = trace_list(S, o, d, T.h.t, anyhit);
+        return true;
+    } else if constexpr (WORLD == kWorldBvh4) {
+        return bvh4_step<STRIDE, STACK>(T, S, o, d, anyhit, stk, ovf);
+    } else {
+        return bvh2_step<STRIDE>(T, S, o, d, anyhit, stk);
+    }
 }
 
 // hit record of a primitive: shading normal + material

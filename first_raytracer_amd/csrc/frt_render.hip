@@ -42,6 +42,7 @@ struct DevWork {
     int tile, ntx, shard_index, shard_count;
     int spi, n_chunks;
     uint32_t n_items, n_slots;
+    int trav_min;                        // shade when at most this many lanes of a wave still traverse
     float *partial;                      // [n_chunks][n_slots][3]
     unsigned *counter;                   // work-queue head
     unsigned long long *wave_rays;       // [n_waves][4]: camera, extension, shadow, samples
@@ -106,10 +107,39 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     int px = 0, py = 0;
     f3 acc = mk3(0, 0, 0);
     PathState P;
+    // ray in flight: tracing = traversal steps remain; pending = finished, not yet shaded
+    Trav T;
+    bool tracing = false, pending = false;
+    int ovf[WORLD == kWorldBvh4 ? kBvh4Overflow : 1];
     // ray counters are wave-uniform (SGPRs): popcounts of per-iteration ballots
     unsigned long long n_cam = 0, n_ext = 0, n_sh = 0, n_smp = 0;
 
     for (;;) {
+        // ---- traversal: steps (descend to a leaf, test it) of every lane's ray,
+        // until at most trav_min lanes are still traversing.  Lanes whose ray is
+        // done wait here only while the rest of the wave needs few more steps;
+        // then they shade together while the stragglers keep their state.
+        for (;;) {
+            if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, P.ro, P.rd, P.shadow, stk, ovf)) {
+                tracing = false;
+                pending = true;
+            }
+            if (__popcll(__ballot(tracing)) <= W.trav_min) break;
+        }
+        // ---- shade the finished rays ----
+        uint32_t ne = 0, ns = 0;
+        bool next_ray = false;
+        if (pending) {
+            pending = false;
+            if (path_shade(P, S, T.h, W.max_depth, ne, ns)) {
+                acc = acc + P.L;
+                active = false;
+            } else {
+                next_ray = true;
+            }
+        }
+        n_ext += __popcll(__ballot(ne != 0));
+        n_sh += __popcll(__ballot(ns != 0));
         // ---- retire a finished item: its chunk sum goes to its own slot ----
         if (!active && have_item && s_cur >= s_end) {
             float *dst = W.partial + 3ull * ((size_t)chunk * W.n_slots + slot);
@@ -155,25 +185,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             path_begin(P, S, px, py, W.nx, W.ny, W.seed, pix, (uint32_t)s_cur);
             ++s_cur;
             active = true;
+            next_ray = true;
         }
         const unsigned long long started = __popcll(__ballot(start));
         n_cam += started;
         n_smp += started;
-        if (__ballot(active) == 0) {
-            if (__ballot(!exhausted) == 0) break;
-            continue;
+        // ---- set up the next ray's traversal (a scene miss is finished at once) ----
+        if (next_ray) {
+            tracing = trav_begin_world<WORLD>(T, S, P.ro, P.rd, P.rtmax);
+            pending = !tracing;
         }
-        // ---- one ray, then shade ----
-        uint32_t ne = 0, ns = 0;
-        if (active) {
-            const Hit h = trace<WORLD, kBlock, STACK>(S, P.ro, P.rd, P.rtmax, P.shadow, stk);
-            if (path_shade(P, S, h, W.max_depth, ne, ns)) {
-                acc = acc + P.L;
-                active = false;
-            }
-        }
-        n_ext += __popcll(__ballot(ne != 0));
-        n_sh += __popcll(__ballot(ns != 0));
+        if (__ballot(active || !exhausted) == 0) break;
     }
     // per-wave ray counters, no atomics: lane 0 writes the wave's sums
     const unsigned long long c[4] = {n_cam, n_ext, n_sh, n_smp};
@@ -488,6 +510,16 @@ struct FlatScene {
     DevScene meta{};     // scalars + camera; pointers filled by the consumer
     int depth = 0;
 };
+
+// Shading starts when at most this many lanes of a wave still traverse
+// (FRT_TRAV_MIN overrides; 0 = every ray of the wave finishes first).  A
+// tuning knob of this library, not part of the C-ABI.
+static int trav_min()
+{
+    const char *e = std::getenv("FRT_TRAV_MIN");
+    const int v = e ? std::atoi(e) : kTravMinDefault;
+    return std::min(std::max(v, 0), 63);
+}
 
 // Triangles per leaf (FRT_LEAF_SIZE overrides, 1 = the reference's one-prim
 // leaves).  A tuning knob of this library, not part of the C-ABI.
@@ -1232,6 +1264,7 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     W.tile = T; W.ntx = (p->nx + T - 1) / T; W.shard_index = p->shard_index; W.shard_count = p->shard_count;
     W.spi = spi; W.n_chunks = n_chunks; W.n_items = (uint32_t)n_items; W.n_slots = n_slots;
     W.partial = c->partial; W.counter = c->counter; W.wave_rays = c->wave_rays;
+    W.trav_min = trav_min();
 
     HIPCHK(c, hipMemsetAsync(c->counter, 0, 64, st));
     HIPCHK(c, hipEventRecord(c->ev0, st));

@@ -6,7 +6,8 @@ kernel ms and Grays/s as JSON lines.
   python tools/perf_ab.py [--scene cornell|cornell_1m|veach] [--spp 64] [--rounds 5]
                           [--variants default,waves5,default/leaf1]
 
-A variant is FLAG[+FLAG...][/leafN]: render flags, on a scene uploaded with
+A variant is FLAG[+FLAG...][/leafN][/travN]: render flags (travN sets
+FRT_TRAV_MIN=N for its renders), on a scene uploaded with
 FRT_LEAF_SIZE=N (one context per leaf size; default = the library default).
 """
 import argparse
@@ -41,10 +42,14 @@ def main():
         if all(p in names for p in parts):
             flags[v.split("/")[0]] = sum(names[p] for p in parts)
     chosen = [v for v in args.variants.split(",") if v.split("/")[0] in flags]
+
+    def opt(v, key):
+        return next((o[len(key):] for o in v.split("/")[1:] if o.startswith(key)), "")
+
     hs = frt.HostScene(kind, obj, nx / ny)
     ctxs = {}
     for v in chosen:
-        leaf = v.split("/")[1][4:] if "/" in v else ""
+        leaf = opt(v, "leaf")
         if leaf not in ctxs:
             if leaf:
                 os.environ["FRT_LEAF_SIZE"] = leaf
@@ -58,7 +63,11 @@ def main():
     films = {}
     for r in range(args.rounds + 1):
         for v in chosen:
-            leaf = v.split("/")[1][4:] if "/" in v else ""
+            leaf = opt(v, "leaf")
+            if opt(v, "trav"):
+                os.environ["FRT_TRAV_MIN"] = opt(v, "trav")
+            else:
+                os.environ.pop("FRT_TRAV_MIN", None)
             p = frt.RenderParams.make(nx, ny, args.spp, seed=0, flags=flags[v.split("/")[0]])
             films[leaf], st = ctxs[leaf].render(p, films.get(leaf))
             if r > 0:
