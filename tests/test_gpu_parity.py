@@ -121,6 +121,24 @@ def test_bvh4_matches_binary(ctx, cornell_obj, tmp_path):
     assert st4.rays == st2.rays
 
 
+@pytest.mark.parametrize("flags", [0, frt.FRT_FLAG_NO_LDS_SCENE, frt.FRT_FLAG_NO_LDS_SCENE | frt.FRT_FLAG_BVH2])
+def test_trav_min_invariance(ctx, cornell_obj, tmp_path, monkeypatch, flags):
+    """When finished rays get shaded (FRT_TRAV_MIN) changes scheduling only:
+    every ray's hit and every item's sum order are the same, so films are
+    bit-identical."""
+    dst = str(tmp_path / "tess.obj")
+    frt.write_tessellated_obj(cornell_obj, 6, dst)
+    nx, ny, spp = 48, 40, 8
+    ctx.upload(frt.HostScene("cornell_box_obj", dst, nx / ny))
+    res = []
+    for tm in ("0", "16", "48"):
+        monkeypatch.setenv("FRT_TRAV_MIN", tm)
+        f, st = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=17, flags=flags))
+        res.append((f, st.rays))
+    for f, r in res[1:]:
+        assert np.array_equal(f, res[0][0]) and r == res[0][1]
+
+
 def test_launch_plan(ctx, cornell_obj, tmp_path):
     """The launcher picks the planned kernel: small scenes from LDS with the
     binary BVH at 5 waves/SIMD, HBM-resident scenes on the 4-wide BVH at 6."""
