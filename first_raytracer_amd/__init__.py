@@ -72,10 +72,11 @@ class RenderParams(ctypes.Structure):
                    mlt_chains=0, mlt_bootstrap=0)
 
     @classmethod
-    def pssmlt(cls, nx, ny, mutations_per_pixel, chains, seed=0, bootstrap=10000, shard_index=0, shard_count=1):
+    def pssmlt(cls, nx, ny, mutations_per_pixel, chains, seed=0, bootstrap=10000, shard_index=0, shard_count=1,
+               flags=0):
         """PSS-MLT (pssmlt.cpp): total mutations = mutations_per_pixel*nx*ny over `chains` chains."""
         return cls(nx=nx, ny=ny, spp=mutations_per_pixel, seed=seed, max_depth=10, integrator=FRT_INTEGRATOR_PSSMLT,
-                   tile_size=32, shard_index=shard_index, shard_count=shard_count, samples_per_item=0, flags=0,
+                   tile_size=32, shard_index=shard_index, shard_count=shard_count, samples_per_item=0, flags=flags,
                    mlt_chains=chains, mlt_bootstrap=bootstrap)
 
 

@@ -57,7 +57,7 @@ struct Hit {
 // BVH leaf ref ~x: x = FRT_PRIM_SPHERE | k, or first triangle | (count - 1) << kLeafCountShift
 constexpr int kLeafCountShift = 28, kLeafIndexMask = (1 << kLeafCountShift) - 1, kLeafIndexLimit = 1 << kLeafCountShift;
 constexpr int kLeafMax = 4, kLeafDefault = 4;
-constexpr int kTravMinDefault = 16;      // path_megakernel: see trav_min()
+constexpr int kTravMinLds = 12, kTravMinHbm = 32;   // path_megakernel: see trav_min()
 
 FRT_HD float4 node_part(const DevScene &S, int i, int k) { return S.nodes[i * S.node_es + k * S.node_ps]; }
 FRT_HD float4 tri_part(const DevScene &S, int i, int k) { return S.tris[i * S.tri_es + k * S.tri_ps]; }

@@ -242,16 +242,17 @@ struct MltWork {
     uint32_t n_local;                    // chains of this shard: global c = shard_index + j * shard_count
     uint64_t steps;                      // mutations per chain
     float b, scale, s2p, logp;           // normaliser, nx*ny/ns, pixel-dim perturb constants
+    int trav_min;                        // see path_megakernel / trav_min()
     float *U;                            // [kMltDims][n_local] current primary samples
     float *film;                         // [nx*ny*3] splat accumulation
     unsigned *counter;
     unsigned long long *wave_rays;
 };
 
-template <int WORLD>
+template <int WORLD, int STACK>
 __device__ __forceinline__ Hit trace_any(const DevScene &S, const PathState &P, int *stk)
 {
-    return trace<WORLD, kBlock>(S, P.ro, P.rd, P.rtmax, P.shadow, stk);
+    return trace<WORLD, kBlock, STACK>(S, P.ro, P.rd, P.rtmax, P.shadow, stk);
 }
 
 // bootstrap: sc of n_init independent eye paths (pssmlt.cpp:303-312); the host
@@ -270,7 +271,7 @@ __global__ __launch_bounds__(kBlock) void mlt_bootstrap(const DevScene S, int nx
     uint32_t ne = 0, ns = 0;
     for (;;) {
         if (mlt_beyond(M)) { M.P.L = M.P.L + M.P.beta * S.env; break; }
-        const Hit h = trace_any<WORLD>(S, M.P, stk);
+        const Hit h = trace_any<WORLD, STACK>(S, M.P, stk);
         if (mlt_shade(M, S, h, src, ne, ns)) break;
     }
     sc[i] = fmaxf(fmaxf(M.P.L.x, M.P.L.y), M.P.L.z);
@@ -286,8 +287,9 @@ __device__ __forceinline__ void mlt_splat(const MltWork &W, float x, float y, f3
     atomicAdd(&W.film[3 * (size_t)pix + 2], k * c.z);
 }
 
-// one lane = one chain; every iteration traces one ray of the chain's current
-// eye path (initial state, then one proposal per mutation)
+// one lane = one chain tracing the rays of its current eye path (initial
+// state, then one proposal per mutation); traversal steps interleave with
+// shading as in path_megakernel
 template <int STACK, int WORLD, bool LDS_SCENE>
 __global__ __launch_bounds__(kBlock) void mlt_megakernel(const DevScene S0, const MltWork W)
 {
@@ -309,7 +311,67 @@ __global__ __launch_bounds__(kBlock) void mlt_megakernel(const DevScene S0, cons
         PrndSource src{W.U, W.n_local, j, key, 2u, init || large, W.s2p, W.logp};
         return src;
     };
+    // ray in flight, as in path_megakernel: tracing = traversal steps remain;
+    // pending = finished (or the path went beyond MaxPathLength), not yet shaded
+    Trav T;
+    bool tracing = false, pending = false, beyond = false;
+    int ovf[WORLD == kWorldBvh4 ? kBvh4Overflow : 1];
     for (;;) {
+        // ---- traversal steps until at most trav_min lanes still traverse ----
+        for (;;) {
+            if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, M.P.ro, M.P.rd, M.P.shadow, stk, ovf)) {
+                tracing = false;
+                pending = true;
+            }
+            if (__popcll(__ballot(tracing)) <= W.trav_min) break;
+        }
+        bool next_ray = false, done = false;
+        if (pending) {
+            pending = false;
+            if (beyond) {                               // pssmlt.cpp:151, :276
+                M.P.L = M.P.L + M.P.beta * S.env;
+                beyond = false;
+                done = true;
+            } else {
+                uint32_t ne = 0, ns = 0;
+                done = mlt_shade(M, S, T.h, source(), ne, ns);
+                n_ext += ne; n_sh += ns;
+                next_ray = !done;
+            }
+        }
+        if (done) {
+            const f3 L = M.P.L;
+            const float sc = fmaxf(fmaxf(L.x, L.y), L.z);
+            const PrndSource src = source();
+            if (init) {                                 // current = initial state, materialised
+                for (int d = 0; d < kMltDims; ++d) W.U[(size_t)d * W.n_local + j] = src.get(d);
+                cx = M.x; cy = M.y; cc = L; csc = sc;
+                init = false;
+            } else {                                    // pssmlt.cpp:200-209
+                float a = 1.0f;
+                if (csc > 0.0f) a = fmaxf(fminf(1.0f, sc / csc), 0.0f);
+                if (sc > 0.0f) mlt_splat(W, M.x, M.y, L, (a + (large ? 1.0f : 0.0f)) / (sc / W.b + kMltLargeStep));
+                if (csc > 0.0f) cw += (1.0f - a) / (csc / W.b + kMltLargeStep);
+                if (rng_u(key, 1) <= a) {               // accept: splat the old state's weight, move
+                    if (csc > 0.0f && cw != 0.0f) mlt_splat(W, cx, cy, cc, cw);
+                    cw = 0.0f;
+                    for (int d = 0; d < kMltDims; ++d) W.U[(size_t)d * W.n_local + j] = src.get(d);
+                    cx = M.x; cy = M.y; cc = L; csc = sc;
+                }
+                ++t;
+                ++n_smp;
+            }
+            if (t >= W.steps) {                         // chain finished
+                if (csc > 0.0f && cw != 0.0f) mlt_splat(W, cx, cy, cc, cw);
+                have = false;
+            } else {
+                key = rng_key(W.seed ^ kMltChainSalt, c, (uint32_t)(t + 1));
+                large = rng_u(key, 0) < kMltLargeStep;  // large_step vs mutate (pssmlt.cpp:187-196)
+                mlt_begin(M, S, source(), W.nx, W.ny);
+                ++n_cam;
+                next_ray = true;
+            }
+        }
         // ---- chains from the queue, one atomic per wave ----
         const bool need = !have && !exhausted;
         const uint64_t m = __ballot(need);
@@ -332,55 +394,21 @@ __global__ __launch_bounds__(kBlock) void mlt_megakernel(const DevScene S0, cons
                     key = rng_key(W.seed ^ kMltChainSalt, c, 0u);   // initial state: TMarkovChain(s)
                     mlt_begin(M, S, source(), W.nx, W.ny);
                     ++n_cam;
+                    next_ray = true;
                 }
             }
         }
-        if (__ballot(have) == 0) {
-            if (__ballot(!exhausted) == 0) break;
-            continue;
-        }
-        if (!have) continue;
-        bool done;
-        if (mlt_beyond(M)) {
-            M.P.L = M.P.L + M.P.beta * S.env;
-            done = true;
-        } else {
-            const Hit h = trace_any<WORLD>(S, M.P, stk);
-            uint32_t ne = 0, ns = 0;
-            done = mlt_shade(M, S, h, source(), ne, ns);
-            n_ext += ne; n_sh += ns;
-        }
-        if (!done) continue;
-        const f3 L = M.P.L;
-        const float sc = fmaxf(fmaxf(L.x, L.y), L.z);
-        const PrndSource src = source();
-        if (init) {                                     // current = initial state, materialised
-            for (int d = 0; d < kMltDims; ++d) W.U[(size_t)d * W.n_local + j] = src.get(d);
-            cx = M.x; cy = M.y; cc = L; csc = sc;
-            init = false;
-        } else {                                        // pssmlt.cpp:200-209
-            float a = 1.0f;
-            if (csc > 0.0f) a = fmaxf(fminf(1.0f, sc / csc), 0.0f);
-            if (sc > 0.0f) mlt_splat(W, M.x, M.y, L, (a + (large ? 1.0f : 0.0f)) / (sc / W.b + kMltLargeStep));
-            if (csc > 0.0f) cw += (1.0f - a) / (csc / W.b + kMltLargeStep);
-            if (rng_u(key, 1) <= a) {                   // accept: splat the old state's weight, move
-                if (csc > 0.0f && cw != 0.0f) mlt_splat(W, cx, cy, cc, cw);
-                cw = 0.0f;
-                for (int d = 0; d < kMltDims; ++d) W.U[(size_t)d * W.n_local + j] = src.get(d);
-                cx = M.x; cy = M.y; cc = L; csc = sc;
+        // ---- next ray of the eye path ----
+        if (next_ray) {
+            if (mlt_beyond(M)) {
+                beyond = true;
+                pending = true;
+            } else {
+                tracing = trav_begin_world<WORLD>(T, S, M.P.ro, M.P.rd, M.P.rtmax);
+                pending = !tracing;
             }
-            ++t;
-            ++n_smp;
         }
-        if (t >= W.steps) {                             // chain finished
-            if (csc > 0.0f && cw != 0.0f) mlt_splat(W, cx, cy, cc, cw);
-            have = false;
-            continue;
-        }
-        key = rng_key(W.seed ^ kMltChainSalt, c, (uint32_t)(t + 1));
-        large = rng_u(key, 0) < kMltLargeStep;          // large_step vs mutate (pssmlt.cpp:187-196)
-        mlt_begin(M, S, source(), W.nx, W.ny);
-        ++n_cam;
+        if (__ballot(have || !exhausted) == 0) break;
     }
     unsigned long long cnt[4] = {n_cam, n_ext, n_sh, n_smp};
     for (int k = 0; k < 4; ++k)
@@ -512,12 +540,14 @@ struct FlatScene {
 };
 
 // Shading starts when at most this many lanes of a wave still traverse
-// (FRT_TRAV_MIN overrides; 0 = every ray of the wave finishes first).  A
-// tuning knob of this library, not part of the C-ABI.
-static int trav_min()
+// (0 = every ray of the wave finishes first).  Per plan: measured best ~8-16
+// for LDS-resident scenes (short traversals), ~32 for HBM-resident ones
+// (profiles/r01_ab_perf6.jsonl).  FRT_TRAV_MIN overrides (tuning knob of this
+// library, not part of the C-ABI).
+static int trav_min(bool lds_scene)
 {
     const char *e = std::getenv("FRT_TRAV_MIN");
-    const int v = e ? std::atoi(e) : kTravMinDefault;
+    const int v = e ? std::atoi(e) : (lds_scene ? kTravMinLds : kTravMinHbm);
     return std::min(std::max(v, 0), 63);
 }
 
@@ -1126,6 +1156,10 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
     const bool lds_scene = c->world_kind == FRT_WORLD_BVH && d < 16 && c->scene_lds_bytes <= kLdsSceneBytes &&
                            !(p->flags & FRT_FLAG_NO_LDS_SCENE);
     if (c->world_kind == FRT_WORLD_LIST) { stack = 0; mlt_kernels<16, FRT_WORLD_LIST>(&kboot, &kchain); }
+    else if (!lds_scene && c->has_bvh4 && !(p->flags & FRT_FLAG_BVH2) && bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
+        stack = kBvh4LdsStack;
+        mlt_kernels<kBvh4LdsStack, kWorldBvh4>(&kboot, &kchain);
+    }
     else if (lds_scene && d < 8) { stack = 8; mlt_kernels<8, FRT_WORLD_BVH, true>(&kboot, &kchain); }
     else if (lds_scene) { stack = 16; mlt_kernels<16, FRT_WORLD_BVH, true>(&kboot, &kchain); }
     else if (d < 16) { stack = 16; mlt_kernels<16, FRT_WORLD_BVH>(&kboot, &kchain); }
@@ -1181,6 +1215,7 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
     W.s2p = 0.1f;
     W.logp = (float)std::log((double)0.1f / (2.0 / (double)(p->nx + p->ny)));
     W.U = c->partial; W.film = dev_film; W.counter = c->counter; W.wave_rays = c->wave_rays;
+    W.trav_min = trav_min(lds_scene);
     HIPCHK(c, hipMemsetAsync(dev_film, 0, (size_t)p->nx * p->ny * 3 * sizeof(float), st));
     HIPCHK(c, hipMemsetAsync(c->counter, 0, 64, st));
     HIPCHK(c, hipEventRecord(c->ev0, st));
@@ -1264,7 +1299,7 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     W.tile = T; W.ntx = (p->nx + T - 1) / T; W.shard_index = p->shard_index; W.shard_count = p->shard_count;
     W.spi = spi; W.n_chunks = n_chunks; W.n_items = (uint32_t)n_items; W.n_slots = n_slots;
     W.partial = c->partial; W.counter = c->counter; W.wave_rays = c->wave_rays;
-    W.trav_min = trav_min();
+    W.trav_min = trav_min(L.lds_scene);
 
     HIPCHK(c, hipMemsetAsync(c->counter, 0, 64, st));
     HIPCHK(c, hipEventRecord(c->ev0, st));

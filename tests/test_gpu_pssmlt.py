@@ -41,6 +41,25 @@ def test_short_chains_match_oracle(ctx, kind, objfix, request):
     assert e <= 1e-3 * scale
 
 
+@pytest.mark.parametrize("flags", [frt.FRT_FLAG_NO_LDS_SCENE, frt.FRT_FLAG_NO_LDS_SCENE | frt.FRT_FLAG_BVH2])
+def test_short_chains_hbm_scene(ctx, cornell_obj, tmp_path, flags):
+    """The HBM-resident chain kernels (4-wide and binary BVH) on a tessellated
+    Cornell box against the oracle's chains."""
+    dst = str(tmp_path / "tess.obj")
+    frt.write_tessellated_obj(cornell_obj, 12, dst)
+    nx, ny, mpp, chains = 48, 32, 4, 1536
+    ctx.upload(frt.HostScene("cornell_box_obj", dst, nx / ny))
+    film = np.zeros((ny, nx, 3), np.float32)
+    film, st = ctx.render(frt.RenderParams.pssmlt(nx, ny, mpp, chains, seed=9, bootstrap=2000, flags=flags), film)
+    steps = mpp * nx * ny // chains
+    ref, b, cnt = oracle.OracleScene("cornell_box_obj", dst, nx / ny).mlt_render(nx, ny, chains, steps, seed=9,
+                                                                                 n_init=2000)
+    assert st.scene_in_lds == 0
+    assert st.samples == chains * steps == cnt.samples
+    assert abs(st.rays - cnt.rays) / cnt.rays < 2e-3
+    assert rmse(film, ref) <= 1e-3 * max(1.0, float(np.abs(ref).max()))
+
+
 def test_sharded_chains_sum_to_single(ctx, cornell_obj):
     nx, ny = 32, 32
     ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, 1.0))
