@@ -36,14 +36,16 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def scene_spec(name, workdir):
+def scene_spec(name, workdir, tag=""):
+    """(scene kind, OBJ path, label).  cornell_1m is generated on first use;
+    `tag` keeps concurrent ranks on their own files."""
     if name == "cornell":
         return "cornell_box_obj", os.path.join(SCENES, "CornellBox-Original.obj"), "CornellBox-Original"
     if name == "veach":
         return "veach_mis", os.path.join(SCENES, "veach_mi.obj"), "veach_mi"
     if name == "cornell_1m":
         import first_raytracer_amd as frt
-        dst = os.path.join(workdir, "cornell_1m_k172.obj")
+        dst = os.path.join(workdir, f"cornell_1m_k172{tag}.obj")
         if not os.path.exists(dst):
             frt.write_tessellated_obj(os.path.join(SCENES, "CornellBox-Original.obj"), 172, dst)
         return "cornell_box_obj", dst, "cornell_1m (k=172, 1,005,858 tris)"
@@ -125,6 +127,8 @@ def main():
     ap.add_argument("--integrator", default="path", choices=["path", "pssmlt"],
                     help="pssmlt: C5 config, --spp = mutations per pixel")
     ap.add_argument("--chains", type=int, default=1 << 18, help="PSS-MLT chains (all ranks)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse the N-rank path with host-staged collectives (e.g. ranks sharing one GPU)")
     args = ap.parse_args()
     nx, ny = (int(x) for x in args.res.lower().split("x"))
 
@@ -138,13 +142,29 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    gloo = args.backend == "gloo"
+    if gloo:
+        local = local % torch.cuda.device_count()
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
+    def all_reduce(t, op=None):
+        """RCCL on device tensors; the gloo rehearsal stages through the host."""
+        kw = {} if op is None else {"op": op}
+        if gloo:
+            h = t.cpu()
+            dist.all_reduce(h, **kw)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, **kw)
+
     workdir = os.path.join(ROOT, "gpurun_out") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else "/tmp"
-    kind, obj, scene_name = scene_spec(args.scene, workdir)
+    kind, obj, scene_name = scene_spec(args.scene, workdir, tag=f"_r{rank}")
     t0 = time.perf_counter()
     hs = frt.HostScene(kind, obj, nx / ny)
     ctx = frt.Context(local)
@@ -164,14 +184,14 @@ def main():
         params = frt.RenderParams.make(nx, ny, args.spp, seed=args.seed, tile_size=args.tile,
                                        shard_index=rank, shard_count=world)
         from first_raytracer_amd.dist import TileGather
-        tg = TileGather(nx, ny, args.tile, world, rank, dev)
+        tg = TileGather(nx, ny, args.tile, world, rank, dev, stage_cpu=gloo)
     stream = torch.cuda.current_stream(dev)
 
     def step():
         if args.integrator == "pssmlt":
             st = ctx.render_device(params, mlt_film.data_ptr(), stream.cuda_stream)
             if world > 1:
-                dist.all_reduce(mlt_film)   # RCCL sum of the per-rank splat films
+                all_reduce(mlt_film)        # RCCL sum of the per-rank splat films
             return st
         st = ctx.render_device(params, tg.my_slots.data_ptr(), stream.cuda_stream)
         tg.gather()       # RCCL all-gather of the tile slots, rank 0 scatters into its film
@@ -198,10 +218,10 @@ def main():
     elapsed = time.perf_counter() - t_start
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         r = torch.tensor([float(rays)], dtype=torch.float64, device=dev)
-        dist.all_reduce(r, op=dist.ReduceOp.SUM)
+        all_reduce(r, op=dist.ReduceOp.SUM)
         rays = int(r.item())
 
     if rank == 0:
@@ -273,6 +293,8 @@ def main():
                           (f"PSS-MLT {cpu['sample']} on the same {nx}x{ny} frame ({cpu['rays']} rays, "
                            f"{cpu['seconds']:.1f} s); fp64 C restatement of pssmlt.cpp")},
         }
+        if gloo:
+            line["config"]["parallelism"] += " (gloo host-staged rehearsal)"
         if args.pfm:
             frt.write_pfm(args.pfm, film_np.reshape(ny, nx, 3))
         print(json.dumps(line), flush=True)

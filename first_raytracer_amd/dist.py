@@ -27,8 +27,11 @@ def shard_layout(nx, ny, tile, world):
 class TileGather:
     """All-gather of per-rank slot buffers + scatter into rank 0's film."""
 
-    def __init__(self, nx, ny, tile, world, rank, device):
+    def __init__(self, nx, ny, tile, world, rank, device, stage_cpu=False):
+        """stage_cpu: gather through host copies (a gloo rehearsal of the GPU
+        path on one device; RCCL gathers device buffers directly)."""
         self.nx, self.ny, self.world, self.rank = nx, ny, world, rank
+        self.stage_cpu = stage_cpu
         counts, slot_pix = shard_layout(nx, ny, tile, world)
         self.max_slots = max(counts)
         self.my_slots = torch.zeros(self.max_slots * 3, dtype=torch.float32, device=device)
@@ -44,7 +47,12 @@ class TileGather:
         """Collective: every rank calls it after rendering into self.my_slots."""
         src = self.my_slots
         if self.world > 1:
-            dist.all_gather_into_tensor(self.gathered, self.my_slots)
+            if self.stage_cpu:
+                g = torch.empty(self.gathered.numel(), dtype=torch.float32)
+                dist.all_gather_into_tensor(g, self.my_slots.cpu())
+                self.gathered.copy_(g)
+            else:
+                dist.all_gather_into_tensor(self.gathered, self.my_slots)
             src = self.gathered
         if self.rank == 0:
             self.film.view(-1, 3)[self.dst] = src.view(-1, 3)[self.valid]
