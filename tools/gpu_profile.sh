@@ -1,18 +1,27 @@
-# rocprofv3 kernel-trace summary + PMC HBM-traffic passes (FETCH_SIZE and
-# WRITE_SIZE in separate passes, MI355X_MICROARCH.md "rocprofv3 PMC slots"),
-# then the cornell_1m bench.  Chained: the first failure ends the script.
+# rocprofv3 kernel-trace summaries of the bench command (Cornell, cornell_1m),
+# then PMC HBM-traffic passes (FETCH_SIZE and WRITE_SIZE in separate passes,
+# MI355X_MICROARCH.md "rocprofv3 PMC slots").  Chained: the first failure ends
+# the script.  Summaries: python tools/pmc_traffic.py (on the CPU side).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 TAG=${TAG:-r01}
-mkdir -p gpurun_out/prof_$TAG
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG/trace -o run -- \
-    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof_$TAG/trace_bench.json 2> gpurun_out/prof_$TAG/trace_bench.log \
- && timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_$TAG/pmc_fetch -o run -- \
-    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/prof_$TAG/pmc_fetch.json 2> gpurun_out/prof_$TAG/pmc_fetch.log \
- && timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_$TAG/pmc_write -o run -- \
-    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/prof_$TAG/pmc_write.json 2> gpurun_out/prof_$TAG/pmc_write.log \
- && timeout -k 10 400 python3 bench.py --scene cornell_1m > gpurun_out/prof_$TAG/bench_1m.json 2> gpurun_out/prof_$TAG/bench_1m.log
+O=gpurun_out/prof_$TAG
+mkdir -p $O
+trace() {  # name, bench args
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$1 -o run -- \
+      python3 bench.py $2 > $O/trace_$1.json 2> $O/trace_$1.log
+}
+pmc() {  # name, counter, bench args
+  timeout -k 10 300 rocprofv3 --pmc $2 --output-format csv -d $O/pmc_$1 -o run -- \
+      python3 bench.py $3 > $O/pmc_$1.json 2> $O/pmc_$1.log
+}
+trace cornell "--steps 3 --warmup 1 --no-cpu-baseline" \
+ && trace 1m "--scene cornell_1m --steps 2 --warmup 1 --no-cpu-baseline" \
+ && pmc fetch_cornell FETCH_SIZE "--steps 1 --warmup 0 --no-cpu-baseline" \
+ && pmc write_cornell WRITE_SIZE "--steps 1 --warmup 0 --no-cpu-baseline" \
+ && pmc fetch_1m FETCH_SIZE "--scene cornell_1m --steps 1 --warmup 0 --no-cpu-baseline" \
+ && pmc write_1m WRITE_SIZE "--scene cornell_1m --steps 1 --warmup 0 --no-cpu-baseline"
 rc=$?
-echo "rc=$rc" > gpurun_out/prof_$TAG/rc.txt
+echo "rc=$rc" > $O/rc.txt
 exit $rc
