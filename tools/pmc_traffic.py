@@ -33,7 +33,7 @@ def main():
     kern = {}
     for src, name, scale in ((f, "FETCH_SIZE", 1.0), (w, "WRITE_SIZE", 1.0)):
         for (did, kname), v in src.items():
-            short = kname.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+            short = kname.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
             kern.setdefault(short, {}).setdefault(name, []).append(v * scale)
     summary = {}
     for k, v in kern.items():
