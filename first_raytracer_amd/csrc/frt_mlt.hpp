@@ -107,10 +107,7 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
 {
     PathState &P = M.P;
     if (P.shadow) {
-        if (h.prim < 0) P.L = P.L + P.nee;
-        P.shadow = false;
-        P.rd = P.nxt_d; P.rtmax = kTMaxClosest;            // P.ro is already the extension origin
-        ++P.depth;
+        path_after_shadow(P, h.prim < 0);
         if (P.depth <= kMltMaxPath) ++n_ext;
         return false;
     }

@@ -416,14 +416,23 @@ FRT_HD void path_begin(PathState &P, const DevScene &S, int px, int py, int nx, 
     P.prev_p = mk3(0, 0, 0);
 }
 
+// Shadow ray done (path.cpp:50-77): add the NEE term if unoccluded, then the
+// extension ray from the same origin.  The megakernel runs this inside its
+// traversal loop, so shading phases only see closest-hit results.
+FRT_HD void path_after_shadow(PathState &P, bool unoccluded)
+{
+    if (unoccluded) P.L = P.L + P.nee;
+    P.shadow = false;
+    P.rd = P.nxt_d; P.rtmax = kTMaxClosest;                // P.ro is already the extension origin
+    ++P.depth;
+}
+
 // Returns true when the path is finished (P.L is the sample's radiance).
 FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_depth, uint32_t &n_ext, uint32_t &n_sh)
 {
-    if (P.shadow) {                                     // path.cpp:50-77
-        if (h.prim < 0) P.L = P.L + P.nee;
-        P.shadow = false;
-        P.rd = P.nxt_d; P.rtmax = kTMaxClosest;            // P.ro is already the extension origin
-        ++P.depth; ++n_ext;
+    if (P.shadow) {
+        path_after_shadow(P, h.prim < 0);
+        ++n_ext;
         return false;
     }
     if (h.prim < 0) {                                   // path.cpp:115 environment

@@ -120,10 +120,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         // done wait here only while the rest of the wave needs few more steps;
         // then they shade together while the stragglers keep their state.
         for (;;) {
+            bool shadow_done = false;
             if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, P.ro, P.rd, P.shadow, stk, ovf)) {
-                tracing = false;
-                pending = true;
+                if (P.shadow) {                 // finish the shadow ray here, keep traversing
+                    path_after_shadow(P, T.h.prim < 0);
+                    shadow_done = true;
+                    tracing = trav_begin_world<WORLD>(T, S, P.ro, P.rd, P.rtmax);
+                    pending = !tracing;
+                } else {
+                    tracing = false;
+                    pending = true;
+                }
             }
+            n_ext += __popcll(__ballot(shadow_done));
             if (__popcll(__ballot(tracing)) <= W.trav_min) break;
         }
         // ---- shade the finished rays ----
@@ -319,10 +328,25 @@ __global__ __launch_bounds__(kBlock) void mlt_megakernel(const DevScene S0, cons
     for (;;) {
         // ---- traversal steps until at most trav_min lanes still traverse ----
         for (;;) {
+            bool ext = false;
             if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, M.P.ro, M.P.rd, M.P.shadow, stk, ovf)) {
-                tracing = false;
-                pending = true;
+                if (M.P.shadow) {               // finish the shadow ray here (mlt_shade's shadow branch)
+                    path_after_shadow(M.P, T.h.prim < 0);
+                    if (mlt_beyond(M)) {
+                        beyond = true;
+                        tracing = false;
+                        pending = true;
+                    } else {
+                        ext = true;
+                        tracing = trav_begin_world<WORLD>(T, S, M.P.ro, M.P.rd, M.P.rtmax);
+                        pending = !tracing;
+                    }
+                } else {
+                    tracing = false;
+                    pending = true;
+                }
             }
+            if (ext) ++n_ext;                   // per-lane counters, reduced at the end
             if (__popcll(__ballot(tracing)) <= W.trav_min) break;
         }
         bool next_ray = false, done = false;
