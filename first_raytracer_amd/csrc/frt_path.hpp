@@ -42,7 +42,8 @@ struct DevScene {
     // element i, part k of nodes / tris / tshade lives at [i * es + k * ps]:
     // interleaved in HBM (es = parts, ps = 1), planar in LDS (es = 1, ps = count)
     // so that lanes reading distinct elements hit distinct LDS bank slots
-    int node_es, node_ps, tri_es, tri_ps, sh_es, sh_ps;
+    int node_es, node_ps, tri_es, tri_ps, sh_es, sh_ps, node4_es, node4_ps;
+    int n_nodes4;
     float root_lo[3], root_hi[3];
     f3 cam_o, cam_llc, cam_h, cam_v, cam_u, cam_vv, cam_w;
     float lens_r, cam_half_height;
@@ -60,6 +61,7 @@ constexpr int kLeafMax = 4, kLeafDefault = 4;
 constexpr int kTravMinLds = 12, kTravMinHbm = 32;   // path_megakernel: see trav_min()
 
 FRT_HD float4 node_part(const DevScene &S, int i, int k) { return S.nodes[i * S.node_es + k * S.node_ps]; }
+FRT_HD uint4 node4_part(const DevScene &S, int i, int k) { return S.nodes4[i * S.node4_es + k * S.node4_ps]; }
 FRT_HD float4 tri_part(const DevScene &S, int i, int k) { return S.tris[i * S.tri_es + k * S.tri_ps]; }
 FRT_HD float4 shade_part(const DevScene &S, int i, int k) { return S.tshade[i * S.sh_es + k * S.sh_ps]; }
 
@@ -188,8 +190,8 @@ FRT_HD bool bvh4_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *
         return sp < LSTACK ? stk[sp * STRIDE] : ovf[sp - LSTACK];
     };
     while ((unsigned)node < (unsigned)kSentinel) {
-        const uint4 w0 = S.nodes4[4 * node], w1 = S.nodes4[4 * node + 1];
-        const uint4 w2 = S.nodes4[4 * node + 2], w3 = S.nodes4[4 * node + 3];
+        const uint4 w0 = node4_part(S, node, 0), w1 = node4_part(S, node, 1);
+        const uint4 w2 = node4_part(S, node, 2), w3 = node4_part(S, node, 3);
         const SlabRay &sr = T.sr;
         const float ax = u2f((w0.w & 0xffu) << 23) * sr.invd.x, bx = fmaf(u2f(w0.x), sr.invd.x, sr.oinv.x);
         const float ay = u2f(((w0.w >> 8) & 0xffu) << 23) * sr.invd.y, by = fmaf(u2f(w0.y), sr.invd.y, sr.oinv.y);

@@ -67,21 +67,33 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t m)
 // (ds_read_b128 instead of L1/L2 round trips).  Planar copies: part k of
 // element i at [k * count + i], so lanes reading different elements of the
 // same part hit different banks.
+template <bool WIDE>
 __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
 {
     float4 *l4 = reinterpret_cast<float4 *>(lds_base);
     const DevScene S0 = S;
-    const int nn = 4 * S0.n_nodes, nt = 3 * S0.n_tris, ns = 2 * S0.n_tris, nm = 2 * S0.n_mats;
-    for (int i = threadIdx.x; i < nn; i += kBlock) l4[(i & 3) * S0.n_nodes + (i >> 2)] = S0.nodes[i];
+    const int nn = WIDE ? 4 * S0.n_nodes4 : 4 * S0.n_nodes;
+    const int nt = 3 * S0.n_tris, ns = 2 * S0.n_tris, nm = 2 * S0.n_mats;
+    if constexpr (WIDE) {
+        const float4 *src = reinterpret_cast<const float4 *>(S0.nodes4);
+        for (int i = threadIdx.x; i < nn; i += kBlock) l4[(i & 3) * S0.n_nodes4 + (i >> 2)] = src[i];
+    } else {
+        for (int i = threadIdx.x; i < nn; i += kBlock) l4[(i & 3) * S0.n_nodes + (i >> 2)] = S0.nodes[i];
+    }
     for (int i = threadIdx.x; i < nt; i += kBlock) l4[nn + (i % 3) * S0.n_tris + i / 3] = S0.tris[i];
     for (int i = threadIdx.x; i < ns; i += kBlock) l4[nn + nt + (i & 1) * S0.n_tris + (i >> 1)] = S0.tshade[i];
     for (int i = threadIdx.x; i < nm; i += kBlock) l4[nn + nt + ns + i] = S0.mats[i];
     __syncthreads();
-    S.nodes = l4;
+    if constexpr (WIDE) {
+        S.nodes4 = reinterpret_cast<const uint4 *>(l4);
+        S.node4_es = 1; S.node4_ps = S0.n_nodes4;
+    } else {
+        S.nodes = l4;
+        S.node_es = 1; S.node_ps = S0.n_nodes;
+    }
     S.tris = l4 + nn;
     S.tshade = l4 + nn + nt;
     S.mats = l4 + nn + nt + ns;
-    S.node_es = 1; S.node_ps = S0.n_nodes;
     S.tri_es = 1; S.tri_ps = S0.n_tris;
     S.sh_es = 1; S.sh_ps = S0.n_tris;
 }
@@ -96,7 +108,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     extern __shared__ __attribute__((aligned(16))) int lds_mem[];   // [STACK][kBlock] stack, then the scene
     int *stk = lds_mem + threadIdx.x;                                 // one LDS column per lane
     DevScene S = S0;
-    if constexpr (LDS_SCENE) scene_to_lds(S, lds_mem + STACK * kBlock);
+    if constexpr (LDS_SCENE) scene_to_lds<WORLD == kWorldBvh4>(S, lds_mem + STACK * kBlock);
     const int lane = threadIdx.x & 63;
     const int T2 = W.tile * W.tile;
 
@@ -305,7 +317,7 @@ __global__ __launch_bounds__(kBlock) void mlt_megakernel(const DevScene S0, cons
     extern __shared__ __attribute__((aligned(16))) int lds_mem[];
     int *stk = lds_mem + threadIdx.x;
     DevScene S = S0;
-    if constexpr (LDS_SCENE) scene_to_lds(S, lds_mem + STACK * kBlock);
+    if constexpr (LDS_SCENE) scene_to_lds<WORLD == kWorldBvh4>(S, lds_mem + STACK * kBlock);
     const int lane = threadIdx.x & 63;
     bool have = false, exhausted = false, init = false, large = false;
     uint32_t j = 0, c = 0;
@@ -460,7 +472,7 @@ struct frt_ctx {
     int world_kind = 0, stack_needed = 0;
     bool has_bvh4 = false;
     int depth4 = 0;
-    size_t scene_lds_bytes = 0;
+    size_t scene_lds_bytes = 0, scene_lds_bytes4 = 0;   // LDS copy with binary / 4-wide nodes
     double last_mlt_b = 0.0;
     std::vector<void *> scene_bufs;
     // workspace
@@ -911,7 +923,9 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     S.n_nodes = (int)(F.nodes.size() / 4);
     S.n_tris = nt;
     S.n_mats = nm;
+    S.n_nodes4 = (int)(F.nodes4.size() / 4);
     S.node_es = 4; S.node_ps = 1;
+    S.node4_es = 4; S.node4_ps = 1;
     S.tri_es = 3; S.tri_ps = 1;
     S.sh_es = 2; S.sh_ps = 1;
     S.world_kind = sv->world_kind;
@@ -962,6 +976,7 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
     c->has_bvh4 = F.has4;
     c->depth4 = F.depth4;
     c->scene_lds_bytes = sizeof(float4) * (F.nodes.size() + F.tris.size() + F.tshade.size() + F.mats.size());
+    c->scene_lds_bytes4 = sizeof(float4) * (F.nodes4.size() + F.tris.size() + F.tshade.size() + F.mats.size());
     c->have_scene = true;
     return FRT_OK;
 }
@@ -1135,6 +1150,7 @@ static Launcher bvh_launcher(int waves, size_t sb)
     return make_launcher<STACK, WORLD, LDS>(sb);
 }
 constexpr int kBvh4LdsStack = 16;   // 16 KiB of LDS per block; deeper entries go to scratch
+constexpr int kBvh4LdsStackSmall = 8;   // LDS-resident scenes (shallow trees)
 static int pick_launcher(const frt_ctx *c, int flags, Launcher &L)
 {
     if (c->world_kind == FRT_WORLD_LIST) { L = make_launcher<16, FRT_WORLD_LIST, false>(0); return FRT_OK; }
@@ -1148,6 +1164,12 @@ static int pick_launcher(const frt_ctx *c, int flags, Launcher &L)
     if (flags & FRT_FLAG_WAVES4) waves = 0;   // the compiler's own allocation (~120 VGPRs, 4 waves)
     if (flags & FRT_FLAG_WAVES5) waves = 5;
     if (flags & FRT_FLAG_WAVES6) waves = 6;
+    // LDS-resident scenes, 4-wide (A/B: FRT_FLAG_BVH4)
+    if (lds && (flags & FRT_FLAG_BVH4) && c->has_bvh4 && c->scene_lds_bytes4 <= kLdsSceneBytes &&
+        bvh4_stack_fits(c->depth4, kBvh4LdsStackSmall)) {
+        L = bvh_launcher<kBvh4LdsStackSmall, true, kWorldBvh4>(waves, c->scene_lds_bytes4);
+        return FRT_OK;
+    }
     // HBM-resident scenes: the 4-wide quantized BVH (half the bytes per box test)
     if (!lds && c->has_bvh4 && !(flags & FRT_FLAG_BVH2) && bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
         L = bvh_launcher<kBvh4LdsStack, false, kWorldBvh4>(waves, 0);
