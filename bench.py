@@ -166,10 +166,12 @@ def main():
     workdir = os.path.join(ROOT, "gpurun_out") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else "/tmp"
     kind, obj, scene_name = scene_spec(args.scene, workdir, tag=f"_r{rank}")
     t0 = time.perf_counter()
-    hs = frt.HostScene(kind, obj, nx / ny)
+    hs = frt.HostScene(kind, obj, nx / ny)       # OBJ load + reference-topology BVH build (host)
+    t1 = time.perf_counter()
     ctx = frt.Context(local)
-    ctx.upload(hs)
-    setup_s = time.perf_counter() - t0
+    ctx.upload(hs)                               # flatten + leaf collapse + BVH4Q + copy to HBM
+    t2 = time.perf_counter()
+    build_s, upload_s, setup_s = t1 - t0, t2 - t1, t2 - t0
 
     if args.integrator == "pssmlt":
         # chains shard over ranks (chain c -> rank c mod N); splat films are summed
@@ -282,7 +284,8 @@ def main():
             "rmse": None if cpu is None else cpu["rmse"],
             "mutations_per_step": int(last.samples) if args.integrator == "pssmlt" else None,
             "rays_per_step": int(rays // args.steps),
-            "setup_s": round(setup_s, 2),
+            "setup_s": round(setup_s, 2), "host_build_s": round(build_s, 2), "upload_s": round(upload_s, 2),
+            "value_per_gpu": round(value / world, 1),
             "image_mean": [round(float(x), 6) for x in film_np.reshape(-1, 3).mean(0)],
             "roofline": roofline,
             "cpu_baseline": None if cpu is None else {

@@ -108,7 +108,8 @@ _lib = None
 
 # every symbol include/frt.h declares
 EXPORTS = ("frt_get_abi_version", "frt_create", "frt_destroy", "frt_last_error", "frt_upload_scene",
-           "frt_shard_slot_count", "frt_shard_slots", "frt_render", "frt_render_device", "frt_scene_create",
+           "frt_shard_slot_count", "frt_shard_slots", "frt_render", "frt_render_multi", "frt_render_device",
+           "frt_scene_create",
            "frt_scene_view_get", "frt_scene_info", "frt_scene_destroy", "frt_write_tessellated_obj",
            "frt_write_pfm", "frt_selftest_path_host", "frt_selftest_mlt_paths_host")
 
@@ -142,6 +143,8 @@ def lib():
     L.frt_shard_slots.argtypes = [ctypes.POINTER(RenderParams), vp]
     L.frt_render.argtypes = [vp, ctypes.POINTER(RenderParams), vp, ctypes.POINTER(Stats)]
     L.frt_render_device.argtypes = [vp, ctypes.POINTER(RenderParams), vp, vp, ctypes.POINTER(Stats)]
+    L.frt_render_multi.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.POINTER(RenderParams), vp,
+                                   ctypes.POINTER(Stats)]
     L.frt_scene_create.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_double, ctypes.POINTER(vp)]
     L.frt_scene_view_get.argtypes = [vp, ctypes.POINTER(SceneView)]
     L.frt_scene_info.argtypes = [vp, ctypes.POINTER(HostSceneInfo)]
@@ -248,6 +251,19 @@ class Context:
             self.close()
         except Exception:
             pass
+
+
+def render_multi(contexts, params, film=None):
+    """One process, several GPUs (frt_render_multi): contexts[i] renders shard
+    (i, n) of the whole-frame `params` on its own host thread.  Returns (film, stats)."""
+    if film is None:
+        film = np.zeros((params.ny, params.nx, 3), np.float32)
+    assert film.dtype == np.float32 and film.flags.c_contiguous and film.size == params.nx * params.ny * 3
+    arr = (ctypes.c_void_p * len(contexts))(*[c.ptr for c in contexts])
+    st = Stats()
+    _check(lib().frt_render_multi(arr, len(contexts), ctypes.byref(params), film.ctypes.data, ctypes.byref(st)),
+           "frt_render_multi", contexts[0].ptr)
+    return film, st
 
 
 def shard_slots(params):

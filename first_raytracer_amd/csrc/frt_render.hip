@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "frt.h"
@@ -1424,6 +1425,55 @@ extern "C" int frt_render(frt_ctx *c, const frt_render_params *p, float *film_rg
         film_rgb[3 * (size_t)px + 0] = host[3 * s + 0];
         film_rgb[3 * (size_t)px + 1] = host[3 * s + 1];
         film_rgb[3 * (size_t)px + 2] = host[3 * s + 2];
+    }
+    return FRT_OK;
+}
+
+// One process, n GPUs (SURVEY 8(b) frt_render_multi; what frt::path_gpu does
+// in C++): context i renders shard (i, n) of the request on its own host
+// thread.  Path shards write disjoint pixels of film_rgb; PSS-MLT shard films
+// are summed into film_rgb in the fixed order 0..n-1.  Stats: ray and sample
+// counts summed, kernel_ms / total_ms the slowest shard's.
+extern "C" int frt_render_multi(frt_ctx **ctxs, int n, const frt_render_params *p, float *film_rgb, frt_stats *st)
+{
+    if (!ctxs || n <= 0 || !p || !film_rgb) return FRT_E_INVALID;
+    for (int i = 0; i < n; ++i)
+        if (!ctxs[i]) return FRT_E_INVALID;
+    if (!params_ok(p) || p->shard_count != 1 || p->shard_index != 0)
+        return set_err(ctxs[0], FRT_E_INVALID, "frt_render_multi: params must describe the whole frame (shard 0 of 1)");
+    const bool mlt = p->integrator == FRT_INTEGRATOR_PSSMLT;
+    const size_t film_n = (size_t)p->nx * p->ny * 3;
+    std::vector<std::vector<float>> part(mlt ? n : 0, std::vector<float>(mlt ? film_n : 0, 0.0f));
+    std::vector<frt_stats> sts(n);
+    std::vector<int> rcs(n, FRT_OK);
+    auto work = [&](int i) {
+        frt_render_params q = *p;
+        q.shard_index = i;
+        q.shard_count = n;
+        rcs[i] = frt_render(ctxs[i], &q, mlt ? part[i].data() : film_rgb, &sts[i]);
+    };
+    std::vector<std::thread> th;
+    for (int i = 1; i < n; ++i) th.emplace_back(work, i);
+    work(0);
+    for (auto &t : th) t.join();
+    for (int i = 0; i < n; ++i)
+        if (rcs[i] != FRT_OK) {
+            if (i != 0) set_err(ctxs[0], rcs[i], std::string("shard ") + std::to_string(i) + ": " + ctxs[i]->err);
+            return rcs[i];
+        }
+    if (mlt)
+        for (int i = 0; i < n; ++i)
+            for (size_t k = 0; k < film_n; ++k) film_rgb[k] += part[i][k];
+    if (st) {
+        frt_stats a = sts[0];
+        for (int i = 1; i < n; ++i) {
+            a.camera_rays += sts[i].camera_rays; a.extension_rays += sts[i].extension_rays;
+            a.shadow_rays += sts[i].shadow_rays; a.samples += sts[i].samples;
+            a.pixels += mlt ? 0 : sts[i].pixels; a.work_items += sts[i].work_items;
+            a.kernel_ms = std::max(a.kernel_ms, sts[i].kernel_ms);
+            a.total_ms = std::max(a.total_ms, sts[i].total_ms);
+        }
+        *st = a;
     }
     return FRT_OK;
 }

@@ -3,7 +3,9 @@
 // compile-time choices.  Writes the linear film as PFM (image.h:89-118).
 //
 //   frt_render --scene cornell|veach|obj --obj FILE [--res 1920x1080] [--ns 512]
-//              [--seed 0] [--gpus 1] [--out out.pfm]
+//              [--seed 0] [--gpus 1] [--integrator path|pssmlt] [--chains 262144] [--out out.pfm]
+//
+// --integrator pssmlt: renderer<pssmlt_gpu>, --ns = mutations per pixel.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -13,8 +15,8 @@
 
 int main(int argc, char **argv)
 {
-    std::string scene = "cornell", obj, out = "out.pfm";
-    int nx = 512, ny = 512, gpus = 1;
+    std::string scene = "cornell", obj, out = "out.pfm", integrator = "path";
+    int nx = 512, ny = 512, gpus = 1, chains = 1 << 18;
     long ns = 100;
     unsigned seed = 0;
     for (int i = 1; i < argc; ++i) {
@@ -30,6 +32,8 @@ int main(int argc, char **argv)
         else if (a == "--seed") seed = (unsigned)std::strtoul(next(), nullptr, 10);
         else if (a == "--gpus") gpus = std::atoi(next());
         else if (a == "--out") out = next();
+        else if (a == "--integrator") integrator = next();
+        else if (a == "--chains") chains = std::atoi(next());
         else { std::fprintf(stderr, "unknown flag %s\n", a.c_str()); return 2; }
     }
     if (obj.empty()) { std::fprintf(stderr, "--obj is required\n"); return 2; }
@@ -40,11 +44,23 @@ int main(int argc, char **argv)
         std::printf("BVH construction took me %g seconds (%d triangles, depth %d).\n", s.info().build_ms * 1e-3,
                     s.info().n_tris, s.info().bvh_depth);
         frt::viewer film(nx, ny, (uint64_t)ns);
-        frt::renderer<frt::path_gpu> render;
-        render.devices.clear();
-        for (int g = 0; g < gpus; ++g) render.devices.push_back(g);
-        render.seed = seed;
-        render.Render(&s, film);
+        auto run = [&](auto &render) {
+            render.devices.clear();
+            for (int g = 0; g < gpus; ++g) render.devices.push_back(g);
+            render.seed = seed;
+            render.Render(&s, film);
+        };
+        if (integrator == "pssmlt") {
+            frt::renderer<frt::pssmlt_gpu> render;
+            render.chains = chains;
+            run(render);
+        } else if (integrator == "path") {
+            frt::renderer<frt::path_gpu> render;
+            run(render);
+        } else {
+            std::fprintf(stderr, "unknown integrator %s\n", integrator.c_str());
+            return 2;
+        }
         film.save_pfm(out);
         std::printf("Saved %s\n", out.c_str());
     } catch (const std::exception &e) {

@@ -158,6 +158,13 @@ int frt_shard_slots(const frt_render_params *p, int32_t *slot_pixel);
  * AccumulatePathContribution pssmlt.cpp:19-38). */
 int frt_render(frt_ctx *ctx, const frt_render_params *p, float *film_rgb, frt_stats *st);
 
+/* One process, n GPUs: ctxs[i] (each with the scene uploaded) renders shard
+ * (i, n) of the whole-frame request `p` (shard_index 0, shard_count 1) on its
+ * own host thread; the full film lands in film_rgb (PSS-MLT: the shard films
+ * summed in order 0..n-1, added to film_rgb).  Replaces the multi-worker
+ * path::Render task graph (path.cpp:118-148) across devices. */
+int frt_render_multi(frt_ctx **ctxs, int n, const frt_render_params *p, float *film_rgb, frt_stats *st);
+
 /* Device variant: writes the shard's slots (frt_shard_slot_count * 3 floats,
  * slot order) into device memory `slots_rgb` on `hip_stream` (NULL = the
  * context's stream) and returns after the work has completed.  PSS-MLT: the

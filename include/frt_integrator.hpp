@@ -99,9 +99,46 @@ struct viewer {
     std::vector<double> fout_image;
 };
 
-// path_gpu: the drop-in for `path` (path.h:8-18).  Render() renders every tile
-// of the frame on the listed GPUs (tile t -> device t % n, one host thread per
-// device, disjoint film writes) and stores the per-pixel means in the viewer.
+// One frt_ctx per listed device with the scene uploaded (uploads run in
+// parallel, one host thread per device).
+class device_set {
+public:
+    device_set(const std::vector<int> &devices, const frt_scene_view &view) : ctx_(devices.size(), nullptr)
+    {
+        std::vector<std::string> errs(devices.size());
+        auto up = [&](size_t i) {
+            try {
+                check(frt_create(devices[i], &ctx_[i]), "frt_create");
+                check(frt_upload_scene(ctx_[i], &view), "frt_upload_scene", ctx_[i]);
+            } catch (const std::exception &e) {
+                errs[i] = e.what();
+            }
+        };
+        std::vector<std::thread> th;
+        for (size_t i = 1; i < devices.size(); ++i) th.emplace_back(up, i);
+        if (!devices.empty()) up(0);
+        for (auto &t : th) t.join();
+        for (const std::string &e : errs)
+            if (!e.empty()) { release(); throw error(FRT_E_HIP, e); }
+    }
+    ~device_set() { release(); }
+    device_set(const device_set &) = delete;
+    device_set &operator=(const device_set &) = delete;
+    frt_ctx **data() { return ctx_.data(); }
+    int size() const { return (int)ctx_.size(); }
+
+private:
+    void release()
+    {
+        for (frt_ctx *&c : ctx_)
+            if (c) { frt_destroy(c); c = nullptr; }
+    }
+    std::vector<frt_ctx *> ctx_;
+};
+
+// path_gpu: the drop-in for `path` (path.h:8-18).  Render() renders the frame
+// on the listed GPUs with frt_render_multi (tile t -> device t % n) and stores
+// the per-pixel means in the viewer.
 struct path_gpu {
     std::vector<int> devices{0};
     uint32_t seed = 0;
@@ -112,48 +149,48 @@ struct path_gpu {
 
     void Render(Scene *scene, viewer *film)
     {
-        const int n = (int)devices.size();
-        std::vector<frt_stats> st(n);
-        std::vector<std::string> errs(n);
-        std::vector<std::vector<float>> films(n, std::vector<float>((size_t)film->nx * film->ny * 3, 0.0f));
-        const frt_scene_view view = scene->view();
-        auto work = [&](int i) {
-            frt_ctx *ctx = nullptr;
-            try {
-                check(frt_create(devices[i], &ctx), "frt_create");
-                check(frt_upload_scene(ctx, &view), "frt_upload_scene", ctx);
-                frt_render_params p{};
-                p.nx = film->nx; p.ny = film->ny; p.spp = (int)film->ns; p.seed = seed;
-                p.max_depth = max_depth; p.integrator = FRT_INTEGRATOR_PATH; p.tile_size = tile_size;
-                p.shard_index = i; p.shard_count = n;
-                check(frt_render(ctx, &p, films[i].data(), &st[i]), "frt_render", ctx);
-            } catch (const std::exception &e) {
-                errs[i] = e.what();
-            }
-            if (ctx) frt_destroy(ctx);
-        };
-        std::vector<std::thread> th;
-        for (int i = 1; i < n; ++i) th.emplace_back(work, i);
-        work(0);
-        for (auto &t : th) t.join();
-        for (int i = 0; i < n; ++i)
-            if (!errs[i].empty()) throw error(FRT_E_HIP, errs[i]);
-        // gather: shard i owns tiles t % n == i
-        const int T = tile_size, ntx = (film->nx + T - 1) / T;
+        device_set gpus(devices, scene->view());
+        frt_render_params p{};
+        p.nx = film->nx; p.ny = film->ny; p.spp = (int)film->ns; p.seed = seed;
+        p.max_depth = max_depth; p.integrator = FRT_INTEGRATOR_PATH; p.tile_size = tile_size;
+        p.shard_index = 0; p.shard_count = 1;
+        std::vector<float> rgb((size_t)film->nx * film->ny * 3, 0.0f);
+        check(frt_render_multi(gpus.data(), gpus.size(), &p, rgb.data(), &last_stats), "frt_render_multi",
+              gpus.data()[0]);
         for (int y = 0; y < film->ny; ++y)
             for (int x = 0; x < film->nx; ++x) {
-                const int owner = ((y / T) * ntx + (x / T)) % n;
-                const float *px = &films[owner][3 * ((size_t)y * film->nx + x)];
+                const float *px = &rgb[3 * ((size_t)y * film->nx + x)];
                 film->store_mean(x, y, px[0], px[1], px[2]);
             }
-        last_stats = frt_stats{};
-        for (const frt_stats &s : st) {
-            last_stats.camera_rays += s.camera_rays; last_stats.extension_rays += s.extension_rays;
-            last_stats.shadow_rays += s.shadow_rays; last_stats.samples += s.samples;
-            last_stats.pixels += s.pixels; last_stats.work_items += s.work_items;
-            last_stats.kernel_ms = std::max(last_stats.kernel_ms, s.kernel_ms);
-            last_stats.total_ms = std::max(last_stats.total_ms, s.total_ms);
-        }
+    }
+};
+
+// pssmlt_gpu: the drop-in for `pssmlt` (pssmlt.h:20-76) -- Kelemen PSS-MLT with
+// film->ns mutations per pixel over `chains` GPU chains (chain c -> device
+// c % n).  The splat film is the image (AccumulatePathContribution).
+struct pssmlt_gpu {
+    std::vector<int> devices{0};
+    uint32_t seed = 0;
+    int chains = 1 << 18;
+    int bootstrap = 10000;  // pssmlt.cpp:303
+    frt_stats last_stats{};
+    static constexpr bool using_custom_viewer = false;
+
+    void Render(Scene *scene, viewer *film)
+    {
+        device_set gpus(devices, scene->view());
+        frt_render_params p{};
+        p.nx = film->nx; p.ny = film->ny; p.spp = (int)film->ns; p.seed = seed;
+        p.max_depth = 10; p.integrator = FRT_INTEGRATOR_PSSMLT; p.tile_size = 32;
+        p.shard_index = 0; p.shard_count = 1; p.mlt_chains = chains; p.mlt_bootstrap = bootstrap;
+        std::vector<float> rgb((size_t)film->nx * film->ny * 3, 0.0f);
+        check(frt_render_multi(gpus.data(), gpus.size(), &p, rgb.data(), &last_stats), "frt_render_multi",
+              gpus.data()[0]);
+        for (int y = 0; y < film->ny; ++y)
+            for (int x = 0; x < film->nx; ++x) {
+                const float *px = &rgb[3 * ((size_t)y * film->nx + x)];
+                film->store_mean(x, y, px[0], px[1], px[2]);
+            }
     }
 };
 

@@ -177,6 +177,30 @@ def test_deterministic_and_shard_invariant(ctx, cornell_obj):
     assert np.allclose(a, c, rtol=1e-5, atol=1e-6)     # chunking only regroups the fp32 sums
 
 
+def test_render_multi_matches_single(ctx, cornell_obj):
+    """frt_render_multi over 3 contexts (all on device 0 here; one per GPU in
+    production) gives the single-context film bit for bit, and PSS-MLT shard
+    films sum to the single-context film within fp32 atomic-order noise."""
+    nx, ny, spp = 80, 60, 8
+    hs = frt.HostScene("cornell_box_obj", cornell_obj, nx / ny)
+    ctx.upload(hs)
+    one, st1 = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=31, tile_size=16))
+    extra = [frt.Context(0) for _ in range(2)]
+    try:
+        for c in extra:
+            c.upload(hs)
+        many, stm = frt.render_multi([ctx] + extra, frt.RenderParams.make(nx, ny, spp, seed=31, tile_size=16))
+        assert np.array_equal(one, many)
+        assert stm.rays == st1.rays and stm.pixels == nx * ny
+        p = frt.RenderParams.pssmlt(nx, ny, 4, 1200, seed=5, bootstrap=1000)
+        m1, _ = ctx.render(p)
+        mm, _ = frt.render_multi([ctx] + extra, p)
+        assert np.allclose(m1, mm, rtol=1e-4, atol=1e-5)
+    finally:
+        for c in extra:
+            c.close()
+
+
 def test_device_output_slots(ctx, cornell_obj):
     import torch
     nx, ny, spp = 64, 48, 4
