@@ -64,7 +64,7 @@ def cpu_baseline(kind, obj, nx, ny, spp, seed, npix, threads, film, seconds):
     """The oracle (fp64 C restatement) on a bounded pixel sample of the same
     frame and RNG streams: CPU Mrays/s, reference traversal counters (for
     B_ray) and the RMSE of the GPU film on those pixels.  npix = 0: calibrate
-    on 512 pixels, then size the sample to about `seconds` of CPU work."""
+    on growing samples (from 512 pixels) until one takes about `seconds` of CPU work."""
     import oracle
     sc = oracle.OracleScene(kind, obj, nx / ny)
 
@@ -74,10 +74,15 @@ def cpu_baseline(kind, obj, nx, ny, spp, seed, npix, threads, film, seconds):
         out, cnt = sc.render(nx, ny, spp, seed=seed, pixels=pix, nthreads=threads)
         return pix, out, cnt, time.perf_counter() - t0
 
-    if npix <= 0:
-        _, _, _, dt = run(512)
-        npix = int(min(nx * ny, max(512, 512 * seconds / max(dt, 1e-3))))
-    pix, out, cnt, dt = run(npix)
+    if npix > 0:
+        pix, out, cnt, dt = run(npix)
+    else:                                   # grow the sample until it takes >= seconds/2
+        npix = 512
+        while True:
+            pix, out, cnt, dt = run(npix)
+            if dt >= 0.5 * seconds or npix >= nx * ny:
+                break
+            npix = int(min(nx * ny, npix * min(16.0, max(2.0, seconds / max(dt, 1e-3)))))
     rays = cnt.rays
     gpu = film.reshape(-1, 3)[pix].astype(np.float64)
     rmse = float(np.sqrt(np.mean((gpu - out) ** 2)))
@@ -90,7 +95,7 @@ def cpu_baseline(kind, obj, nx, ny, spp, seed, npix, threads, film, seconds):
 
 def cpu_baseline_mlt(kind, obj, nx, ny, seed, threads, seconds):
     """The oracle's PSS-MLT on a bounded sample of the same frame: chains x 512
-    mutations, the chain count calibrated (256 chains first) to about
+    mutations, the chain count grown (from 256) until a run takes about
     `seconds` of CPU work."""
     import oracle
     sc = oracle.OracleScene(kind, obj, nx / ny)
@@ -101,9 +106,12 @@ def cpu_baseline_mlt(kind, obj, nx, ny, seed, threads, seconds):
         _, _, cnt = sc.mlt_render(nx, ny, chains, steps, seed=seed, n_init=10000, nthreads=threads)
         return cnt, time.perf_counter() - t0
 
-    _, dt = run(256)
-    chains = int(min(1 << 20, max(256, 256 * seconds / max(dt, 1e-3))))
-    cnt, dt = run(chains)
+    chains = 256
+    while True:                             # grow the sample until it takes >= seconds/2
+        cnt, dt = run(chains)
+        if dt >= 0.5 * seconds or chains >= 1 << 20:
+            break
+        chains = int(min(1 << 20, chains * min(16.0, max(2.0, seconds / max(dt, 1e-3)))))
     return {"mrays": cnt.rays / dt / 1e6, "seconds": dt, "rays": cnt.rays, "npix": 0,
             "V": cnt.node_visits / cnt.rays, "T": (cnt.tri_tests + cnt.sphere_tests) / cnt.rays,
             "rmse": None, "sample": f"{chains} chains x {steps} mutations"}
