@@ -21,6 +21,7 @@ FRT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
 constexpr int kSentinel = 0x7fffffff;   // "stack empty"; never a node index
 constexpr int kEmptyChild = kSentinel;  // unused slot of a 4-wide node (never pushed)
 constexpr int kWorldBvh4 = 2;           // internal world kind: 4-wide quantized BVH
+constexpr int kWorldBrute = 3;          // internal world kind: every triangle, in lockstep (tiny scenes)
 constexpr int kBvh4Overflow = 40;       // private stack entries after the LDS ones
 
 // device scene (fp32, HBM-resident; DESIGN.md "Data layout")
@@ -278,13 +279,32 @@ FRT_HD bool trav_begin_world(Trav &T, const DevScene &S, f3 o, f3 d, float tmax)
         T.h = Hit{-1, tmax, 0.0f, 0.0f};
         return true;
     } else {
-        return trav_begin(T, S, WORLD == kWorldBvh4 ? S.root4 : S.root, o, d, tmax);
+        return trav_begin(T, S, WORLD == kWorldBvh4 ? S.root4 : S.root, o, d, tmax);   // brute: root box + t_min
     }
 }
+// Tiny triangle-only BVH scenes: test every triangle in index order.  All
+// lanes of a wave read the same triangle (an LDS broadcast) and run the same
+// trip count, so no lane idles; the (t, DFS rank) minimum is the BVH's hit,
+// and the BVH's root box test and t_min stay (trav_begin).
+FRT_HD bool brute_all(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit)
+{
+    for (int ref = 0; ref < S.n_tris; ++ref) {
+        float u, v;
+        const float t = prim_t(S, ref, o, d, T.tmin, T.h.t, u, v);
+        if (t > 0.0f && (t < T.h.t || (T.h.prim >= 0 && ref < T.h.prim))) {
+            T.h.prim = ref; T.h.t = t; T.h.u = u; T.h.v = v;
+            if (anyhit) break;
+        }
+    }
+    return true;
+}
+
 template <int WORLD, int STRIDE, int STACK>
 FRT_HD bool trav_step_world(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int *ovf)
 {
-    if constexpr (WORLD == FRT_WORLD_LIST) {
+    if constexpr (WORLD == kWorldBrute) {
+        return brute_all(T, S, o, d, anyhit);
+    } else if constexpr (WORLD == FRT_WORLD_LIST) {
         T.h = trace_list(S, o, d, T.h.t, anyhit);
         return true;
     } else if constexpr (WORLD == kWorldBvh4) {

@@ -473,6 +473,7 @@ struct frt_ctx {
     int world_kind = 0, stack_needed = 0;
     bool has_bvh4 = false;
     int depth4 = 0;
+    int n_tris = 0, n_spheres = 0;
     size_t scene_lds_bytes = 0, scene_lds_bytes4 = 0;   // LDS copy with binary / 4-wide nodes
     double last_mlt_b = 0.0;
     std::vector<void *> scene_bufs;
@@ -975,6 +976,8 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
     c->world_kind = S.world_kind;
     c->stack_needed = F.depth;
     c->has_bvh4 = F.has4;
+    c->n_tris = S.n_tris;
+    c->n_spheres = (int)F.spheres.size();
     c->depth4 = F.depth4;
     c->scene_lds_bytes = sizeof(float4) * (F.nodes.size() + F.tris.size() + F.tshade.size() + F.mats.size());
     c->scene_lds_bytes4 = sizeof(float4) * (F.nodes4.size() + F.tris.size() + F.tshade.size() + F.mats.size());
@@ -1002,7 +1005,8 @@ extern "C" int frt_selftest_path_host(const frt_scene_view *sv, const frt_render
     S.spheres = F.spheres.data(); S.sphere_mat = F.smat.data(); S.mats = F.mats.data();
     S.lights = F.lights.data(); S.list = F.list.data();
     std::vector<int> stack(std::max(F.depth + 1, kSelftestStack));
-    const bool wide = S.world_kind == FRT_WORLD_BVH && F.has4 && !(p->flags & FRT_FLAG_BVH2) &&
+    const bool brute = S.world_kind == FRT_WORLD_BVH && (p->flags & FRT_FLAG_BRUTE) && F.spheres.empty();
+    const bool wide = !brute && S.world_kind == FRT_WORLD_BVH && F.has4 && !(p->flags & FRT_FLAG_BVH2) &&
                       bvh4_stack_fits(F.depth4, kSelftestStack);
     uint32_t n_ext = 0, n_sh = 0;
     uint64_t n_cam = 0, ext = 0, sh = 0;
@@ -1016,10 +1020,17 @@ extern "C" int frt_selftest_path_host(const frt_scene_view *sv, const frt_render
             path_begin(P, S, px, py, p->nx, p->ny, p->seed, (uint32_t)pix, (uint32_t)smp);
             ++n_cam;
             for (;;) {
-                const Hit h = (S.world_kind == FRT_WORLD_LIST)
-                                  ? trace<FRT_WORLD_LIST, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data())
-                              : wide ? trace<kWorldBvh4, 1, kSelftestStack>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data())
-                                     : trace<FRT_WORLD_BVH, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data());
+                Hit h;
+                if (brute) {
+                    Trav T;
+                    if (trav_begin(T, S, S.root, P.ro, P.rd, P.rtmax)) brute_all(T, S, P.ro, P.rd, P.shadow);
+                    h = T.h;
+                } else {
+                    h = (S.world_kind == FRT_WORLD_LIST)
+                            ? trace<FRT_WORLD_LIST, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data())
+                        : wide ? trace<kWorldBvh4, 1, kSelftestStack>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data())
+                               : trace<FRT_WORLD_BVH, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data());
+                }
                 n_ext = n_sh = 0;
                 const bool done = path_shade(P, S, h, p->max_depth, n_ext, n_sh);
                 ext += n_ext; sh += n_sh;
@@ -1152,6 +1163,7 @@ static Launcher bvh_launcher(int waves, size_t sb)
 }
 constexpr int kBvh4LdsStack = 16;   // 16 KiB of LDS per block; deeper entries go to scratch
 constexpr int kBvh4LdsStackSmall = 8;   // LDS-resident scenes (shallow trees)
+constexpr int kBruteMaxTris = 128;
 static int pick_launcher(const frt_ctx *c, int flags, Launcher &L)
 {
     if (c->world_kind == FRT_WORLD_LIST) { L = make_launcher<16, FRT_WORLD_LIST, false>(0); return FRT_OK; }
@@ -1165,6 +1177,11 @@ static int pick_launcher(const frt_ctx *c, int flags, Launcher &L)
     if (flags & FRT_FLAG_WAVES4) waves = 0;   // the compiler's own allocation (~120 VGPRs, 4 waves)
     if (flags & FRT_FLAG_WAVES5) waves = 5;
     if (flags & FRT_FLAG_WAVES6) waves = 6;
+    // tiny triangle-only scenes from LDS, every triangle in lockstep (A/B: FRT_FLAG_BRUTE)
+    if (lds && (flags & FRT_FLAG_BRUTE) && c->n_spheres == 0 && c->n_tris <= kBruteMaxTris) {
+        L = bvh_launcher<8, true, kWorldBrute>(waves, sb);
+        return FRT_OK;
+    }
     // LDS-resident scenes, 4-wide (A/B: FRT_FLAG_BVH4)
     if (lds && (flags & FRT_FLAG_BVH4) && c->has_bvh4 && c->scene_lds_bytes4 <= kLdsSceneBytes &&
         bvh4_stack_fits(c->depth4, kBvh4LdsStackSmall)) {

@@ -112,3 +112,5 @@ def test_bvh4_matches_binary(kind, objfix, tess, request, tmp_path):
     assert np.array_equal(wide, bin2)
     assert st4.rays == st2.rays
     assert st4.stack_entries == 8 and 0 < st4.bvh_depth < st2.bvh_depth   # the wide tree was traversed
+    brute, stb = frt.selftest_path_host(hs, frt.RenderParams.make(nx, ny, 8, seed=13, flags=frt.FRT_FLAG_BRUTE), pix)
+    assert np.array_equal(brute, bin2) and stb.rays == st2.rays                 # every triangle, index order

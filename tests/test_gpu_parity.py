@@ -125,6 +125,9 @@ def test_bvh4_matches_binary(ctx, cornell_obj, tmp_path):
     b_lds, stb = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21))
     assert stw.scene_in_lds == 1 and stb.scene_in_lds == 1 and stw.stack_entries == 8
     assert np.array_equal(w_lds, b_lds)
+    # tiny scene: every triangle in lockstep (FRT_FLAG_BRUTE)
+    br, stbr = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21, flags=frt.FRT_FLAG_BRUTE))
+    assert stbr.scene_in_lds == 1 and np.array_equal(br, b_lds) and stbr.rays == stb.rays
 
 
 @pytest.mark.parametrize("flags", [0, frt.FRT_FLAG_NO_LDS_SCENE, frt.FRT_FLAG_NO_LDS_SCENE | frt.FRT_FLAG_BVH2])
