@@ -28,11 +28,11 @@ FRT_HD float mlt_perturb(float value, float s2, float log_ratio, float r)
     float result;
     if (r < 0.5f) {
         r = r * 2.0f;
-        result = value + s2 * expf(-log_ratio * r);
+        result = value + s2 * fexp(-log_ratio * r);
         if (result > 1.0f) result -= 1.0f;
     } else {
         r = (r - 0.5f) * 2.0f;
-        result = value - s2 * expf(-log_ratio * r);
+        result = value - s2 * fexp(-log_ratio * r);
         if (result < 0.0f) result += 1.0f;
     }
     return result;
@@ -92,7 +92,7 @@ FRT_HD void mlt_begin(MltPath &M, const DevScene &S, const PrndSource &src, int 
     const f3 dir = normalize(P.rd);
     const float dist = (float)ny / (2.0f * S.cam_half_height);
     const f3 center = S.cam_o + dist * S.cam_w;
-    const f3 pos = (S.cam_o + (dist / dot(dir, S.cam_w)) * dir) - center;
+    const f3 pos = (S.cam_o + fdiv(dist, dot(dir, S.cam_w)) * dir) - center;
     M.x = -dot(S.cam_u, pos) + (float)nx * 0.5f;
     M.y = -dot(S.cam_vv, pos) + (float)ny * 0.5f;
 }
@@ -130,7 +130,7 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
             const float cos_wo = dot(n, -normalize(P.rd));
             float d2 = h.t * h.t;
             if (d2 <= kEps) d2 = kEps;
-            const float light_pdf = prim_pdf(S, h.prim, p, h.t, n, P.rd) * d2 / fabsf(cos_wo);
+            const float light_pdf = fdiv(prim_pdf(S, h.prim, p, h.t, n, P.rd) * d2, fabsf(cos_wo));
             P.L = P.L + mi_weight(P.prev_pdf, light_pdf) * (P.beta * Le);
         }
         return true;
@@ -147,7 +147,7 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
     const float pdf = fmaxf(cw, 0.0f) * kInvPi;
     if (pdf == 0.0f) return true;                       // drops this vertex's NEE (pssmlt.cpp:261-264)
     const f3 f = kInvPi * xyz(m0);
-    const f3 beta_next = (fabsf(cw) / pdf) * (P.beta * f);
+    const f3 beta_next = fdiv(fabsf(cw), pdf) * (P.beta * f);
     const f3 origin = p + kEps * n;
     P.nxt_d = wo;
     const int nl = S.n_lights;
@@ -164,12 +164,12 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
         const float cos_lo = dot(ln, -tu);
         P.nee = mk3(0, 0, 0);
         if (cos_lo != 0.0f) {
-            const float light_pdf = prim_pdf(S, lref, p, h.t, n, tu) * dist2 / fabsf(cos_lo);
+            const float light_pdf = fdiv(prim_pdf(S, lref, p, h.t, n, tu) * dist2, fabsf(cos_lo));
             const float bsdf_pdf = fmaxf(cos_wi, 0.0f) * kInvPi;
             const float wgt = mi_weight(light_pdf, bsdf_pdf);
             const float4 lm0 = S.mats[2 * lmat], lm1 = S.mats[2 * lmat + 1];
             if (f2i(lm0.w) == FRT_MAT_DIFFUSE_LIGHT && dot(ln, tu) < 0.0f)
-                P.nee = (wgt / light_pdf * cos_wi) * (P.beta * (xyz(lm1) * f));
+                P.nee = (fdiv(wgt, light_pdf) * cos_wi) * (P.beta * (xyz(lm1) * f));
         }
         P.ro = origin; P.rd = tl; P.rtmax = 1.0f - kShadowEps;
         P.shadow = true;

@@ -320,7 +320,7 @@ FRT_HD void prim_shade(const DevScene &S, int ref, f3 ro, f3 p, float u, float v
     if (ref & FRT_PRIM_SPHERE) {                               // sphere.h:47-50
         const int k = ref & ~FRT_PRIM_SPHERE;
         const float4 sp = S.spheres[k];
-        n = (1.0f / sp.w) * (p - xyz(sp));
+        n = rcp(sp.w) * (p - xyz(sp));
         if (len2(ro - xyz(sp)) < sp.w * sp.w) n = -n;          // origin inside: flip
         mat = S.sphere_mat[k];
         return;
@@ -344,10 +344,10 @@ FRT_HD float prim_pdf(const DevScene &S, int ref, f3 rec_p, float rec_t, f3 rec_
     const f3 dir = xyz(sp) - o;
     const float d2 = len2(dir);
     const float r2 = sp.w * sp.w;
-    if (d2 <= r2) return 1.0f / (4.0f * kPi * r2);
-    const float cos_max = sqrtf(1.0f - r2 / d2);
+    if (d2 <= r2) return rcp(4.0f * kPi * r2);
+    const float cos_max = fsqrt(1.0f - fdiv(r2, d2));
     const float solid = 2.0f * kPi * (1.0f - cos_max);
-    return (1.0f / solid) * fabsf(dot(to_light, rec_n)) / d2;
+    return fdiv(rcp(solid) * fabsf(dot(to_light, rec_n)), d2);
 }
 
 // sample_direct: returns to_light (unnormalised, as the reference), light normal, material
@@ -371,7 +371,7 @@ FRT_HD f3 prim_sample(const DevScene &S, int ref, f3 o, float u0, float u1, f3 &
         return p;
     }
     const float4 a = tri_part(S, ref, 0), b = tri_part(S, ref, 1), c = tri_part(S, ref, 2);   // triangle.h:145-175
-    const float su0 = sqrtf(u0);
+    const float su0 = fsqrt(u0);
     const float b0 = 1.0f - su0;
     const float b1 = u1 * su0;
     const f3 lp = xyz(a) + b0 * xyz(b) + b1 * xyz(c);            // (1-b0-b1) v0 + b0 v1 + b1 v2
@@ -409,8 +409,8 @@ FRT_HD void path_begin(PathState &P, const DevScene &S, int px, int py, int nx, 
                        uint32_t pixel, uint32_t sample)
 {
     P.key = rng_key(seed, pixel, sample);
-    const float u = ((float)px + rng_u(P.key, 0)) / (float)nx;
-    const float v = ((float)py + rng_u(P.key, 1)) / (float)ny;
+    const float u = fdiv((float)px + rng_u(P.key, 0), (float)nx);
+    const float v = fdiv((float)py + rng_u(P.key, 1), (float)ny);
     f3 off = mk3(0, 0, 0);
     if (S.lens_r != 0.0f) {
         const float a = rng_u(P.key, 2) * 2.0f - 1.0f, b = rng_u(P.key, 3) * 2.0f - 1.0f;
@@ -472,7 +472,7 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
             const float cos_wo = dot(n, -normalize(P.rd));
             float d2 = len2(p - P.prev_p);
             if (d2 <= kEps) d2 = kEps;
-            const float light_pdf = prim_pdf(S, h.prim, p, h.t, n, P.rd) * d2 / fabsf(cos_wo);
+            const float light_pdf = fdiv(prim_pdf(S, h.prim, p, h.t, n, P.rd) * d2, fabsf(cos_wo));
             P.L = P.L + mi_weight(P.prev_pdf, light_pdf) * (P.beta * Le);
         }
         return true;
@@ -486,7 +486,7 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
     const float pdf = fmaxf(cw, 0.0f) * kInvPi;
     if (pdf == 0.0f) return true;
     const f3 f = kInvPi * xyz(m0);                      // lambertian::eval_bsdf (material.h:62-65)
-    const f3 beta_next = (fabsf(cw) / pdf) * (P.beta * f);
+    const f3 beta_next = fdiv(fabsf(cw), pdf) * (P.beta * f);
     const f3 origin = p + kEps * n;
     P.nxt_d = wo;
     // next-event estimation (path.cpp:38-77)
@@ -504,12 +504,12 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
         const float cos_lo = dot(ln, -tu);
         P.nee = mk3(0, 0, 0);
         if (cos_lo != 0.0f) {
-            const float light_pdf = prim_pdf(S, lref, p, h.t, n, tu) * dist2 / fabsf(cos_lo);
+            const float light_pdf = fdiv(prim_pdf(S, lref, p, h.t, n, tu) * dist2, fabsf(cos_lo));
             const float bsdf_pdf = fmaxf(cos_wi, 0.0f) * kInvPi;
             const float wgt = mi_weight(light_pdf, bsdf_pdf);
             const float4 lm0 = S.mats[2 * lmat], lm1 = S.mats[2 * lmat + 1];
             if (f2i(lm0.w) == FRT_MAT_DIFFUSE_LIGHT && dot(ln, tu) < 0.0f)
-                P.nee = (wgt / light_pdf * cos_wi) * (P.beta * (xyz(lm1) * f));
+                P.nee = (fdiv(wgt, light_pdf) * cos_wi) * (P.beta * (xyz(lm1) * f));
         }
         P.ro = origin; P.rd = tl; P.rtmax = 1.0f - kShadowEps;
         P.shadow = true;
