@@ -25,6 +25,7 @@ FRT_FLAG_WAVES4 = 8
 FRT_FLAG_BVH2 = 16
 FRT_FLAG_BVH4 = 32
 FRT_FLAG_BRUTE = 64
+FRT_FLAG_SPEC = 128
 FRT_INTEGRATOR_PATH, FRT_INTEGRATOR_PSSMLT = 0, 1
 
 ERRORS = {0: "ok", -1: "invalid", -2: "hip", -3: "no scene", -4: "unsupported", -5: "io", -6: "no gfx950 device"}

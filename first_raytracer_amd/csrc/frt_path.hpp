@@ -17,6 +17,15 @@ namespace frt {
 FRT_HD int f2i(float f) { return __builtin_bit_cast(int, f); }
 FRT_HD float i2f(int i) { return __builtin_bit_cast(float, i); }
 FRT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
+// true if the predicate holds on any active lane of the wave (the host self-test is one lane)
+FRT_HD bool wave_any(bool x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __ballot(x) != 0;
+#else
+    return x;
+#endif
+}
 
 constexpr int kSentinel = 0x7fffffff;   // "stack empty"; never a node index
 constexpr int kEmptyChild = kSentinel;  // unused slot of a 4-wide node (never pushed)
@@ -172,10 +181,15 @@ FRT_HD bool bvh2_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *
 // one FMA.  Quantised planes round outward and the boxes keep their padding,
 // so culling stays conservative and the hit equals the binary traversal's
 // bit for bit (the (t, DFS rank) minimum does not depend on visit order).
-template <int STRIDE, int LSTACK>
+// SPEC (speculative traversal, Aila & Laine 2009): a lane that reaches a leaf
+// parks it and keeps descending while other lanes of its wave still search
+// for one; then every lane tests its parked leaf at once.  Visits more nodes
+// with a stale t_best (still conservative), keeps lanes busy.
+template <int STRIDE, int LSTACK, bool SPEC = false>
 FRT_HD bool bvh4_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int *ovf)
 {
     int node = T.node, sp = T.sp;
+    int parked = 0;                                     // leaf refs are negative; 0 = none
     auto push = [&](int v) {
         if (sp < LSTACK) stk[sp * STRIDE] = v;
         else ovf[sp - LSTACK] = v;
@@ -186,6 +200,7 @@ FRT_HD bool bvh4_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *
         --sp;
         return sp < LSTACK ? stk[sp * STRIDE] : ovf[sp - LSTACK];
     };
+    if (SPEC && node < 0) { parked = node; node = pop(); }
     while ((unsigned)node < (unsigned)kSentinel) {
         const uint4 w0 = node4_part(S, node, 0), w1 = node4_part(S, node, 1);
         const uint4 w2 = node4_part(S, node, 2), w3 = node4_part(S, node, 3);
@@ -217,6 +232,20 @@ FRT_HD bool bvh4_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *
         if (t[2] != __builtin_inff()) push(c[2]);
         if (t[1] != __builtin_inff()) push(c[1]);
         node = (t[0] != __builtin_inff()) ? c[0] : pop();
+        if constexpr (SPEC) {
+            if (parked == 0 && node < 0) { parked = node; node = pop(); }
+            // keep going while some lane of the wave still has no leaf to test
+            if (!wave_any(parked == 0 && (unsigned)node < (unsigned)kSentinel)) break;
+        }
+    }
+    if constexpr (SPEC) {
+        if (parked != 0 && leaf_hit(S, ~parked, o, d, T.tmin, anyhit, T.h)) {
+            T.node = node; T.sp = sp;
+            return true;
+        }
+        T.node = node;
+        T.sp = sp;
+        return node == kSentinel;
     }
     bool done = node == kSentinel || leaf_hit(S, ~node, o, d, T.tmin, anyhit, T.h);
     if (!done) {
@@ -299,7 +328,7 @@ FRT_HD bool brute_all(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit)
     return true;
 }
 
-template <int WORLD, int STRIDE, int STACK>
+template <int WORLD, int STRIDE, int STACK, bool SPEC = false>
 FRT_HD bool trav_step_world(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int *ovf)
 {
     if constexpr (WORLD == kWorldBrute) {
@@ -308,7 +337,7 @@ FRT_HD bool trav_step_world(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit,
         T.h = trace_list(S, o, d, T.h.t, anyhit);
         return true;
     } else if constexpr (WORLD == kWorldBvh4) {
-        return bvh4_step<STRIDE, STACK>(T, S, o, d, anyhit, stk, ovf);
+        return bvh4_step<STRIDE, STACK, SPEC>(T, S, o, d, anyhit, stk, ovf);
     } else {
         return bvh2_step<STRIDE>(T, S, o, d, anyhit, stk);
     }

@@ -102,7 +102,7 @@ __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
 // ------------------------------------------------------------------------
 // the persistent path megakernel
 // ------------------------------------------------------------------------
-template <int STACK, int WORLD, bool LDS_SCENE, int WAVES = 1>
+template <int STACK, int WORLD, bool LDS_SCENE, int WAVES = 1, bool SPEC = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void path_megakernel(
     const DevScene S0, const DevWork W)
 {
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         // then they shade together while the stragglers keep their state.
         for (;;) {
             bool shadow_done = false;
-            if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, P.ro, P.rd, P.shadow, stk, ovf)) {
+            if (tracing && trav_step_world<WORLD, kBlock, STACK, SPEC>(T, S, P.ro, P.rd, P.shadow, stk, ovf)) {
                 if (P.shadow) {                 // finish the shadow ray here, keep traversing
                     path_after_shadow(P, T.h.prim < 0);
                     shadow_done = true;
@@ -1142,11 +1142,11 @@ struct Launcher {
     bool lds_scene = false;
     bool wide = false;      // 4-wide quantized BVH
 };
-template <int STACK, int WORLD, bool LDS, int WAVES = 1>
+template <int STACK, int WORLD, bool LDS, int WAVES = 1, bool SPEC = false>
 static Launcher make_launcher(size_t scene_bytes)
 {
     Launcher L;
-    L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES>);
+    L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES, SPEC>);
     L.lds = (WORLD != FRT_WORLD_LIST ? (size_t)STACK * kBlock * sizeof(int) : 0) + (LDS ? scene_bytes : 0);
     L.stack = STACK;
     L.waves = WAVES > 1 ? WAVES : 0;
@@ -1154,12 +1154,12 @@ static Launcher make_launcher(size_t scene_bytes)
     L.wide = WORLD == kWorldBvh4;
     return L;
 }
-template <int STACK, bool LDS, int WORLD = FRT_WORLD_BVH>
+template <int STACK, bool LDS, int WORLD = FRT_WORLD_BVH, bool SPEC = false>
 static Launcher bvh_launcher(int waves, size_t sb)
 {
-    if (waves == 6) return make_launcher<STACK, WORLD, LDS, 6>(sb);
-    if (waves == 5) return make_launcher<STACK, WORLD, LDS, 5>(sb);
-    return make_launcher<STACK, WORLD, LDS>(sb);
+    if (waves == 6) return make_launcher<STACK, WORLD, LDS, 6, SPEC>(sb);
+    if (waves == 5) return make_launcher<STACK, WORLD, LDS, 5, SPEC>(sb);
+    return make_launcher<STACK, WORLD, LDS, 1, SPEC>(sb);
 }
 constexpr int kBvh4LdsStack = 16;   // 16 KiB of LDS per block; deeper entries go to scratch
 constexpr int kBvh4LdsStackSmall = 8;   // LDS-resident scenes (shallow trees)
@@ -1190,7 +1190,8 @@ static int pick_launcher(const frt_ctx *c, int flags, Launcher &L)
     }
     // HBM-resident scenes: the 4-wide quantized BVH (half the bytes per box test)
     if (!lds && c->has_bvh4 && !(flags & FRT_FLAG_BVH2) && bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
-        L = bvh_launcher<kBvh4LdsStack, false, kWorldBvh4>(waves, 0);
+        L = (flags & FRT_FLAG_SPEC) ? bvh_launcher<kBvh4LdsStack, false, kWorldBvh4, true>(waves, 0)
+                                    : bvh_launcher<kBvh4LdsStack, false, kWorldBvh4>(waves, 0);
         return FRT_OK;
     }
     if (d < 8) L = lds ? bvh_launcher<8, true>(waves, sb) : bvh_launcher<8, false>(waves, 0);

@@ -119,6 +119,9 @@ def test_bvh4_matches_binary(ctx, cornell_obj, tmp_path):
     assert st4.scene_in_lds == 0 and st4.bvh_depth < st2.bvh_depth
     assert np.array_equal(wide, bin2)
     assert st4.rays == st2.rays
+    spec, sts = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21,
+                                                 flags=frt.FRT_FLAG_NO_LDS_SCENE | frt.FRT_FLAG_SPEC))
+    assert np.array_equal(spec, bin2) and sts.rays == st2.rays        # speculative traversal
     # small scene: 4-wide nodes from LDS (FRT_FLAG_BVH4) vs the default binary LDS plan
     ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, nx / ny))
     w_lds, stw = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21, flags=frt.FRT_FLAG_BVH4))
