@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libfrt.so")
+# FRT_LIB_PATH: an experiment build (Makefile `exp` target) for timing A/B only
+LIB_PATH = os.environ.get("FRT_LIB_PATH") or os.path.join(HERE, "libfrt.so")
 
 FRT_WORLD_BVH, FRT_WORLD_LIST = 0, 1
 FRT_MAT_LAMBERTIAN, FRT_MAT_DIFFUSE_LIGHT = 0, 1

@@ -68,6 +68,17 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t m)
 // (ds_read_b128 instead of L1/L2 round trips).  Planar copies: part k of
 // element i at [k * count + i], so lanes reading different elements of the
 // same part hit different banks.
+// HBM-resident scenes: the interleaved strides flatten_scene uses, as
+// constants the compiler folds into the address arithmetic (kernel arguments
+// would cost a quarter-rate v_mul_lo_u32 per node / triangle access).
+__device__ __forceinline__ void scene_strides_hbm(DevScene &S)
+{
+    S.node_es = 4; S.node_ps = 1;
+    S.node4_es = 4; S.node4_ps = 1;
+    S.tri_es = 3; S.tri_ps = 1;
+    S.sh_es = 2; S.sh_ps = 1;
+}
+
 template <bool WIDE>
 __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
 {
@@ -110,6 +121,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     int *stk = lds_mem + threadIdx.x;                                 // one LDS column per lane
     DevScene S = S0;
     if constexpr (LDS_SCENE) scene_to_lds<WORLD == kWorldBvh4>(S, lds_mem + STACK * kBlock);
+    else scene_strides_hbm(S);
     const int lane = threadIdx.x & 63;
     const int T2 = W.tile * W.tile;
 
@@ -280,9 +292,11 @@ __device__ __forceinline__ Hit trace_any(const DevScene &S, const PathState &P, 
 // bootstrap: sc of n_init independent eye paths (pssmlt.cpp:303-312); the host
 // sums them in a fixed order
 template <int STACK, int WORLD>
-__global__ __launch_bounds__(kBlock) void mlt_bootstrap(const DevScene S, int nx, int ny, uint32_t seed, int n_init,
+__global__ __launch_bounds__(kBlock) void mlt_bootstrap(const DevScene S0, int nx, int ny, uint32_t seed, int n_init,
                                                         float *sc)
 {
+    DevScene S = S0;
+    scene_strides_hbm(S);
     extern __shared__ __attribute__((aligned(16))) int lds_mem[];
     int *stk = lds_mem + threadIdx.x;
     const int i = blockIdx.x * kBlock + threadIdx.x;
@@ -319,6 +333,7 @@ __global__ __launch_bounds__(kBlock) void mlt_megakernel(const DevScene S0, cons
     int *stk = lds_mem + threadIdx.x;
     DevScene S = S0;
     if constexpr (LDS_SCENE) scene_to_lds<WORLD == kWorldBvh4>(S, lds_mem + STACK * kBlock);
+    else scene_strides_hbm(S);
     const int lane = threadIdx.x & 63;
     bool have = false, exhausted = false, init = false, large = false;
     uint32_t j = 0, c = 0;
