@@ -41,13 +41,8 @@ FRT_HD f3 xyz(float4 v) { return f3{v.x, v.y, v.z}; }
 // ---------------------------------------------------------------------------
 FRT_HD uint32_t mix32(uint32_t x)
 {
-#if defined(FRT_EXP_CHEAP_RNG)   // timing experiment only: no 32-bit multiplies (not the stream spec)
-    x ^= x >> 16; x ^= x << 7; x ^= x >> 13; x += x << 9; x ^= x >> 11;
-    return x;
-#else
     x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
     return x;
-#endif
 }
 struct RngKey { uint32_t k0, k1; };
 FRT_HD RngKey rng_key(uint32_t seed, uint32_t pixel, uint32_t sample)

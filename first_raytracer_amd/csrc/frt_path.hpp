@@ -147,7 +147,8 @@ template <int STRIDE>
 FRT_HD bool bvh2_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk)
 {
     int node = T.node, sp = T.sp;
-#if defined(FRT_EXP_BRANCHY_BVH2)
+    // (a branch-free body -- speculative stack-top read, predicated push -- was
+    // 4.5 % slower on Cornell: profiles/r01_exp1_branchy.txt)
     while ((unsigned)node < (unsigned)kSentinel) {   // interior node
         const float4 n0 = node_part(S, node, 0), n1 = node_part(S, node, 1);
         const float4 n2 = node_part(S, node, 2), n3 = node_part(S, node, 3);
@@ -168,24 +169,7 @@ FRT_HD bool bvh2_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *
             node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel;
         }
     }
-#else
-    while ((unsigned)node < (unsigned)kSentinel) {   // interior node, branch-free body
-        // the stack top, read before the node so its latency hides under the slab math
-        const int top = stk[(sp > 0 ? sp - 1 : 0) * STRIDE];
-        const float4 n0 = node_part(S, node, 0), n1 = node_part(S, node, 1);
-        const float4 n2 = node_part(S, node, 2), n3 = node_part(S, node, 3);
-        const float t0 = slab_entry(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, T.tmin, T.h.t);
-        const float t1 = slab_entry(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, T.sr, T.tmin, T.h.t);
-        const int c0 = f2i(n3.x), c1 = f2i(n3.y);
-        const bool h0 = t0 != __builtin_inff(), h1 = t1 != __builtin_inff();
-        // bitwise, not short-circuit: no exec-mask branches in the body
-        const bool near0 = h0 & (!h1 | (t0 <= t1));      // nearer child first, ties left
-        const bool both = h0 & h1, any = h0 | h1;
-        if (both) stk[sp * STRIDE] = near0 ? c1 : c0;    // push the farther child
-        node = any ? (near0 ? c0 : c1) : (sp > 0 ? top : kSentinel);
-        sp += both ? 1 : ((any | (sp == 0)) ? 0 : -1);
-    }
-#endif
+
     bool done = node == kSentinel || leaf_hit(S, ~node, o, d, T.tmin, anyhit, T.h);
     if (!done) {
         node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel;
