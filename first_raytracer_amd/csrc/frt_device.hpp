@@ -74,7 +74,7 @@ FRT_HD uint32_t dim_bounce(int depth) { return 4u + 8u * (uint32_t)depth; }
 // kernel variants (same instructions everywhere).
 FRT_HD float rcp(float x)
 {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(FRT_EXP_IEEE_MATH)
     return __builtin_amdgcn_rcpf(x);
 #else
     return 1.0f / x;
@@ -83,7 +83,7 @@ FRT_HD float rcp(float x)
 FRT_HD float fdiv(float a, float b) { return a * rcp(b); }
 FRT_HD float fsqrt(float x)
 {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(FRT_EXP_IEEE_MATH)
     return __builtin_amdgcn_sqrtf(x);
 #else
     return sqrtf(x);
@@ -91,7 +91,7 @@ FRT_HD float fsqrt(float x)
 }
 FRT_HD float frsqrt(float x)
 {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(FRT_EXP_IEEE_MATH)
     return __builtin_amdgcn_rsqf(x);
 #else
     return 1.0f / sqrtf(x);
@@ -100,7 +100,7 @@ FRT_HD float frsqrt(float x)
 // sin / cos of 2*pi*r for r in [0, 1) (v_sin_f32 / v_cos_f32 take revolutions)
 FRT_HD void sincos_2pi(float r, float &s, float &c)
 {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(FRT_EXP_IEEE_MATH)
     s = __builtin_amdgcn_sinf(r);
     c = __builtin_amdgcn_cosf(r);
 #else
@@ -110,7 +110,7 @@ FRT_HD void sincos_2pi(float r, float &s, float &c)
 // e^x for moderate |x| (PSS-MLT perturbation: x in [-8, 0])
 FRT_HD float fexp(float x)
 {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(FRT_EXP_IEEE_MATH)
     return __builtin_amdgcn_exp2f(x * 1.44269504088896340736f);
 #else
     return expf(x);
