@@ -7,11 +7,12 @@
 //   perturb / mutate        pssmlt.cpp:6-17, 62-73
 //   Render (chain loop)     pssmlt.cpp:301-365, AccumulatePathContribution :19-38
 //
-// Primary samples: a chain's current state u[0..91] lives in HBM as
-// U[dim][chain] (coalesced).  A proposal is never stored: its dimension d is
-// computed when the path reads it -- a fresh uniform on a large step, else
-// perturb(U[d][c], r) -- and written back for all 92 dimensions only when the
-// proposal is accepted.  Random numbers follow DESIGN.md "PSS-MLT streams".
+// Primary samples: a chain's current state u[0..91] lives in HBM chain-major,
+// U[chain][dim] (one 368-B row per chain).  A proposal is never stored: its
+// dimension d is computed when the path reads it -- a fresh uniform on a large
+// step, else perturb(U[c][d], r) -- and written back for all 92 dimensions
+// only when the proposal is accepted (by the whole wave, one chain's row at a
+// time: mlt_megakernel).  Random numbers follow DESIGN.md "PSS-MLT streams".
 #pragma once
 #include "frt_path.hpp"
 
@@ -38,6 +39,13 @@ FRT_HD float mlt_perturb(float value, float s2, float log_ratio, float r)
     return result;
 }
 
+// small-step mutation of dimension d (pixel dims 0, 1 use s1 = 2/(nx+ny), s2 = 0.1)
+FRT_HD float mlt_mutate(float cur, float r, int d, float s2p, float logp)
+{
+    if (d < 2) return mlt_perturb(cur, s2p, logp, r);
+    return mlt_perturb(cur, 1.0f / 64.0f, 2.77258872223978123767f /* log(16) */, r);
+}
+
 // Source of primary samples for one eye path.
 struct PrndSource {
     const float *U;        // chain states [dim][n_chains] (null: bootstrap / fresh)
@@ -50,9 +58,7 @@ struct PrndSource {
     {
         const float r = rng_u(key, dim0 + (uint32_t)d);
         if (fresh) return r;
-        const float cur = U[(size_t)d * n_chains + chain];
-        if (d < 2) return mlt_perturb(cur, s2p, logp, r);
-        return mlt_perturb(cur, 1.0f / 64.0f, 2.77258872223978123767f /* log(16) */, r);
+        return mlt_mutate(U[(size_t)chain * kMltDims + d], r, d, s2p, logp);
     }
 };
 

@@ -391,12 +391,14 @@ __global__ __launch_bounds__(kBlock) void mlt_megakernel(const DevScene S0, cons
                 next_ray = !done;
             }
         }
+        // accept / reject (per lane); the accepted proposal's row is written below
+        bool mat = false, mat_fresh = false, setup_next = false;
+        RngKey mat_key = key;
         if (done) {
             const f3 L = M.P.L;
             const float sc = fmaxf(fmaxf(L.x, L.y), L.z);
-            const PrndSource src = source();
             if (init) {                                 // current = initial state, materialised
-                for (int d = 0; d < kMltDims; ++d) W.U[(size_t)d * W.n_local + j] = src.get(d);
+                mat = true; mat_fresh = true;
                 cx = M.x; cy = M.y; cc = L; csc = sc;
                 init = false;
             } else {                                    // pssmlt.cpp:200-209
@@ -407,7 +409,7 @@ __global__ __launch_bounds__(kBlock) void mlt_megakernel(const DevScene S0, cons
                 if (rng_u(key, 1) <= a) {               // accept: splat the old state's weight, move
                     if (csc > 0.0f && cw != 0.0f) mlt_splat(W, cx, cy, cc, cw);
                     cw = 0.0f;
-                    for (int d = 0; d < kMltDims; ++d) W.U[(size_t)d * W.n_local + j] = src.get(d);
+                    mat = true; mat_fresh = large;
                     cx = M.x; cy = M.y; cc = L; csc = sc;
                 }
                 ++t;
@@ -417,12 +419,28 @@ __global__ __launch_bounds__(kBlock) void mlt_megakernel(const DevScene S0, cons
                 if (csc > 0.0f && cw != 0.0f) mlt_splat(W, cx, cy, cc, cw);
                 have = false;
             } else {
-                key = rng_key(W.seed ^ kMltChainSalt, c, (uint32_t)(t + 1));
-                large = rng_u(key, 0) < kMltLargeStep;  // large_step vs mutate (pssmlt.cpp:187-196)
-                mlt_begin(M, S, source(), W.nx, W.ny);
-                ++n_cam;
-                next_ray = true;
+                setup_next = true;
             }
+        }
+        // ---- materialise accepted proposals: the whole wave writes one chain's
+        // 92-dimension row at a time (lane = dimension; coalesced, no idle lanes) ----
+        for (uint64_t mm = __ballot(mat); mm; mm &= mm - 1) {
+            const int l = __ffsll((unsigned long long)mm) - 1;
+            const uint32_t jl = __shfl(j, l);
+            const RngKey kl{(uint32_t)__shfl((int)mat_key.k0, l), (uint32_t)__shfl((int)mat_key.k1, l)};
+            const bool fresh_l = __shfl((int)mat_fresh, l) != 0;
+            float *row = W.U + (size_t)jl * kMltDims;
+            for (int d = lane; d < kMltDims; d += 64) {
+                const float r = rng_u(kl, 2u + (uint32_t)d);
+                row[d] = fresh_l ? r : mlt_mutate(row[d], r, d, W.s2p, W.logp);
+            }
+        }
+        if (setup_next) {                               // next proposal reads the new state
+            key = rng_key(W.seed ^ kMltChainSalt, c, (uint32_t)(t + 1));
+            large = rng_u(key, 0) < kMltLargeStep;      // large_step vs mutate (pssmlt.cpp:187-196)
+            mlt_begin(M, S, source(), W.nx, W.ny);
+            ++n_cam;
+            next_ray = true;
         }
         // ---- chains from the queue, one atomic per wave ----
         const bool need = !have && !exhausted;
