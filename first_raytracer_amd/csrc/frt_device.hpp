@@ -71,7 +71,8 @@ FRT_HD uint32_t dim_bounce(int depth) { return 4u + 8u * (uint32_t)depth; }
 // sequences they replace (div_scale/fmas/fixup, denormal-scaled sqrt, sin/cos
 // range reduction) dominated the shading code; the parity gate is RMSE 1e-3
 // against the fp64 oracle, and the device results stay bit-identical across
-// kernel variants (same instructions everywhere).
+// kernel variants (same instructions everywhere).  -DFRT_EXP_IEEE_MATH builds
+// the IEEE versions (6 % slower on Cornell, 11 % on 1M: profiles/r01_exp2.txt).
 FRT_HD float rcp(float x)
 {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(FRT_EXP_IEEE_MATH)

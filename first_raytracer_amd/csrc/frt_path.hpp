@@ -234,11 +234,8 @@ FRT_HD bool bvh4_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *
                 const int cc = c[i]; c[i] = c[j]; c[j] = cc;
             }
         };
-#if defined(FRT_EXP_BVH4_NEAREST)
-        cx(0, 1); cx(2, 3); cx(0, 2);            // timing experiment: nearest first, the rest unsorted
-#else
+        // (nearest-only ordering, the rest unsorted, was 5.6 % slower on 1M: profiles/r01_exp2.txt)
         cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
-#endif
         if (t[3] != __builtin_inff()) push(c[3]);
         if (t[2] != __builtin_inff()) push(c[2]);
         if (t[1] != __builtin_inff()) push(c[1]);
