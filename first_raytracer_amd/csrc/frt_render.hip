@@ -326,8 +326,12 @@ __device__ __forceinline__ void mlt_splat(const MltWork &W, float x, float y, f3
 // one lane = one chain tracing the rays of its current eye path (initial
 // state, then one proposal per mutation); traversal steps interleave with
 // shading as in path_megakernel
+#ifndef FRT_EXP_MLT_WAVES
+#define FRT_EXP_MLT_WAVES 1      // register cap of the chain kernel (experiment builds: 5, 6)
+#endif
 template <int STACK, int WORLD, bool LDS_SCENE>
-__global__ __launch_bounds__(kBlock) void mlt_megakernel(const DevScene S0, const MltWork W)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_MLT_WAVES))) void mlt_megakernel(
+    const DevScene S0, const MltWork W)
 {
     extern __shared__ __attribute__((aligned(16))) int lds_mem[];
     int *stk = lds_mem + threadIdx.x;
