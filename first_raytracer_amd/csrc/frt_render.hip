@@ -36,6 +36,8 @@ using namespace frt;
 namespace {
 
 constexpr int kBlock = 256;
+constexpr size_t kLdsSceneBytes = 16 * 1024;   // LDS plan: 5-6 blocks/CU x (stack + scene) must fit 160 KiB
+constexpr int kLdsMaxDepth = 16;                // LDS plan: binary stacks of 8 or 16 entries
 
 struct DevWork {
     int nx, ny, spp, max_depth;
@@ -327,8 +329,8 @@ __device__ __forceinline__ void mlt_splat(const MltWork &W, float x, float y, f3
 // state, then one proposal per mutation); traversal steps interleave with
 // shading as in path_megakernel
 #ifndef FRT_EXP_MLT_WAVES
-#define FRT_EXP_MLT_WAVES 1      // register cap of the chain kernel (experiment builds: 5, 6)
-#endif
+#define FRT_EXP_MLT_WAVES 5      // register cap of the chain kernel: 5 waves/SIMD, +17 % over the
+#endif                           // compiler's 4 (profiles/r01_expmlt1.txt); experiment builds vary it
 template <int STACK, int WORLD, bool LDS_SCENE>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_MLT_WAVES))) void mlt_megakernel(
     const DevScene S0, const MltWork W)
@@ -626,13 +628,13 @@ static int trav_min(bool lds_scene)
     return std::min(std::max(v, 0), 63);
 }
 
-// Triangles per leaf (FRT_LEAF_SIZE overrides, 1 = the reference's one-prim
-// leaves).  A tuning knob of this library, not part of the C-ABI.
-static int leaf_size()
+// Triangles per leaf: FRT_LEAF_SIZE overrides (1 = the reference's one-prim
+// leaves), else 0 = by plan (see flatten_scene).  A tuning knob of this
+// library, not part of the C-ABI.
+static int leaf_size_override()
 {
     const char *e = std::getenv("FRT_LEAF_SIZE");
-    const int v = e ? std::atoi(e) : kLeafDefault;
-    return std::min(std::max(v, 1), kLeafMax);
+    return e ? std::min(std::max(std::atoi(e), 1), kLeafMax) : 0;
 }
 
 // Multi-triangle leaves: every subtree of the DFS-ordered binary tree holding
@@ -888,7 +890,22 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
             F.nodes[4 * i + 3] = make_float4(i2f(cref[0]), i2f(cref[1]), 0.0f, 0.0f);
         }
         if (nt >= kLeafIndexLimit) return fail(FRT_E_INVALID, "scene view: too many triangles");
-        collapse_leaves(F, leaf_size());
+        // leaf size by plan (profiles/r01_leaf_ab.txt): 2 triangles when the scene
+        // fits the LDS plan (Cornell +6 % over 4), else 4 (cornell_1m: +11 % over 2)
+        const int forced = leaf_size_override();
+        if (forced) {
+            collapse_leaves(F, forced);
+        } else {
+            const std::vector<float4> binary = F.nodes;
+            const int depth = F.depth;
+            collapse_leaves(F, kLeafSmallScene);
+            const size_t bytes = sizeof(float4) * (F.nodes.size() + 5 * (size_t)nt + 2 * (size_t)nm);
+            if (bytes > kLdsSceneBytes || F.depth >= kLdsMaxDepth) {
+                F.nodes = binary;
+                F.depth = depth;
+                collapse_leaves(F, kLeafDefault);
+            }
+        }
         for (int i = 0; i < nt; ++i)   // triangles outside the tree: trailing ids, never intersected
             if (tri_dev[i] < 0) { tri_dev[i] = (int)tri_order.size(); tri_order.push_back(i); }
     } else if (sv->world_kind == FRT_WORLD_LIST) {
@@ -1169,7 +1186,6 @@ extern "C" int frt_shard_slots(const frt_render_params *p, int32_t *slot_pixel)
     return FRT_OK;
 }
 
-constexpr size_t kLdsSceneBytes = 16 * 1024;   // 5-6 blocks/CU x (stack + scene) must fit 160 KiB
 
 struct Launcher {
     const void *fn = nullptr;
@@ -1206,7 +1222,7 @@ static int pick_launcher(const frt_ctx *c, int flags, Launcher &L)
     if (c->world_kind == FRT_WORLD_LIST) { L = make_launcher<16, FRT_WORLD_LIST, false>(0); return FRT_OK; }
     const int d = c->stack_needed;
     const size_t sb = c->scene_lds_bytes;
-    const bool lds = d < 16 && sb <= kLdsSceneBytes && !(flags & FRT_FLAG_NO_LDS_SCENE);
+    const bool lds = d < kLdsMaxDepth && sb <= kLdsSceneBytes && !(flags & FRT_FLAG_NO_LDS_SCENE);
     // register cap: waves/SIMD the compiler must fit (its spills land in the
     // shading code, not the traversal loops).  Measured (profiles/r01_ab_perf3.jsonl):
     // 5 waves best for LDS-resident scenes, 6 for HBM-resident ones.
@@ -1255,7 +1271,7 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
     int stack;
     const void *kboot = nullptr, *kchain = nullptr;
     const int d = c->stack_needed;
-    const bool lds_scene = c->world_kind == FRT_WORLD_BVH && d < 16 && c->scene_lds_bytes <= kLdsSceneBytes &&
+    const bool lds_scene = c->world_kind == FRT_WORLD_BVH && d < kLdsMaxDepth && c->scene_lds_bytes <= kLdsSceneBytes &&
                            !(p->flags & FRT_FLAG_NO_LDS_SCENE);
     if (c->world_kind == FRT_WORLD_LIST) { stack = 0; mlt_kernels<16, FRT_WORLD_LIST>(&kboot, &kchain); }
     else if (!lds_scene && c->has_bvh4 && !(p->flags & FRT_FLAG_BVH2) && bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
