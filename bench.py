@@ -86,10 +86,17 @@ def cpu_baseline(kind, obj, nx, ny, spp, seed, npix, threads, film, seconds):
     rays = cnt.rays
     gpu = film.reshape(-1, 3)[pix].astype(np.float64)
     rmse = float(np.sqrt(np.mean((gpu - out) ** 2)))
+    # fp32 vs fp64 rounding occasionally sends one sample down another branch
+    # (a silhouette, the light's edge); such a pixel differs by ~radiance/spp.
+    # Reported apart so a systematic error would show in rmse_converged.
+    dev = np.abs(gpu - out).max(axis=1)
+    bad = dev > 1e-3
+    rmse_conv = float(np.sqrt(np.mean((gpu[~bad] - out[~bad]) ** 2))) if (~bad).any() else None
     return {
         "mrays": rays / dt / 1e6, "seconds": dt, "rays": rays, "npix": len(pix),
         "V": cnt.node_visits / rays, "T": (cnt.tri_tests + cnt.sphere_tests) / rays,
         "rays_per_sample": rays / cnt.samples, "rmse": rmse,
+        "diverged_pixels": int(bad.sum()), "rmse_converged": rmse_conv,
     }
 
 
@@ -290,6 +297,9 @@ def main():
                        "parallelism": (f"tiles-interleaved x{world} + rccl all-gather" if args.integrator == "path"
                                        else f"chains-interleaved x{world} + rccl all-reduce")},
             "rmse": None if cpu is None else cpu["rmse"],
+            "rmse_detail": None if cpu is None or "diverged_pixels" not in cpu else {
+                "pixels": cpu["npix"], "diverged_pixels": cpu["diverged_pixels"],
+                "rmse_converged": cpu["rmse_converged"], "diverged_threshold": 1e-3},
             "mutations_per_step": int(last.samples) if args.integrator == "pssmlt" else None,
             "rays_per_step": int(rays // args.steps),
             "setup_s": round(setup_s, 2), "host_build_s": round(build_s, 2), "upload_s": round(upload_s, 2),
