@@ -62,6 +62,9 @@ def lib():
         L.ora_kat_camera.argtypes = [dp, dp, dp, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                      ctypes.c_double, ctypes.c_double, dp, dp]
         L.ora_kat_cosine.argtypes = [dp, dp, dp]
+        L.ora_kat_fresnel.argtypes = [dp, dp, ctypes.c_double, dp]
+        L.ora_kat_phong.argtypes = [dp, dp, ctypes.c_double, ctypes.c_double, ctypes.c_double, dp, dp, dp, dp]
+        L.ora_kat_dielectric.argtypes = [dp, dp, ctypes.c_double, ctypes.c_double, dp, dp, dp]
         L.ora_kat_tri_sample.argtypes = [dp, dp, ctypes.c_int, ctypes.c_int, dp, dp, dp]
         L.ora_kat_sphere_sample.argtypes = [dp, ctypes.c_double, dp, dp, dp]
         L.ora_kat_miweight.argtypes = [ctypes.c_double, ctypes.c_double]

@@ -204,6 +204,91 @@ static inline double cosine_pdf_value(v3 w, v3 direction)
     return cosine / (double)M_PI;
 }
 
+/* ---- specular materials (material.h:75-171, pdf.h:99-184, util.h:73-117) ---- */
+static const double DELTA_EPSILON = 1e-3f;                                   /* util.h:12 */
+static inline v3 ref_reflect(v3 v, v3 n)                                     /* util.h:73-76 */
+{
+    return unit(vsub(v, smul(2 * dot(v, n), n)));
+}
+static inline v3 ref_refract(v3 wi, v3 n, double eta, double cosThetaT)      /* util.h:79-84 */
+{
+    if (cosThetaT < 0) eta = 1 / eta;
+    return unit(vsub(smul(dot(wi, n) * eta + cosThetaT, n), smul(eta, wi)));
+}
+static inline double fresnelDielectricExt(double cosThetaI_, double *cosThetaT_, double eta)   /* util.h:86-117 */
+{
+    if (eta == 1) { *cosThetaT_ = -cosThetaI_; return 0.0; }
+    double scale = (cosThetaI_ > 0) ? 1 / eta : eta,
+           cosThetaTSqr = 1 - (1 - cosThetaI_ * cosThetaI_) * (scale * scale);
+    if (cosThetaTSqr <= 0.0) { *cosThetaT_ = 0.0; return 1.0; }
+    double cosThetaI = fabs(cosThetaI_);
+    double cosThetaT = sqrt(cosThetaTSqr);
+    double Rs = (cosThetaI - eta * cosThetaT) / (cosThetaI + eta * cosThetaT);
+    double Rp = (eta * cosThetaI - cosThetaT) / (eta * cosThetaI + cosThetaT);
+    *cosThetaT_ = (cosThetaI_ > 0) ? -cosThetaT : cosThetaT;
+    return 0.5 * (Rs * Rs + Rp * Rp);
+}
+/* cosine_power_pdf (pdf.h:99-136); uvw.w() is the normal, wi = hrec.wi */
+static inline double cosine_power_value(v3 n, v3 wi, double e, v3 wo)
+{
+    if (dot(n, wo) <= 0 || dot(n, wi) <= 0) return 0.0;
+    const double alpha = std_max(0.0, dot(ref_reflect(vneg(wi), n), wo));
+    const double specular_pdf = pow(alpha, e);
+    return specular_pdf * (e + 1.0) / (2 * (double)M_PI);
+}
+static inline v3 cosine_power_generate(v3 n, v3 wi, double e, double s0, double s1)
+{
+    v3 R = ref_reflect(vneg(wi), n);
+    double sinAlpha = sqrt(1 - pow(s1, 2 / (e + 1)));
+    double cosAlpha = pow(s1, 1 / (e + 1));
+    double phi = (2.0 * M_PI) * s0;
+    v3 localDir = mk(sinAlpha * cos(phi), sinAlpha * sin(phi), cosAlpha);
+    onb b = onb_from_w(R);
+    return onb_from_local(&b, localDir);
+}
+/* modified_phong::eval_bsdf (material.h:92-100), cosine included */
+static inline v3 phong_eval(v3 kd, const double ks[3], double e, v3 n, v3 wi, v3 wo)
+{
+    const v3 reflected = unit(ref_reflect(vneg(wi), n));
+    const double alpha = std_max(0.0, dot(reflected, wo));
+    const double k = (e + 2) / (2 * M_PI), pw = pow(alpha, e);
+    const v3 spec = mk(ks[0] * k * pw, ks[1] * k * pw, ks[2] * k * pw);
+    const v3 result = vadd(sdiv(kd, M_PI), spec);
+    return smul(dot(n, wo), result);
+}
+/* dielectric_pdf (pdf.h:138-184) */
+static inline double dielectric_value(v3 n, v3 wi, double ior, v3 wo)
+{
+    double cosThetaT;
+    double F = fresnelDielectricExt(dot(wi, n), &cosThetaT, ior);
+    if (dot(wi, n) * dot(wo, n) >= 0) {
+        if (fabs(dot(ref_reflect(vneg(wi), n), wo) - 1) > DELTA_EPSILON) return 0.0;
+        return F;
+    }
+    if (fabs(dot(ref_refract(wi, n, ior, cosThetaT), wo) - 1) > DELTA_EPSILON) return 0.0;
+    return 1.0 - F;
+}
+static inline v3 dielectric_generate(v3 n, v3 wi, double ior, double s0)
+{
+    double cosThetaT;
+    double F = fresnelDielectricExt(dot(wi, n), &cosThetaT, ior);
+    if (s0 <= F) return ref_reflect(vneg(wi), n);
+    return ref_refract(wi, n, ior, cosThetaT);
+}
+/* dielectric::eval_bsdf (material.h:146-171) */
+static inline v3 dielectric_eval(const double ks[3], double ior, v3 n, v3 wi, v3 wo)
+{
+    double cosThetaT;
+    double F = fresnelDielectricExt(dot(wi, n), &cosThetaT, ior);
+    if (dot(wi, n) * dot(wo, n) >= 0) {
+        if (fabs(dot(ref_reflect(vneg(wi), n), wo) - 1) > DELTA_EPSILON) return mk(0.0, 0.0, 0.0);
+        return mk(ks[0] * F, ks[1] * F, ks[2] * F);
+    }
+    if (fabs(dot(ref_refract(wi, n, ior, cosThetaT), wo) - 1) > DELTA_EPSILON) return mk(0.0, 0.0, 0.0);
+    double factor = cosThetaT < 0 ? (1.0 / ior) : (ior);
+    return mk(ks[0] * factor * factor * (1 - F), ks[1] * factor * factor * (1 - F), ks[2] * factor * factor * (1 - F));
+}
+
 /* util.h:21-41 */
 static inline void random_in_unit_disk(double s0, double s1, double *ox, double *oy)
 {
@@ -253,7 +338,7 @@ static inline ray camera_get_ray(const camera *c, double s, double t, double l0,
 /* ------------------------------------------------------------------------ */
 /* scene                                                                    */
 /* ------------------------------------------------------------------------ */
-enum { MAT_LAMBERT = 0, MAT_LIGHT = 1, MAT_PHONG = 2, MAT_DIELECTRIC = 3 };
+enum { MAT_LAMBERT = 0, MAT_LIGHT = 1, MAT_PHONG = 2, MAT_DIELECTRIC = 4 };   /* = FRT_MAT_* */
 typedef struct { int type; v3 albedo; v3 emit; double ks[3], ior, shininess; } material;
 
 typedef struct {
@@ -484,9 +569,9 @@ static inline int pick_sample(double sample, int list_size)
 typedef struct { const ora_scene *s; rng_key key; ora_counters *cnt; } li_ctx;
 
 /* path::Li (path.cpp:4-116), recursive like the reference so the
- * association order of every product/sum matches.  Only the non-specular
- * (lambertian) scatter branch and diffuse_light emission are reachable in the
- * hot-path scenes; other material types are rejected at load. */
+ * association order of every product/sum matches.  Materials: lambertian,
+ * diffuse_light, modified_phong and dielectric (the ones mesh_loader.cpp:59-112
+ * creates); the specular branch is path.cpp:78-95. */
 static v3 Li(li_ctx *c, const ray *r, int depth, const hit_record *prev, double prev_bsdf_pdf)
 {
     const ora_scene *s = c->s;
@@ -506,11 +591,20 @@ static v3 Li(li_ctx *c, const ray *r, int depth, const hit_record *prev, double 
             return smul(weight, Le);
         }
         const material *m = &s->mats[hrec.mat];
-        /* lambertian::scatter always succeeds; diffuse_light::scatter fails (material.h:55-60,183) */
-        if (depth <= 33 && m->type == MAT_LAMBERT) {
+        /* lambertian / modified_phong / dielectric::scatter succeed; diffuse_light's fails (material.h) */
+        if (depth <= 33 && (m->type == MAT_LAMBERT || m->type == MAT_PHONG || m->type == MAT_DIELECTRIC)) {
             const uint32_t base = DIM_BOUNCE(depth);
+            const int specular = m->type != MAT_LAMBERT;
+            const v3 wi = vneg(unit(r->d));                   /* hrec.wi (triangle.h:108, sphere.h:47) */
+            /* scatter's get3d sample: phong / dielectric direction (material.h:83-88, 139-145) */
+            v3 spec_dir = mk(0, 0, 0);
+            if (m->type == MAT_PHONG)
+                spec_dir = cosine_power_generate(hrec.normal, wi, m->shininess, rng_u(c->key, base + 0),
+                                                 rng_u(c->key, base + 1));
+            else if (m->type == MAT_DIELECTRIC)
+                spec_dir = dielectric_generate(hrec.normal, wi, m->ior, rng_u(c->key, base + 0));
             const int index = pick_sample(rng_u(c->key, base + 3), s->nlights);
-            if (index >= 0) {
+            if (index >= 0 && m->type != MAT_DIELECTRIC) {
                 hit_record lrec;
                 v3 offset_origin = vadd(hrec.p, smul(EPSILON, hrec.normal));
                 v3 to_light = prim_sample_direct(s, s->lights[index], &lrec, offset_origin,
@@ -521,20 +615,38 @@ static v3 Li(li_ctx *c, const ray *r, int depth, const hit_record *prev, double 
                 if (!world_hit(s, &shadow, EPSILON, 1 - SHADOW_EPSILON, &lrec, c->cnt)) {
                     to_light = make_unit(to_light);
                     shadow.d = to_light;
-                    v3 surface_bsdf = sdiv(m->albedo, M_PI);
+                    v3 surface_bsdf = specular ? phong_eval(m->albedo, m->ks, m->shininess, hrec.normal, wi, to_light)
+                                               : sdiv(m->albedo, M_PI);
                     const double cos_wi = dot(hrec.normal, unit(to_light));
                     const double cos_wo = dot(lrec.normal, vneg(unit(to_light)));
                     if (cos_wo != 0) {
                         double distance_squared = dist_to_light * dist_to_light;
-                        surface_bsdf = vscale_inplace(surface_bsdf, cos_wi);
+                        if (!specular) surface_bsdf = vscale_inplace(surface_bsdf, cos_wi);
                         const double light_pdf = prim_pdf_direct(s, s->lights[index], &hrec, to_light)
                                                  * distance_squared / fabs(cos_wo);
-                        const double surface_bsdf_pdf = cosine_pdf_value(hrec.normal, to_light);
+                        const double surface_bsdf_pdf =
+                            specular ? cosine_power_value(hrec.normal, wi, m->shininess, to_light)
+                                     : cosine_pdf_value(hrec.normal, to_light);
                         const double weight = miWeight(light_pdf, surface_bsdf_pdf);
                         v3 em = mat_emitted(s, lrec.mat, shadow.d, lrec.normal);
                         Le = vadd(Le, sdiv(smul(weight, vmul(em, surface_bsdf)), light_pdf));
                     }
                 }
+            }
+            if (specular) {                                   /* path.cpp:78-95 */
+                const double surface_bsdf_pdf = (m->type == MAT_PHONG)
+                    ? cosine_power_value(hrec.normal, wi, m->shininess, spec_dir)
+                    : dielectric_value(hrec.normal, wi, m->ior, spec_dir);
+                const v3 surface_bsdf = (m->type == MAT_PHONG)
+                    ? phong_eval(m->albedo, m->ks, m->shininess, hrec.normal, wi, spec_dir)
+                    : dielectric_eval(m->ks, m->ior, hrec.normal, wi, spec_dir);
+                if (surface_bsdf_pdf == 0) return mk(0, 0, 0);
+                const int outside = dot(hrec.normal, spec_dir) > 0;
+                ray sr;
+                sr.o = outside ? vadd(hrec.p, smul(EPSILON, hrec.normal)) : vsub(hrec.p, smul(EPSILON, hrec.normal));
+                sr.d = spec_dir;
+                v3 li = Li(c, &sr, depth + 1, &hrec, surface_bsdf_pdf);
+                return vadd(Le, sdiv(vmul(surface_bsdf, li), surface_bsdf_pdf));
             }
             /* diffuse bounce (path.cpp:96-110) */
             onb uvw = onb_from_w(hrec.normal);
@@ -649,7 +761,8 @@ static v3 mlt_Li(const ora_scene *s, const ray *r, mlt_state *st)
     if (st->depth == 0) st->cnt->camera_rays++; else if (st->depth <= MLT_MAX_PATH) st->cnt->extension_rays++;
     if (st->depth <= MLT_MAX_PATH && world_hit(s, r, EPSILON, FLT_MAX, &hrec, st->cnt)) {
         v3 Le = mat_emitted(s, hrec.mat, r->d, hrec.normal);
-        st->off += 3;                                          /* scatter rnd (unused by lambertian) */
+        const double rnd_s0 = st->prnds[st->off + 0], rnd_s1 = st->prnds[st->off + 1];   /* scatter rnd */
+        st->off += 3;
         if ((Le.e[0] != 0.0) || (Le.e[1] != 0.0) || (Le.e[2] != 0.0)) {
             if (st->depth == 0 || s->mats[st->prev.mat].type == MAT_PHONG || s->mats[st->prev.mat].type == MAT_DIELECTRIC)
                 return Le;
@@ -661,11 +774,16 @@ static v3 mlt_Li(const ora_scene *s, const ray *r, mlt_state *st)
             return smul(weight, Le);
         }
         const material *m = &s->mats[hrec.mat];
-        if (m->type == MAT_LAMBERT) {
+        if (m->type == MAT_LAMBERT || m->type == MAT_PHONG || m->type == MAT_DIELECTRIC) {
+            const int specular = m->type != MAT_LAMBERT;
+            const v3 wi = vneg(unit(r->d));
+            v3 spec_dir = mk(0, 0, 0);
+            if (m->type == MAT_PHONG) spec_dir = cosine_power_generate(hrec.normal, wi, m->shininess, rnd_s0, rnd_s1);
+            else if (m->type == MAT_DIELECTRIC) spec_dir = dielectric_generate(hrec.normal, wi, m->ior, rnd_s0);
             const double rnd0 = st->prnds[st->off + 0], rnd1 = st->prnds[st->off + 1], rnd2 = st->prnds[st->off + 2];
             st->off += 3;
             const int index = pick_sample(rnd0, s->nlights);
-            if (index >= 0) {
+            if (index >= 0 && m->type != MAT_DIELECTRIC) {
                 hit_record lrec;
                 v3 offset_origin = vadd(hrec.p, smul(EPSILON, hrec.normal));
                 v3 to_light = prim_sample_direct(s, s->lights[index], &lrec, offset_origin, rnd1, rnd2);
@@ -675,20 +793,41 @@ static v3 mlt_Li(const ora_scene *s, const ray *r, mlt_state *st)
                 if (!world_hit(s, &shadow, EPSILON, 1 - SHADOW_EPSILON, &lrec, st->cnt)) {
                     to_light = make_unit(to_light);
                     shadow.d = to_light;
-                    v3 surface_bsdf = sdiv(m->albedo, M_PI);
+                    v3 surface_bsdf = specular ? phong_eval(m->albedo, m->ks, m->shininess, hrec.normal, wi, to_light)
+                                               : sdiv(m->albedo, M_PI);
                     const double cos_wi = dot(hrec.normal, unit(to_light));
                     const double cos_wo = dot(lrec.normal, vneg(unit(to_light)));
                     if (cos_wo != 0) {
                         double distance_squared = dist_to_light * dist_to_light;
-                        surface_bsdf = vscale_inplace(surface_bsdf, cos_wi);
+                        if (!specular) surface_bsdf = vscale_inplace(surface_bsdf, cos_wi);
                         const double light_pdf = prim_pdf_direct(s, s->lights[index], &hrec, to_light)
                                                  * distance_squared / fabs(cos_wo);
-                        const double surface_bsdf_pdf = cosine_pdf_value(hrec.normal, to_light);
+                        const double surface_bsdf_pdf =
+                            specular ? cosine_power_value(hrec.normal, wi, m->shininess, to_light)
+                                     : cosine_pdf_value(hrec.normal, to_light);
                         const double weight = miWeight(light_pdf, surface_bsdf_pdf);
                         v3 em = mat_emitted(s, lrec.mat, shadow.d, lrec.normal);
                         Le = vadd(Le, sdiv(smul(weight, vmul(em, surface_bsdf)), light_pdf));
                     }
                 }
+            }
+            if (specular) {                                   /* pssmlt.cpp:232-249 */
+                const double surface_bsdf_pdf = (m->type == MAT_PHONG)
+                    ? cosine_power_value(hrec.normal, wi, m->shininess, spec_dir)
+                    : dielectric_value(hrec.normal, wi, m->ior, spec_dir);
+                const v3 surface_bsdf = (m->type == MAT_PHONG)
+                    ? phong_eval(m->albedo, m->ks, m->shininess, hrec.normal, wi, spec_dir)
+                    : dielectric_eval(m->ks, m->ior, hrec.normal, wi, spec_dir);
+                if (surface_bsdf_pdf == 0) return mk(0, 0, 0);
+                const int outside = dot(hrec.normal, spec_dir) > 0;
+                ray sr;
+                sr.o = outside ? vadd(hrec.p, smul(EPSILON, hrec.normal)) : vsub(hrec.p, smul(EPSILON, hrec.normal));
+                sr.d = spec_dir;
+                st->depth += 1;
+                st->prev_pdf = surface_bsdf_pdf;
+                st->prev = hrec;
+                v3 li = mlt_Li(s, &sr, st);
+                return vadd(Le, sdiv(vmul(surface_bsdf, li), surface_bsdf_pdf));
             }
             /* diffuse bounce: hrec.p is moved off the surface first (pssmlt.cpp:253) */
             hrec.p = vadd(hrec.p, smul(EPSILON, hrec.normal));
@@ -1344,7 +1483,8 @@ int ora_load_scene(const char *kind, const char *obj_path, double aspect, ora_sc
     }
     s->lights = lights; s->nlights = nlights;
     for (int i = 0; i < s->nmats; ++i)
-        if (s->mats[i].type != MAT_LAMBERT && s->mats[i].type != MAT_LIGHT) { ora_free_scene(s); return -4; }
+        if (s->mats[i].type != MAT_LAMBERT && s->mats[i].type != MAT_LIGHT && s->mats[i].type != MAT_PHONG &&
+            s->mats[i].type != MAT_DIELECTRIC) { ora_free_scene(s); return -4; }
     *out = s;
     return 0;
 }
@@ -1456,6 +1596,40 @@ void ora_kat_cosine(const double *n, const double *smp, double *out4)
     v3 d = onb_from_local(&b, hemisphere_to_cosine_direction(smp[0], smp[1]));
     vstore(out4, d);
     out4[3] = cosine_pdf_value(vload(n), d);
+}
+/* specular KATs (ref_kat.cpp kat_specular) */
+void ora_kat_fresnel(const double *n, const double *wi, double eta, double *out8)
+{
+    double cosT = 0;
+    const double F = fresnelDielectricExt(dot(vload(wi), vload(n)), &cosT, eta);
+    out8[0] = F; out8[1] = cosT;
+    vstore(out8 + 2, ref_reflect(vneg(vload(wi)), vload(n)));
+    vstore(out8 + 5, ref_refract(vload(wi), vload(n), eta, cosT));
+}
+void ora_kat_phong(const double *n, const double *wi, double e, double s0, double s1, const double *wo,
+                   const double *kd, const double *ks, double *out11)
+{
+    const v3 N = vload(n), WI = vload(wi), WO = vload(wo);
+    const v3 d = cosine_power_generate(N, WI, e, s0, s1);
+    vstore(out11, d);
+    out11[3] = cosine_power_value(N, WI, e, d);
+    out11[4] = cosine_power_value(N, WI, e, WO);
+    vstore(out11 + 5, phong_eval(vload(kd), ks, e, N, WI, d));
+    vstore(out11 + 8, phong_eval(vload(kd), ks, e, N, WI, WO));
+}
+void ora_kat_dielectric(const double *n, const double *wi, double ior, double u0, const double *wo, const double *ks,
+                        double *out12)
+{
+    const v3 N = vload(n), WI = vload(wi), WO = vload(wo);
+    const v3 d = dielectric_generate(N, WI, ior, u0);
+    double cosT = 0;
+    const double F = fresnelDielectricExt(dot(WI, N), &cosT, ior);
+    vstore(out12, d);
+    out12[3] = (u0 <= F) ? 1.0 : (cosT < 0 ? ior : (1.0 / ior));   /* srec.eta (pdf.h:171-181) */
+    out12[4] = dielectric_value(N, WI, ior, d);
+    out12[5] = dielectric_value(N, WI, ior, WO);
+    vstore(out12 + 6, dielectric_eval(ks, ior, N, WI, d));
+    vstore(out12 + 9, dielectric_eval(ks, ior, N, WI, WO));
 }
 void ora_kat_tri_sample(const double *v9, const double *n9, int geo, int n_tris_in_mesh, const double *o,
                         const double *smp, double *out10)

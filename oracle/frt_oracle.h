@@ -102,6 +102,11 @@ void ora_kat_camera(const double *from, const double *at, const double *vup, dou
                     double aperture, double focus, double s, double t, const double *smp, double *out6);
 /* cosine pdf around unit normal n: generate(sample2) -> dir[3], value(dir) */
 void ora_kat_cosine(const double *n, const double *smp, double *out4);
+void ora_kat_fresnel(const double *n, const double *wi, double eta, double *out8);
+void ora_kat_phong(const double *n, const double *wi, double e, double s0, double s1, const double *wo,
+                   const double *kd, const double *ks, double *out11);
+void ora_kat_dielectric(const double *n, const double *wi, double ior, double u0, const double *wo, const double *ks,
+                        double *out12);
 /* triangle sample_direct from o: out p[3], normal[3], to_light[3], pdf */
 void ora_kat_tri_sample(const double *v9, const double *n9, int geo, int n_tris_in_mesh, const double *o,
                         const double *smp, double *out10);

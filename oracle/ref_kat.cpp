@@ -20,6 +20,7 @@
 #include "bvh.h"
 #include "hitable_list.h"
 #include "image.h"
+#include "material.h"
 
 #include <cstdio>
 #include <cstdint>
@@ -308,6 +309,53 @@ static void kat_list_hit(int ncases)
 }
 
 // image_pfm::save_image byte layout (image.h:89-118).  Writes to $HOME/<name>.
+// specular materials: util.h reflect / refract / fresnelDielectricExt,
+// cosine_power_pdf + modified_phong::eval_bsdf, dielectric_pdf + dielectric::eval_bsdf
+static void kat_specular(int ncases)
+{
+    for (int c = 0; c < ncases; ++c) {
+        double n[3], w[3];
+        rand_unit(n);
+        rand_unit(w);
+        Vector3f nv(n[0], n[1], n[2]), wi(w[0], w[1], w[2]);
+        if (c % 4 == 0 && dot(nv, wi) < 0) wi = -wi;         // mostly from outside
+        // reflect / fresnel / refract
+        const double eta = (c % 9 == 0) ? 1.0 : (double)(float)(1.05 + 1.5 * urand());
+        double cosT = 0;
+        const double F = fresnelDielectricExt(dot(wi, nv), cosT, eta);
+        Vector3f rfl = reflect(-wi, nv);
+        Vector3f rfr = refract(wi, nv, eta, cosT);
+        printf("fresnel"); pv(nv); pv(wi); p(eta); bar(); p(F); p(cosT); pv(rfl); pv(rfr); printf("\n");
+        // cosine_power_pdf + modified_phong
+        const double e = (c % 3 == 0) ? 1024.0 : (double)(float)(1 + 200 * urand());
+        hit_record h;
+        h.normal = nv; h.wi = wi; h.p = Vector3f(0, 0, 0);
+        ray r_in(Vector3f(0, 0, 0), -wi);
+        cosine_power_pdf cpp(r_in, nv, e);
+        scatter_record srec(h);
+        const double s0 = urand(), s1 = urand();
+        Vector3f d = cpp.generate(Vector2f(s0, s1), srec);
+        double dr[3];
+        rand_unit(dr);
+        Vector3f wo(dr[0], dr[1], dr[2]);
+        const Vector3f kd(urand(), urand(), urand()), ks(urand(), urand(), urand());
+        modified_phong ph(new constant_texture(kd), new constant_texture(ks), e);
+        printf("phong"); pv(nv); pv(wi); p(e); p(s0); p(s1); pv(wo); pv(kd); pv(ks); bar();
+        pv(d); p(cpp.value(h, d)); p(cpp.value(h, wo)); pv(ph.eval_bsdf(r_in, h, d)); pv(ph.eval_bsdf(r_in, h, wo));
+        printf("\n");
+        // dielectric_pdf + dielectric
+        const double ior = (c % 7 == 0) ? 1.0 : (double)(float)(1.1 + 1.5 * urand());
+        dielectric_pdf dp(nv, ior);
+        scatter_record srec2(h);
+        const double u0 = (c % 5 == 0) ? 0.999999 : urand();
+        Vector3f dd = dp.generate(Vector2f(u0, 0.5), srec2);
+        dielectric de(ior, new constant_texture(ks), new constant_texture(Vector3f(1.0, 1.0, 1.0)));
+        printf("dielectric"); pv(nv); pv(wi); p(ior); p(u0); pv(wo); pv(ks); bar();
+        pv(dd); p(srec2.eta); p(dp.value(h, dd)); p(dp.value(h, wo)); pv(de.eval_bsdf(r_in, h, dd)); pv(de.eval_bsdf(r_in, h, wo));
+        printf("\n");
+    }
+}
+
 static void kat_pfm()
 {
     const int nx = 3, ny = 2, nn = 3;
@@ -330,6 +378,7 @@ int main(int argc, char **argv)
     kat_scalar(n / 2);
     kat_sort(n / 4);
     kat_list_hit(n / 2);
+    kat_specular(n);
     kat_pfm();
     return 0;
 }

@@ -76,6 +76,38 @@ def test_cosine_pdf(kat):
         assert bits_equal(out, want), (ins, out, want)
 
 
+def test_specular_fresnel_reflect_refract(kat):
+    """util.h reflect / refract / fresnelDielectricExt (incl. eta == 1 and total internal reflection)."""
+    L = oracle.lib()
+    for ins, outs in kat["fresnel"]:
+        x = H(ins); want = H(outs)
+        out = np.zeros(8)
+        L.ora_kat_fresnel(darr(x[0:3])[1], darr(x[3:6])[1], x[6], out.ctypes.data_as(darr([0])[1].__class__))
+        assert bits_equal(out, want), (ins, out, want)
+
+
+def test_specular_phong(kat):
+    """cosine_power_pdf generate / value and modified_phong::eval_bsdf (pdf.h:99-136, material.h:75-108)."""
+    L = oracle.lib()
+    for ins, outs in kat["phong"]:
+        x = H(ins); want = H(outs)
+        out = np.zeros(11)
+        L.ora_kat_phong(darr(x[0:3])[1], darr(x[3:6])[1], x[6], x[7], x[8], darr(x[9:12])[1], darr(x[12:15])[1],
+                        darr(x[15:18])[1], out.ctypes.data_as(darr([0])[1].__class__))
+        assert bits_equal(out, want), (ins, out, want)
+
+
+def test_specular_dielectric(kat):
+    """dielectric_pdf generate / value (+ srec.eta) and dielectric::eval_bsdf (pdf.h:138-184, material.h:133-177)."""
+    L = oracle.lib()
+    for ins, outs in kat["dielectric"]:
+        x = H(ins); want = H(outs)
+        out = np.zeros(12)
+        L.ora_kat_dielectric(darr(x[0:3])[1], darr(x[3:6])[1], x[6], x[7], darr(x[8:11])[1], darr(x[11:14])[1],
+                             out.ctypes.data_as(darr([0])[1].__class__))
+        assert bits_equal(out, want), (ins, out, want)
+
+
 def test_tri_sample_direct(kat):
     L = oracle.lib()
     for ins, outs in kat["tri_sample"]:
@@ -142,6 +174,6 @@ def test_kat_coverage(kat):
     # every component kind the reference harness emits is checked above
     assert {k for k in kat if not k.startswith("_")} == {
         "tri_hit", "sphere_hit", "aabb_hit", "camera", "cosine", "tri_sample", "sphere_sample",
-        "miweight", "fromsrgb", "pick", "sort", "list_hit", "pfm"}
+        "miweight", "fromsrgb", "pick", "sort", "list_hit", "pfm", "fresnel", "phong", "dielectric"}
     hits = sum(int(float.fromhex(o[0])) for _, o in kat["tri_hit"])
     assert 20 < hits < len(kat["tri_hit"]) - 20, "KAT set should mix hits and misses"
