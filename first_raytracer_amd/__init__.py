@@ -18,7 +18,8 @@ LIB_PATH = os.environ.get("FRT_LIB_PATH") or os.path.join(HERE, "libfrt.so")
 FRT_WORLD_BVH, FRT_WORLD_LIST = 0, 1
 FRT_MAT_LAMBERTIAN, FRT_MAT_DIFFUSE_LIGHT = 0, 1
 FRT_PRIM_SPHERE = 1 << 30
-ABI_VERSION = 2                 # include/frt.h FRT_ABI_VERSION (frt_stats layout)
+ABI_VERSION = 3                 # include/frt.h FRT_ABI_VERSION (frt_stats / frt_material layout)
+FRT_MAT_LAMBERTIAN, FRT_MAT_DIFFUSE_LIGHT, FRT_MAT_MODIFIED_PHONG, FRT_MAT_DIELECTRIC = 0, 1, 2, 4
 FRT_FLAG_NO_LDS_SCENE = 1
 FRT_FLAG_WAVES5 = 2
 FRT_FLAG_WAVES6 = 4
@@ -38,7 +39,8 @@ class FrtError(RuntimeError):
 
 class Material(ctypes.Structure):
     _fields_ = [("type", ctypes.c_int32), ("reserved", ctypes.c_int32),
-                ("albedo", ctypes.c_double * 3), ("emit", ctypes.c_double * 3)]
+                ("albedo", ctypes.c_double * 3), ("emit", ctypes.c_double * 3),
+                ("specular", ctypes.c_double * 3), ("exponent", ctypes.c_double), ("ior", ctypes.c_double)]
 
 
 class SceneView(ctypes.Structure):

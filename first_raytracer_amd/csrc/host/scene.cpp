@@ -400,12 +400,15 @@ struct frt_host_scene {
     int bvh_depth = 0;
     double load_ms = 0, build_ms = 0;
 
-    int add_material(int type, V3 albedo, V3 emit)
+    int add_material(int type, V3 albedo, V3 emit, V3 specular = {}, double exponent = 0, double ior = 0)
     {
         frt_material m{};
         m.type = type;
         m.albedo[0] = albedo.x; m.albedo[1] = albedo.y; m.albedo[2] = albedo.z;
         m.emit[0] = emit.x; m.emit[1] = emit.y; m.emit[2] = emit.z;
+        m.specular[0] = specular.x; m.specular[1] = specular.y; m.specular[2] = specular.z;
+        m.exponent = exponent;
+        m.ior = ior;
         mats.push_back(m);
         return (int)mats.size() - 1;
     }
@@ -446,7 +449,8 @@ bool add_obj(frt_host_scene &s, const std::string &path, bool geo)
         if (nf == 0) continue;  // Assimp drops empty meshes
         const Mtl *mt = (m.mtl >= 0) ? &od.mats[m.mtl] : nullptr;
         int type;
-        V3 albedo, emit;
+        V3 albedo, emit, spec;
+        double exponent = 0, ior = 0;
         if (!mt) {  // DefaultMaterial -> lambertian 0.5 (mesh_loader.cpp:107-111)
             type = FRT_MAT_LAMBERTIAN;
             albedo = {0.5, 0.5, 0.5};
@@ -454,13 +458,18 @@ bool add_obj(frt_host_scene &s, const std::string &path, bool geo)
             type = FRT_MAT_DIFFUSE_LIGHT;
             emit = {mt->ke[0], mt->ke[1], mt->ke[2]};
         } else if (mt->ks[0] != 0 || mt->ks[1] != 0 || mt->ks[2] != 0) {
-            type = (mt->d < 1.0f) ? 4 : 2;  // dielectric / modified_phong: outside the hot path
+            // opacity < 1: dielectric(Ni, FromSrgb(Ks), 1); else modified_phong(FromSrgb(Kd), FromSrgb(Ks), Ns)
+            // (mesh_loader.cpp:78-100)
+            type = (mt->d < 1.0f) ? FRT_MAT_DIELECTRIC : FRT_MAT_MODIFIED_PHONG;
             albedo = {from_srgb(mt->kd[0]), from_srgb(mt->kd[1]), from_srgb(mt->kd[2])};
+            spec = {from_srgb(mt->ks[0]), from_srgb(mt->ks[1]), from_srgb(mt->ks[2])};
+            exponent = mt->ns;
+            ior = mt->ni;
         } else {
             type = FRT_MAT_LAMBERTIAN;
             albedo = {from_srgb(mt->kd[0]), from_srgb(mt->kd[1]), from_srgb(mt->kd[2])};
         }
-        const int mat = s.add_material(type, albedo, emit);
+        const int mat = s.add_material(type, albedo, emit, spec, exponent, ior);
         bool has_vn = true;
         for (int x : m.vn) if (x < 0) { has_vn = false; break; }
         std::vector<float> cn;

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FRT_ABI_VERSION 2
+#define FRT_ABI_VERSION 3
 
 enum {
     FRT_OK = 0,
@@ -40,7 +40,10 @@ enum {
 };
 
 enum { FRT_WORLD_BVH = 0, FRT_WORLD_LIST = 1 };          /* parallel_bvh_node | hitable_list */
-enum { FRT_MAT_LAMBERTIAN = 0, FRT_MAT_DIFFUSE_LIGHT = 1 }; /* material.h:50-73, 179-192 */
+enum { FRT_MAT_LAMBERTIAN = 0,      /* material.h:50-73                                  */
+       FRT_MAT_DIFFUSE_LIGHT = 1,   /* material.h:179-192                                */
+       FRT_MAT_MODIFIED_PHONG = 2,  /* material.h:75-108 + cosine_power_pdf (pdf.h:99)   */
+       FRT_MAT_DIELECTRIC = 4 };    /* material.h:133-177 + dielectric_pdf (pdf.h:138)   */
 enum { FRT_INTEGRATOR_PATH = 0, FRT_INTEGRATOR_PSSMLT = 1 };  /* path.h:8-18, pssmlt.h:29-76 */
 enum { FRT_FLAG_NO_LDS_SCENE = 1,      /* render_params.flags: keep small scenes in HBM/L2 (A/B timing)  */
        FRT_FLAG_WAVES5 = 2,            /* register cap for 5 waves/SIMD (A/B timing)                     */
@@ -55,10 +58,13 @@ enum { FRT_FLAG_NO_LDS_SCENE = 1,      /* render_params.flags: keep small scenes
 #define FRT_PRIM_SPHERE (1 << 30)
 
 typedef struct frt_material {
-    int32_t type;            /* FRT_MAT_*                                     */
+    int32_t type;            /* FRT_MAT_*                                                 */
     int32_t reserved;
-    double albedo[3];        /* lambertian: constant_texture colour (linear)  */
-    double emit[3];          /* diffuse_light: constant_texture colour        */
+    double albedo[3];        /* lambertian albedo / modified_phong diffuse_reflectance    */
+    double emit[3];          /* diffuse_light: constant_texture colour                    */
+    double specular[3];      /* modified_phong / dielectric: specular_reflectance         */
+    double exponent;         /* modified_phong: specular_exponent                         */
+    double ior;              /* dielectric: ref_idx                                       */
 } frt_material;
 
 typedef struct frt_scene_view {

@@ -135,7 +135,7 @@ class OracleScene:
         return out[:self.info.n_lights]
 
     def materials(self):
-        out = np.zeros((max(self.info.n_materials, 1), 7))
+        out = np.zeros((max(self.info.n_materials, 1), 12))
         lib().ora_scene_export_materials(self.ptr, out.ctypes.data)
         return out[:self.info.n_materials]
 

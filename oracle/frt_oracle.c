@@ -1532,11 +1532,14 @@ int ora_scene_export_lights(const ora_scene *s, int32_t *refs)
     for (int i = 0; i < s->nlights; ++i) refs[i] = s->lights[i];
     return s->nlights;
 }
-int ora_scene_export_materials(const ora_scene *s, double *out7)
+int ora_scene_export_materials(const ora_scene *s, double *out12)
 {
     for (int i = 0; i < s->nmats; ++i) {
-        out7[7 * i] = s->mats[i].type;
-        vstore(out7 + 7 * i + 1, s->mats[i].albedo); vstore(out7 + 7 * i + 4, s->mats[i].emit);
+        double *o = out12 + 12 * i;
+        o[0] = s->mats[i].type;
+        vstore(o + 1, s->mats[i].albedo); vstore(o + 4, s->mats[i].emit);
+        o[7] = s->mats[i].ks[0]; o[8] = s->mats[i].ks[1]; o[9] = s->mats[i].ks[2];
+        o[10] = s->mats[i].shininess; o[11] = s->mats[i].ior;
     }
     return s->nmats;
 }

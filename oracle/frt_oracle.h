@@ -63,7 +63,7 @@ int  ora_scene_export_tris(const ora_scene *s, double *v9, int32_t *mat);
 
 void ora_scene_export_camera(const ora_scene *s, double *out19);
 int  ora_scene_export_lights(const ora_scene *s, int32_t *refs);
-int  ora_scene_export_materials(const ora_scene *s, double *out7);
+int  ora_scene_export_materials(const ora_scene *s, double *out12);   /* type, albedo, emit, ks, Ns, Ni */
 
 /* Render pixels (linear index y*nx+x, y=0 bottom row) with `spp` samples each,
  * frame seed `seed`, on `nthreads` threads.  out_rgb[3*i..] = mean radiance

@@ -13,7 +13,12 @@ import os
 REF = "/root/reference/first_ray"
 DST = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scenes")
 FILES = ["CornellBox/CornellBox-Original.obj", "CornellBox/CornellBox-Original.mtl",
-         "veach_mi/veach_mi.obj", "veach_mi/veach_mi.mtl"]
+         "veach_mi/veach_mi.obj", "veach_mi/veach_mi.mtl",
+         # modified_phong variants (Ks != 0, opacity 1: mesh_loader.cpp:78-100)
+         "CornellBox/CornellBox-Glossy-Floor.obj",
+         "CornellBox/CornellBox-Glossy.mtl",   # the mtllib CornellBox-Glossy-Floor.obj names
+         "CornellBox/CornellBox-Sphere.obj", "CornellBox/CornellBox-Sphere.mtl",
+         "CornellBox/CornellBox-Mirror.obj", "CornellBox/CornellBox-Mirror.mtl"]
 
 
 def normalise(text):

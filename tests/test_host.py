@@ -21,7 +21,7 @@ def test_library_exports_every_declared_symbol():
     L = frt.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert L.frt_get_abi_version() == frt.ABI_VERSION == 2
+    assert L.frt_get_abi_version() == frt.ABI_VERSION == 3
 
 
 def test_create_without_device_fails_cleanly():
@@ -72,8 +72,8 @@ def test_cornell_scene_matches_oracle(cornell_obj, aspect):
     cam = np.concatenate([list(v.cam_origin), list(v.cam_lower_left), list(v.cam_horizontal),
                           list(v.cam_vertical), list(v.cam_u), list(v.cam_v), [v.cam_lens_radius]])
     assert np.array_equal(cam, osc.camera())
-    # materials: type, albedo, emit
-    mats = np.array([[m.type, *m.albedo, *m.emit] for m in
+    # materials: type, albedo, emit, specular, exponent, ior
+    mats = np.array([[m.type, *m.albedo, *m.emit, *m.specular, m.exponent, m.ior] for m in
                      (ctypes.cast(v.materials, ctypes.POINTER(frt.Material))[i] for i in range(v.n_materials))])
     assert np.array_equal(mats, osc.materials())
 
@@ -147,3 +147,21 @@ def test_pfm_writer_matches_reference_layout(tmp_path):
     frt.write_pfm(p1, film)
     oracle.lib().ora_write_pfm(p2.encode(), 3, 2, oracle.darr(film.astype(np.float64).ravel())[1])
     assert open(p1, "rb").read() == open(p2, "rb").read()
+
+
+@pytest.mark.parametrize("objfix", ["glossy_floor_obj", "sphere_obj", "mirror_obj", "glass_obj"])
+def test_specular_scene_materials_and_topology(objfix, request):
+    """Specular CornellBox variants: the host loader and the oracle loader agree
+    on every material (type, Kd, Ks, Ns, Ni via mesh_loader.cpp:59-112) and on
+    the BVH topology."""
+    obj = request.getfixturevalue(objfix)
+    hs = frt.HostScene("cornell_box_obj", obj, 1.0)
+    osc = oracle.OracleScene("cornell_box_obj", obj, 1.0)
+    v = hs.view()
+    mats = np.array([[m.type, *m.albedo, *m.emit, *m.specular, m.exponent, m.ior] for m in
+                     (ctypes.cast(v.materials, ctypes.POINTER(frt.Material))[i] for i in range(v.n_materials))])
+    assert np.array_equal(mats, osc.materials())
+    types = set(mats[:, 0].astype(int))
+    want = frt.FRT_MAT_DIELECTRIC if objfix == "glass_obj" else frt.FRT_MAT_MODIFIED_PHONG
+    assert want in types
+    assert hs.info.n_nodes == osc.info.n_nodes and hs.info.bvh_depth == osc.info.bvh_depth
