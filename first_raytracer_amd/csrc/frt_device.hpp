@@ -230,6 +230,87 @@ FRT_HD f3 random_to_sphere(float radius, float dist2, float r1, float r2)
     const float s = fsqrt(1.0f - z * z);
     return f3{cp * s, sp * s, z};
 }
+// x^y for x in [0, 1], y > 0 (phong lobes): exp2(y log2 x) on the hardware units
+FRT_HD float fpow01(float x, float y)
+{
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(FRT_EXP_IEEE_MATH)
+    return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
+#else
+    return powf(x, y);
+#endif
+}
+
+// ---- specular materials (material.h:75-171, pdf.h:99-184, util.h:73-117) ----
+constexpr float kDeltaEps = 1e-3f;                               // util.h:12 DELTA_EPSILON
+FRT_HD f3 reflect(f3 v, f3 n) { return normalize(v - (2.0f * dot(v, n)) * n); }   // util.h:73-76
+FRT_HD f3 refract(f3 wi, f3 n, float eta, float cos_t)                            // util.h:79-84
+{
+    if (cos_t < 0.0f) eta = rcp(eta);
+    return normalize((dot(wi, n) * eta + cos_t) * n - eta * wi);
+}
+FRT_HD float fresnel_dielectric(float cos_i, float &cos_t_out, float eta)       // util.h:86-117
+{
+    if (eta == 1.0f) { cos_t_out = -cos_i; return 0.0f; }
+    const float scale = (cos_i > 0.0f) ? rcp(eta) : eta;
+    const float cos_t2 = 1.0f - (1.0f - cos_i * cos_i) * (scale * scale);
+    if (cos_t2 <= 0.0f) { cos_t_out = 0.0f; return 1.0f; }      // total internal reflection
+    const float ci = fabsf(cos_i), ct = fsqrt(cos_t2);
+    const float rs = fdiv(ci - eta * ct, ci + eta * ct);
+    const float rp = fdiv(eta * ci - ct, eta * ci + ct);
+    cos_t_out = (cos_i > 0.0f) ? -ct : ct;
+    return 0.5f * (rs * rs + rp * rp);
+}
+// cosine_power_pdf (pdf.h:99-136); the onb's w is the shading normal
+FRT_HD float cosine_power_value(f3 n, f3 wi, float e, f3 wo)
+{
+    if (dot(n, wo) <= 0.0f || dot(n, wi) <= 0.0f) return 0.0f;
+    const float alpha = fmaxf(0.0f, dot(reflect(-wi, n), wo));
+    return fpow01(alpha, e) * (e + 1.0f) * (0.5f * kInvPi);
+}
+FRT_HD f3 cosine_power_generate(f3 n, f3 wi, float e, float s0, float s1)
+{
+    const f3 r = reflect(-wi, n);
+    const float sin_a = fsqrt(1.0f - fpow01(s1, fdiv(2.0f, e + 1.0f)));
+    const float cos_a = fpow01(s1, rcp(e + 1.0f));
+    float sp, cp;
+    sincos_2pi(s0, sp, cp);
+    return onb_local(onb_from_w(r), f3{sin_a * cp, sin_a * sp, cos_a});
+}
+// modified_phong::eval_bsdf (material.h:92-100), cosine included
+FRT_HD f3 phong_eval(f3 kd, f3 ks, float e, f3 n, f3 wi, f3 wo)
+{
+    const float alpha = fmaxf(0.0f, dot(normalize(reflect(-wi, n)), wo));
+    const f3 result = kInvPi * kd + ((e + 2.0f) * (0.5f * kInvPi) * fpow01(alpha, e)) * ks;
+    return dot(n, wo) * result;
+}
+// dielectric_pdf (pdf.h:138-184) and dielectric::eval_bsdf (material.h:146-171)
+FRT_HD float dielectric_value(f3 n, f3 wi, float ior, f3 wo)
+{
+    float cos_t;
+    const float F = fresnel_dielectric(dot(wi, n), cos_t, ior);
+    if (dot(wi, n) * dot(wo, n) >= 0.0f)
+        return (fabsf(dot(reflect(-wi, n), wo) - 1.0f) > kDeltaEps) ? 0.0f : F;
+    return (fabsf(dot(refract(wi, n, ior, cos_t), wo) - 1.0f) > kDeltaEps) ? 0.0f : 1.0f - F;
+}
+FRT_HD f3 dielectric_generate(f3 n, f3 wi, float ior, float s0)
+{
+    float cos_t;
+    const float F = fresnel_dielectric(dot(wi, n), cos_t, ior);
+    return (s0 <= F) ? reflect(-wi, n) : refract(wi, n, ior, cos_t);
+}
+FRT_HD f3 dielectric_eval(f3 ks, float ior, f3 n, f3 wi, f3 wo)
+{
+    float cos_t;
+    const float F = fresnel_dielectric(dot(wi, n), cos_t, ior);
+    if (dot(wi, n) * dot(wo, n) >= 0.0f) {
+        if (fabsf(dot(reflect(-wi, n), wo) - 1.0f) > kDeltaEps) return f3{0.0f, 0.0f, 0.0f};
+        return F * ks;
+    }
+    if (fabsf(dot(refract(wi, n, ior, cos_t), wo) - 1.0f) > kDeltaEps) return f3{0.0f, 0.0f, 0.0f};
+    const float factor = cos_t < 0.0f ? rcp(ior) : ior;
+    return (factor * factor * (1.0f - F)) * ks;
+}
+
 // util.h:55-60
 FRT_HD float mi_weight(float p1, float p2)
 {

@@ -63,7 +63,7 @@ struct PrndSource {
 };
 
 struct MltPath {
-    PathState P;           // ro, rd, rtmax, shadow, beta, L, nee, nxt_d, depth (prev_p unused)
+    PathState P;           // ro, rd, rtmax, shadow, beta, L, nee, nxt_d, depth, prev_spec (prev_p unused)
     int off;               // PathRndsOffset
     float x, y;            // film position of the eye ray (GenerateEyePath)
 };
@@ -94,6 +94,7 @@ FRT_HD void mlt_begin(MltPath &M, const DevScene &S, const PrndSource &src, int 
     P.beta = mk3(1, 1, 1);
     P.L = mk3(0, 0, 0);
     P.prev_pdf = 0.0f;
+    P.prev_spec = false;
     M.off = 4;
     const f3 dir = normalize(P.rd);
     const float dist = (float)ny / (2.0f * S.cam_half_height);
@@ -127,10 +128,11 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
     prim_shade(S, h.prim, P.ro, p, h.u, h.v, n, mat);
     const float4 m0 = S.mats[2 * mat], m1 = S.mats[2 * mat + 1];
     const int mtype = f2i(m0.w);
-    M.off += 3;                                         // scatter rnd, consumed at every hit
+    const float sc0 = src.get(M.off), sc1 = src.get(M.off + 1);   // scatter rnd (pssmlt.cpp:159-163)
+    M.off += 3;                                         // consumed at every hit
     if (mtype == FRT_MAT_DIFFUSE_LIGHT && dot(n, P.rd) < 0.0f) {
         const f3 Le = xyz(m1);
-        if (P.depth == 0) {
+        if (P.depth == 0 || P.prev_spec) {
             P.L = P.L + P.beta * Le;
         } else {                                        // pssmlt.cpp:175-184: distance^2 = t^2
             const float cos_wo = dot(n, -normalize(P.rd));
@@ -141,29 +143,49 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
         }
         return true;
     }
-    if (mtype != FRT_MAT_LAMBERTIAN) return true;      // diffuse_light seen from behind
-    // NEE prnds (pssmlt.cpp:190-195), then the bsdf prnds after the offset move
+    const bool lamb = mtype == FRT_MAT_LAMBERTIAN, phong = mtype == FRT_MAT_MODIFIED_PHONG,
+               diel = mtype == FRT_MAT_DIELECTRIC;
+    if (!(lamb || phong || diel)) return true;          // diffuse_light seen from behind
+    const f3 wi = -normalize(P.rd);
+    // NEE prnds (pssmlt.cpp:190-195); the bsdf prnds follow only for the diffuse branch
     const float rnd0 = src.get(M.off), rnd1 = src.get(M.off + 1), rnd2 = src.get(M.off + 2);
     M.off += 3;
-    const float b0 = src.get(M.off), b1 = src.get(M.off + 1);
-    M.off += 2;
-    const Onb uvw = onb_from_w(n);
-    const f3 wo = onb_local(uvw, cosine_direction(b0, b1));
-    const float cw = dot(n, normalize(wo));
-    const float pdf = fmaxf(cw, 0.0f) * kInvPi;
-    if (pdf == 0.0f) return true;                       // drops this vertex's NEE (pssmlt.cpp:261-264)
-    const f3 f = kInvPi * xyz(m0);
-    const f3 beta_next = fdiv(fabsf(cw), pdf) * (P.beta * f);
-    const f3 origin = p + kEps * n;
+    f3 wo, beta_next;
+    float pdf;
+    if (lamb) {
+        const float b0 = src.get(M.off), b1 = src.get(M.off + 1);
+        M.off += 2;
+        const Onb uvw = onb_from_w(n);
+        wo = onb_local(uvw, cosine_direction(b0, b1));
+        const float cw = dot(n, normalize(wo));
+        pdf = fmaxf(cw, 0.0f) * kInvPi;
+        if (pdf == 0.0f) return true;                   // drops this vertex's NEE (pssmlt.cpp:261-264)
+        beta_next = fdiv(fabsf(cw), pdf) * (P.beta * (kInvPi * xyz(m0)));
+    } else {                                            // pssmlt.cpp:232-249
+        f3 bsdf;
+        if (phong) {
+            wo = cosine_power_generate(n, wi, m1.w, sc0, sc1);
+            pdf = cosine_power_value(n, wi, m1.w, wo);
+            bsdf = phong_eval(xyz(m0), xyz(m1), m1.w, n, wi, wo);
+        } else {
+            wo = dielectric_generate(n, wi, m1.w, sc0);
+            pdf = dielectric_value(n, wi, m1.w, wo);
+            bsdf = dielectric_eval(xyz(m1), m1.w, n, wi, wo);
+        }
+        if (pdf == 0.0f) return true;
+        beta_next = P.beta * (rcp(pdf) * bsdf);
+    }
+    const f3 origin = (dot(n, wo) > 0.0f || lamb) ? p + kEps * n : p - kEps * n;   // hrec.p moved off (:243, :253)
     P.nxt_d = wo;
     const int nl = S.n_lights;
     int idx = (int)(rnd0 * (float)nl);
     if (idx == nl) idx -= 1;
-    if (idx >= 0) {
+    if (idx >= 0 && !diel) {
         const int lref = S.lights[idx];
         f3 ln;
         int lmat;
-        const f3 tl = prim_sample(S, lref, origin, rnd1, rnd2, ln, lmat);
+        const f3 nee_o = p + kEps * n;
+        const f3 tl = prim_sample(S, lref, nee_o, rnd1, rnd2, ln, lmat);
         const float dist2 = len2(tl);
         const f3 tu = rlen(tl) * tl;
         const float cos_wi = dot(n, tu);
@@ -171,20 +193,22 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
         P.nee = mk3(0, 0, 0);
         if (cos_lo != 0.0f) {
             const float light_pdf = fdiv(prim_pdf(S, lref, p, h.t, n, tu) * dist2, fabsf(cos_lo));
-            const float bsdf_pdf = fmaxf(cos_wi, 0.0f) * kInvPi;
+            const f3 f = lamb ? cos_wi * (kInvPi * xyz(m0)) : phong_eval(xyz(m0), xyz(m1), m1.w, n, wi, tu);
+            const float bsdf_pdf = lamb ? fmaxf(cos_wi, 0.0f) * kInvPi : cosine_power_value(n, wi, m1.w, tu);
             const float wgt = mi_weight(light_pdf, bsdf_pdf);
             const float4 lm0 = S.mats[2 * lmat], lm1 = S.mats[2 * lmat + 1];
             if (f2i(lm0.w) == FRT_MAT_DIFFUSE_LIGHT && dot(ln, tu) < 0.0f)
-                P.nee = (fdiv(wgt, light_pdf) * cos_wi) * (P.beta * (xyz(lm1) * f));
+                P.nee = fdiv(wgt, light_pdf) * (P.beta * (xyz(lm1) * f));
         }
-        P.ro = origin; P.rd = tl; P.rtmax = 1.0f - kShadowEps;
+        P.ro = nee_o; P.rd = tl; P.rtmax = 1.0f - kShadowEps;
         P.shadow = true;
         ++n_sh;
     }
     P.beta = beta_next;
     P.prev_pdf = pdf;
+    P.prev_spec = !lamb;
     if (!P.shadow) {
-        P.ro = origin; P.rd = wo; P.rtmax = kTMaxClosest;   // hrec.p moved off the surface (pssmlt.cpp:253)
+        P.ro = origin; P.rd = wo; P.rtmax = kTMaxClosest;
         ++P.depth;
         if (P.depth <= kMltMaxPath) ++n_ext;
     }

@@ -438,6 +438,7 @@ struct PathState {
     f3 nxt_d;             // extension direction after the shadow ray (its origin is the shadow ray's)
     f3 prev_p;            // previous hit point (MIS distance, path.cpp:25)
     float prev_pdf;       // bsdf pdf of the previous bounce
+    bool prev_spec;       // previous bounce was specular (modified_phong / dielectric): no MIS on light hits
     int depth;
     RngKey key;
 };
@@ -470,6 +471,7 @@ FRT_HD void path_begin(PathState &P, const DevScene &S, int px, int py, int nx, 
     P.L = mk3(0, 0, 0);
     P.prev_pdf = 0.0f;
     P.prev_p = mk3(0, 0, 0);
+    P.prev_spec = false;
 }
 
 // Shadow ray done (path.cpp:50-77): add the NEE term if unoccluded, then the
@@ -504,8 +506,8 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
     // diffuse_light::emitted is one-sided (material.h:184-190)
     if (mtype == FRT_MAT_DIFFUSE_LIGHT && dot(n, P.rd) < 0.0f) {
         const f3 Le = xyz(m1);
-        if (P.depth == 0) {
-            P.L = P.L + P.beta * Le;                    // path.cpp:16-22
+        if (P.depth == 0 || P.prev_spec) {
+            P.L = P.L + P.beta * Le;                    // path.cpp:16-22 (camera ray / after phong, dielectric)
         } else {                                        // path.cpp:24-31: MIS against the bsdf sample
             const float cos_wo = dot(n, -normalize(P.rd));
             float d2 = len2(p - P.prev_p);
@@ -515,27 +517,51 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
         }
         return true;
     }
-    if (mtype != FRT_MAT_LAMBERTIAN || P.depth > max_depth) return true;   // no scatter: Le (= 0)
+    const bool lamb = mtype == FRT_MAT_LAMBERTIAN, phong = mtype == FRT_MAT_MODIFIED_PHONG,
+               diel = mtype == FRT_MAT_DIELECTRIC;
+    if (!(lamb || phong || diel) || P.depth > max_depth) return true;   // no scatter: Le (= 0)
     const uint32_t base = dim_bounce(P.depth);
-    // bsdf sample first: a zero pdf drops this vertex's NEE too (path.cpp:96-106)
-    const Onb uvw = onb_from_w(n);
-    const f3 wo = onb_local(uvw, cosine_direction(rng_u(P.key, base + 6), rng_u(P.key, base + 7)));
-    const float cw = dot(n, normalize(wo));
-    const float pdf = fmaxf(cw, 0.0f) * kInvPi;
-    if (pdf == 0.0f) return true;
-    const f3 f = kInvPi * xyz(m0);                      // lambertian::eval_bsdf (material.h:62-65)
-    const f3 beta_next = fdiv(fabsf(cw), pdf) * (P.beta * f);
-    const f3 origin = p + kEps * n;
+    // The scattered direction first: a zero pdf returns 0 for this vertex,
+    // dropping its NEE too (path.cpp:84-86, 103-106).
+    f3 wo, beta_next;
+    float pdf;
+    const f3 wi = -normalize(P.rd);                     // hrec.wi (triangle.h:108, sphere.h:47)
+    if (lamb) {                                         // cosine_pdf (path.cpp:96-110)
+        const Onb uvw = onb_from_w(n);
+        wo = onb_local(uvw, cosine_direction(rng_u(P.key, base + 6), rng_u(P.key, base + 7)));
+        const float cw = dot(n, normalize(wo));
+        pdf = fmaxf(cw, 0.0f) * kInvPi;
+        if (pdf == 0.0f) return true;
+        beta_next = fdiv(fabsf(cw), pdf) * (P.beta * (kInvPi * xyz(m0)));   // lambertian::eval_bsdf
+    } else {                                            // specular branch (path.cpp:78-95); the
+        f3 bsdf;                                        // scatter sample is get3d's (base + 0, 1)
+        if (phong) {
+            const float e = m1.w;
+            wo = cosine_power_generate(n, wi, e, rng_u(P.key, base + 0), rng_u(P.key, base + 1));
+            pdf = cosine_power_value(n, wi, e, wo);
+            bsdf = phong_eval(xyz(m0), xyz(m1), e, n, wi, wo);
+        } else {
+            wo = dielectric_generate(n, wi, m1.w, rng_u(P.key, base + 0));
+            pdf = dielectric_value(n, wi, m1.w, wo);
+            bsdf = dielectric_eval(xyz(m1), m1.w, n, wi, wo);
+        }
+        if (pdf == 0.0f) return true;
+        beta_next = P.beta * (rcp(pdf) * bsdf);
+    }
+    // origin of the next ray: off the surface on the side it leaves (path.cpp:91-93, 99);
+    // equal to the NEE origin whenever NEE runs (phong's pdf > 0 means dot(n, wo) > 0)
+    const f3 origin = (dot(n, wo) > 0.0f || lamb) ? p + kEps * n : p - kEps * n;
     P.nxt_d = wo;
-    // next-event estimation (path.cpp:38-77)
+    // next-event estimation (path.cpp:38-77); not from dielectrics (path.cpp:40)
     const int nl = S.n_lights;
     int idx = (int)(rng_u(P.key, base + 3) * (float)nl);
     if (idx == nl) idx -= 1;
-    if (idx >= 0) {
+    if (idx >= 0 && !diel) {
         const int lref = S.lights[idx];
         f3 ln;
         int lmat;
-        const f3 tl = prim_sample(S, lref, origin, rng_u(P.key, base + 4), rng_u(P.key, base + 5), ln, lmat);
+        const f3 nee_o = p + kEps * n;
+        const f3 tl = prim_sample(S, lref, nee_o, rng_u(P.key, base + 4), rng_u(P.key, base + 5), ln, lmat);
         const float dist2 = len2(tl);
         const f3 tu = rlen(tl) * tl;
         const float cos_wi = dot(n, tu);
@@ -543,16 +569,19 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
         P.nee = mk3(0, 0, 0);
         if (cos_lo != 0.0f) {
             const float light_pdf = fdiv(prim_pdf(S, lref, p, h.t, n, tu) * dist2, fabsf(cos_lo));
-            const float bsdf_pdf = fmaxf(cos_wi, 0.0f) * kInvPi;
+            // eval_bsdf toward the light; only the non-specular bsdf gets the cosine (path.cpp:61-62)
+            const f3 f = lamb ? cos_wi * (kInvPi * xyz(m0)) : phong_eval(xyz(m0), xyz(m1), m1.w, n, wi, tu);
+            const float bsdf_pdf = lamb ? fmaxf(cos_wi, 0.0f) * kInvPi : cosine_power_value(n, wi, m1.w, tu);
             const float wgt = mi_weight(light_pdf, bsdf_pdf);
             const float4 lm0 = S.mats[2 * lmat], lm1 = S.mats[2 * lmat + 1];
             if (f2i(lm0.w) == FRT_MAT_DIFFUSE_LIGHT && dot(ln, tu) < 0.0f)
-                P.nee = (fdiv(wgt, light_pdf) * cos_wi) * (P.beta * (xyz(lm1) * f));
+                P.nee = fdiv(wgt, light_pdf) * (P.beta * (xyz(lm1) * f));
         }
-        P.ro = origin; P.rd = tl; P.rtmax = 1.0f - kShadowEps;
+        P.ro = nee_o; P.rd = tl; P.rtmax = 1.0f - kShadowEps;
         P.shadow = true;
         ++n_sh;
     }
+    P.prev_spec = !lamb;
     P.beta = beta_next;
     P.prev_p = p;
     P.prev_pdf = pdf;

@@ -797,10 +797,13 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     if (nt < 0 || ns < 0 || nm <= 0 || !sv->materials || (nt > 0 && (!sv->tri_v || !sv->tri_material || !sv->tri_inv_area)))
         return fail(FRT_E_INVALID, "scene view: missing triangle arrays or materials");
     if (ns > 0 && (!sv->sphere || !sv->sphere_material)) return fail(FRT_E_INVALID, "scene view: missing sphere arrays");
-    for (int i = 0; i < nm; ++i)
-        if (sv->materials[i].type != FRT_MAT_LAMBERTIAN && sv->materials[i].type != FRT_MAT_DIFFUSE_LIGHT)
-            return fail(FRT_E_UNSUPPORTED, "material type " + std::to_string(sv->materials[i].type) +
-                                               " is outside the hot path (lambertian/diffuse_light only)");
+    for (int i = 0; i < nm; ++i) {
+        const int t = sv->materials[i].type;
+        if (t != FRT_MAT_LAMBERTIAN && t != FRT_MAT_DIFFUSE_LIGHT && t != FRT_MAT_MODIFIED_PHONG &&
+            t != FRT_MAT_DIELECTRIC)
+            return fail(FRT_E_UNSUPPORTED, "material type " + std::to_string(t) +
+                                               " is not supported (lambertian, diffuse_light, modified_phong, dielectric)");
+    }
     auto valid_ref = [&](int ref) {
         if (ref < 0) return false;
         if (ref & FRT_PRIM_SPHERE) return (ref & ~FRT_PRIM_SPHERE) < ns;
@@ -958,8 +961,13 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     F.mats.resize(2 * (size_t)nm);
     for (int i = 0; i < nm; ++i) {
         const frt_material &m = sv->materials[i];
+        // (albedo | kd, type) | (emit, -) for lights, (ks, exponent | ior) for phong / dielectric
         F.mats[2 * i] = make_float4((float)m.albedo[0], (float)m.albedo[1], (float)m.albedo[2], i2f(m.type));
-        F.mats[2 * i + 1] = make_float4((float)m.emit[0], (float)m.emit[1], (float)m.emit[2], 0.0f);
+        if (m.type == FRT_MAT_MODIFIED_PHONG || m.type == FRT_MAT_DIELECTRIC)
+            F.mats[2 * i + 1] = make_float4((float)m.specular[0], (float)m.specular[1], (float)m.specular[2],
+                                            (float)(m.type == FRT_MAT_MODIFIED_PHONG ? m.exponent : m.ior));
+        else
+            F.mats[2 * i + 1] = make_float4((float)m.emit[0], (float)m.emit[1], (float)m.emit[2], 0.0f);
     }
     if (sv->n_lights < 0 || (sv->n_lights > 0 && !sv->lights)) return fail(FRT_E_INVALID, "scene view: bad lights");
     F.lights.resize(sv->n_lights);

@@ -45,7 +45,8 @@ def test_tessellated(cornell_obj, tmp_path):
     assert float(np.sqrt(np.mean((out.astype(np.float64) - ref) ** 2))) < 1e-4
 
 
-@pytest.mark.parametrize("kind,objfix", [("cornell_box_obj", "cornell_obj"), ("veach_mis", "veach_obj")])
+@pytest.mark.parametrize("kind,objfix", [("cornell_box_obj", "cornell_obj"), ("veach_mis", "veach_obj"),
+                                         ("cornell_box_obj", "sphere_obj"), ("cornell_box_obj", "glass_obj")])
 def test_pssmlt_eye_paths(kind, objfix, request):
     """PSS-MLT eye paths (frt_mlt.hpp, pssmlt.cpp:105-277) vs the oracle on the
     bootstrap primary-sample stream: film position and contribution."""
@@ -114,3 +115,15 @@ def test_bvh4_matches_binary(kind, objfix, tess, request, tmp_path):
     assert st4.stack_entries == 8 and 0 < st4.bvh_depth < st2.bvh_depth   # the wide tree was traversed
     brute, stb = frt.selftest_path_host(hs, frt.RenderParams.make(nx, ny, 8, seed=13, flags=frt.FRT_FLAG_BRUTE), pix)
     assert np.array_equal(brute, bin2) and stb.rays == st2.rays                 # every triangle, index order
+
+
+@pytest.mark.parametrize("objfix", ["sphere_obj", "mirror_obj", "glass_obj"])
+def test_specular_scenes(objfix, request):
+    """modified_phong (Sphere, Mirror: Ns 1024 lobes) and dielectric (Glass):
+    the specular branch of path::Li (path.cpp:78-95) on the host build of the
+    device code vs the oracle, same streams."""
+    obj = request.getfixturevalue(objfix)
+    out, st, ref, cnt = run("cornell_box_obj", obj, 40, 40, 16, seed=3)
+    assert float(np.sqrt(np.mean((out.astype(np.float64).reshape(-1, 3) - ref.reshape(-1, 3)) ** 2))) < 1e-4
+    assert st.rays == pytest.approx(cnt.rays, rel=1e-3)
+    assert float(ref.mean()) > 0.01

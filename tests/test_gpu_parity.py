@@ -88,6 +88,20 @@ def test_tessellated_cornell(ctx, cornell_obj, tmp_path):
     assert rmse(film, ref) <= RMSE_TOL
 
 
+@pytest.mark.parametrize("objfix", ["sphere_obj", "mirror_obj", "glass_obj"])
+def test_specular_materials(ctx, objfix, request):
+    """modified_phong and dielectric (the specular branch, path.cpp:78-95) vs the
+    oracle: Sphere / Mirror (phong, Ns up to 1024) and Glass (dielectric)."""
+    obj = request.getfixturevalue(objfix)
+    nx, ny, spp = 96, 96, 32
+    film, st, ref, cnt = render_pair(ctx, "cornell_box_obj", obj, nx, ny, spp, seed=13)
+    e, nbad = split_diverged(film, ref)
+    print(objfix, "rmse(all)", rmse(film, ref), "rmse(non-diverged)", e, "diverged pixels", nbad)
+    assert abs(st.rays - cnt.rays) / cnt.rays < 2e-3
+    assert nbad <= max(2, nx * ny // 500)
+    assert e <= RMSE_TOL and rmse(film, ref) <= 10 * RMSE_TOL
+
+
 @pytest.mark.parametrize("flags", [0, frt.FRT_FLAG_NO_LDS_SCENE])
 def test_leaf_size_invariance(ctx, cornell_obj, tmp_path, monkeypatch, flags):
     """Multi-triangle leaves change node visits only: bit-identical films to the

@@ -60,6 +60,23 @@ def test_short_chains_hbm_scene(ctx, cornell_obj, tmp_path, flags):
     assert rmse(film, ref) <= 1e-3 * max(1.0, float(np.abs(ref).max()))
 
 
+@pytest.mark.parametrize("objfix", ["sphere_obj", "glass_obj"])
+def test_short_chains_specular(ctx, objfix, request):
+    """pssmlt::Li's specular branch (pssmlt.cpp:232-249) vs the oracle's chains:
+    phong spheres (Sphere) and a dielectric sphere (Glass)."""
+    obj = request.getfixturevalue(objfix)
+    nx, ny, mpp, chains = 48, 48, 4, 2304
+    ctx.upload(frt.HostScene("cornell_box_obj", obj, 1.0))
+    film = np.zeros((ny, nx, 3), np.float32)
+    film, st = ctx.render(frt.RenderParams.pssmlt(nx, ny, mpp, chains, seed=4, bootstrap=2000), film)
+    steps = mpp * nx * ny // chains
+    ref, b, cnt = oracle.OracleScene("cornell_box_obj", obj, 1.0).mlt_render(nx, ny, chains, steps, seed=4,
+                                                                            n_init=2000)
+    assert st.samples == chains * steps == cnt.samples
+    assert abs(st.rays - cnt.rays) / cnt.rays < 5e-3
+    assert rmse(film, ref) <= 2e-3 * max(1.0, float(np.abs(ref).max()))
+
+
 def test_sharded_chains_sum_to_single(ctx, cornell_obj):
     nx, ny = 32, 32
     ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, 1.0))
