@@ -109,6 +109,7 @@ FRT_HD void mlt_begin(MltPath &M, const DevScene &S, const PrndSource &src, int 
 FRT_HD bool mlt_beyond(const MltPath &M) { return !M.P.shadow && M.P.depth > kMltMaxPath; }
 
 // pssmlt::Li, one hit at a time.  Returns true when the path is finished.
+template <bool MATS = true>   // false: lambertian / diffuse_light scenes (see path_shade)
 FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSource &src, uint32_t &n_ext,
                       uint32_t &n_sh)
 {
@@ -143,8 +144,8 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
         }
         return true;
     }
-    const bool lamb = mtype == FRT_MAT_LAMBERTIAN, phong = mtype == FRT_MAT_MODIFIED_PHONG,
-               diel = mtype == FRT_MAT_DIELECTRIC;
+    const bool lamb = mtype == FRT_MAT_LAMBERTIAN, phong = MATS && mtype == FRT_MAT_MODIFIED_PHONG,
+               diel = MATS && mtype == FRT_MAT_DIELECTRIC;
     if (!(lamb || phong || diel)) return true;          // diffuse_light seen from behind
     const f3 wi = -normalize(P.rd);
     // NEE prnds (pssmlt.cpp:190-195); the bsdf prnds follow only for the diffuse branch
@@ -152,7 +153,7 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
     M.off += 3;
     f3 wo, beta_next;
     float pdf;
-    if (lamb) {
+    if (!MATS || lamb) {
         const float b0 = src.get(M.off), b1 = src.get(M.off + 1);
         M.off += 2;
         const Onb uvw = onb_from_w(n);
@@ -175,7 +176,7 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
         if (pdf == 0.0f) return true;
         beta_next = P.beta * (rcp(pdf) * bsdf);
     }
-    const f3 origin = (dot(n, wo) > 0.0f || lamb) ? p + kEps * n : p - kEps * n;   // hrec.p moved off (:243, :253)
+    const f3 origin = (!MATS || lamb || dot(n, wo) > 0.0f) ? p + kEps * n : p - kEps * n;   // hrec.p moved off (:243, :253)
     P.nxt_d = wo;
     const int nl = S.n_lights;
     int idx = (int)(rnd0 * (float)nl);
@@ -193,8 +194,9 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
         P.nee = mk3(0, 0, 0);
         if (cos_lo != 0.0f) {
             const float light_pdf = fdiv(prim_pdf(S, lref, p, h.t, n, tu) * dist2, fabsf(cos_lo));
-            const f3 f = lamb ? cos_wi * (kInvPi * xyz(m0)) : phong_eval(xyz(m0), xyz(m1), m1.w, n, wi, tu);
-            const float bsdf_pdf = lamb ? fmaxf(cos_wi, 0.0f) * kInvPi : cosine_power_value(n, wi, m1.w, tu);
+            const bool l = !MATS || lamb;
+            const f3 f = l ? cos_wi * (kInvPi * xyz(m0)) : phong_eval(xyz(m0), xyz(m1), m1.w, n, wi, tu);
+            const float bsdf_pdf = l ? fmaxf(cos_wi, 0.0f) * kInvPi : cosine_power_value(n, wi, m1.w, tu);
             const float wgt = mi_weight(light_pdf, bsdf_pdf);
             const float4 lm0 = S.mats[2 * lmat], lm1 = S.mats[2 * lmat + 1];
             if (f2i(lm0.w) == FRT_MAT_DIFFUSE_LIGHT && dot(ln, tu) < 0.0f)
@@ -206,7 +208,7 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
     }
     P.beta = beta_next;
     P.prev_pdf = pdf;
-    P.prev_spec = !lamb;
+    P.prev_spec = MATS && !lamb;
     if (!P.shadow) {
         P.ro = origin; P.rd = wo; P.rtmax = kTMaxClosest;
         ++P.depth;

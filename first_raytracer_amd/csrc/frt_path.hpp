@@ -486,6 +486,9 @@ FRT_HD void path_after_shadow(PathState &P, bool unoccluded)
 }
 
 // Returns true when the path is finished (P.L is the sample's radiance).
+// MATS = false compiles the lambertian / diffuse_light scenes' kernel: the
+// specular branch is dead code there (it would cost registers and code size).
+template <bool MATS = true>
 FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_depth, uint32_t &n_ext, uint32_t &n_sh)
 {
     if (P.shadow) {
@@ -517,8 +520,8 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
         }
         return true;
     }
-    const bool lamb = mtype == FRT_MAT_LAMBERTIAN, phong = mtype == FRT_MAT_MODIFIED_PHONG,
-               diel = mtype == FRT_MAT_DIELECTRIC;
+    const bool lamb = mtype == FRT_MAT_LAMBERTIAN, phong = MATS && mtype == FRT_MAT_MODIFIED_PHONG,
+               diel = MATS && mtype == FRT_MAT_DIELECTRIC;
     if (!(lamb || phong || diel) || P.depth > max_depth) return true;   // no scatter: Le (= 0)
     const uint32_t base = dim_bounce(P.depth);
     // The scattered direction first: a zero pdf returns 0 for this vertex,
@@ -526,7 +529,7 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
     f3 wo, beta_next;
     float pdf;
     const f3 wi = -normalize(P.rd);                     // hrec.wi (triangle.h:108, sphere.h:47)
-    if (lamb) {                                         // cosine_pdf (path.cpp:96-110)
+    if (!MATS || lamb) {                                // cosine_pdf (path.cpp:96-110)
         const Onb uvw = onb_from_w(n);
         wo = onb_local(uvw, cosine_direction(rng_u(P.key, base + 6), rng_u(P.key, base + 7)));
         const float cw = dot(n, normalize(wo));
@@ -550,7 +553,7 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
     }
     // origin of the next ray: off the surface on the side it leaves (path.cpp:91-93, 99);
     // equal to the NEE origin whenever NEE runs (phong's pdf > 0 means dot(n, wo) > 0)
-    const f3 origin = (dot(n, wo) > 0.0f || lamb) ? p + kEps * n : p - kEps * n;
+    const f3 origin = (!MATS || lamb || dot(n, wo) > 0.0f) ? p + kEps * n : p - kEps * n;
     P.nxt_d = wo;
     // next-event estimation (path.cpp:38-77); not from dielectrics (path.cpp:40)
     const int nl = S.n_lights;
@@ -570,8 +573,9 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
         if (cos_lo != 0.0f) {
             const float light_pdf = fdiv(prim_pdf(S, lref, p, h.t, n, tu) * dist2, fabsf(cos_lo));
             // eval_bsdf toward the light; only the non-specular bsdf gets the cosine (path.cpp:61-62)
-            const f3 f = lamb ? cos_wi * (kInvPi * xyz(m0)) : phong_eval(xyz(m0), xyz(m1), m1.w, n, wi, tu);
-            const float bsdf_pdf = lamb ? fmaxf(cos_wi, 0.0f) * kInvPi : cosine_power_value(n, wi, m1.w, tu);
+            const bool l = !MATS || lamb;
+            const f3 f = l ? cos_wi * (kInvPi * xyz(m0)) : phong_eval(xyz(m0), xyz(m1), m1.w, n, wi, tu);
+            const float bsdf_pdf = l ? fmaxf(cos_wi, 0.0f) * kInvPi : cosine_power_value(n, wi, m1.w, tu);
             const float wgt = mi_weight(light_pdf, bsdf_pdf);
             const float4 lm0 = S.mats[2 * lmat], lm1 = S.mats[2 * lmat + 1];
             if (f2i(lm0.w) == FRT_MAT_DIFFUSE_LIGHT && dot(ln, tu) < 0.0f)
@@ -581,7 +585,7 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
         P.shadow = true;
         ++n_sh;
     }
-    P.prev_spec = !lamb;
+    P.prev_spec = MATS && !lamb;
     P.beta = beta_next;
     P.prev_p = p;
     P.prev_pdf = pdf;

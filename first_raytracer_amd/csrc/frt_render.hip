@@ -115,7 +115,7 @@ __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
 // ------------------------------------------------------------------------
 // the persistent path megakernel
 // ------------------------------------------------------------------------
-template <int STACK, int WORLD, bool LDS_SCENE, int WAVES = 1, bool SPEC = false>
+template <int STACK, int WORLD, bool LDS_SCENE, int WAVES = 1, bool SPEC = false, bool MATS = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void path_megakernel(
     const DevScene S0, const DevWork W)
 {
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         bool next_ray = false;
         if (pending) {
             pending = false;
-            if (path_shade(P, S, T.h, W.max_depth, ne, ns)) {
+            if (path_shade<MATS>(P, S, T.h, W.max_depth, ne, ns)) {
                 acc = acc + P.L;
                 active = false;
             } else {
@@ -293,7 +293,7 @@ __device__ __forceinline__ Hit trace_any(const DevScene &S, const PathState &P, 
 
 // bootstrap: sc of n_init independent eye paths (pssmlt.cpp:303-312); the host
 // sums them in a fixed order
-template <int STACK, int WORLD>
+template <int STACK, int WORLD, bool MATS>
 __global__ __launch_bounds__(kBlock) void mlt_bootstrap(const DevScene S0, int nx, int ny, uint32_t seed, int n_init,
                                                         float *sc)
 {
@@ -310,7 +310,7 @@ __global__ __launch_bounds__(kBlock) void mlt_bootstrap(const DevScene S0, int n
     for (;;) {
         if (mlt_beyond(M)) { M.P.L = M.P.L + M.P.beta * S.env; break; }
         const Hit h = trace_any<WORLD, STACK>(S, M.P, stk);
-        if (mlt_shade(M, S, h, src, ne, ns)) break;
+        if (mlt_shade<MATS>(M, S, h, src, ne, ns)) break;
     }
     sc[i] = fmaxf(fmaxf(M.P.L.x, M.P.L.y), M.P.L.z);
 }
@@ -331,7 +331,7 @@ __device__ __forceinline__ void mlt_splat(const MltWork &W, float x, float y, f3
 #ifndef FRT_EXP_MLT_WAVES
 #define FRT_EXP_MLT_WAVES 5      // register cap of the chain kernel: 5 waves/SIMD, +17 % over the
 #endif                           // compiler's 4 (profiles/r01_expmlt1.txt); experiment builds vary it
-template <int STACK, int WORLD, bool LDS_SCENE>
+template <int STACK, int WORLD, bool LDS_SCENE, bool MATS>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_MLT_WAVES))) void mlt_megakernel(
     const DevScene S0, const MltWork W)
 {
@@ -392,7 +392,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
                 done = true;
             } else {
                 uint32_t ne = 0, ns = 0;
-                done = mlt_shade(M, S, T.h, source(), ne, ns);
+                done = mlt_shade<MATS>(M, S, T.h, source(), ne, ns);
                 n_ext += ne; n_sh += ns;
                 next_ray = !done;
             }
@@ -513,6 +513,7 @@ struct frt_ctx {
     bool has_bvh4 = false;
     int depth4 = 0;
     int n_tris = 0, n_spheres = 0;
+    bool has_spec_mats = false;   // modified_phong / dielectric present: kernels with the specular branch
     size_t scene_lds_bytes = 0, scene_lds_bytes4 = 0;   // LDS copy with binary / 4-wide nodes
     double last_mlt_b = 0.0;
     std::vector<void *> scene_bufs;
@@ -1040,6 +1041,10 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
     c->has_bvh4 = F.has4;
     c->n_tris = S.n_tris;
     c->n_spheres = (int)F.spheres.size();
+    c->has_spec_mats = false;
+    for (int i = 0; i < sv->n_materials; ++i)
+        if (sv->materials[i].type == FRT_MAT_MODIFIED_PHONG || sv->materials[i].type == FRT_MAT_DIELECTRIC)
+            c->has_spec_mats = true;
     c->depth4 = F.depth4;
     c->scene_lds_bytes = sizeof(float4) * (F.nodes.size() + F.tris.size() + F.tshade.size() + F.mats.size());
     c->scene_lds_bytes4 = sizeof(float4) * (F.nodes4.size() + F.tris.size() + F.tshade.size() + F.mats.size());
@@ -1203,11 +1208,11 @@ struct Launcher {
     bool lds_scene = false;
     bool wide = false;      // 4-wide quantized BVH
 };
-template <int STACK, int WORLD, bool LDS, int WAVES = 1, bool SPEC = false>
+template <int STACK, int WORLD, bool LDS, int WAVES = 1, bool SPEC = false, bool MATS = false>
 static Launcher make_launcher(size_t scene_bytes)
 {
     Launcher L;
-    L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES, SPEC>);
+    L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES, SPEC, MATS>);
     L.lds = (WORLD != FRT_WORLD_LIST ? (size_t)STACK * kBlock * sizeof(int) : 0) + (LDS ? scene_bytes : 0);
     L.stack = STACK;
     L.waves = WAVES > 1 ? WAVES : 0;
@@ -1215,19 +1220,21 @@ static Launcher make_launcher(size_t scene_bytes)
     L.wide = WORLD == kWorldBvh4;
     return L;
 }
-template <int STACK, bool LDS, int WORLD = FRT_WORLD_BVH, bool SPEC = false>
+template <int STACK, bool LDS, int WORLD = FRT_WORLD_BVH, bool SPEC = false, bool MATS = false>
 static Launcher bvh_launcher(int waves, size_t sb)
 {
-    if (waves == 6) return make_launcher<STACK, WORLD, LDS, 6, SPEC>(sb);
-    if (waves == 5) return make_launcher<STACK, WORLD, LDS, 5, SPEC>(sb);
-    return make_launcher<STACK, WORLD, LDS, 1, SPEC>(sb);
+    if (waves == 6) return make_launcher<STACK, WORLD, LDS, 6, SPEC, MATS>(sb);
+    if (waves == 5) return make_launcher<STACK, WORLD, LDS, 5, SPEC, MATS>(sb);
+    return make_launcher<STACK, WORLD, LDS, 1, SPEC, MATS>(sb);
 }
 constexpr int kBvh4LdsStack = 16;   // 16 KiB of LDS per block; deeper entries go to scratch
 constexpr int kBvh4LdsStackSmall = 8;   // LDS-resident scenes (shallow trees)
 constexpr int kBruteMaxTris = 128;
-static int pick_launcher(const frt_ctx *c, int flags, Launcher &L)
+// MATS: the scene has modified_phong / dielectric materials (specular branch compiled in)
+template <bool MATS>
+static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
 {
-    if (c->world_kind == FRT_WORLD_LIST) { L = make_launcher<16, FRT_WORLD_LIST, false>(0); return FRT_OK; }
+    if (c->world_kind == FRT_WORLD_LIST) { L = make_launcher<16, FRT_WORLD_LIST, false, 1, false, MATS>(0); return FRT_OK; }
     const int d = c->stack_needed;
     const size_t sb = c->scene_lds_bytes;
     const bool lds = d < kLdsMaxDepth && sb <= kLdsSceneBytes && !(flags & FRT_FLAG_NO_LDS_SCENE);
@@ -1238,39 +1245,57 @@ static int pick_launcher(const frt_ctx *c, int flags, Launcher &L)
     if (flags & FRT_FLAG_WAVES4) waves = 0;   // the compiler's own allocation (~120 VGPRs, 4 waves)
     if (flags & FRT_FLAG_WAVES5) waves = 5;
     if (flags & FRT_FLAG_WAVES6) waves = 6;
-    // tiny triangle-only scenes from LDS, every triangle in lockstep (A/B: FRT_FLAG_BRUTE)
-    if (lds && (flags & FRT_FLAG_BRUTE) && c->n_spheres == 0 && c->n_tris <= kBruteMaxTris) {
-        L = bvh_launcher<8, true, kWorldBrute>(waves, sb);
-        return FRT_OK;
-    }
-    // LDS-resident scenes, 4-wide (A/B: FRT_FLAG_BVH4)
-    if (lds && (flags & FRT_FLAG_BVH4) && c->has_bvh4 && c->scene_lds_bytes4 <= kLdsSceneBytes &&
-        bvh4_stack_fits(c->depth4, kBvh4LdsStackSmall)) {
-        L = bvh_launcher<kBvh4LdsStackSmall, true, kWorldBvh4>(waves, c->scene_lds_bytes4);
-        return FRT_OK;
+    if constexpr (!MATS) {   // A/B plans, lambertian scenes only
+        // tiny triangle-only scenes from LDS, every triangle in lockstep (FRT_FLAG_BRUTE)
+        if (lds && (flags & FRT_FLAG_BRUTE) && c->n_spheres == 0 && c->n_tris <= kBruteMaxTris) {
+            L = bvh_launcher<8, true, kWorldBrute>(waves, sb);
+            return FRT_OK;
+        }
+        // LDS-resident scenes, 4-wide (FRT_FLAG_BVH4)
+        if (lds && (flags & FRT_FLAG_BVH4) && c->has_bvh4 && c->scene_lds_bytes4 <= kLdsSceneBytes &&
+            bvh4_stack_fits(c->depth4, kBvh4LdsStackSmall)) {
+            L = bvh_launcher<kBvh4LdsStackSmall, true, kWorldBvh4>(waves, c->scene_lds_bytes4);
+            return FRT_OK;
+        }
+        // speculative 4-wide traversal (FRT_FLAG_SPEC)
+        if (!lds && (flags & FRT_FLAG_SPEC) && c->has_bvh4 && !(flags & FRT_FLAG_BVH2) &&
+            bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
+            L = bvh_launcher<kBvh4LdsStack, false, kWorldBvh4, true>(waves, 0);
+            return FRT_OK;
+        }
     }
     // HBM-resident scenes: the 4-wide quantized BVH (half the bytes per box test)
     if (!lds && c->has_bvh4 && !(flags & FRT_FLAG_BVH2) && bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
-        L = (flags & FRT_FLAG_SPEC) ? bvh_launcher<kBvh4LdsStack, false, kWorldBvh4, true>(waves, 0)
-                                    : bvh_launcher<kBvh4LdsStack, false, kWorldBvh4>(waves, 0);
+        L = bvh_launcher<kBvh4LdsStack, false, kWorldBvh4, false, MATS>(waves, 0);
         return FRT_OK;
     }
-    if (d < 8) L = lds ? bvh_launcher<8, true>(waves, sb) : bvh_launcher<8, false>(waves, 0);
-    else if (d < 16) L = lds ? bvh_launcher<16, true>(waves, sb) : bvh_launcher<16, false>(waves, 0);
-    else if (d < 24) L = bvh_launcher<24, false>(waves, 0);
-    else if (d < 32) L = bvh_launcher<32, false>(waves, 0);
-    else if (d < 64) L = make_launcher<64, FRT_WORLD_BVH, false>(0);
+    if (d < 8) L = lds ? bvh_launcher<8, true, FRT_WORLD_BVH, false, MATS>(waves, sb)
+                       : bvh_launcher<8, false, FRT_WORLD_BVH, false, MATS>(waves, 0);
+    else if (d < 16) L = lds ? bvh_launcher<16, true, FRT_WORLD_BVH, false, MATS>(waves, sb)
+                             : bvh_launcher<16, false, FRT_WORLD_BVH, false, MATS>(waves, 0);
+    else if (d < 24) L = bvh_launcher<24, false, FRT_WORLD_BVH, false, MATS>(waves, 0);
+    else if (d < 32) L = bvh_launcher<32, false, FRT_WORLD_BVH, false, MATS>(waves, 0);
+    else if (d < 64) L = make_launcher<64, FRT_WORLD_BVH, false, 1, false, MATS>(0);
     else return FRT_E_UNSUPPORTED;
     return FRT_OK;
+}
+static int pick_launcher(const frt_ctx *c, int flags, Launcher &L)
+{
+    return c->has_spec_mats ? pick_launcher_t<true>(c, flags, L) : pick_launcher_t<false>(c, flags, L);
 }
 
 
 // ---- PSS-MLT render: bootstrap b, then the chain megakernel splatting into dev_film ----
 template <int STACK, int WORLD, bool LDS = false>
-static void mlt_kernels(const void **boot, const void **chains)
+static void mlt_kernels(bool mats, const void **boot, const void **chains)
 {
-    *boot = reinterpret_cast<const void *>(&mlt_bootstrap<STACK, WORLD>);
-    *chains = reinterpret_cast<const void *>(&mlt_megakernel<STACK, WORLD, LDS>);
+    if (mats) {
+        *boot = reinterpret_cast<const void *>(&mlt_bootstrap<STACK, WORLD, true>);
+        *chains = reinterpret_cast<const void *>(&mlt_megakernel<STACK, WORLD, LDS, true>);
+    } else {
+        *boot = reinterpret_cast<const void *>(&mlt_bootstrap<STACK, WORLD, false>);
+        *chains = reinterpret_cast<const void *>(&mlt_megakernel<STACK, WORLD, LDS, false>);
+    }
 }
 
 static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, hipStream_t st, frt_stats *stats)
@@ -1281,16 +1306,16 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
     const int d = c->stack_needed;
     const bool lds_scene = c->world_kind == FRT_WORLD_BVH && d < kLdsMaxDepth && c->scene_lds_bytes <= kLdsSceneBytes &&
                            !(p->flags & FRT_FLAG_NO_LDS_SCENE);
-    if (c->world_kind == FRT_WORLD_LIST) { stack = 0; mlt_kernels<16, FRT_WORLD_LIST>(&kboot, &kchain); }
+    if (c->world_kind == FRT_WORLD_LIST) { stack = 0; mlt_kernels<16, FRT_WORLD_LIST>(c->has_spec_mats, &kboot, &kchain); }
     else if (!lds_scene && c->has_bvh4 && !(p->flags & FRT_FLAG_BVH2) && bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
         stack = kBvh4LdsStack;
-        mlt_kernels<kBvh4LdsStack, kWorldBvh4>(&kboot, &kchain);
+        mlt_kernels<kBvh4LdsStack, kWorldBvh4>(c->has_spec_mats, &kboot, &kchain);
     }
-    else if (lds_scene && d < 8) { stack = 8; mlt_kernels<8, FRT_WORLD_BVH, true>(&kboot, &kchain); }
-    else if (lds_scene) { stack = 16; mlt_kernels<16, FRT_WORLD_BVH, true>(&kboot, &kchain); }
-    else if (d < 16) { stack = 16; mlt_kernels<16, FRT_WORLD_BVH>(&kboot, &kchain); }
-    else if (d < 32) { stack = 32; mlt_kernels<32, FRT_WORLD_BVH>(&kboot, &kchain); }
-    else if (d < 64) { stack = 64; mlt_kernels<64, FRT_WORLD_BVH>(&kboot, &kchain); }
+    else if (lds_scene && d < 8) { stack = 8; mlt_kernels<8, FRT_WORLD_BVH, true>(c->has_spec_mats, &kboot, &kchain); }
+    else if (lds_scene) { stack = 16; mlt_kernels<16, FRT_WORLD_BVH, true>(c->has_spec_mats, &kboot, &kchain); }
+    else if (d < 16) { stack = 16; mlt_kernels<16, FRT_WORLD_BVH>(c->has_spec_mats, &kboot, &kchain); }
+    else if (d < 32) { stack = 32; mlt_kernels<32, FRT_WORLD_BVH>(c->has_spec_mats, &kboot, &kchain); }
+    else if (d < 64) { stack = 64; mlt_kernels<64, FRT_WORLD_BVH>(c->has_spec_mats, &kboot, &kchain); }
     else return set_err(c, FRT_E_UNSUPPORTED, "BVH deeper than 63 levels");
     const size_t lds_boot = (size_t)stack * kBlock * sizeof(int);
     const size_t lds = lds_boot + (lds_scene ? c->scene_lds_bytes : 0);
