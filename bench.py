@@ -43,6 +43,8 @@ def scene_spec(name, workdir, tag=""):
         return "cornell_box_obj", os.path.join(SCENES, "CornellBox-Original.obj"), "CornellBox-Original"
     if name == "veach":
         return "veach_mis", os.path.join(SCENES, "veach_mi.obj"), "veach_mi"
+    if name == "sphere":   # modified_phong spheres (specular branch)
+        return "cornell_box_obj", os.path.join(SCENES, "CornellBox-Sphere.obj"), "CornellBox-Sphere"
     if name == "cornell_1m":
         import first_raytracer_amd as frt
         dst = os.path.join(workdir, f"cornell_1m_k172{tag}.obj")
@@ -129,7 +131,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scene", default="cornell", choices=["cornell", "cornell_1m", "veach"])
+    ap.add_argument("--scene", default="cornell", choices=["cornell", "cornell_1m", "veach", "sphere"])
     ap.add_argument("--res", default="1920x1080")
     ap.add_argument("--spp", type=int, default=512)
     ap.add_argument("--seed", type=int, default=0)
