@@ -62,18 +62,20 @@ def load_traversal_stats(key):
     return None
 
 
-def cpu_baseline(kind, obj, nx, ny, spp, seed, npix, threads, film, seconds):
+def cpu_baseline(kind, obj, nx, ny, spp, seed, npix, threads, film, seconds, integrator=0, env=None):
     """The oracle (fp64 C restatement) on a bounded pixel sample of the same
     frame and RNG streams: CPU Mrays/s, reference traversal counters (for
     B_ray) and the RMSE of the GPU film on those pixels.  npix = 0: calibrate
     on growing samples (from 512 pixels) until one takes about `seconds` of CPU work."""
     import oracle
     sc = oracle.OracleScene(kind, obj, nx / ny)
+    if env is not None:
+        sc.set_env(env)
 
     def run(n):
         pix = np.unique(np.linspace(0, nx * ny - 1, n).astype(np.int32))
         t0 = time.perf_counter()
-        out, cnt = sc.render(nx, ny, spp, seed=seed, pixels=pix, nthreads=threads)
+        out, cnt = sc.render(nx, ny, spp, seed=seed, pixels=pix, nthreads=threads, integrator=integrator)
         return pix, out, cnt, time.perf_counter() - t0
 
     if npix > 0:
@@ -141,8 +143,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pfm", default="", help="write the rank-0 film here")
-    ap.add_argument("--integrator", default="path", choices=["path", "pssmlt"],
-                    help="pssmlt: C5 config, --spp = mutations per pixel")
+    ap.add_argument("--integrator", default="path", choices=["path", "pssmlt", "ao", "normals"],
+                    help="pssmlt: C5 config, --spp = mutations per pixel; ao (ao.cpp), normals (debug_renderer.h)")
+    ap.add_argument("--env", default="", help="constant environment r,g,b (default: the scene's; 1,1,1 for ao)")
     ap.add_argument("--chains", type=int, default=1 << 18, help="PSS-MLT chains (all ranks)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the N-rank path with host-staged collectives (e.g. ranks sharing one GPU)")
@@ -184,6 +187,15 @@ def main():
     kind, obj, scene_name = scene_spec(args.scene, workdir, tag=f"_r{rank}")
     t0 = time.perf_counter()
     hs = frt.HostScene(kind, obj, nx / ny)       # OBJ load + reference-topology BVH build (host)
+    env = None
+    if args.env:
+        env = tuple(float(x) for x in args.env.split(","))
+    elif args.integrator == "ao":
+        env = (1.0, 1.0, 1.0)                    # the scenes' black environment would make every AO sample 0
+    if env is not None:
+        hs.set_env(env)
+    integ = {"path": frt.FRT_INTEGRATOR_PATH, "ao": frt.FRT_INTEGRATOR_AO,
+             "normals": frt.FRT_INTEGRATOR_NORMALS}.get(args.integrator, frt.FRT_INTEGRATOR_PSSMLT)
     t1 = time.perf_counter()
     ctx = frt.Context(local)
     ctx.upload(hs)                               # flatten + leaf collapse + BVH4Q + copy to HBM
@@ -201,7 +213,7 @@ def main():
         tg = _Film()
     else:
         params = frt.RenderParams.make(nx, ny, args.spp, seed=args.seed, tile_size=args.tile,
-                                       shard_index=rank, shard_count=world)
+                                       shard_index=rank, shard_count=world, integrator=integ)
         from first_raytracer_amd.dist import TileGather
         tg = TileGather(nx, ny, args.tile, world, rank, dev, stage_cpu=gloo)
     stream = torch.cuda.current_stream(dev)
@@ -254,7 +266,7 @@ def main():
                 cpu = cpu_baseline_mlt(kind, obj, nx, ny, args.seed, threads, args.cpu_seconds)
             else:
                 cpu = cpu_baseline(kind, obj, nx, ny, args.spp, args.seed, args.cpu_pixels, threads, film_np,
-                                   args.cpu_seconds)
+                                   args.cpu_seconds, integrator=integ, env=env)
             cpu["threads"] = threads
         ts = load_traversal_stats(key)
         if cpu is not None:
@@ -276,7 +288,7 @@ def main():
                     traffic = json.load(f).get(f"{args.integrator}:{key}:n{world}")
             roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "kernel": "path_megakernel" if args.integrator == "path" else "mlt_megakernel",
+                        "kernel": "mlt_megakernel" if args.integrator == "pssmlt" else "path_megakernel",
                         "bytes_per_ray": round(b_ray, 1),
                         "V_node": round(V, 3), "T_tri": round(T, 3), "rays_per_launch": int(rays_per_launch),
                         "avg_launch_ms": round(avg_kernel_s * 1e3, 3),
@@ -287,17 +299,22 @@ def main():
                         "lds_frac": round(achieved / LDS_PEAK_GBS, 4) if last.scene_in_lds else None,
                         "launch": {"waves_cap": int(last.waves_cap), "stack": int(last.stack_entries),
                                    "bvh_depth": int(last.bvh_depth)}}
+        li_name = {"path": "path::Li", "ao": "ao::Li", "normals": "normals_renderer::Li"}.get(args.integrator)
+        workload = {"path": f"{scene_name} {nx}x{ny} {args.spp}spp path+NEE+MIS",
+                    "ao": f"{scene_name} {nx}x{ny} {args.spp}spp ambient occlusion (ao.cpp)",
+                    "normals": f"{scene_name} {nx}x{ny} {args.spp}spp shading normals (debug_renderer.h)",
+                    "pssmlt": f"{scene_name} {nx}x{ny} PSS-MLT {args.spp} mutations/pixel, {args.chains} chains"
+                    }[args.integrator]
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": (f"{scene_name} {nx}x{ny} {args.spp}spp path+NEE+MIS" if args.integrator == "path"
-                                    else f"{scene_name} {nx}x{ny} PSS-MLT {args.spp} mutations/pixel, "
-                                         f"{args.chains} chains"),
+            "config": {"workload": workload,
                        "integrator": args.integrator, "scene": args.scene,
                        "nx": nx, "ny": ny, "spp": args.spp, "seed": args.seed, "tile": args.tile,
-                       "parallelism": (f"tiles-interleaved x{world} + rccl all-gather" if args.integrator == "path"
-                                       else f"chains-interleaved x{world} + rccl all-reduce")},
+                       "env": env,
+                       "parallelism": (f"chains-interleaved x{world} + rccl all-reduce" if args.integrator == "pssmlt"
+                                       else f"tiles-interleaved x{world} + rccl all-gather")},
             "rmse": None if cpu is None else cpu["rmse"],
             "rmse_detail": None if cpu is None or "diverged_pixels" not in cpu else {
                 "pixels": cpu["npix"], "diverged_pixels": cpu["diverged_pixels"],
@@ -311,8 +328,8 @@ def main():
             "cpu_baseline": None if cpu is None else {
                 "value": round(cpu["mrays"], 3), "unit": "Mrays/s", "cores": cpu["threads"], "kind": "port",
                 "sample": (f"{cpu['npix']} evenly spaced pixels of the same {nx}x{ny} frame at {args.spp} spp "
-                           f"({cpu['rays']} rays, {cpu['seconds']:.1f} s); fp64 C restatement of path::Li")
-                if args.integrator == "path" else
+                           f"({cpu['rays']} rays, {cpu['seconds']:.1f} s); fp64 C restatement of {li_name}")
+                if args.integrator != "pssmlt" else
                           (f"PSS-MLT {cpu['sample']} on the same {nx}x{ny} frame ({cpu['rays']} rays, "
                            f"{cpu['seconds']:.1f} s); fp64 C restatement of pssmlt.cpp")},
         }

@@ -28,7 +28,7 @@ FRT_FLAG_BVH2 = 16
 FRT_FLAG_BVH4 = 32
 FRT_FLAG_BRUTE = 64
 FRT_FLAG_SPEC = 128
-FRT_INTEGRATOR_PATH, FRT_INTEGRATOR_PSSMLT = 0, 1
+FRT_INTEGRATOR_PATH, FRT_INTEGRATOR_PSSMLT, FRT_INTEGRATOR_AO, FRT_INTEGRATOR_NORMALS = 0, 1, 2, 3
 
 ERRORS = {0: "ok", -1: "invalid", -2: "hip", -3: "no scene", -4: "unsupported", -5: "io", -6: "no gfx950 device"}
 
@@ -72,8 +72,9 @@ class RenderParams(ctypes.Structure):
 
     @classmethod
     def make(cls, nx, ny, spp, seed=0, max_depth=33, tile_size=32, shard_index=0, shard_count=1,
-             samples_per_item=0, flags=0):
-        return cls(nx=nx, ny=ny, spp=spp, seed=seed, max_depth=max_depth, integrator=0, tile_size=tile_size,
+             samples_per_item=0, flags=0, integrator=0):
+        """integrator: FRT_INTEGRATOR_PATH (path.cpp), _AO (ao.cpp) or _NORMALS (debug_renderer.h)."""
+        return cls(nx=nx, ny=ny, spp=spp, seed=seed, max_depth=max_depth, integrator=integrator, tile_size=tile_size,
                    shard_index=shard_index, shard_count=shard_count, samples_per_item=samples_per_item, flags=flags,
                    mlt_chains=0, mlt_bootstrap=0)
 
@@ -182,10 +183,18 @@ class HostScene:
                f"frt_scene_create({kind})")
         self.info = HostSceneInfo()
         lib().frt_scene_info(self.ptr, ctypes.byref(self.info))
+        self.env = None
+
+    def set_env(self, rgb):
+        """Constant environment colour of the views this scene hands out
+        (material.h:206-232; the reference scenes use black)."""
+        self.env = tuple(float(x) for x in rgb)
 
     def view(self):
         v = SceneView()
         _check(lib().frt_scene_view_get(self.ptr, ctypes.byref(v)), "frt_scene_view_get")
+        if self.env is not None:
+            v.env_color[:] = self.env
         return v
 
     def arrays(self):

@@ -55,6 +55,8 @@ struct DevScene {
     int node_es, node_ps, tri_es, tri_ps, sh_es, sh_ps, node4_es, node4_ps;
     int n_nodes4;
     float root_lo[3], root_hi[3];
+    float ao_tmax;           // ao.cpp:21 world box height * 0.5
+    int ao_spheres_only;     // list world: ao.cpp's t_max is NaN (see ao_shade)
     f3 cam_o, cam_llc, cam_h, cam_v, cam_u, cam_vv, cam_w;
     float lens_r, cam_half_height;
     f3 env;
@@ -594,6 +596,88 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
         ++P.depth; ++n_ext;
     }
     return false;
+}
+
+// ---- the reference's other integrators on the same traversal ----
+
+// ao::Li (ao.cpp:4-27).  Camera hit on a scattering material: one
+// visibility ray from the hit point (no offset, ao.cpp:15) along the
+// material pdf's generate() -- dims dim_bounce(0) + 6, 7 -- up to
+// S.ao_tmax (half the world box height, ao.cpp:19-21); occluded -> 0,
+// otherwise, and for misses and lights, the environment.  The visibility
+// ray is an any-hit query traced like path's shadow rays.  List worlds
+// have no box (hitable_list::bounding_box returns before assigning it,
+// hitable_list.cpp:27-29: t_max is NaN): only spheres can occlude there
+// (sphere.h's `t > t_max` test passes NaN, triangle.h's `t < t_max` does
+// not), answered here with a loop over the list's spheres.
+template <bool MATS = true>
+FRT_HD bool ao_shade(PathState &P, const DevScene &S, const Hit &h, uint32_t &n_sh)
+{
+    if (P.shadow) {                                     // visibility ray done
+        P.L = h.prim < 0 ? S.env : mk3(0, 0, 0);
+        return true;
+    }
+    P.L = S.env;
+    if (h.prim < 0) return true;
+    const f3 p = P.ro + h.t * P.rd;
+    f3 n;
+    int mat;
+    prim_shade(S, h.prim, P.ro, p, h.u, h.v, n, mat);
+    const float4 m0 = S.mats[2 * mat], m1 = S.mats[2 * mat + 1];
+    const int mtype = f2i(m0.w);
+    const uint32_t base = dim_bounce(0);
+    const float u0 = rng_u(P.key, base + 6), u1 = rng_u(P.key, base + 7);
+    f3 wo;
+    if (mtype == FRT_MAT_LAMBERTIAN) {
+        wo = onb_local(onb_from_w(n), cosine_direction(u0, u1));
+    } else if (MATS && mtype == FRT_MAT_MODIFIED_PHONG) {
+        wo = cosine_power_generate(n, -normalize(P.rd), m1.w, u0, u1);
+    } else if (MATS && mtype == FRT_MAT_DIELECTRIC) {
+        wo = dielectric_generate(n, -normalize(P.rd), m1.w, u0);
+    } else {
+        return true;                                    // no scatter (diffuse_light)
+    }
+    ++n_sh;
+    if (S.ao_spheres_only) {
+        for (int i = 0; i < S.n_list; ++i) {
+            const int ref = S.list[i];
+            if (!(ref & FRT_PRIM_SPHERE)) continue;
+            const float4 sp = S.spheres[ref & ~FRT_PRIM_SPHERE];
+            if (sphere_intersect(p, wo, xyz(sp), sp.w, kEps, kTMaxClosest) > 0.0f) {
+                P.L = mk3(0, 0, 0);
+                break;
+            }
+        }
+        return true;
+    }
+    P.ro = p; P.rd = wo; P.rtmax = S.ao_tmax;
+    P.shadow = true;
+    return false;
+}
+
+// normals_renderer::Li (debug_renderer.h:8-17): the shading normal of the
+// camera hit, the environment on a miss.
+FRT_HD bool normals_shade(PathState &P, const DevScene &S, const Hit &h)
+{
+    if (h.prim < 0) {
+        P.L = S.env;
+        return true;
+    }
+    const f3 p = P.ro + h.t * P.rd;
+    f3 n;
+    int mat;
+    prim_shade(S, h.prim, P.ro, p, h.u, h.v, n, mat);
+    P.L = n;
+    return true;
+}
+
+// integrator dispatch of the megakernel / self-test (KIND = FRT_INTEGRATOR_*)
+template <int KIND, bool MATS>
+FRT_HD bool shade_kind(PathState &P, const DevScene &S, const Hit &h, int max_depth, uint32_t &n_ext, uint32_t &n_sh)
+{
+    if constexpr (KIND == FRT_INTEGRATOR_AO) return ao_shade<MATS>(P, S, h, n_sh);
+    else if constexpr (KIND == FRT_INTEGRATOR_NORMALS) return normals_shade(P, S, h);
+    else return path_shade<MATS>(P, S, h, max_depth, n_ext, n_sh);
 }
 
 }  // namespace frt

@@ -115,7 +115,9 @@ __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
 // ------------------------------------------------------------------------
 // the persistent path megakernel
 // ------------------------------------------------------------------------
-template <int STACK, int WORLD, bool LDS_SCENE, int WAVES = 1, bool SPEC = false, bool MATS = false>
+// KIND = FRT_INTEGRATOR_PATH, _AO or _NORMALS: the per-sample integrator (shade_kind)
+template <int STACK, int WORLD, bool LDS_SCENE, int WAVES = 1, bool SPEC = false, bool MATS = false,
+          int KIND = FRT_INTEGRATOR_PATH>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void path_megakernel(
     const DevScene S0, const DevWork W)
 {
@@ -149,7 +151,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         for (;;) {
             bool shadow_done = false;
             if (tracing && trav_step_world<WORLD, kBlock, STACK, SPEC>(T, S, P.ro, P.rd, P.shadow, stk, ovf)) {
-                if (P.shadow) {                 // finish the shadow ray here, keep traversing
+                if (KIND == FRT_INTEGRATOR_PATH && P.shadow) {   // finish the shadow ray here, keep traversing
                     path_after_shadow(P, T.h.prim < 0);
                     shadow_done = true;
                     tracing = trav_begin_world<WORLD>(T, S, P.ro, P.rd, P.rtmax);
@@ -167,7 +169,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         bool next_ray = false;
         if (pending) {
             pending = false;
-            if (path_shade<MATS>(P, S, T.h, W.max_depth, ne, ns)) {
+            if (shade_kind<KIND, MATS>(P, S, T.h, W.max_depth, ne, ns)) {
                 acc = acc + P.L;
                 active = false;
             } else {
@@ -845,6 +847,7 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
             for (int k = 0; k < 3; ++k) { flo[k] = round_down(lo[k] - pad); fhi[k] = round_up(hi[k] + pad); }
         };
         padded(rlo, rhi, S.root_lo, S.root_hi);
+        S.ao_tmax = (float)((rhi[1] - rlo[1]) * 0.50f);   // ao.cpp:19-21 (unpadded root box, fp64)
         std::vector<int> new_id(std::max(nn, 1), -1), order;
         order.reserve(nn);
         // left-first DFS: node ids in pre-order, triangle leaves numbered in visit order
@@ -913,6 +916,7 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
         for (int i = 0; i < nt; ++i)   // triangles outside the tree: trailing ids, never intersected
             if (tri_dev[i] < 0) { tri_dev[i] = (int)tri_order.size(); tri_order.push_back(i); }
     } else if (sv->world_kind == FRT_WORLD_LIST) {
+        S.ao_spheres_only = 1;                              // ao.cpp:21 t_max is NaN (ao_shade)
         if (sv->n_list < 0 || (sv->n_list > 0 && !sv->list)) return fail(FRT_E_INVALID, "scene view: bad list");
         for (int i = 0; i < nt; ++i) { tri_dev[i] = i; tri_order.push_back(i); }
         for (int i = 0; i < sv->n_list; ++i)
@@ -1099,7 +1103,9 @@ extern "C" int frt_selftest_path_host(const frt_scene_view *sv, const frt_render
                                : trace<FRT_WORLD_BVH, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data());
                 }
                 n_ext = n_sh = 0;
-                const bool done = path_shade(P, S, h, p->max_depth, n_ext, n_sh);
+                const bool done = p->integrator == FRT_INTEGRATOR_AO ? ao_shade(P, S, h, n_sh)
+                                  : p->integrator == FRT_INTEGRATOR_NORMALS ? normals_shade(P, S, h)
+                                  : path_shade(P, S, h, p->max_depth, n_ext, n_sh);
                 ext += n_ext; sh += n_sh;
                 if (done) break;
             }
@@ -1161,7 +1167,9 @@ static bool params_ok(const frt_render_params *p)
     if (!(p && p->nx > 0 && p->ny > 0 && p->spp > 0 && (T % 8) == 0 && T <= 256 && p->shard_count >= 1 &&
           p->shard_index >= 0 && p->shard_index < p->shard_count && p->max_depth >= -1 && p->max_depth < 100000))
         return false;
-    if (p->integrator == FRT_INTEGRATOR_PATH) return true;
+    if (p->integrator == FRT_INTEGRATOR_PATH || p->integrator == FRT_INTEGRATOR_AO ||
+        p->integrator == FRT_INTEGRATOR_NORMALS)
+        return true;
     return p->integrator == FRT_INTEGRATOR_PSSMLT && p->mlt_chains > 0 && p->mlt_bootstrap > 0;
 }
 static int my_tiles(const frt_render_params *p)
@@ -1208,11 +1216,12 @@ struct Launcher {
     bool lds_scene = false;
     bool wide = false;      // 4-wide quantized BVH
 };
-template <int STACK, int WORLD, bool LDS, int WAVES = 1, bool SPEC = false, bool MATS = false>
+template <int STACK, int WORLD, bool LDS, int WAVES = 1, bool SPEC = false, bool MATS = false,
+          int KIND = FRT_INTEGRATOR_PATH>
 static Launcher make_launcher(size_t scene_bytes)
 {
     Launcher L;
-    L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES, SPEC, MATS>);
+    L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES, SPEC, MATS, KIND>);
     L.lds = (WORLD != FRT_WORLD_LIST ? (size_t)STACK * kBlock * sizeof(int) : 0) + (LDS ? scene_bytes : 0);
     L.stack = STACK;
     L.waves = WAVES > 1 ? WAVES : 0;
@@ -1279,8 +1288,36 @@ static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
     else return FRT_E_UNSUPPORTED;
     return FRT_OK;
 }
-static int pick_launcher(const frt_ctx *c, int flags, Launcher &L)
+// AO / normals: the default plans only (LDS-resident binary BVH, HBM 4-wide or
+// binary), register caps as for path; ao keeps the specular generate() code.
+template <int KIND>
+static int pick_launcher_kind(const frt_ctx *c, int flags, Launcher &L)
 {
+    constexpr bool M = KIND == FRT_INTEGRATOR_AO;
+    if (c->world_kind == FRT_WORLD_LIST) { L = make_launcher<16, FRT_WORLD_LIST, false, 1, false, M, KIND>(0); return FRT_OK; }
+    const int d = c->stack_needed;
+    const size_t sb = c->scene_lds_bytes;
+    const bool lds = d < kLdsMaxDepth && sb <= kLdsSceneBytes && !(flags & FRT_FLAG_NO_LDS_SCENE);
+    if (lds) {
+        L = d < 8 ? make_launcher<8, FRT_WORLD_BVH, true, 5, false, M, KIND>(sb)
+                  : make_launcher<16, FRT_WORLD_BVH, true, 5, false, M, KIND>(sb);
+    } else if (c->has_bvh4 && !(flags & FRT_FLAG_BVH2) && bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
+        L = make_launcher<kBvh4LdsStack, kWorldBvh4, false, 6, false, M, KIND>(0);
+    } else if (d < 16) {
+        L = make_launcher<16, FRT_WORLD_BVH, false, 6, false, M, KIND>(0);
+    } else if (d < 32) {
+        L = make_launcher<32, FRT_WORLD_BVH, false, 6, false, M, KIND>(0);
+    } else if (d < 64) {
+        L = make_launcher<64, FRT_WORLD_BVH, false, 1, false, M, KIND>(0);
+    } else {
+        return FRT_E_UNSUPPORTED;
+    }
+    return FRT_OK;
+}
+static int pick_launcher(const frt_ctx *c, int integrator, int flags, Launcher &L)
+{
+    if (integrator == FRT_INTEGRATOR_AO) return pick_launcher_kind<FRT_INTEGRATOR_AO>(c, flags, L);
+    if (integrator == FRT_INTEGRATOR_NORMALS) return pick_launcher_kind<FRT_INTEGRATOR_NORMALS>(c, flags, L);
     return c->has_spec_mats ? pick_launcher_t<true>(c, flags, L) : pick_launcher_t<false>(c, flags, L);
 }
 
@@ -1414,7 +1451,7 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     const uint32_t n_slots = (uint32_t)nmt * T * T;
     // kernel variant: stack depth, world kind, LDS-resident scene
     Launcher L;
-    if (pick_launcher(c, p->flags, L) != FRT_OK) return set_err(c, FRT_E_UNSUPPORTED, "BVH deeper than 63 levels");
+    if (pick_launcher(c, p->integrator, p->flags, L) != FRT_OK) return set_err(c, FRT_E_UNSUPPORTED, "BVH deeper than 63 levels");
     int bpc = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, L.fn, kBlock, L.lds) != hipSuccess || bpc <= 0) bpc = 1;
     const int grid = c->n_cu * bpc;

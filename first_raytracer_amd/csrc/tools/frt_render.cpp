@@ -3,9 +3,12 @@
 // compile-time choices.  Writes the linear film as PFM (image.h:89-118).
 //
 //   frt_render --scene cornell|veach|obj --obj FILE [--res 1920x1080] [--ns 512]
-//              [--seed 0] [--gpus 1] [--integrator path|pssmlt] [--chains 262144] [--out out.pfm]
+//              [--seed 0] [--gpus 1] [--integrator path|pssmlt|ao|normals] [--chains 262144]
+//              [--env r,g,b] [--out out.pfm]
 //
 // --integrator pssmlt: renderer<pssmlt_gpu>, --ns = mutations per pixel.
+// --integrator ao / normals: renderer<ao_gpu> / renderer<normals_gpu> (ao.h, debug_renderer.h).
+// --env: constant environment colour (the reference scenes' is black).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -19,6 +22,8 @@ int main(int argc, char **argv)
     int nx = 512, ny = 512, gpus = 1, chains = 1 << 18;
     long ns = 100;
     unsigned seed = 0;
+    double env[3] = {0, 0, 0};
+    bool has_env = false;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
         auto next = [&]() -> const char * {
@@ -34,6 +39,10 @@ int main(int argc, char **argv)
         else if (a == "--out") out = next();
         else if (a == "--integrator") integrator = next();
         else if (a == "--chains") chains = std::atoi(next());
+        else if (a == "--env") {
+            if (std::sscanf(next(), "%lf,%lf,%lf", &env[0], &env[1], &env[2]) != 3) return 2;
+            has_env = true;
+        }
         else { std::fprintf(stderr, "unknown flag %s\n", a.c_str()); return 2; }
     }
     if (obj.empty()) { std::fprintf(stderr, "--obj is required\n"); return 2; }
@@ -41,6 +50,7 @@ int main(int argc, char **argv)
         std::printf("Resolution: %dx%d\nSetting number of samples to %ld\n", nx, ny, ns);
         const std::string kind = scene == "cornell" ? "cornell_box_obj" : scene == "veach" ? "veach_mis" : "obj_smooth";
         frt::Scene s(kind, obj, double(nx) / double(ny));
+        if (has_env) s.set_env(env[0], env[1], env[2]);
         std::printf("BVH construction took me %g seconds (%d triangles, depth %d).\n", s.info().build_ms * 1e-3,
                     s.info().n_tris, s.info().bvh_depth);
         frt::viewer film(nx, ny, (uint64_t)ns);
@@ -56,6 +66,12 @@ int main(int argc, char **argv)
             run(render);
         } else if (integrator == "path") {
             frt::renderer<frt::path_gpu> render;
+            run(render);
+        } else if (integrator == "ao") {
+            frt::renderer<frt::ao_gpu> render;
+            run(render);
+        } else if (integrator == "normals") {
+            frt::renderer<frt::normals_gpu> render;
             run(render);
         } else {
             std::fprintf(stderr, "unknown integrator %s\n", integrator.c_str());

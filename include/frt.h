@@ -44,7 +44,10 @@ enum { FRT_MAT_LAMBERTIAN = 0,      /* material.h:50-73                         
        FRT_MAT_DIFFUSE_LIGHT = 1,   /* material.h:179-192                                */
        FRT_MAT_MODIFIED_PHONG = 2,  /* material.h:75-108 + cosine_power_pdf (pdf.h:99)   */
        FRT_MAT_DIELECTRIC = 4 };    /* material.h:133-177 + dielectric_pdf (pdf.h:138)   */
-enum { FRT_INTEGRATOR_PATH = 0, FRT_INTEGRATOR_PSSMLT = 1 };  /* path.h:8-18, pssmlt.h:29-76 */
+enum { FRT_INTEGRATOR_PATH = 0,     /* path::Li           path.h:8-18, path.cpp:4-116      */
+       FRT_INTEGRATOR_PSSMLT = 1,   /* pssmlt             pssmlt.h:29-76                   */
+       FRT_INTEGRATOR_AO = 2,       /* ao::Li             ao.h:8-43, ao.cpp:4-27           */
+       FRT_INTEGRATOR_NORMALS = 3   /* normals_renderer   debug_renderer.h:6-50            */ };
 enum { FRT_FLAG_NO_LDS_SCENE = 1,      /* render_params.flags: keep small scenes in HBM/L2 (A/B timing)  */
        FRT_FLAG_WAVES5 = 2,            /* register cap for 5 waves/SIMD (A/B timing)                     */
        FRT_FLAG_WAVES6 = 4,            /* register cap for 6 waves/SIMD (A/B timing)                     */
@@ -111,7 +114,7 @@ typedef struct frt_render_params {
     int32_t spp;             /* samples per pixel (viewer ns)                              */
     uint32_t seed;           /* frame seed of the counter RNG (DESIGN.md "RNG stream spec") */
     int32_t max_depth;       /* scatter while depth <= max_depth; reference: 33 (path.cpp:36) */
-    int32_t integrator;      /* FRT_INTEGRATOR_PATH or FRT_INTEGRATOR_PSSMLT                */
+    int32_t integrator;      /* FRT_INTEGRATOR_*                                           */
     int32_t tile_size;       /* square tiles, multiple of 8; 0 = 32                        */
     int32_t shard_index;     /* this call renders tiles t with t % shard_count == index    */
     int32_t shard_count;     /* 1 = whole frame                                            */

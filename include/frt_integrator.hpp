@@ -50,11 +50,17 @@ public:
     {
         frt_scene_view v;
         check(frt_scene_view_get(scene_.get(), &v), "frt_scene_view_get");
+        if (has_env_)
+            for (int k = 0; k < 3; ++k) v.env_color[k] = env_[k];
         return v;
     }
+    // Scene::env_map with another constant colour (material.h:206-232)
+    void set_env(double r, double g, double b) { env_[0] = r; env_[1] = g; env_[2] = b; has_env_ = true; }
     const frt_host_scene_info &info() const { return info_; }
 
 private:
+    double env_[3] = {0, 0, 0};
+    bool has_env_ = false;
     struct del { void operator()(frt_host_scene *s) const { frt_scene_destroy(s); } };
     std::unique_ptr<frt_host_scene, del> scene_;
     frt_host_scene_info info_{};
@@ -136,10 +142,13 @@ private:
     std::vector<frt_ctx *> ctx_;
 };
 
-// path_gpu: the drop-in for `path` (path.h:8-18).  Render() renders the frame
-// on the listed GPUs with frt_render_multi (tile t -> device t % n) and stores
+// tile_gpu<I>: the drop-ins for the per-pixel integrators -- path_gpu for
+// `path` (path.h:8-18), ao_gpu for `ao` (ao.h:8-43), normals_gpu for
+// `normals_renderer` (debug_renderer.h:6-50).  Render() renders the frame on
+// the listed GPUs with frt_render_multi (tile t -> device t % n) and stores
 // the per-pixel means in the viewer.
-struct path_gpu {
+template <int INTEGRATOR>
+struct tile_gpu {
     std::vector<int> devices{0};
     uint32_t seed = 0;
     int max_depth = 33;     // path.cpp:36
@@ -152,7 +161,7 @@ struct path_gpu {
         device_set gpus(devices, scene->view());
         frt_render_params p{};
         p.nx = film->nx; p.ny = film->ny; p.spp = (int)film->ns; p.seed = seed;
-        p.max_depth = max_depth; p.integrator = FRT_INTEGRATOR_PATH; p.tile_size = tile_size;
+        p.max_depth = max_depth; p.integrator = INTEGRATOR; p.tile_size = tile_size;
         p.shard_index = 0; p.shard_count = 1;
         std::vector<float> rgb((size_t)film->nx * film->ny * 3, 0.0f);
         check(frt_render_multi(gpus.data(), gpus.size(), &p, rgb.data(), &last_stats), "frt_render_multi",
@@ -164,6 +173,10 @@ struct path_gpu {
             }
     }
 };
+
+using path_gpu = tile_gpu<FRT_INTEGRATOR_PATH>;
+using ao_gpu = tile_gpu<FRT_INTEGRATOR_AO>;
+using normals_gpu = tile_gpu<FRT_INTEGRATOR_NORMALS>;
 
 // pssmlt_gpu: the drop-in for `pssmlt` (pssmlt.h:20-76) -- Kelemen PSS-MLT with
 // film->ns mutations per pixel over `chains` GPU chains (chain c -> device

@@ -52,6 +52,13 @@ def lib():
         L.ora_scene_export_materials.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.ora_render.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
                                  ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(Counters)]
+        L.ora_render_integrator.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_void_p, ctypes.POINTER(Counters)]
+        L.ora_scene_set_env.argtypes = [ctypes.c_void_p, dp]
+        L.ora_scene_set_env.restype = None
+        L.ora_scene_ao_tmax.argtypes = [ctypes.c_void_p]
+        L.ora_scene_ao_tmax.restype = ctypes.c_double
         L.ora_world_hit.argtypes = [ctypes.c_void_p, dp, dp, ctypes.c_double, ctypes.c_double, dp,
                                     ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(Counters)]
         L.ora_rng_uniform.argtypes = [ctypes.c_uint32] * 4
@@ -139,16 +146,25 @@ class OracleScene:
         lib().ora_scene_export_materials(self.ptr, out.ctypes.data)
         return out[:self.info.n_materials]
 
-    def render(self, nx, ny, spp, seed=0, pixels=None, nthreads=None):
-        """Mean radiance per pixel (viewer::add_sample semantics) + counters."""
+    def set_env(self, rgb):
+        """Constant environment colour (material.h:206-232)."""
+        a, p = darr(rgb)
+        lib().ora_scene_set_env(self.ptr, p)
+
+    def ao_tmax(self):
+        return lib().ora_scene_ao_tmax(self.ptr)
+
+    def render(self, nx, ny, spp, seed=0, pixels=None, nthreads=None, integrator=0):
+        """Mean radiance per pixel (viewer::add_sample semantics) + counters.
+        integrator: 0 path (path.cpp), 2 ao (ao.cpp), 3 normals (debug_renderer.h)."""
         if pixels is None:
             pixels = np.arange(nx * ny, dtype=np.int32)
         pixels = np.ascontiguousarray(pixels, dtype=np.int32)
         out = np.zeros((len(pixels), 3))
         cnt = Counters()
         nthreads = nthreads or min(16, os.cpu_count() or 1)
-        rc = lib().ora_render(self.ptr, nx, ny, spp, seed, pixels.ctypes.data, len(pixels), nthreads,
-                              out.ctypes.data, ctypes.byref(cnt))
+        rc = lib().ora_render_integrator(self.ptr, integrator, nx, ny, spp, seed, pixels.ctypes.data, len(pixels),
+                                         nthreads, out.ctypes.data, ctypes.byref(cnt))
         if rc != 0:
             raise RuntimeError(f"ora_render failed: {rc}")
         return out, cnt

@@ -667,8 +667,65 @@ static v3 Li(li_ctx *c, const ray *r, int depth, const hit_record *prev, double 
     return s->env;
 }
 
-/* one pixel, path.cpp:120-143 (loop over s, add_sample divides by ns: *= 1/ns) */
-static void render_pixel(const ora_scene *s, int nx, int ny, int spp, uint32_t seed, int x, int y,
+/* scene->world->bounding_box (ao.cpp:19-21): the root node's box
+ * (parallel_bvh.h:33-37), a lone primitive's box, or -- hitable_list
+ * (hitable_list.cpp:23-31) returns before assigning when its first element
+ * reports a box -- the default aabb, whose Vector3 members are quiet NaNs
+ * (geometry.h:345-348). */
+static double world_box_size_y(const ora_scene *s)
+{
+    if (s->world_kind == WORLD_LIST) return NAN;
+    const aabb b = s->root >= 0 ? s->nodes[s->root].box : prim_box(s, ~s->root);
+    return b.size.e[1];
+}
+
+/* ao::Li (ao.cpp:4-27).  The camera hit's material scatters (lambertian,
+ * modified_phong, dielectric) -> one visibility ray from hrec.p (no offset)
+ * along the scattering pdf's generate(get2d()) up to t_max = half the world
+ * box height; occluded -> 0, otherwise (and for misses / lights) the
+ * environment.  RNG: the get2d is dims DIM_BOUNCE(0) + 6, 7 (the scatter's
+ * get3d has no effect on the result). */
+static v3 ao_Li(li_ctx *c, const ray *r)
+{
+    const ora_scene *s = c->s;
+    hit_record hrec;
+    c->cnt->camera_rays++;
+    if (world_hit(s, r, EPSILON, FLT_MAX, &hrec, c->cnt)) {
+        const material *m = &s->mats[hrec.mat];
+        if (m->type == MAT_LAMBERT || m->type == MAT_PHONG || m->type == MAT_DIELECTRIC) {
+            const uint32_t base = DIM_BOUNCE(0);
+            const double u0 = rng_u(c->key, base + 6), u1 = rng_u(c->key, base + 7);
+            const v3 wi = vneg(unit(r->d));
+            v3 dir;
+            if (m->type == MAT_LAMBERT) {                       /* cosine_pdf::generate (pdf.h:91-94) */
+                onb uvw = onb_from_w(hrec.normal);
+                dir = onb_from_local(&uvw, hemisphere_to_cosine_direction(u0, u1));
+            } else if (m->type == MAT_PHONG) {                  /* cosine_power_pdf::generate (pdf.h:115-132) */
+                dir = cosine_power_generate(hrec.normal, wi, m->shininess, u0, u1);
+            } else {                                            /* dielectric_pdf::generate (pdf.h:164-178) */
+                dir = dielectric_generate(hrec.normal, wi, m->ior, u0);
+            }
+            ray shadow; shadow.o = hrec.p; shadow.d = dir;
+            const double t_max = world_box_size_y(s) * 0.50f;
+            c->cnt->shadow_rays++;
+            if (world_hit(s, &shadow, EPSILON, t_max, &hrec, c->cnt)) return mk(0.0, 0.0, 0.0);
+        }
+    }
+    return s->env;
+}
+
+/* normals_renderer::Li (debug_renderer.h:8-17): the hit's shading normal, else the environment */
+static v3 normals_Li(li_ctx *c, const ray *r)
+{
+    hit_record hrec;
+    c->cnt->camera_rays++;
+    if (world_hit(c->s, r, EPSILON, FLT_MAX, &hrec, c->cnt)) return hrec.normal;
+    return c->s->env;
+}
+
+/* one pixel, path.cpp:120-143 (loop over s, add_sample divides by ns: *= 1/ns);
+ * ao.h:15-38 and debug_renderer.h:19-45 are the same loop around their Li */
+static void render_pixel(const ora_scene *s, int kind, int nx, int ny, int spp, uint32_t seed, int x, int y,
                          double *out, ora_counters *cnt)
 {
     v3 col = mk(0.0, 0.0, 0.0);
@@ -679,7 +736,9 @@ static void render_pixel(const ora_scene *s, int nx, int ny, int spp, uint32_t s
         double v = (double)(y + rng_u(c.key, 1)) / (double)ny;
         ray r = camera_get_ray(&s->cam, u, v, rng_u(c.key, 2), rng_u(c.key, 3));
         hit_record h; memset(&h, 0, sizeof(h)); h.mat = 0;
-        v3 sample = Li(&c, &r, 0, &h, 0.0);
+        v3 sample = kind == ORA_INTEGRATOR_AO        ? ao_Li(&c, &r)
+                  : kind == ORA_INTEGRATOR_NORMALS ? normals_Li(&c, &r)
+                                                   : Li(&c, &r, 0, &h, 0.0);
         col = vadd(col, sample);
         cnt->samples++;
     }
@@ -688,7 +747,7 @@ static void render_pixel(const ora_scene *s, int nx, int ny, int spp, uint32_t s
 }
 
 typedef struct {
-    const ora_scene *s; int nx, ny, spp; uint32_t seed;
+    const ora_scene *s; int kind, nx, ny, spp; uint32_t seed;
     const int32_t *pixels; int npix; int tid, nth;
     double *out; ora_counters cnt;
 } job;
@@ -698,21 +757,27 @@ static void *render_worker(void *arg)
     memset(&j->cnt, 0, sizeof(j->cnt));
     for (int i = j->tid; i < j->npix; i += j->nth) {
         int p = j->pixels[i];
-        render_pixel(j->s, j->nx, j->ny, j->spp, j->seed, p % j->nx, p / j->nx, &j->out[3 * (size_t)i], &j->cnt);
+        render_pixel(j->s, j->kind, j->nx, j->ny, j->spp, j->seed, p % j->nx, p / j->nx, &j->out[3 * (size_t)i], &j->cnt);
     }
     return NULL;
 }
 int ora_render(const ora_scene *s, int nx, int ny, int spp, uint32_t seed, const int32_t *pixels, int npix,
                int nthreads, double *out_rgb, ora_counters *cnt)
 {
+    return ora_render_integrator(s, ORA_INTEGRATOR_PATH, nx, ny, spp, seed, pixels, npix, nthreads, out_rgb, cnt);
+}
+int ora_render_integrator(const ora_scene *s, int kind, int nx, int ny, int spp, uint32_t seed,
+                          const int32_t *pixels, int npix, int nthreads, double *out_rgb, ora_counters *cnt)
+{
     if (!s || nx <= 0 || ny <= 0 || spp <= 0 || npix < 0) return -1;
+    if (kind != ORA_INTEGRATOR_PATH && kind != ORA_INTEGRATOR_AO && kind != ORA_INTEGRATOR_NORMALS) return -3;
     for (int i = 0; i < npix; ++i)
         if (pixels[i] < 0 || pixels[i] >= nx * ny) return -2;
     if (nthreads < 1) nthreads = 1;
     job *jobs = (job *)calloc((size_t)nthreads, sizeof(job));
     pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
     for (int t = 0; t < nthreads; ++t) {
-        jobs[t].s = s; jobs[t].nx = nx; jobs[t].ny = ny; jobs[t].spp = spp; jobs[t].seed = seed;
+        jobs[t].s = s; jobs[t].kind = kind; jobs[t].nx = nx; jobs[t].ny = ny; jobs[t].spp = spp; jobs[t].seed = seed;
         jobs[t].pixels = pixels; jobs[t].npix = npix; jobs[t].tid = t; jobs[t].nth = nthreads; jobs[t].out = out_rgb;
         if (nthreads > 1) pthread_create(&th[t], NULL, render_worker, &jobs[t]);
     }
@@ -1493,6 +1558,10 @@ void ora_free_scene(ora_scene *s)
     if (!s) return;
     free(s->tris); free(s->sph); free(s->mats); free(s->nodes); free(s->list); free(s->lights); free(s);
 }
+/* Scene::env_map with another constant texture (material.h:206-232); the
+ * reference scenes' environment is black, so AO / normals tests set one. */
+void ora_scene_set_env(ora_scene *s, const double *rgb) { s->env = vload(rgb); }
+double ora_scene_ao_tmax(const ora_scene *s) { return world_box_size_y(s) * 0.50f; }
 void ora_scene_get_info(const ora_scene *s, ora_scene_info *info)
 {
     info->n_tris = s->ntris; info->n_spheres = s->nsph; info->n_materials = s->nmats;

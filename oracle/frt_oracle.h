@@ -72,6 +72,16 @@ int  ora_render(const ora_scene *s, int nx, int ny, int spp, uint32_t seed,
                 const int32_t *pixels, int npix, int nthreads,
                 double *out_rgb, ora_counters *cnt);
 
+/* The same with the integrator chosen: ORA_INTEGRATOR_PATH (path.cpp:4-116),
+ * _AO (ao.cpp:4-27) or _NORMALS (debug_renderer.h:8-17).  Values = FRT_INTEGRATOR_*. */
+enum { ORA_INTEGRATOR_PATH = 0, ORA_INTEGRATOR_AO = 2, ORA_INTEGRATOR_NORMALS = 3 };
+int  ora_render_integrator(const ora_scene *s, int integrator, int nx, int ny, int spp, uint32_t seed,
+                           const int32_t *pixels, int npix, int nthreads, double *out_rgb, ora_counters *cnt);
+/* constant environment colour (the reference scenes use black) */
+void ora_scene_set_env(ora_scene *s, const double *rgb);
+/* ao.cpp:21 t_max = world bounding box height * 0.5 (NaN for list worlds) */
+double ora_scene_ao_tmax(const ora_scene *s);
+
 /* PSS-MLT (pssmlt.cpp): bootstrap b, full render (splat film, caller-zeroed),
  * and a single eye path for given primary samples (92 doubles -> x, y, rgb, sc). */
 double ora_mlt_bootstrap(const ora_scene *s, int nx, int ny, uint32_t seed, int n_init);

@@ -47,3 +47,23 @@ def test_cli_pssmlt(cornell_obj, tmp_path):
     assert r.returncode == 0, r.stderr
     img = read_pfm(out)
     assert np.isfinite(img).all() and img.mean() > 0.01
+
+
+@pytest.mark.parametrize("integ,code", [("ao", frt.FRT_INTEGRATOR_AO), ("normals", frt.FRT_INTEGRATOR_NORMALS)])
+def test_cli_ao_normals_match_binding(cornell_obj, tmp_path, integ, code):
+    """renderer<ao_gpu> / renderer<normals_gpu> (ao.h, debug_renderer.h) with --env."""
+    out = str(tmp_path / f"{integ}.pfm")
+    r = subprocess.run([CLI, "--scene", "cornell", "--obj", cornell_obj, "--res", "64x48", "--ns", "4",
+                        "--seed", "5", "--integrator", integ, "--env", "1,0.5,0.25", "--out", out],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    img = read_pfm(out)
+    ctx = frt.Context(0)
+    try:
+        hs = frt.HostScene("cornell_box_obj", cornell_obj, 64 / 48)
+        hs.set_env((1.0, 0.5, 0.25))
+        ctx.upload(hs)
+        film, _ = ctx.render(frt.RenderParams.make(64, 48, 4, seed=5, integrator=code))
+    finally:
+        ctx.close()
+    assert np.array_equal(img, film)
