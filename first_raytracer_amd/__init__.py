@@ -18,8 +18,10 @@ LIB_PATH = os.environ.get("FRT_LIB_PATH") or os.path.join(HERE, "libfrt.so")
 FRT_WORLD_BVH, FRT_WORLD_LIST = 0, 1
 FRT_MAT_LAMBERTIAN, FRT_MAT_DIFFUSE_LIGHT = 0, 1
 FRT_PRIM_SPHERE = 1 << 30
-ABI_VERSION = 3                 # include/frt.h FRT_ABI_VERSION (frt_stats / frt_material layout)
-FRT_MAT_LAMBERTIAN, FRT_MAT_DIFFUSE_LIGHT, FRT_MAT_MODIFIED_PHONG, FRT_MAT_DIELECTRIC = 0, 1, 2, 4
+ABI_VERSION = 4                 # include/frt.h FRT_ABI_VERSION (frt_stats / frt_material layout)
+FRT_MAT_LAMBERTIAN, FRT_MAT_DIFFUSE_LIGHT, FRT_MAT_MODIFIED_PHONG, FRT_MAT_METAL, FRT_MAT_DIELECTRIC = 0, 1, 2, 3, 4
+FRT_MAT_ROUGH_CONDUCTOR = 5
+FRT_DIST_GGX, FRT_DIST_BECKMANN = 0, 1
 FRT_FLAG_NO_LDS_SCENE = 1
 FRT_FLAG_WAVES5 = 2
 FRT_FLAG_WAVES6 = 4
@@ -38,9 +40,29 @@ class FrtError(RuntimeError):
 
 
 class Material(ctypes.Structure):
-    _fields_ = [("type", ctypes.c_int32), ("reserved", ctypes.c_int32),
+    _fields_ = [("type", ctypes.c_int32), ("distribution", ctypes.c_int32),
                 ("albedo", ctypes.c_double * 3), ("emit", ctypes.c_double * 3),
-                ("specular", ctypes.c_double * 3), ("exponent", ctypes.c_double), ("ior", ctypes.c_double)]
+                ("specular", ctypes.c_double * 3), ("exponent", ctypes.c_double), ("ior", ctypes.c_double),
+                ("alpha", ctypes.c_double), ("eta", ctypes.c_double * 3), ("k", ctypes.c_double * 3)]
+
+    @classmethod
+    def from_spec(cls, m):
+        """frt_material from a scene-spec material dict (see HostScene.from_spec)."""
+        r = cls()
+        r.type = MAT_TYPES[m["type"]]
+        r.distribution = DISTRIBUTIONS[m.get("distribution", "ggx").lower()]
+        for k in ("albedo", "emit", "specular", "eta", "k"):
+            getattr(r, k)[:] = [float(x) for x in m.get(k, (0.0, 0.0, 0.0))]
+        r.exponent = float(m.get("exponent", 0.0))
+        r.ior = float(m.get("ior", 0.0))
+        r.alpha = float(m.get("alpha", 0.0))
+        return r
+
+
+MAT_TYPES = {"lambertian": 0, "diffuse_light": 1, "modified_phong": 2, "metal": 3, "dielectric": 4,
+             "rough_conductor": 5}                      # FRT_MAT_*
+DISTRIBUTIONS = {"ggx": 0, "beckmann": 1}               # FRT_DIST_*
+SPHERE_WHERE = {"world": 1, "lights": 2, "both": 3}     # FRT_SPHERE_*
 
 
 class SceneView(ctypes.Structure):
@@ -115,7 +137,8 @@ _lib = None
 # every symbol include/frt.h declares
 EXPORTS = ("frt_get_abi_version", "frt_create", "frt_destroy", "frt_last_error", "frt_upload_scene",
            "frt_shard_slot_count", "frt_shard_slots", "frt_render", "frt_render_multi", "frt_render_device",
-           "frt_scene_create",
+           "frt_scene_create", "frt_scene_new", "frt_scene_add_obj", "frt_scene_add_sphere", "frt_scene_set_camera",
+           "frt_scene_set_env", "frt_scene_finish",
            "frt_scene_view_get", "frt_scene_info", "frt_scene_destroy", "frt_write_tessellated_obj",
            "frt_write_pfm", "frt_selftest_path_host", "frt_selftest_mlt_paths_host")
 
@@ -156,6 +179,14 @@ def lib():
     L.frt_scene_info.argtypes = [vp, ctypes.POINTER(HostSceneInfo)]
     L.frt_scene_destroy.argtypes = [vp]
     L.frt_scene_destroy.restype = None
+    dp = ctypes.POINTER(ctypes.c_double)
+    L.frt_scene_new.argtypes = [ctypes.POINTER(vp)]
+    L.frt_scene_add_obj.argtypes = [vp, ctypes.c_char_p, dp, ctypes.POINTER(Material), ctypes.c_int]
+    L.frt_scene_add_sphere.argtypes = [vp, dp, ctypes.c_double, ctypes.POINTER(Material), ctypes.c_int]
+    L.frt_scene_set_camera.argtypes = [vp, dp, dp, dp, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                       ctypes.c_double]
+    L.frt_scene_set_env.argtypes = [vp, dp]
+    L.frt_scene_finish.argtypes = [vp, ctypes.c_int]
     L.frt_write_tessellated_obj.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p]
     L.frt_write_pfm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, vp]
     L.frt_selftest_path_host.argtypes = [ctypes.POINTER(SceneView), ctypes.POINTER(RenderParams), vp,
@@ -189,6 +220,54 @@ class HostScene:
         """Constant environment colour of the views this scene hands out
         (material.h:206-232; the reference scenes use black)."""
         self.env = tuple(float(x) for x in rgb)
+
+    @classmethod
+    def from_spec(cls, spec, aspect):
+        """Build a scene the way main.cpp's scene functions do (frt_scene_new ...
+        frt_scene_finish).  `spec`:
+          {"objects": [{"obj": path, "to_world": 16 floats (row-major) | None,
+                        "bsdf": material | None, "geo": use_geometry_normals},
+                       {"sphere": (x, y, z), "radius": r, "material": material,
+                        "where": "world" | "lights" | "both"}, ...],
+           "camera": {"lookfrom", "lookat", "vup", "vfov", "aperture", "focus"},
+           "world": "bvh" | "list", "env": (r, g, b) | None}
+        material: {"type": "lambertian" | "diffuse_light" | "modified_phong" |
+                   "metal" | "dielectric" | "rough_conductor", "albedo", "emit",
+                   "specular", "exponent", "ior", "alpha", "distribution":
+                   "ggx" | "beckmann", "eta", "k"}.
+        oracle.OracleScene.from_spec builds the same scene in the oracle."""
+        self = cls.__new__(cls)
+        self.ptr = ctypes.c_void_p()
+        self.env = None
+        L = lib()
+        _check(L.frt_scene_new(ctypes.byref(self.ptr)), "frt_scene_new")
+
+        def dptr(x):
+            a = np.ascontiguousarray(np.asarray(x, np.float64))
+            return a, a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+        for o in spec["objects"]:
+            if "obj" in o:
+                tw = dptr(o["to_world"]) if o.get("to_world") is not None else (None, None)
+                bs = ctypes.byref(Material.from_spec(o["bsdf"])) if o.get("bsdf") is not None else None
+                _check(L.frt_scene_add_obj(self.ptr, o["obj"].encode(), tw[1], bs, int(bool(o.get("geo", False)))),
+                       f"frt_scene_add_obj({o['obj']})")
+            else:
+                c = dptr(o["sphere"])
+                _check(L.frt_scene_add_sphere(self.ptr, c[1], float(o["radius"]),
+                                              ctypes.byref(Material.from_spec(o["material"])),
+                                              SPHERE_WHERE[o.get("where", "world")]), "frt_scene_add_sphere")
+        cam = spec["camera"]
+        f, a, u = dptr(cam["lookfrom"]), dptr(cam["lookat"]), dptr(cam.get("vup", (0, 1, 0)))
+        _check(L.frt_scene_set_camera(self.ptr, f[1], a[1], u[1], float(cam["vfov"]), float(aspect),
+                                      float(cam.get("aperture", 0.0)), float(cam.get("focus", 10.0))),
+               "frt_scene_set_camera")
+        if spec.get("env") is not None:
+            e = dptr(spec["env"])
+            _check(L.frt_scene_set_env(self.ptr, e[1]), "frt_scene_set_env")
+        _check(L.frt_scene_finish(self.ptr, {"bvh": 0, "list": 1}[spec.get("world", "bvh")]), "frt_scene_finish")
+        self.info = HostSceneInfo()
+        L.frt_scene_info(self.ptr, ctypes.byref(self.info))
+        return self
 
     def view(self):
         v = SceneView()

@@ -90,6 +90,7 @@ FRT_HD void mlt_begin(MltPath &M, const DevScene &S, const PrndSource &src, int 
     P.rd = ((S.cam_llc + s * S.cam_h + t * S.cam_v) - S.cam_o) - off;
     P.rtmax = kTMaxClosest;
     P.shadow = false;
+    P.term = false;
     P.depth = 0;
     P.beta = mk3(1, 1, 1);
     P.L = mk3(0, 0, 0);
@@ -115,10 +116,11 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
 {
     PathState &P = M.P;
     if (P.shadow) {
-        path_after_shadow(P, h.prim < 0);
+        if (!path_after_shadow<MATS>(P, h.prim < 0)) return true;
         if (P.depth <= kMltMaxPath) ++n_ext;
         return false;
     }
+    if (P.term) return true;                            // finished in the traversal loop
     if (h.prim < 0) {
         P.L = P.L + P.beta * S.env;
         return true;
@@ -127,7 +129,7 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
     f3 n;
     int mat;
     prim_shade(S, h.prim, P.ro, p, h.u, h.v, n, mat);
-    const float4 m0 = S.mats[2 * mat], m1 = S.mats[2 * mat + 1];
+    const float4 m0 = S.mats[kMatStride * mat], m1 = S.mats[kMatStride * mat + 1];
     const int mtype = f2i(m0.w);
     const float sc0 = src.get(M.off), sc1 = src.get(M.off + 1);   // scatter rnd (pssmlt.cpp:159-163)
     M.off += 3;                                         // consumed at every hit
@@ -144,48 +146,47 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
         }
         return true;
     }
-    const bool lamb = mtype == FRT_MAT_LAMBERTIAN, phong = MATS && mtype == FRT_MAT_MODIFIED_PHONG,
+    const bool lamb = mtype == FRT_MAT_LAMBERTIAN, spec = MATS && mat_is_specular(mtype),
                diel = MATS && mtype == FRT_MAT_DIELECTRIC;
-    if (!(lamb || phong || diel)) return true;          // diffuse_light seen from behind
+    if (!(lamb || spec)) return true;                   // diffuse_light seen from behind
     const f3 wi = -normalize(P.rd);
     // NEE prnds (pssmlt.cpp:190-195); the bsdf prnds follow only for the diffuse branch
     const float rnd0 = src.get(M.off), rnd1 = src.get(M.off + 1), rnd2 = src.get(M.off + 2);
     M.off += 3;
     f3 wo, beta_next;
     float pdf;
+    SpecMat SM{};
     if (!MATS || lamb) {
         const float b0 = src.get(M.off), b1 = src.get(M.off + 1);
         M.off += 2;
         const Onb uvw = onb_from_w(n);
         wo = onb_local(uvw, cosine_direction(b0, b1));
         const float cw = dot(n, normalize(wo));
-        pdf = fmaxf(cw, 0.0f) * kInvPi;
-        if (pdf == 0.0f) return true;                   // drops this vertex's NEE (pssmlt.cpp:261-264)
+        pdf = fmaxf(cw, 0.0f) * kInvPi;                 // pdf 0: the vertex returns 0 (pssmlt.cpp:261-264)
         beta_next = fdiv(fabsf(cw), pdf) * (P.beta * (kInvPi * xyz(m0)));
     } else {                                            // pssmlt.cpp:232-249
-        f3 bsdf;
-        if (phong) {
-            wo = cosine_power_generate(n, wi, m1.w, sc0, sc1);
-            pdf = cosine_power_value(n, wi, m1.w, wo);
-            bsdf = phong_eval(xyz(m0), xyz(m1), m1.w, n, wi, wo);
-        } else {
-            wo = dielectric_generate(n, wi, m1.w, sc0);
-            pdf = dielectric_value(n, wi, m1.w, wo);
-            bsdf = dielectric_eval(xyz(m1), m1.w, n, wi, wo);
-        }
-        if (pdf == 0.0f) return true;
+        SM = spec_mat(S, mat, mtype, m0, m1);
+        float sampled;
+        wo = spec_generate(SM, n, wi, sc0, sc1, sampled);
+        pdf = spec_value(SM, n, wi, wo);
+        if (sampled > 0.0f) pdf = sampled;
+        const f3 bsdf = spec_eval(SM, n, wi, wo);
         beta_next = P.beta * (rcp(pdf) * bsdf);
     }
-    const f3 origin = (!MATS || lamb || dot(n, wo) > 0.0f) ? p + kEps * n : p - kEps * n;   // hrec.p moved off (:243, :253)
-    P.nxt_d = wo;
+    // a zero pdf ends the path after the shadow ray the reference traces first (P.term)
     const int nl = S.n_lights;
     int idx = (int)(rnd0 * (float)nl);
     if (idx == nl) idx -= 1;
+    P.term = pdf == 0.0f;
+    if (P.term && !(idx >= 0 && !diel)) return true;
+    const f3 nee_o = p + kEps * n;
+    const f3 origin = (!MATS || lamb || dot(n, wo) > 0.0f) ? nee_o : p - kEps * n;   // hrec.p moved off (:243, :253)
+    P.nxt_d = wo;
+    if constexpr (MATS) P.nxt_o = origin;
     if (idx >= 0 && !diel) {
         const int lref = S.lights[idx];
         f3 ln;
         int lmat;
-        const f3 nee_o = p + kEps * n;
         const f3 tl = prim_sample(S, lref, nee_o, rnd1, rnd2, ln, lmat);
         const float dist2 = len2(tl);
         const f3 tu = rlen(tl) * tl;
@@ -195,10 +196,10 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
         if (cos_lo != 0.0f) {
             const float light_pdf = fdiv(prim_pdf(S, lref, p, h.t, n, tu) * dist2, fabsf(cos_lo));
             const bool l = !MATS || lamb;
-            const f3 f = l ? cos_wi * (kInvPi * xyz(m0)) : phong_eval(xyz(m0), xyz(m1), m1.w, n, wi, tu);
-            const float bsdf_pdf = l ? fmaxf(cos_wi, 0.0f) * kInvPi : cosine_power_value(n, wi, m1.w, tu);
+            const f3 f = l ? cos_wi * (kInvPi * xyz(m0)) : spec_eval(SM, n, wi, tu);
+            const float bsdf_pdf = l ? fmaxf(cos_wi, 0.0f) * kInvPi : spec_value(SM, n, wi, tu);
             const float wgt = mi_weight(light_pdf, bsdf_pdf);
-            const float4 lm0 = S.mats[2 * lmat], lm1 = S.mats[2 * lmat + 1];
+            const float4 lm0 = S.mats[kMatStride * lmat], lm1 = S.mats[kMatStride * lmat + 1];
             if (f2i(lm0.w) == FRT_MAT_DIFFUSE_LIGHT && dot(ln, tu) < 0.0f)
                 P.nee = fdiv(wgt, light_pdf) * (P.beta * (xyz(lm1) * f));
         }
@@ -208,7 +209,7 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
     }
     P.beta = beta_next;
     P.prev_pdf = pdf;
-    P.prev_spec = MATS && !lamb;
+    P.prev_spec = MATS && mat_no_mis(mtype);
     if (!P.shadow) {
         P.ro = origin; P.rd = wo; P.rtmax = kTMaxClosest;
         ++P.depth;

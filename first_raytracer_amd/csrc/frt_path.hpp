@@ -16,6 +16,10 @@ namespace frt {
 
 FRT_HD int f2i(float f) { return __builtin_bit_cast(int, f); }
 FRT_HD float i2f(int i) { return __builtin_bit_cast(float, i); }
+// materials: kMatStride float4 per material (frt_upload_scene packs them):
+// m0 = (albedo | kd | metal albedo | rough eta, type), m1 = (emit | ks,
+// exponent | ior | alpha), m2 = (rough k, distribution)
+constexpr int kMatStride = 3;
 FRT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
 // true if the predicate holds on any active lane of the wave (the host self-test is one lane)
 FRT_HD bool wave_any(bool x)
@@ -435,12 +439,14 @@ struct PathState {
     f3 ro, rd;            // ray to trace next
     float rtmax;
     bool shadow;          // any-hit query
+    bool term;            // the path ends after this shadow ray (zero bsdf pdf)
     f3 beta, L;           // throughput, radiance of this sample
     f3 nee;               // NEE contribution if the shadow ray is unoccluded
-    f3 nxt_d;             // extension direction after the shadow ray (its origin is the shadow ray's)
+    f3 nxt_d;             // extension direction after the shadow ray
+    f3 nxt_o;             // its origin when it differs from the shadow ray's (specular kernels only)
     f3 prev_p;            // previous hit point (MIS distance, path.cpp:25)
     float prev_pdf;       // bsdf pdf of the previous bounce
-    bool prev_spec;       // previous bounce was specular (modified_phong / dielectric): no MIS on light hits
+    bool prev_spec;       // previous bounce was modified_phong / metal / dielectric: no MIS on light hits
     int depth;
     RngKey key;
 };
@@ -468,6 +474,7 @@ FRT_HD void path_begin(PathState &P, const DevScene &S, int px, int py, int nx, 
     P.rd = ((S.cam_llc + u * S.cam_h + v * S.cam_v) - S.cam_o) - off;
     P.rtmax = kTMaxClosest;
     P.shadow = false;
+    P.term = false;
     P.depth = 0;
     P.beta = mk3(1, 1, 1);
     P.L = mk3(0, 0, 0);
@@ -477,15 +484,75 @@ FRT_HD void path_begin(PathState &P, const DevScene &S, int px, int py, int nx, 
 }
 
 // Shadow ray done (path.cpp:50-77): add the NEE term if unoccluded, then the
-// extension ray from the same origin.  The megakernel runs this inside its
-// traversal loop, so shading phases only see closest-hit results.
-FRT_HD void path_after_shadow(PathState &P, bool unoccluded)
+// extension ray.  The megakernel runs this inside its traversal loop, so
+// shading phases only see closest-hit results.  Lambertian bounces leave from
+// the NEE origin (p + eps n); specular ones may leave from the other side
+// (path.cpp:91-93), so the specular kernels carry the origin (MATS).
+// Returns false when the path ends here: its scattered direction had pdf 0,
+// so the reference returns 0 for the vertex after tracing the shadow ray
+// (path.cpp:45-77 run before :87-90 / :103-106) -- the ray is traced and
+// counted like the reference's, its NEE term dropped.
+template <bool MATS = true>
+FRT_HD bool path_after_shadow(PathState &P, bool unoccluded)
 {
-    if (unoccluded) P.L = P.L + P.nee;
     P.shadow = false;
-    P.rd = P.nxt_d; P.rtmax = kTMaxClosest;                // P.ro is already the extension origin
+    if (P.term) return false;
+    if (unoccluded) P.L = P.L + P.nee;
+    if constexpr (MATS) P.ro = P.nxt_o;
+    P.rd = P.nxt_d; P.rtmax = kTMaxClosest;
     ++P.depth;
+    return true;
 }
+
+// The specular materials of path.cpp:78-95 behind one interface (the
+// oracle's spec_generate / spec_value / spec_eval): modified_phong, metal,
+// dielectric, rough_conductor.
+struct SpecMat {
+    int type;
+    float4 m0, m1, m2;
+};
+FRT_HD SpecMat spec_mat(const DevScene &S, int mat, int type, float4 m0, float4 m1)
+{
+    SpecMat M{type, m0, m1, make_float4(0.0f, 0.0f, 0.0f, 0.0f)};
+    if (type == FRT_MAT_ROUGH_CONDUCTOR) M.m2 = S.mats[kMatStride * mat + 2];
+    return M;
+}
+// scatter's direction from the get3d sample (material.h:83-88, 117-119, 139-145,
+// 262-268) and srec.sampled_pdf (-1 unless the rough conductor sets it)
+FRT_HD f3 spec_generate(const SpecMat &M, f3 n, f3 wi, float s0, float s1, float &sampled_pdf)
+{
+    sampled_pdf = -1.0f;
+    switch (M.type) {
+    case FRT_MAT_MODIFIED_PHONG: return cosine_power_generate(n, wi, M.m1.w, s0, s1);
+    case FRT_MAT_DIELECTRIC: return dielectric_generate(n, wi, M.m1.w, s0);
+    case FRT_MAT_METAL: return reflect(-wi, n);          // reflect(unit(r_in.d), n); -wi = unit(r_in.d)
+    default: return normalize(rough_generate(n, wi, M.m1.w, f2i(M.m2.w), s0, s1, sampled_pdf));
+    }
+}
+FRT_HD float spec_value(const SpecMat &M, f3 n, f3 wi, f3 wo)     // srec.pdf_ptr->value
+{
+    switch (M.type) {
+    case FRT_MAT_MODIFIED_PHONG: return cosine_power_value(n, wi, M.m1.w, wo);
+    case FRT_MAT_DIELECTRIC: return dielectric_value(n, wi, M.m1.w, wo);
+    case FRT_MAT_METAL: return 1.0f;                     // constant_pdf(1) (pdf.h:186-201)
+    default: return rough_value(n, wi, M.m1.w, f2i(M.m2.w), wo);
+    }
+}
+FRT_HD f3 spec_eval(const SpecMat &M, f3 n, f3 wi, f3 wo)          // eval_bsdf
+{
+    switch (M.type) {
+    case FRT_MAT_MODIFIED_PHONG: return phong_eval(xyz(M.m0), xyz(M.m1), M.m1.w, n, wi, wo);
+    case FRT_MAT_DIELECTRIC: return dielectric_eval(xyz(M.m1), M.m1.w, n, wi, wo);
+    case FRT_MAT_METAL: return xyz(M.m0);
+    default: return rough_eval(xyz(M.m0), xyz(M.m2), xyz(M.m1), M.m1.w, f2i(M.m2.w), n, wi, wo);
+    }
+}
+FRT_HD bool mat_is_specular(int t)
+{
+    return t == FRT_MAT_MODIFIED_PHONG || t == FRT_MAT_METAL || t == FRT_MAT_DIELECTRIC || t == FRT_MAT_ROUGH_CONDUCTOR;
+}
+// light hits after these return Le unweighted (path.cpp:18-22)
+FRT_HD bool mat_no_mis(int t) { return t == FRT_MAT_MODIFIED_PHONG || t == FRT_MAT_METAL || t == FRT_MAT_DIELECTRIC; }
 
 // Returns true when the path is finished (P.L is the sample's radiance).
 // MATS = false compiles the lambertian / diffuse_light scenes' kernel: the
@@ -494,10 +561,11 @@ template <bool MATS = true>
 FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_depth, uint32_t &n_ext, uint32_t &n_sh)
 {
     if (P.shadow) {
-        path_after_shadow(P, h.prim < 0);
+        if (!path_after_shadow<MATS>(P, h.prim < 0)) return true;
         ++n_ext;
         return false;
     }
+    if (P.term) return true;                            // finished in the traversal loop
     if (h.prim < 0) {                                   // path.cpp:115 environment
         P.L = P.L + P.beta * S.env;
         return true;
@@ -506,13 +574,13 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
     f3 n;
     int mat;
     prim_shade(S, h.prim, P.ro, p, h.u, h.v, n, mat);
-    const float4 m0 = S.mats[2 * mat], m1 = S.mats[2 * mat + 1];
+    const float4 m0 = S.mats[kMatStride * mat], m1 = S.mats[kMatStride * mat + 1];
     const int mtype = f2i(m0.w);
     // diffuse_light::emitted is one-sided (material.h:184-190)
     if (mtype == FRT_MAT_DIFFUSE_LIGHT && dot(n, P.rd) < 0.0f) {
         const f3 Le = xyz(m1);
         if (P.depth == 0 || P.prev_spec) {
-            P.L = P.L + P.beta * Le;                    // path.cpp:16-22 (camera ray / after phong, dielectric)
+            P.L = P.L + P.beta * Le;                    // path.cpp:16-22 (camera ray / after phong, metal, dielectric)
         } else {                                        // path.cpp:24-31: MIS against the bsdf sample
             const float cos_wo = dot(n, -normalize(P.rd));
             float d2 = len2(p - P.prev_p);
@@ -522,50 +590,49 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
         }
         return true;
     }
-    const bool lamb = mtype == FRT_MAT_LAMBERTIAN, phong = MATS && mtype == FRT_MAT_MODIFIED_PHONG,
-               diel = MATS && mtype == FRT_MAT_DIELECTRIC;
-    if (!(lamb || phong || diel) || P.depth > max_depth) return true;   // no scatter: Le (= 0)
+    const bool lamb = mtype == FRT_MAT_LAMBERTIAN, spec = MATS && mat_is_specular(mtype);
+    if (!(lamb || spec) || P.depth > max_depth) return true;   // no scatter: Le (= 0)
+    const bool diel = MATS && mtype == FRT_MAT_DIELECTRIC;
     const uint32_t base = dim_bounce(P.depth);
+    // NEE's light pick (path.cpp:39-40)
+    const int nl = S.n_lights;
+    int idx = (int)(rng_u(P.key, base + 3) * (float)nl);
+    if (idx == nl) idx -= 1;
+    const bool nee = idx >= 0 && !diel;
     // The scattered direction first: a zero pdf returns 0 for this vertex,
-    // dropping its NEE too (path.cpp:84-86, 103-106).
+    // dropping its NEE too (path.cpp:84-86, 103-106) -- after the reference has
+    // traced the shadow ray, so that ray is still traced (P.term).
     f3 wo, beta_next;
     float pdf;
     const f3 wi = -normalize(P.rd);                     // hrec.wi (triangle.h:108, sphere.h:47)
+    SpecMat M{};
     if (!MATS || lamb) {                                // cosine_pdf (path.cpp:96-110)
         const Onb uvw = onb_from_w(n);
         wo = onb_local(uvw, cosine_direction(rng_u(P.key, base + 6), rng_u(P.key, base + 7)));
         const float cw = dot(n, normalize(wo));
         pdf = fmaxf(cw, 0.0f) * kInvPi;
-        if (pdf == 0.0f) return true;
         beta_next = fdiv(fabsf(cw), pdf) * (P.beta * (kInvPi * xyz(m0)));   // lambertian::eval_bsdf
     } else {                                            // specular branch (path.cpp:78-95); the
-        f3 bsdf;                                        // scatter sample is get3d's (base + 0, 1)
-        if (phong) {
-            const float e = m1.w;
-            wo = cosine_power_generate(n, wi, e, rng_u(P.key, base + 0), rng_u(P.key, base + 1));
-            pdf = cosine_power_value(n, wi, e, wo);
-            bsdf = phong_eval(xyz(m0), xyz(m1), e, n, wi, wo);
-        } else {
-            wo = dielectric_generate(n, wi, m1.w, rng_u(P.key, base + 0));
-            pdf = dielectric_value(n, wi, m1.w, wo);
-            bsdf = dielectric_eval(xyz(m1), m1.w, n, wi, wo);
-        }
-        if (pdf == 0.0f) return true;
+        M = spec_mat(S, mat, mtype, m0, m1);            // scatter sample is get3d's (base + 0, 1)
+        float sampled;
+        wo = spec_generate(M, n, wi, rng_u(P.key, base + 0), rng_u(P.key, base + 1), sampled);
+        pdf = spec_value(M, n, wi, wo);
+        if (sampled > 0.0f) pdf = sampled;              // path.cpp:82
+        const f3 bsdf = spec_eval(M, n, wi, wo);
         beta_next = P.beta * (rcp(pdf) * bsdf);
     }
-    // origin of the next ray: off the surface on the side it leaves (path.cpp:91-93, 99);
-    // equal to the NEE origin whenever NEE runs (phong's pdf > 0 means dot(n, wo) > 0)
-    const f3 origin = (!MATS || lamb || dot(n, wo) > 0.0f) ? p + kEps * n : p - kEps * n;
+    P.term = pdf == 0.0f;
+    if (P.term && !nee) return true;
+    // origin of the next ray: off the surface on the side it leaves (path.cpp:91-93, 99)
+    const f3 nee_o = p + kEps * n;
+    const f3 origin = (!MATS || lamb || dot(n, wo) > 0.0f) ? nee_o : p - kEps * n;
     P.nxt_d = wo;
+    if constexpr (MATS) P.nxt_o = origin;
     // next-event estimation (path.cpp:38-77); not from dielectrics (path.cpp:40)
-    const int nl = S.n_lights;
-    int idx = (int)(rng_u(P.key, base + 3) * (float)nl);
-    if (idx == nl) idx -= 1;
-    if (idx >= 0 && !diel) {
+    if (nee) {
         const int lref = S.lights[idx];
         f3 ln;
         int lmat;
-        const f3 nee_o = p + kEps * n;
         const f3 tl = prim_sample(S, lref, nee_o, rng_u(P.key, base + 4), rng_u(P.key, base + 5), ln, lmat);
         const float dist2 = len2(tl);
         const f3 tu = rlen(tl) * tl;
@@ -576,10 +643,10 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
             const float light_pdf = fdiv(prim_pdf(S, lref, p, h.t, n, tu) * dist2, fabsf(cos_lo));
             // eval_bsdf toward the light; only the non-specular bsdf gets the cosine (path.cpp:61-62)
             const bool l = !MATS || lamb;
-            const f3 f = l ? cos_wi * (kInvPi * xyz(m0)) : phong_eval(xyz(m0), xyz(m1), m1.w, n, wi, tu);
-            const float bsdf_pdf = l ? fmaxf(cos_wi, 0.0f) * kInvPi : cosine_power_value(n, wi, m1.w, tu);
+            const f3 f = l ? cos_wi * (kInvPi * xyz(m0)) : spec_eval(M, n, wi, tu);
+            const float bsdf_pdf = l ? fmaxf(cos_wi, 0.0f) * kInvPi : spec_value(M, n, wi, tu);
             const float wgt = mi_weight(light_pdf, bsdf_pdf);
-            const float4 lm0 = S.mats[2 * lmat], lm1 = S.mats[2 * lmat + 1];
+            const float4 lm0 = S.mats[kMatStride * lmat], lm1 = S.mats[kMatStride * lmat + 1];
             if (f2i(lm0.w) == FRT_MAT_DIFFUSE_LIGHT && dot(ln, tu) < 0.0f)
                 P.nee = fdiv(wgt, light_pdf) * (P.beta * (xyz(lm1) * f));
         }
@@ -587,7 +654,7 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
         P.shadow = true;
         ++n_sh;
     }
-    P.prev_spec = MATS && !lamb;
+    P.prev_spec = MATS && mat_no_mis(mtype);
     P.beta = beta_next;
     P.prev_p = p;
     P.prev_pdf = pdf;
@@ -623,7 +690,7 @@ FRT_HD bool ao_shade(PathState &P, const DevScene &S, const Hit &h, uint32_t &n_
     f3 n;
     int mat;
     prim_shade(S, h.prim, P.ro, p, h.u, h.v, n, mat);
-    const float4 m0 = S.mats[2 * mat], m1 = S.mats[2 * mat + 1];
+    const float4 m0 = S.mats[kMatStride * mat], m1 = S.mats[kMatStride * mat + 1];
     const int mtype = f2i(m0.w);
     const uint32_t base = dim_bounce(0);
     const float u0 = rng_u(P.key, base + 6), u1 = rng_u(P.key, base + 7);
@@ -634,6 +701,10 @@ FRT_HD bool ao_shade(PathState &P, const DevScene &S, const Hit &h, uint32_t &n_
         wo = cosine_power_generate(n, -normalize(P.rd), m1.w, u0, u1);
     } else if (MATS && mtype == FRT_MAT_DIELECTRIC) {
         wo = dielectric_generate(n, -normalize(P.rd), m1.w, u0);
+    } else if (MATS && mtype == FRT_MAT_ROUGH_CONDUCTOR) {   // pdf.h:465-482 (metal is refused at launch)
+        const float4 m2 = S.mats[kMatStride * mat + 2];
+        float unused;
+        wo = rough_generate(n, -normalize(P.rd), m1.w, f2i(m2.w), u0, u1, unused);
     } else {
         return true;                                    // no scatter (diffuse_light)
     }

@@ -87,7 +87,7 @@ __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
     float4 *l4 = reinterpret_cast<float4 *>(lds_base);
     const DevScene S0 = S;
     const int nn = WIDE ? 4 * S0.n_nodes4 : 4 * S0.n_nodes;
-    const int nt = 3 * S0.n_tris, ns = 2 * S0.n_tris, nm = 2 * S0.n_mats;
+    const int nt = 3 * S0.n_tris, ns = 2 * S0.n_tris, nm = kMatStride * S0.n_mats;
     if constexpr (WIDE) {
         const float4 *src = reinterpret_cast<const float4 *>(S0.nodes4);
         for (int i = threadIdx.x; i < nn; i += kBlock) l4[(i & 3) * S0.n_nodes4 + (i >> 2)] = src[i];
@@ -152,10 +152,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             bool shadow_done = false;
             if (tracing && trav_step_world<WORLD, kBlock, STACK, SPEC>(T, S, P.ro, P.rd, P.shadow, stk, ovf)) {
                 if (KIND == FRT_INTEGRATOR_PATH && P.shadow) {   // finish the shadow ray here, keep traversing
-                    path_after_shadow(P, T.h.prim < 0);
-                    shadow_done = true;
-                    tracing = trav_begin_world<WORLD>(T, S, P.ro, P.rd, P.rtmax);
-                    pending = !tracing;
+                    if (path_after_shadow<MATS>(P, T.h.prim < 0)) {
+                        shadow_done = true;
+                        tracing = trav_begin_world<WORLD>(T, S, P.ro, P.rd, P.rtmax);
+                        pending = !tracing;
+                    } else {                                      // path ended (P.term): shade finishes it
+                        tracing = false;
+                        pending = true;
+                    }
                 } else {
                     tracing = false;
                     pending = true;
@@ -367,8 +371,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
             bool ext = false;
             if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, M.P.ro, M.P.rd, M.P.shadow, stk, ovf)) {
                 if (M.P.shadow) {               // finish the shadow ray here (mlt_shade's shadow branch)
-                    path_after_shadow(M.P, T.h.prim < 0);
-                    if (mlt_beyond(M)) {
+                    if (!path_after_shadow<MATS>(M.P, T.h.prim < 0)) {   // path ended (P.term)
+                        tracing = false;
+                        pending = true;
+                    } else if (mlt_beyond(M)) {
                         beyond = true;
                         tracing = false;
                         pending = true;
@@ -515,7 +521,8 @@ struct frt_ctx {
     bool has_bvh4 = false;
     int depth4 = 0;
     int n_tris = 0, n_spheres = 0;
-    bool has_spec_mats = false;   // modified_phong / dielectric present: kernels with the specular branch
+    bool has_spec_mats = false;   // a non-lambertian scattering material: kernels with the specular branch
+    bool has_metal = false;       // ao::Li cannot sample metal (constant_pdf::generate throws, pdf.h:195-198)
     size_t scene_lds_bytes = 0, scene_lds_bytes4 = 0;   // LDS copy with binary / 4-wide nodes
     double last_mlt_b = 0.0;
     std::vector<void *> scene_bufs;
@@ -803,9 +810,12 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     for (int i = 0; i < nm; ++i) {
         const int t = sv->materials[i].type;
         if (t != FRT_MAT_LAMBERTIAN && t != FRT_MAT_DIFFUSE_LIGHT && t != FRT_MAT_MODIFIED_PHONG &&
-            t != FRT_MAT_DIELECTRIC)
-            return fail(FRT_E_UNSUPPORTED, "material type " + std::to_string(t) +
-                                               " is not supported (lambertian, diffuse_light, modified_phong, dielectric)");
+            t != FRT_MAT_METAL && t != FRT_MAT_DIELECTRIC && t != FRT_MAT_ROUGH_CONDUCTOR)
+            return fail(FRT_E_UNSUPPORTED, "material type " + std::to_string(t) + " is not supported");
+        if (t == FRT_MAT_ROUGH_CONDUCTOR &&
+            (!(sv->materials[i].alpha > 0.0) || (sv->materials[i].distribution != FRT_DIST_GGX &&
+                                                  sv->materials[i].distribution != FRT_DIST_BECKMANN)))
+            return fail(FRT_E_INVALID, "rough_conductor needs alpha > 0 and a GGX / Beckmann distribution");
     }
     auto valid_ref = [&](int ref) {
         if (ref < 0) return false;
@@ -963,16 +973,18 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
         F.smat[k] = sv->sphere_material[k];
         if (F.smat[k] < 0 || F.smat[k] >= nm) return fail(FRT_E_INVALID, "scene view: bad sphere material");
     }
-    F.mats.resize(2 * (size_t)nm);
+    F.mats.assign(kMatStride * (size_t)nm, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     for (int i = 0; i < nm; ++i) {
         const frt_material &m = sv->materials[i];
-        // (albedo | kd, type) | (emit, -) for lights, (ks, exponent | ior) for phong / dielectric
-        F.mats[2 * i] = make_float4((float)m.albedo[0], (float)m.albedo[1], (float)m.albedo[2], i2f(m.type));
-        if (m.type == FRT_MAT_MODIFIED_PHONG || m.type == FRT_MAT_DIELECTRIC)
-            F.mats[2 * i + 1] = make_float4((float)m.specular[0], (float)m.specular[1], (float)m.specular[2],
-                                            (float)(m.type == FRT_MAT_MODIFIED_PHONG ? m.exponent : m.ior));
-        else
-            F.mats[2 * i + 1] = make_float4((float)m.emit[0], (float)m.emit[1], (float)m.emit[2], 0.0f);
+        float4 *d = &F.mats[kMatStride * i];
+        auto f4 = [](const double *v, float w) { return make_float4((float)v[0], (float)v[1], (float)v[2], w); };
+        // m0 = (albedo | kd | metal albedo | rough eta, type); m1 = (emit, -) for lights,
+        // (ks, exponent | ior | alpha) otherwise; m2 = (rough k, distribution)
+        d[0] = f4(m.type == FRT_MAT_ROUGH_CONDUCTOR ? m.eta : m.albedo, i2f(m.type));
+        if (m.type == FRT_MAT_DIFFUSE_LIGHT) d[1] = f4(m.emit, 0.0f);
+        else d[1] = f4(m.specular, (float)(m.type == FRT_MAT_MODIFIED_PHONG ? m.exponent
+                                           : m.type == FRT_MAT_DIELECTRIC ? m.ior : m.alpha));
+        d[2] = f4(m.k, i2f(m.distribution));
     }
     if (sv->n_lights < 0 || (sv->n_lights > 0 && !sv->lights)) return fail(FRT_E_INVALID, "scene view: bad lights");
     F.lights.resize(sv->n_lights);
@@ -1046,9 +1058,12 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
     c->n_tris = S.n_tris;
     c->n_spheres = (int)F.spheres.size();
     c->has_spec_mats = false;
-    for (int i = 0; i < sv->n_materials; ++i)
-        if (sv->materials[i].type == FRT_MAT_MODIFIED_PHONG || sv->materials[i].type == FRT_MAT_DIELECTRIC)
-            c->has_spec_mats = true;
+    c->has_metal = false;
+    for (int i = 0; i < sv->n_materials; ++i) {
+        const int t = sv->materials[i].type;
+        if (t != FRT_MAT_LAMBERTIAN && t != FRT_MAT_DIFFUSE_LIGHT) c->has_spec_mats = true;
+        if (t == FRT_MAT_METAL) c->has_metal = true;
+    }
     c->depth4 = F.depth4;
     c->scene_lds_bytes = sizeof(float4) * (F.nodes.size() + F.tris.size() + F.tshade.size() + F.mats.size());
     c->scene_lds_bytes4 = sizeof(float4) * (F.nodes4.size() + F.tris.size() + F.tshade.size() + F.mats.size());
@@ -1071,6 +1086,9 @@ extern "C" int frt_selftest_path_host(const frt_scene_view *sv, const frt_render
     std::string err;
     const int rc = flatten_scene(sv, F, err);
     if (rc != FRT_OK) return rc;
+    if (p->integrator == FRT_INTEGRATOR_AO)
+        for (int i = 0; i < sv->n_materials; ++i)
+            if (sv->materials[i].type == FRT_MAT_METAL) return FRT_E_UNSUPPORTED;
     DevScene S = F.meta;
     S.nodes = F.nodes.data(); S.nodes4 = F.nodes4.data(); S.tris = F.tris.data(); S.tshade = F.tshade.data(); S.tnorm = F.tnorm.data();
     S.spheres = F.spheres.data(); S.sphere_mat = F.smat.data(); S.mats = F.mats.data();
@@ -1446,6 +1464,8 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     if (!c->have_scene) return set_err(c, FRT_E_NO_SCENE, "no scene uploaded");
     HIPCHK(c, hipSetDevice(c->device));
     if (p->integrator == FRT_INTEGRATOR_PSSMLT) return render_mlt(c, p, dev_slots, st, stats);
+    if (p->integrator == FRT_INTEGRATOR_AO && c->has_metal)   // ao::Li -> constant_pdf::generate throws (pdf.h:195-198)
+        return set_err(c, FRT_E_UNSUPPORTED, "ao integrator: metal has no sampling pdf (constant_pdf::generate)");
     const int T = eff_tile(p);
     const int nmt = my_tiles(p);
     const uint32_t n_slots = (uint32_t)nmt * T * T;

@@ -22,6 +22,7 @@
 #include <fstream>
 #include <map>
 #include <memory>
+#include <new>
 #include <sstream>
 #include <string>
 #include <thread>
@@ -394,11 +395,13 @@ struct frt_host_scene {
     int32_t root = 0;
     int32_t world_kind = FRT_WORLD_BVH;
     std::vector<int32_t> list, lights;
+    std::vector<int32_t> world;   // world prims in insertion order (frt_scene_add_*)
     double cam[7][3] = {};   // origin, llc, horizontal, vertical, u, v, w
     double lens_radius = 0, half_height = 0;
     double env[3] = {0, 0, 0};
     int bvh_depth = 0;
     double load_ms = 0, build_ms = 0;
+    bool finished = true;    // false between frt_scene_new and frt_scene_finish
 
     int add_material(int type, V3 albedo, V3 emit, V3 specular = {}, double exponent = 0, double ior = 0)
     {
@@ -439,11 +442,75 @@ struct frt_host_scene {
 
 namespace {
 
-// mesh_loader::load_obj + create_triangle_mesh
-bool add_obj(frt_host_scene &s, const std::string &path, bool geo)
+// Matrix4x4 (geometry.h:919-1065), row-major double[16]: point transform with
+// the w divide (:966-983), Gauss-Jordan inverse with full pivoting
+// (Matrix::invert, :857-907), normal_transform = inverse-transpose product (:830-838)
+V3 mat4_point(const double *m, const double *v)
 {
+    const double x = m[0] * v[0] + m[1] * v[1] + m[2] * v[2] + m[3];
+    const double y = m[4] * v[0] + m[5] * v[1] + m[6] * v[2] + m[7];
+    const double z = m[8] * v[0] + m[9] * v[1] + m[10] * v[2] + m[11];
+    const double w = m[12] * v[0] + m[13] * v[1] + m[14] * v[2] + m[15];
+    if (w == 1.0) return {x, y, z};
+    return {x / w, y / w, z / w};
+}
+V3 mat4_normal(const double *inv, const double *v)
+{
+    return {inv[0] * v[0] + inv[4] * v[1] + inv[8] * v[2], inv[1] * v[0] + inv[5] * v[1] + inv[9] * v[2],
+            inv[2] * v[0] + inv[6] * v[1] + inv[10] * v[2]};
+}
+bool mat4_invert(const double *src, double *t)
+{
+    int indxc[4], indxr[4], ipiv[4] = {0, 0, 0, 0};
+    memcpy(t, src, 16 * sizeof(double));
+    for (int i = 0; i < 4; i++) {
+        int irow = -1, icol = -1;
+        double big = 0;
+        for (int j = 0; j < 4; j++) {
+            if (ipiv[j] == 1) continue;
+            for (int k = 0; k < 4; k++) {
+                if (ipiv[k] == 0) {
+                    if (std::fabs(t[4 * j + k]) >= big) { big = std::fabs(t[4 * j + k]); irow = j; icol = k; }
+                } else if (ipiv[k] > 1) {
+                    return false;
+                }
+            }
+        }
+        ++ipiv[icol];
+        if (irow != icol)
+            for (int k = 0; k < 4; ++k) std::swap(t[4 * irow + k], t[4 * icol + k]);
+        indxr[i] = irow;
+        indxc[i] = icol;
+        if (t[4 * icol + icol] == 0) return false;
+        const double pivinv = 1.0 / t[4 * icol + icol];
+        t[4 * icol + icol] = 1.0;
+        for (int j = 0; j < 4; j++) t[4 * icol + j] *= pivinv;
+        for (int j = 0; j < 4; j++) {
+            if (j == icol) continue;
+            const double save = t[4 * j + icol];
+            t[4 * j + icol] = 0;
+            for (int k = 0; k < 4; k++) t[4 * j + k] -= t[4 * icol + k] * save;
+        }
+    }
+    for (int j = 3; j >= 0; j--)
+        if (indxr[j] != indxc[j])
+            for (int k = 0; k < 4; k++) std::swap(t[4 * k + indxr[j]], t[4 * k + indxc[j]]);
+    return true;
+}
+
+// mesh_loader::load_obj + create_triangle_mesh (triangle.cpp:9-23), and its
+// (file, toWorld, bsdf) overload (triangle.cpp:26-60): every mesh of the file
+// takes `bsdf` when given (one material object for all of them), vertices go
+// through toWorld and normals through its inverse transpose.  Emissive meshes
+// join Scene::lights.  Returns FRT_OK, FRT_E_IO or FRT_E_INVALID (singular matrix).
+int add_obj(frt_host_scene &s, const std::string &path, bool geo, const double *to_world = nullptr,
+            const frt_material *bsdf = nullptr)
+{
+    double inv[16];
+    if (to_world && !mat4_invert(to_world, inv)) return FRT_E_INVALID;
     ObjData od;
-    if (!parse_obj(path, od)) return false;
+    if (!parse_obj(path, od)) return FRT_E_IO;
+    int shared_mat = -1;
     for (const ObjMesh &m : od.meshes) {
         const size_t nf = m.v.size() / 3;
         if (nf == 0) continue;  // Assimp drops empty meshes
@@ -469,7 +536,17 @@ bool add_obj(frt_host_scene &s, const std::string &path, bool geo)
             type = FRT_MAT_LAMBERTIAN;
             albedo = {from_srgb(mt->kd[0]), from_srgb(mt->kd[1]), from_srgb(mt->kd[2])};
         }
-        const int mat = s.add_material(type, albedo, emit, spec, exponent, ior);
+        int mat;
+        if (bsdf) {                                   // mesh->mat.reset(bsdf)
+            if (shared_mat < 0) {
+                s.mats.push_back(*bsdf);
+                shared_mat = (int)s.mats.size() - 1;
+            }
+            mat = shared_mat;
+            type = bsdf->type;
+        } else {
+            mat = s.add_material(type, albedo, emit, spec, exponent, ior);
+        }
         bool has_vn = true;
         for (int x : m.vn) if (x < 0) { has_vn = false; break; }
         std::vector<float> cn;
@@ -489,6 +566,13 @@ bool add_obj(frt_host_scene &s, const std::string &path, bool geo)
                     v[3 * k + d] = od.v[3 * m.v[3 * f + k] + d];
                     n[3 * k + d] = cn[3 * (3 * f + k) + d];
                 }
+            if (to_world) {
+                for (int k = 0; k < 3; ++k) {
+                    const V3 pv = mat4_point(to_world, v + 3 * k), nv = mat4_normal(inv, n + 3 * k);
+                    v[3 * k] = pv.x; v[3 * k + 1] = pv.y; v[3 * k + 2] = pv.z;
+                    n[3 * k] = nv.x; n[3 * k + 1] = nv.y; n[3 * k + 2] = nv.z;
+                }
+            }
             s.tri_v.insert(s.tri_v.end(), v, v + 9);
             s.tri_n.insert(s.tri_n.end(), n, n + 9);
             const V3 e1{v[3] - v[0], v[4] - v[1], v[5] - v[2]}, e2{v[6] - v[0], v[7] - v[1], v[8] - v[2]};
@@ -496,9 +580,10 @@ bool add_obj(frt_host_scene &s, const std::string &path, bool geo)
             s.tri_mat.push_back(mat);
             s.tri_geo.push_back(geo ? 1 : 0);
             if (type == FRT_MAT_DIFFUSE_LIGHT) s.lights.push_back(base + (int)f);
+            s.world.push_back(base + (int)f);
         }
     }
-    return true;
+    return FRT_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -647,11 +732,11 @@ extern "C" int frt_scene_create(const char *kind, const char *obj_path, double a
     const std::string k = kind;
     const auto t0 = std::chrono::steady_clock::now();
     if (k == "cornell_box_obj" || k == "obj_geo" || k == "obj_smooth") {
-        if (!add_obj(*s, obj_path, k != "obj_smooth")) return FRT_E_IO;
+        if (const int rc = add_obj(*s, obj_path, k != "obj_smooth")) return rc;
         s->world_kind = FRT_WORLD_BVH;
         s->set_camera({0, 1, (double)3.9f}, {0, 1, 0}, {0, 1, 0}, 40.0, aspect, 0.0, 10.0);  // main.cpp:236-242
     } else if (k == "veach_mis") {
-        if (!add_obj(*s, obj_path, false)) return FRT_E_IO;
+        if (const int rc = add_obj(*s, obj_path, false)) return rc;
         // main.cpp:292-302: five emissive spheres in the world list, and five
         // separate identical sphere objects in Scene::lights
         const double cx[5] = {10, (double)-1.25f, (double)-3.75f, (double)1.25f, (double)3.75f};
@@ -686,9 +771,81 @@ extern "C" int frt_scene_create(const char *kind, const char *obj_path, double a
     return FRT_OK;
 }
 
+// ---- incremental construction (what main.cpp's scene functions do) ----
+extern "C" int frt_scene_new(frt_host_scene **out)
+{
+    if (!out) return FRT_E_INVALID;
+    *out = new (std::nothrow) frt_host_scene();
+    if (!*out) return FRT_E_INVALID;
+    (*out)->finished = false;
+    return FRT_OK;
+}
+
+static bool material_ok(const frt_material *m)
+{
+    if (!m) return false;
+    switch (m->type) {
+    case FRT_MAT_LAMBERTIAN: case FRT_MAT_DIFFUSE_LIGHT: case FRT_MAT_MODIFIED_PHONG: case FRT_MAT_METAL:
+    case FRT_MAT_DIELECTRIC: return true;
+    case FRT_MAT_ROUGH_CONDUCTOR:
+        return m->alpha > 0.0 && (m->distribution == FRT_DIST_GGX || m->distribution == FRT_DIST_BECKMANN);
+    default: return false;
+    }
+}
+
+extern "C" int frt_scene_add_obj(frt_host_scene *s, const char *obj_path, const double *to_world16,
+                                 const frt_material *bsdf, int use_geometry_normals)
+{
+    if (!s || !obj_path || s->finished || (bsdf && !material_ok(bsdf))) return FRT_E_INVALID;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = add_obj(*s, obj_path, use_geometry_normals != 0, to_world16, bsdf);
+    s->load_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
+extern "C" int frt_scene_add_sphere(frt_host_scene *s, const double *center, double radius, const frt_material *m,
+                                    int where)
+{
+    if (!s || !center || s->finished || !material_ok(m) || !(where & FRT_SPHERE_BOTH)) return FRT_E_INVALID;
+    s->mats.push_back(*m);
+    const int id = s->add_sphere({center[0], center[1], center[2]}, radius, (int)s->mats.size() - 1);
+    if (where & FRT_SPHERE_WORLD) s->world.push_back(FRT_PRIM_SPHERE | id);
+    if (where & FRT_SPHERE_LIGHTS) s->lights.push_back(FRT_PRIM_SPHERE | id);
+    return FRT_OK;
+}
+
+extern "C" int frt_scene_set_camera(frt_host_scene *s, const double *lookfrom, const double *lookat, const double *vup,
+                                    double vfov, double aspect, double aperture, double focus_dist)
+{
+    if (!s || !lookfrom || !lookat || !vup) return FRT_E_INVALID;
+    s->set_camera({lookfrom[0], lookfrom[1], lookfrom[2]}, {lookat[0], lookat[1], lookat[2]}, {vup[0], vup[1], vup[2]},
+                  vfov, aspect, aperture, focus_dist);
+    return FRT_OK;
+}
+
+extern "C" int frt_scene_set_env(frt_host_scene *s, const double *rgb)
+{
+    if (!s || !rgb) return FRT_E_INVALID;
+    for (int k = 0; k < 3; ++k) s->env[k] = rgb[k];
+    return FRT_OK;
+}
+
+extern "C" int frt_scene_finish(frt_host_scene *s, int world_kind)
+{
+    if (!s || s->finished || (world_kind != FRT_WORLD_BVH && world_kind != FRT_WORLD_LIST) || s->world.empty())
+        return FRT_E_INVALID;
+    const auto t0 = std::chrono::steady_clock::now();
+    s->world_kind = world_kind;
+    if (world_kind == FRT_WORLD_BVH) build_bvh(*s, s->world);
+    else s->list = s->world;
+    s->finished = true;
+    s->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return FRT_OK;
+}
+
 extern "C" int frt_scene_view_get(const frt_host_scene *s, frt_scene_view *v)
 {
-    if (!s || !v) return FRT_E_INVALID;
+    if (!s || !v || !s->finished) return FRT_E_INVALID;
     memset(v, 0, sizeof(*v));
     v->world_kind = s->world_kind;
     v->n_tris = (int32_t)s->tri_mat.size();

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FRT_ABI_VERSION 3
+#define FRT_ABI_VERSION 4
 
 enum {
     FRT_OK = 0,
@@ -43,7 +43,10 @@ enum { FRT_WORLD_BVH = 0, FRT_WORLD_LIST = 1 };          /* parallel_bvh_node | 
 enum { FRT_MAT_LAMBERTIAN = 0,      /* material.h:50-73                                  */
        FRT_MAT_DIFFUSE_LIGHT = 1,   /* material.h:179-192                                */
        FRT_MAT_MODIFIED_PHONG = 2,  /* material.h:75-108 + cosine_power_pdf (pdf.h:99)   */
-       FRT_MAT_DIELECTRIC = 4 };    /* material.h:133-177 + dielectric_pdf (pdf.h:138)   */
+       FRT_MAT_METAL = 3,           /* material.h:110-130 + constant_pdf (pdf.h:186)     */
+       FRT_MAT_DIELECTRIC = 4,      /* material.h:133-177 + dielectric_pdf (pdf.h:138)   */
+       FRT_MAT_ROUGH_CONDUCTOR = 5 };/* material.h:246-315 + roughconductor_pdf (pdf.h:231) */
+enum { FRT_DIST_GGX = 0, FRT_DIST_BECKMANN = 1 };   /* microfacet_distributions (util.h:48-52) */
 enum { FRT_INTEGRATOR_PATH = 0,     /* path::Li           path.h:8-18, path.cpp:4-116      */
        FRT_INTEGRATOR_PSSMLT = 1,   /* pssmlt             pssmlt.h:29-76                   */
        FRT_INTEGRATOR_AO = 2,       /* ao::Li             ao.h:8-43, ao.cpp:4-27           */
@@ -62,12 +65,16 @@ enum { FRT_FLAG_NO_LDS_SCENE = 1,      /* render_params.flags: keep small scenes
 
 typedef struct frt_material {
     int32_t type;            /* FRT_MAT_*                                                 */
-    int32_t reserved;
-    double albedo[3];        /* lambertian albedo / modified_phong diffuse_reflectance    */
+    int32_t distribution;    /* rough_conductor: FRT_DIST_GGX / FRT_DIST_BECKMANN         */
+    double albedo[3];        /* lambertian albedo / modified_phong diffuse_reflectance /
+                                metal albedo                                              */
     double emit[3];          /* diffuse_light: constant_texture colour                    */
-    double specular[3];      /* modified_phong / dielectric: specular_reflectance         */
+    double specular[3];      /* modified_phong / dielectric / rough_conductor:
+                                specular_reflectance (constant texture)                   */
     double exponent;         /* modified_phong: specular_exponent                         */
     double ior;              /* dielectric: ref_idx                                       */
+    double alpha;            /* rough_conductor: roughness (alphaU = alphaV)              */
+    double eta[3], k[3];     /* rough_conductor: complex IOR (fresnelConductorExact)      */
 } frt_material;
 
 typedef struct frt_scene_view {
@@ -195,6 +202,33 @@ typedef struct frt_host_scene_info {
  *       "obj_geo" / "obj_smooth" (any OBJ, cornell camera, geometric / vertex normals) */
 int frt_scene_create(const char *kind, const char *obj_path, double aspect, frt_host_scene **out);
 int frt_scene_view_get(const frt_host_scene *s, frt_scene_view *view);
+
+/* Incremental construction, what main.cpp's scene functions do (e.g.
+ * veach_ajar main.cpp:318-412, glass_of_water :414-480): OBJ files through
+ * create_triangle_mesh(file, toWorld, bsdf, lights, use_geometry_normals)
+ * (triangle.cpp:26-60), spheres, the camera, then parallel_bvh_node::create_bvh
+ * or a hitable_list over the world prims in insertion order.
+ *   frt_scene_new -> frt_scene_add_obj / _add_sphere ... -> frt_scene_set_camera
+ *   -> frt_scene_finish -> frt_scene_view_get
+ * add_obj: to_world16 = row-major Matrix4x4 or NULL (identity); bsdf = the one
+ * material every mesh of the file takes, or NULL for the file's MTL materials
+ * (mesh_loader.cpp:59-112); meshes whose material is a diffuse_light join
+ * Scene::lights.  Returns FRT_E_IO (unreadable file) or FRT_E_INVALID (singular
+ * matrix, bad material). */
+enum { FRT_SPHERE_WORLD = 1, FRT_SPHERE_LIGHTS = 2, FRT_SPHERE_BOTH = 3 };
+int frt_scene_new(frt_host_scene **out);
+int frt_scene_add_obj(frt_host_scene *s, const char *obj_path, const double *to_world16, const frt_material *bsdf,
+                      int use_geometry_normals);
+/* where: FRT_SPHERE_WORLD (the world list), FRT_SPHERE_LIGHTS (a separate
+ * Scene::lights object, as veach_mis main.cpp:298-302 does), or both (one object) */
+int frt_scene_add_sphere(frt_host_scene *s, const double *center, double radius, const frt_material *m, int where);
+/* camera.h:10-28; the reference constructs every scene's camera this way */
+int frt_scene_set_camera(frt_host_scene *s, const double *lookfrom, const double *lookat, const double *vup,
+                         double vfov, double aspect, double aperture, double focus_dist);
+/* environment_map with a constant texture (material.h:206-232) */
+int frt_scene_set_env(frt_host_scene *s, const double *rgb);
+/* world_kind FRT_WORLD_BVH (create_bvh) or FRT_WORLD_LIST */
+int frt_scene_finish(frt_host_scene *s, int world_kind);
 int frt_scene_info(const frt_host_scene *s, frt_host_scene_info *info);
 void frt_scene_destroy(frt_host_scene *s);
 

@@ -204,6 +204,13 @@ static inline double cosine_pdf_value(v3 w, v3 direction)
     return cosine / (double)M_PI;
 }
 
+enum { MAT_LAMBERT = 0, MAT_LIGHT = 1, MAT_PHONG = 2, MAT_METAL = 3, MAT_DIELECTRIC = 4,
+       MAT_ROUGH = 5 };                                                      /* = FRT_MAT_* */
+enum { DIST_GGX = 0, DIST_BECKMANN = 1 };                                     /* util.h:48-52 */
+/* albedo: lambertian / modified_phong diffuse / metal albedo; ks: specular
+ * reflectance (phong, dielectric, rough_conductor's constant texture) */
+typedef struct { int type; v3 albedo; v3 emit; double ks[3], ior, shininess; int dist; double alpha; v3 eta, k; } material;
+
 /* ---- specular materials (material.h:75-171, pdf.h:99-184, util.h:73-117) ---- */
 static const double DELTA_EPSILON = 1e-3f;                                   /* util.h:12 */
 static inline v3 ref_reflect(v3 v, v3 n)                                     /* util.h:73-76 */
@@ -289,6 +296,287 @@ static inline v3 dielectric_eval(const double ks[3], double ior, v3 n, v3 wi, v3
     return mk(ks[0] * factor * factor * (1 - F), ks[1] * factor * factor * (1 - F), ks[2] * factor * factor * (1 - F));
 }
 
+/* ---- metal (material.h:110-130) ---- */
+/* metal::scatter: reflect(unit(r_in.d), n) (util.h:73-76); constant_pdf(1)
+ * (pdf.h:186-201); eval_bsdf = albedo */
+
+/* ---- rough_conductor (material.h:246-315), roughconductor_pdf (pdf.h:231-486,
+ *      pdf.cpp:5-12), microfacet.h; isotropic (alphaU = alphaV = alpha) ---- */
+static inline double safe_sqrt1(double v) { return std_max(0.0, sqrt(v)); }       /* util.h:43-46 */
+static inline v3 safe_sqrt3(v3 v)                                                 /* geometry.h:451-460 */
+{
+    return mk(std_max(0.0, sqrt(v.e[0])), std_max(0.0, sqrt(v.e[1])), std_max(0.0, sqrt(v.e[2])));
+}
+static inline v3 vdiv(v3 a, v3 b) { return mk(a.e[0] / b.e[0], a.e[1] / b.e[1], a.e[2] / b.e[2]); }
+static inline v3 vsplat(double x) { return mk(x, x, x); }
+static inline double hypot2(double a, double b)                                   /* util.h:239-254 */
+{
+    double r;
+    if (fabs(a) > fabs(b)) { r = b / a; r = fabs(a) * sqrt(1.0 + r * r); }
+    else if (b != 0.0) { r = a / b; r = fabs(b) * sqrt(1.0 + r * r); }
+    else r = 0.0;
+    return r;
+}
+static inline double erfinv(double x)                                             /* util.h:185-214 */
+{
+    double w = -log(((double)1 - x) * ((double)1 + x));
+    double p;
+    if (w < (double)5) {
+        w = w - (double)2.5;
+        p = (double)2.81022636e-08;
+        p = (double)3.43273939e-07 + p * w;
+        p = (double)-3.5233877e-06 + p * w;
+        p = (double)-4.39150654e-06 + p * w;
+        p = (double)0.00021858087 + p * w;
+        p = (double)-0.00125372503 + p * w;
+        p = (double)-0.00417768164 + p * w;
+        p = (double)0.246640727 + p * w;
+        p = (double)1.50140941 + p * w;
+    } else {
+        w = sqrt(w) - (double)3;
+        p = (double)-0.000200214257;
+        p = (double)0.000100950558 + p * w;
+        p = (double)0.00134934322 + p * w;
+        p = (double)-0.00367342844 + p * w;
+        p = (double)0.00573950773 + p * w;
+        p = (double)-0.0076224613 + p * w;
+        p = (double)0.00943887047 + p * w;
+        p = (double)1.00167406 + p * w;
+        p = (double)2.83297682 + p * w;
+    }
+    return p * x;
+}
+static inline double erf_(double x)                                               /* util.h:216-236 */
+{
+    const double a1 = 0.254829592, a2 = -0.284496736, a3 = 1.421413741, a4 = -1.453152027, a5 = 1.061405429,
+                 pp = 0.3275911;
+    const double sign = copysignf(1.0f, (float)x);
+    x = fabs(x);
+    const double t = 1.0 / (1.0 + pp * x);
+    const double y = 1.0 - (((((a5 * t + a4) * t) + a3) * t + a2) * t + a1) * t * exp(-x * x);
+    return sign * y;
+}
+/* util.h:139-148: sincos of a double through sinf / cosf.  (Under _GNU_SOURCE,
+ * util.h:134-136 makes sincos(double) call itself and never return; this is
+ * the reference's other configuration, see oracle/ref_kat_conductor.cpp.) */
+static inline void sincos_f(double theta, double *sn, double *cs)
+{
+    *sn = sinf((float)theta);
+    *cs = cosf((float)theta);
+}
+static inline v3 onb_to_local(const onb *b, v3 a)                                 /* onb.h:17 */
+{
+    return mk(dot(a, b->axis[0]), dot(a, b->axis[1]), dot(a, b->axis[2]));
+}
+/* microfacet::fresnelConductorExact (microfacet.h:8-31) */
+static inline v3 fresnel_conductor_exact(double cosThetaI, v3 eta, v3 k)
+{
+    const double cosThetaI2 = cosThetaI * cosThetaI, sinThetaI2 = 1 - cosThetaI2, sinThetaI4 = sinThetaI2 * sinThetaI2;
+    const v3 temp1 = vsub(vsub(vmul(eta, eta), vmul(k, k)), vsplat(sinThetaI2));
+    const v3 a2pb2 = safe_sqrt3(vadd(vmul(temp1, temp1), smul(4, vmul(vmul(vmul(k, k), eta), eta))));
+    const v3 a = safe_sqrt3(smul(0.5, vadd(a2pb2, temp1)));
+    const v3 term1 = vadd(a2pb2, vsplat(cosThetaI2)), term2 = smul(2 * cosThetaI, a);
+    const v3 Rs2 = vdiv(vsub(term1, term2), vadd(term1, term2));
+    const v3 term3 = vadd(smul(cosThetaI2, a2pb2), vsplat(sinThetaI4)), term4 = smul(sinThetaI2, term2);
+    const v3 Rp2 = vdiv(vmul(Rs2, vsub(term3, term4)), vadd(term3, term4));
+    return smul(0.5, vadd(Rp2, Rs2));
+}
+/* microfacet::smithG1 (microfacet.h:48-88); projectRoughness returns alpha
+ * for the isotropic case (microfacet.h:33-46) */
+static inline double smith_g1(v3 v, v3 m, v3 n, double alpha, int dist)
+{
+    const double cosTheta = dot(n, v);
+    if (dot(v, m) * cosTheta <= 0) return 0.0;
+    const double temp = 1 - (cosTheta * cosTheta);
+    if (temp <= 0.0) return 1.0;
+    const double tanTheta = sqrt(temp) / cosTheta;
+    if (dist == DIST_BECKMANN) {
+        const double a = 1.0 / (alpha * tanTheta);
+        if (a >= 1.6f) return 1.0;
+        const double aSqr = a * a;
+        return ((double)3.535f * a + (double)2.181f * aSqr) / (1.0 + (double)2.276f * a + (double)2.577f * aSqr);
+    }
+    const double root = alpha * tanTheta;
+    return 2.0 / (1.0 + hypot2(1.0, root));
+}
+/* microfacet::eval (microfacet.h:90-135) */
+static inline double microfacet_d(v3 m, v3 n, double alpha, int dist)
+{
+    const onb b = onb_from_w(n);
+    const v3 ml = onb_to_local(&b, m);
+    const double cosTheta = ml.e[2];
+    if (cosTheta <= 0) return 0.0;
+    const double cosTheta2 = cosTheta * cosTheta;
+    const double be = ((ml.e[0] * ml.e[0]) / (alpha * alpha) + (ml.e[1] * ml.e[1]) / (alpha * alpha)) / cosTheta2;
+    double result;
+    if (dist == DIST_BECKMANN) {
+        result = exp(-be) / (M_PI * alpha * alpha * cosTheta2 * cosTheta2);
+    } else {
+        const double root = ((double)1 + be) * cosTheta2;
+        result = (double)1 / (M_PI * alpha * alpha * root * root);
+    }
+    if (result * cosTheta < (double)1e-20f) result = 0;
+    return result;
+}
+/* roughconductor_pdf::sampleVisible11 (pdf.h:280-397) */
+static void sample_visible11(double thetaI, double sx, double sy, int dist, double *slope_x, double *slope_y)
+{
+    const double SQRT_PI_INV = 1 / sqrt(M_PI);
+    if (dist == DIST_BECKMANN) {
+        if (thetaI < 1e-4f) {
+            double sinPhi, cosPhi;
+            const double r = sqrt(-log(1.0 - sx));
+            sincos_f(2 * M_PI * sy, &sinPhi, &cosPhi);
+            *slope_x = r * cosPhi; *slope_y = r * sinPhi;
+            return;
+        }
+        const double tanThetaI = tan(thetaI), cotThetaI = 1 / tanThetaI;
+        double a = -1, c = erf_(cotThetaI);
+        const double sample_x = std_max(sx, (double)1e-6f);
+        const double fit = 1 + thetaI * ((double)-0.876f + thetaI * ((double)0.4265f - (double)0.0594f * thetaI));
+        double b = c - (1 + c) * pow(1 - sample_x, fit);
+        const double normalization = 1 / (1 + c + SQRT_PI_INV * tanThetaI * exp(-cotThetaI * cotThetaI));
+        int it = 0;
+        while (++it < 10) {
+            if (!(b >= a && b <= c)) b = 0.5 * (a + c);
+            const double invErf = erfinv(b);
+            const double value = normalization * (1 + b + SQRT_PI_INV * tanThetaI * exp(-invErf * invErf)) - sample_x;
+            const double derivative = normalization * (1 - invErf * tanThetaI);
+            if (fabs(value) < 1e-5f) break;
+            if (value > 0) c = b; else a = b;
+            b -= value / derivative;
+        }
+        *slope_x = erfinv(b);
+        *slope_y = erfinv(2.0 * std_max(sy, (double)1e-6f) - 1.0);
+        return;
+    }
+    if (thetaI < 1e-4f) {
+        double sinPhi, cosPhi;
+        const double r = safe_sqrt1(sx / (1 - sx));
+        sincos_f(2 * M_PI * sy, &sinPhi, &cosPhi);
+        *slope_x = r * cosPhi; *slope_y = r * sinPhi;
+        return;
+    }
+    const double tanThetaI = tan(thetaI);
+    const double a = 1 / tanThetaI;
+    const double G1 = 2.0 / (1.0 + safe_sqrt1(1.0 + 1.0 / (a * a)));
+    double A = 2.0 * sx / G1 - 1.0;
+    if (fabs(A) == 1) A -= (double)copysignf(1.0f, (float)A) * EPSILON;
+    const double tmp = 1.0 / (A * A - 1.0);
+    const double B = tanThetaI;
+    const double D = safe_sqrt1(B * B * tmp * tmp - (A * A - B * B) * tmp);
+    const double slope_x_1 = B * tmp - D, slope_x_2 = B * tmp + D;
+    *slope_x = (A < 0.0 || slope_x_2 > 1.0 / tanThetaI) ? slope_x_1 : slope_x_2;
+    double S;
+    if (sy > 0.5) { S = 1.0; sy = 2.0 * (sy - 0.5); }
+    else { S = -1.0; sy = 2.0 * (0.5 - sy); }
+    const double z = (sy * (sy * (sy * (-(double)0.365728915865723) + (double)0.790235037209296) -
+                            (double)0.424965825137544) + (double)0.000152998850436920) /
+                     (sy * (sy * (sy * (sy * (double)0.169507819808272 - (double)0.397203533833404) -
+                                  (double)0.232500544458471) + (double)1) - (double)0.539825872510702);
+    *slope_y = S * z * sqrt(1.0 + *slope_x * *slope_x);
+}
+/* roughconductor_pdf::sampleVisible (pdf.h:409-455), local frame */
+static v3 sample_visible(v3 wi_l, double sx, double sy, double alpha, int dist)
+{
+    const v3 wi = unit(mk(alpha * wi_l.e[0], alpha * wi_l.e[1], wi_l.e[2]));
+    double theta = 0, phi = 0;
+    if (wi.e[2] < (double)0.99999) {
+        theta = acos(wi.e[2]);
+        phi = atan2(wi.e[1], wi.e[0]);
+    }
+    double sinPhi, cosPhi;
+    sincos_f(phi, &sinPhi, &cosPhi);
+    double slx, sly;
+    sample_visible11(theta, sx, sy, dist, &slx, &sly);
+    if (!isfinite(slx)) slx = 0.0;
+    const double rx = cosPhi * slx - sinPhi * sly, ry = sinPhi * slx + cosPhi * sly;
+    slx = rx * alpha;
+    sly = ry * alpha;
+    const double normalization = (double)1 / sqrt(slx * slx + sly * sly + (double)1.0);
+    return mk(-slx * normalization, -sly * normalization, normalization);
+}
+/* roughconductor_pdf::pdfVisible (pdf.cpp:5-12) */
+static inline double pdf_visible(const onb *uvw, v3 wi_l, v3 m_l, v3 n, double alpha, int dist)
+{
+    const double cosTheta = wi_l.e[2];
+    if (cosTheta == 0) return 0.0;
+    const v3 mw = onb_from_local(uvw, m_l);
+    return smith_g1(onb_from_local(uvw, wi_l), mw, n, alpha, dist) * fabs(dot(wi_l, m_l)) *
+           microfacet_d(mw, n, alpha, dist) / fabs(cosTheta);
+}
+/* roughconductor_pdf::generate (pdf.h:465-482): wo and srec.sampled_pdf */
+static v3 rough_generate(v3 n, v3 wi, double alpha, int dist, double s0, double s1, double *sampled_pdf)
+{
+    const onb uvw = onb_from_w(n);
+    const v3 wi_l = onb_to_local(&uvw, wi);
+    const v3 m = sample_visible(wi_l, s0, s1, alpha, dist);
+    double pdf = pdf_visible(&uvw, wi_l, m, n, alpha, dist);
+    const v3 mw = onb_from_local(&uvw, m);
+    const v3 wo = ref_reflect(vneg(wi), mw);
+    pdf /= 4.0 * dot(wo, mw);
+    *sampled_pdf = pdf;
+    return wo;
+}
+/* roughconductor_pdf::value (pdf.h:237-250) */
+static inline double rough_value(v3 n, v3 wi, double alpha, int dist, v3 wo)
+{
+    if (dot(n, wo) <= 0 || dot(n, wi) <= 0) return 0.0;
+    const v3 H = unit(vadd(wo, wi));
+    const double e = microfacet_d(H, n, alpha, dist);
+    return e * smith_g1(wi, H, n, alpha, dist) / (4.0 * dot(wi, n));
+}
+/* rough_conductor::eval_bsdf (material.h:277-307) */
+static inline v3 rough_eval(const material *m, v3 n, v3 wi, v3 wo)
+{
+    const double cosWi = dot(wi, n);
+    if (cosWi <= 0 || dot(wo, n) <= 0) return mk(0.0, 0.0, 0.0);
+    const v3 H = unit(vadd(wo, wi));
+    const double D = microfacet_d(H, n, m->alpha, m->dist);
+    if (D == 0) return mk(0.0, 0.0, 0.0);
+    const v3 F = vmul(fresnel_conductor_exact(dot(wi, H), m->eta, m->k), vload(m->ks));
+    const double G = smith_g1(wi, H, n, m->alpha, m->dist) * smith_g1(wo, H, n, m->alpha, m->dist);
+    const double model = D * G / (4.0 * cosWi);
+    return smul(model, F);
+}
+
+/* ---- the specular materials behind one interface (path.cpp:78-95) ---- */
+static inline int mat_scatters(int t)
+{
+    return t == MAT_LAMBERT || t == MAT_PHONG || t == MAT_METAL || t == MAT_DIELECTRIC || t == MAT_ROUGH;
+}
+/* light hits after these return Le unweighted (path.cpp:18-22, pssmlt.cpp:168-172) */
+static inline int mat_no_mis(int t) { return t == MAT_PHONG || t == MAT_METAL || t == MAT_DIELECTRIC; }
+/* scatter's direction (srec.specular_ray.d) from the get3d sample, and srec.sampled_pdf */
+static inline v3 spec_generate(const material *m, v3 n, v3 wi, v3 rd, double s0, double s1, double *sampled_pdf)
+{
+    *sampled_pdf = -1.0;                                   /* scatter_record ctor (pdf.h:69) */
+    switch (m->type) {
+    case MAT_PHONG: return cosine_power_generate(n, wi, m->shininess, s0, s1);
+    case MAT_DIELECTRIC: return dielectric_generate(n, wi, m->ior, s0);
+    case MAT_METAL: return ref_reflect(unit(rd), n);       /* reflect(unit(r_in.d), n) */
+    default: return unit(rough_generate(n, wi, m->alpha, m->dist, s0, s1, sampled_pdf));
+    }
+}
+static inline double spec_value(const material *m, v3 n, v3 wi, v3 wo)   /* srec.pdf_ptr->value */
+{
+    switch (m->type) {
+    case MAT_PHONG: return cosine_power_value(n, wi, m->shininess, wo);
+    case MAT_DIELECTRIC: return dielectric_value(n, wi, m->ior, wo);
+    case MAT_METAL: return 1.0;
+    default: return rough_value(n, wi, m->alpha, m->dist, wo);
+    }
+}
+static inline v3 spec_eval(const material *m, v3 n, v3 wi, v3 wo)        /* eval_bsdf */
+{
+    switch (m->type) {
+    case MAT_PHONG: return phong_eval(m->albedo, m->ks, m->shininess, n, wi, wo);
+    case MAT_DIELECTRIC: return dielectric_eval(m->ks, m->ior, n, wi, wo);
+    case MAT_METAL: return m->albedo;
+    default: return rough_eval(m, n, wi, wo);
+    }
+}
+
 /* util.h:21-41 */
 static inline void random_in_unit_disk(double s0, double s1, double *ox, double *oy)
 {
@@ -338,8 +626,6 @@ static inline ray camera_get_ray(const camera *c, double s, double t, double l0,
 /* ------------------------------------------------------------------------ */
 /* scene                                                                    */
 /* ------------------------------------------------------------------------ */
-enum { MAT_LAMBERT = 0, MAT_LIGHT = 1, MAT_PHONG = 2, MAT_DIELECTRIC = 4 };   /* = FRT_MAT_* */
-typedef struct { int type; v3 albedo; v3 emit; double ks[3], ior, shininess; } material;
 
 typedef struct {
     v3 v0, v1, v2, e1, e2;      /* triangle.h:58-66 (edges from the fp64 vertices) */
@@ -580,7 +866,7 @@ static v3 Li(li_ctx *c, const ray *r, int depth, const hit_record *prev, double 
     if (world_hit(s, r, EPSILON, FLT_MAX, &hrec, c->cnt)) {
         v3 Le = mat_emitted(s, hrec.mat, r->d, hrec.normal);
         if ((Le.e[0] != 0.0) || (Le.e[1] != 0.0) || (Le.e[2] != 0.0)) {
-            if (depth == 0 || s->mats[prev->mat].type == MAT_PHONG || s->mats[prev->mat].type == MAT_DIELECTRIC)
+            if (depth == 0 || mat_no_mis(s->mats[prev->mat].type))
                 return Le;
             const double cos_wo = dot(hrec.normal, vneg(unit(r->d)));
             double distance_squared = vlen2(vsub(hrec.p, prev->p));
@@ -592,17 +878,16 @@ static v3 Li(li_ctx *c, const ray *r, int depth, const hit_record *prev, double 
         }
         const material *m = &s->mats[hrec.mat];
         /* lambertian / modified_phong / dielectric::scatter succeed; diffuse_light's fails (material.h) */
-        if (depth <= 33 && (m->type == MAT_LAMBERT || m->type == MAT_PHONG || m->type == MAT_DIELECTRIC)) {
+        if (depth <= 33 && mat_scatters(m->type)) {
             const uint32_t base = DIM_BOUNCE(depth);
             const int specular = m->type != MAT_LAMBERT;
             const v3 wi = vneg(unit(r->d));                   /* hrec.wi (triangle.h:108, sphere.h:47) */
-            /* scatter's get3d sample: phong / dielectric direction (material.h:83-88, 139-145) */
+            /* scatter's get3d sample: the specular direction (material.h:83-88, 117-119, 139-145, 262-268) */
             v3 spec_dir = mk(0, 0, 0);
-            if (m->type == MAT_PHONG)
-                spec_dir = cosine_power_generate(hrec.normal, wi, m->shininess, rng_u(c->key, base + 0),
-                                                 rng_u(c->key, base + 1));
-            else if (m->type == MAT_DIELECTRIC)
-                spec_dir = dielectric_generate(hrec.normal, wi, m->ior, rng_u(c->key, base + 0));
+            double sampled_pdf = -1.0;
+            if (specular)
+                spec_dir = spec_generate(m, hrec.normal, wi, r->d, rng_u(c->key, base + 0), rng_u(c->key, base + 1),
+                                         &sampled_pdf);
             const int index = pick_sample(rng_u(c->key, base + 3), s->nlights);
             if (index >= 0 && m->type != MAT_DIELECTRIC) {
                 hit_record lrec;
@@ -615,8 +900,7 @@ static v3 Li(li_ctx *c, const ray *r, int depth, const hit_record *prev, double 
                 if (!world_hit(s, &shadow, EPSILON, 1 - SHADOW_EPSILON, &lrec, c->cnt)) {
                     to_light = make_unit(to_light);
                     shadow.d = to_light;
-                    v3 surface_bsdf = specular ? phong_eval(m->albedo, m->ks, m->shininess, hrec.normal, wi, to_light)
-                                               : sdiv(m->albedo, M_PI);
+                    v3 surface_bsdf = specular ? spec_eval(m, hrec.normal, wi, to_light) : sdiv(m->albedo, M_PI);
                     const double cos_wi = dot(hrec.normal, unit(to_light));
                     const double cos_wo = dot(lrec.normal, vneg(unit(to_light)));
                     if (cos_wo != 0) {
@@ -625,8 +909,7 @@ static v3 Li(li_ctx *c, const ray *r, int depth, const hit_record *prev, double 
                         const double light_pdf = prim_pdf_direct(s, s->lights[index], &hrec, to_light)
                                                  * distance_squared / fabs(cos_wo);
                         const double surface_bsdf_pdf =
-                            specular ? cosine_power_value(hrec.normal, wi, m->shininess, to_light)
-                                     : cosine_pdf_value(hrec.normal, to_light);
+                            specular ? spec_value(m, hrec.normal, wi, to_light) : cosine_pdf_value(hrec.normal, to_light);
                         const double weight = miWeight(light_pdf, surface_bsdf_pdf);
                         v3 em = mat_emitted(s, lrec.mat, shadow.d, lrec.normal);
                         Le = vadd(Le, sdiv(smul(weight, vmul(em, surface_bsdf)), light_pdf));
@@ -634,12 +917,9 @@ static v3 Li(li_ctx *c, const ray *r, int depth, const hit_record *prev, double 
                 }
             }
             if (specular) {                                   /* path.cpp:78-95 */
-                const double surface_bsdf_pdf = (m->type == MAT_PHONG)
-                    ? cosine_power_value(hrec.normal, wi, m->shininess, spec_dir)
-                    : dielectric_value(hrec.normal, wi, m->ior, spec_dir);
-                const v3 surface_bsdf = (m->type == MAT_PHONG)
-                    ? phong_eval(m->albedo, m->ks, m->shininess, hrec.normal, wi, spec_dir)
-                    : dielectric_eval(m->ks, m->ior, hrec.normal, wi, spec_dir);
+                double surface_bsdf_pdf = spec_value(m, hrec.normal, wi, spec_dir);
+                if (sampled_pdf > 0.0) surface_bsdf_pdf = sampled_pdf;
+                const v3 surface_bsdf = spec_eval(m, hrec.normal, wi, spec_dir);
                 if (surface_bsdf_pdf == 0) return mk(0, 0, 0);
                 const int outside = dot(hrec.normal, spec_dir) > 0;
                 ray sr;
@@ -692,7 +972,7 @@ static v3 ao_Li(li_ctx *c, const ray *r)
     c->cnt->camera_rays++;
     if (world_hit(s, r, EPSILON, FLT_MAX, &hrec, c->cnt)) {
         const material *m = &s->mats[hrec.mat];
-        if (m->type == MAT_LAMBERT || m->type == MAT_PHONG || m->type == MAT_DIELECTRIC) {
+        if (mat_scatters(m->type)) {                            /* (metal: rejected up front) */
             const uint32_t base = DIM_BOUNCE(0);
             const double u0 = rng_u(c->key, base + 6), u1 = rng_u(c->key, base + 7);
             const v3 wi = vneg(unit(r->d));
@@ -702,8 +982,11 @@ static v3 ao_Li(li_ctx *c, const ray *r)
                 dir = onb_from_local(&uvw, hemisphere_to_cosine_direction(u0, u1));
             } else if (m->type == MAT_PHONG) {                  /* cosine_power_pdf::generate (pdf.h:115-132) */
                 dir = cosine_power_generate(hrec.normal, wi, m->shininess, u0, u1);
-            } else {                                            /* dielectric_pdf::generate (pdf.h:164-178) */
+            } else if (m->type == MAT_DIELECTRIC) {             /* dielectric_pdf::generate (pdf.h:164-178) */
                 dir = dielectric_generate(hrec.normal, wi, m->ior, u0);
+            } else {                                            /* roughconductor_pdf::generate (pdf.h:465-482) */
+                double unused;
+                dir = rough_generate(hrec.normal, wi, m->alpha, m->dist, u0, u1, &unused);
             }
             ray shadow; shadow.o = hrec.p; shadow.d = dir;
             const double t_max = world_box_size_y(s) * 0.50f;
@@ -771,6 +1054,9 @@ int ora_render_integrator(const ora_scene *s, int kind, int nx, int ny, int spp,
 {
     if (!s || nx <= 0 || ny <= 0 || spp <= 0 || npix < 0) return -1;
     if (kind != ORA_INTEGRATOR_PATH && kind != ORA_INTEGRATOR_AO && kind != ORA_INTEGRATOR_NORMALS) return -3;
+    /* ao::Li calls srec.pdf_ptr->generate, which metal's constant_pdf throws on (pdf.h:195-198) */
+    if (kind == ORA_INTEGRATOR_AO)
+        for (int i = 0; i < s->nmats; ++i) if (s->mats[i].type == MAT_METAL) return -4;
     for (int i = 0; i < npix; ++i)
         if (pixels[i] < 0 || pixels[i] >= nx * ny) return -2;
     if (nthreads < 1) nthreads = 1;
@@ -829,7 +1115,7 @@ static v3 mlt_Li(const ora_scene *s, const ray *r, mlt_state *st)
         const double rnd_s0 = st->prnds[st->off + 0], rnd_s1 = st->prnds[st->off + 1];   /* scatter rnd */
         st->off += 3;
         if ((Le.e[0] != 0.0) || (Le.e[1] != 0.0) || (Le.e[2] != 0.0)) {
-            if (st->depth == 0 || s->mats[st->prev.mat].type == MAT_PHONG || s->mats[st->prev.mat].type == MAT_DIELECTRIC)
+            if (st->depth == 0 || mat_no_mis(s->mats[st->prev.mat].type))
                 return Le;
             const double cos_wo = dot(hrec.normal, vneg(unit(r->d)));
             double distance_squared = hrec.t * hrec.t;
@@ -839,12 +1125,12 @@ static v3 mlt_Li(const ora_scene *s, const ray *r, mlt_state *st)
             return smul(weight, Le);
         }
         const material *m = &s->mats[hrec.mat];
-        if (m->type == MAT_LAMBERT || m->type == MAT_PHONG || m->type == MAT_DIELECTRIC) {
+        if (mat_scatters(m->type)) {
             const int specular = m->type != MAT_LAMBERT;
             const v3 wi = vneg(unit(r->d));
             v3 spec_dir = mk(0, 0, 0);
-            if (m->type == MAT_PHONG) spec_dir = cosine_power_generate(hrec.normal, wi, m->shininess, rnd_s0, rnd_s1);
-            else if (m->type == MAT_DIELECTRIC) spec_dir = dielectric_generate(hrec.normal, wi, m->ior, rnd_s0);
+            double sampled_pdf = -1.0;
+            if (specular) spec_dir = spec_generate(m, hrec.normal, wi, r->d, rnd_s0, rnd_s1, &sampled_pdf);
             const double rnd0 = st->prnds[st->off + 0], rnd1 = st->prnds[st->off + 1], rnd2 = st->prnds[st->off + 2];
             st->off += 3;
             const int index = pick_sample(rnd0, s->nlights);
@@ -858,8 +1144,7 @@ static v3 mlt_Li(const ora_scene *s, const ray *r, mlt_state *st)
                 if (!world_hit(s, &shadow, EPSILON, 1 - SHADOW_EPSILON, &lrec, st->cnt)) {
                     to_light = make_unit(to_light);
                     shadow.d = to_light;
-                    v3 surface_bsdf = specular ? phong_eval(m->albedo, m->ks, m->shininess, hrec.normal, wi, to_light)
-                                               : sdiv(m->albedo, M_PI);
+                    v3 surface_bsdf = specular ? spec_eval(m, hrec.normal, wi, to_light) : sdiv(m->albedo, M_PI);
                     const double cos_wi = dot(hrec.normal, unit(to_light));
                     const double cos_wo = dot(lrec.normal, vneg(unit(to_light)));
                     if (cos_wo != 0) {
@@ -868,8 +1153,7 @@ static v3 mlt_Li(const ora_scene *s, const ray *r, mlt_state *st)
                         const double light_pdf = prim_pdf_direct(s, s->lights[index], &hrec, to_light)
                                                  * distance_squared / fabs(cos_wo);
                         const double surface_bsdf_pdf =
-                            specular ? cosine_power_value(hrec.normal, wi, m->shininess, to_light)
-                                     : cosine_pdf_value(hrec.normal, to_light);
+                            specular ? spec_value(m, hrec.normal, wi, to_light) : cosine_pdf_value(hrec.normal, to_light);
                         const double weight = miWeight(light_pdf, surface_bsdf_pdf);
                         v3 em = mat_emitted(s, lrec.mat, shadow.d, lrec.normal);
                         Le = vadd(Le, sdiv(smul(weight, vmul(em, surface_bsdf)), light_pdf));
@@ -877,12 +1161,9 @@ static v3 mlt_Li(const ora_scene *s, const ray *r, mlt_state *st)
                 }
             }
             if (specular) {                                   /* pssmlt.cpp:232-249 */
-                const double surface_bsdf_pdf = (m->type == MAT_PHONG)
-                    ? cosine_power_value(hrec.normal, wi, m->shininess, spec_dir)
-                    : dielectric_value(hrec.normal, wi, m->ior, spec_dir);
-                const v3 surface_bsdf = (m->type == MAT_PHONG)
-                    ? phong_eval(m->albedo, m->ks, m->shininess, hrec.normal, wi, spec_dir)
-                    : dielectric_eval(m->ks, m->ior, hrec.normal, wi, spec_dir);
+                double surface_bsdf_pdf = spec_value(m, hrec.normal, wi, spec_dir);
+                if (sampled_pdf > 0.0) surface_bsdf_pdf = sampled_pdf;
+                const v3 surface_bsdf = spec_eval(m, hrec.normal, wi, spec_dir);
                 if (surface_bsdf_pdf == 0) return mk(0, 0, 0);
                 const int outside = dot(hrec.normal, spec_dir) > 0;
                 ray sr;
@@ -1422,9 +1703,94 @@ static void smooth_normals(const objdata *od, const omesh *m, float *cn /* 9 per
     free(fnrm);
 }
 
+/* Matrix4x4 (geometry.h:919-1065): point transform with the w divide
+ * (:966-983), Gauss-Jordan inverse with full pivoting (Matrix::invert,
+ * :857-907) and normal_transform = inverse-transpose product (:830-838). */
+static inline v3 mat4_point(const double *m, v3 v)
+{
+    const double x = m[0] * v.e[0] + m[1] * v.e[1] + m[2] * v.e[2] + m[3];
+    const double y = m[4] * v.e[0] + m[5] * v.e[1] + m[6] * v.e[2] + m[7];
+    const double z = m[8] * v.e[0] + m[9] * v.e[1] + m[10] * v.e[2] + m[11];
+    const double w = m[12] * v.e[0] + m[13] * v.e[1] + m[14] * v.e[2] + m[15];
+    if (w == 1.0) return mk(x, y, z);
+    return sdiv(mk(x, y, z), w);
+}
+static inline v3 mat4_normal(const double *inv, v3 v)
+{
+    return mk(inv[0] * v.e[0] + inv[4] * v.e[1] + inv[8] * v.e[2],
+              inv[1] * v.e[0] + inv[5] * v.e[1] + inv[9] * v.e[2],
+              inv[2] * v.e[0] + inv[6] * v.e[1] + inv[10] * v.e[2]);
+}
+static int mat4_invert(const double *src, double *t)
+{
+    int indxc[4], indxr[4], ipiv[4] = {0, 0, 0, 0};
+    memcpy(t, src, 16 * sizeof(double));
+    for (int i = 0; i < 4; i++) {
+        int irow = -1, icol = -1;
+        double big = 0;
+        for (int j = 0; j < 4; j++) {
+            if (ipiv[j] != 1) {
+                for (int k = 0; k < 4; k++) {
+                    if (ipiv[k] == 0) {
+                        if (fabs(t[4 * j + k]) >= big) { big = fabs(t[4 * j + k]); irow = j; icol = k; }
+                    } else if (ipiv[k] > 1) {
+                        return 0;
+                    }
+                }
+            }
+        }
+        ++ipiv[icol];
+        if (irow != icol)
+            for (int k = 0; k < 4; ++k) { double x = t[4 * irow + k]; t[4 * irow + k] = t[4 * icol + k]; t[4 * icol + k] = x; }
+        indxr[i] = irow; indxc[i] = icol;
+        if (t[4 * icol + icol] == 0) return 0;
+        const double pivinv = 1.0 / t[4 * icol + icol];
+        t[4 * icol + icol] = 1.0;
+        for (int j = 0; j < 4; j++) t[4 * icol + j] *= pivinv;
+        for (int j = 0; j < 4; j++) {
+            if (j != icol) {
+                const double save = t[4 * j + icol];
+                t[4 * j + icol] = 0;
+                for (int k = 0; k < 4; k++) t[4 * j + k] -= t[4 * icol + k] * save;
+            }
+        }
+    }
+    for (int j = 3; j >= 0; j--)
+        if (indxr[j] != indxc[j])
+            for (int k = 0; k < 4; k++) {
+                double x = t[4 * k + indxr[j]]; t[4 * k + indxr[j]] = t[4 * k + indxc[j]]; t[4 * k + indxc[j]] = x;
+            }
+    return 1;
+}
+
+/* material from the 20-double description of ora_scene_add_obj / _add_sphere */
+static material material_from_desc(const double *d)
+{
+    material m; memset(&m, 0, sizeof(m));
+    m.type = (int)d[0];
+    m.albedo = vload(d + 1); m.emit = vload(d + 4);
+    m.ks[0] = d[7]; m.ks[1] = d[8]; m.ks[2] = d[9];
+    m.shininess = d[10]; m.ior = d[11]; m.dist = (int)d[12]; m.alpha = d[13];
+    m.eta = vload(d + 14); m.k = vload(d + 17);
+    return m;
+}
+
+static int add_obj_x(ora_scene *s, const char *path, int geo, int32_t **lights, int *nlights,
+                     const double *to_world, const double *bsdf);
 /* create_triangle_mesh (triangle.cpp:9-23) + mesh_loader material mapping */
 static int add_obj(ora_scene *s, const char *path, int geo, int32_t **lights, int *nlights)
 {
+    return add_obj_x(s, path, geo, lights, nlights, NULL, NULL);
+}
+/* ... and its (file, toWorld, bsdf) overload (triangle.cpp:26-60): every mesh
+ * of the file takes `bsdf` when given; vertices go through toWorld, normals
+ * through its inverse transpose. */
+static int add_obj_x(ora_scene *s, const char *path, int geo, int32_t **lights, int *nlights,
+                     const double *to_world, const double *bsdf)
+{
+    double inv[16];
+    if (to_world && !mat4_invert(to_world, inv)) return -2;
+    int shared_mat = -1;
     objdata od; memset(&od, 0, sizeof(od));
     if (parse_obj(path, &od) != 0) return -1;
     for (int mi = 0; mi < od.nmeshes; ++mi) {
@@ -1446,9 +1812,20 @@ static int add_obj(ora_scene *s, const char *path, int geo, int32_t **lights, in
             mat.type = MAT_LAMBERT;
             mat.albedo = mk(FromSrgb(mt->kd[0]), FromSrgb(mt->kd[1]), FromSrgb(mt->kd[2]));
         }
-        s->mats = (material *)realloc(s->mats, sizeof(material) * (size_t)(s->nmats + 1));
-        s->mats[s->nmats] = mat;
-        int mat_idx = s->nmats++;
+        int mat_idx;
+        if (bsdf) {                                     /* mesh->mat.reset(bsdf): one material for all */
+            if (shared_mat < 0) {
+                s->mats = (material *)realloc(s->mats, sizeof(material) * (size_t)(s->nmats + 1));
+                s->mats[s->nmats] = material_from_desc(bsdf);
+                shared_mat = s->nmats++;
+            }
+            mat_idx = shared_mat;
+            mat = s->mats[mat_idx];
+        } else {
+            s->mats = (material *)realloc(s->mats, sizeof(material) * (size_t)(s->nmats + 1));
+            s->mats[s->nmats] = mat;
+            mat_idx = s->nmats++;
+        }
         /* normals: vn when every corner has one, else GenSmoothNormals */
         int has_vn = 1;
         for (int fi = 0; fi < m->nfaces && has_vn; ++fi)
@@ -1472,6 +1849,10 @@ static int add_obj(ora_scene *s, const char *path, int geo, int32_t **lights, in
             t->n0 = mk(cn[9 * fi], cn[9 * fi + 1], cn[9 * fi + 2]);
             t->n1 = mk(cn[9 * fi + 3], cn[9 * fi + 4], cn[9 * fi + 5]);
             t->n2 = mk(cn[9 * fi + 6], cn[9 * fi + 7], cn[9 * fi + 8]);
+            if (to_world) {
+                t->v0 = mat4_point(to_world, t->v0); t->v1 = mat4_point(to_world, t->v1); t->v2 = mat4_point(to_world, t->v2);
+                t->n0 = mat4_normal(inv, t->n0); t->n1 = mat4_normal(inv, t->n1); t->n2 = mat4_normal(inv, t->n2);
+            }
             t->e1 = vsub(t->v1, t->v0);
             t->e2 = vsub(t->v2, t->v0);
             t->inv_area = 1 / (0.5 * vlen(cross(t->e1, t->e2)) * m->nfaces);
@@ -1547,10 +1928,65 @@ int ora_load_scene(const char *kind, const char *obj_path, double aspect, ora_sc
         return -3;
     }
     s->lights = lights; s->nlights = nlights;
-    for (int i = 0; i < s->nmats; ++i)
-        if (s->mats[i].type != MAT_LAMBERT && s->mats[i].type != MAT_LIGHT && s->mats[i].type != MAT_PHONG &&
-            s->mats[i].type != MAT_DIELECTRIC) { ora_free_scene(s); return -4; }
     *out = s;
+    return 0;
+}
+
+/* ---- incremental construction: what main.cpp's scene functions do with
+ *      create_triangle_mesh / new sphere / camera / create_bvh ---- */
+int ora_scene_new(ora_scene **out)
+{
+    ora_scene *s = (ora_scene *)calloc(1, sizeof(ora_scene));
+    if (!s) return -1;
+    s->env = mk(0.0, 0.0, 0.0);
+    s->nodes = NULL; s->nnodes = 0; s->root = 0;
+    *out = s;
+    return 0;
+}
+/* world prims in insertion order; kept in `list` until ora_scene_finish */
+static void push_world(ora_scene *s, int32_t ref)
+{
+    s->list = (int32_t *)realloc(s->list, sizeof(int32_t) * (size_t)(s->nlist + 1));
+    s->list[s->nlist++] = ref;
+}
+int ora_scene_add_obj(ora_scene *s, const char *obj_path, const double *to_world16, const double *bsdf20,
+                      int use_geometry_normals)
+{
+    const int t0 = s->ntris;
+    const int rc = add_obj_x(s, obj_path, use_geometry_normals, &s->lights, &s->nlights, to_world16, bsdf20);
+    if (rc != 0) return rc == -2 ? -2 : -1;
+    for (int i = t0; i < s->ntris; ++i) push_world(s, i);
+    return 0;
+}
+/* where: 1 = the world list, 2 = Scene::lights (a separate sphere object, as
+ * veach_mis and random_scene do), 3 = both (one object) */
+int ora_scene_add_sphere(ora_scene *s, const double *c, double r, const double *mat20, int where)
+{
+    s->mats = (material *)realloc(s->mats, sizeof(material) * (size_t)(s->nmats + 1));
+    s->mats[s->nmats] = material_from_desc(mat20);
+    const int m = s->nmats++;
+    const int id = add_sphere(s, vload(c), r, m);
+    if (where & 1) push_world(s, REF_SPHERE | id);
+    if (where & 2) {
+        s->lights = (int32_t *)realloc(s->lights, sizeof(int32_t) * (size_t)(s->nlights + 1));
+        s->lights[s->nlights++] = REF_SPHERE | id;
+    }
+    return 0;
+}
+void ora_scene_set_camera(ora_scene *s, const double *from, const double *at, const double *vup, double vfov,
+                          double aspect, double aperture, double focus)
+{
+    s->cam = camera_mk(vload(from), vload(at), vload(vup), vfov, aspect, aperture, focus);
+}
+/* world_kind 0: parallel_bvh_node::create_bvh over the world prims in
+ * insertion order; 1: hitable_list */
+int ora_scene_finish(ora_scene *s, int world_kind)
+{
+    s->world_kind = world_kind;
+    if (world_kind == WORLD_BVH) {
+        if (s->nlist > 0) build_bvh(s, s->list, s->nlist);
+        free(s->list); s->list = NULL; s->nlist = 0;
+    }
     return 0;
 }
 void ora_free_scene(ora_scene *s)
@@ -1601,14 +2037,16 @@ int ora_scene_export_lights(const ora_scene *s, int32_t *refs)
     for (int i = 0; i < s->nlights; ++i) refs[i] = s->lights[i];
     return s->nlights;
 }
-int ora_scene_export_materials(const ora_scene *s, double *out12)
+int ora_scene_export_materials(const ora_scene *s, double *out20)
 {
     for (int i = 0; i < s->nmats; ++i) {
-        double *o = out12 + 12 * i;
+        double *o = out20 + 20 * i;
         o[0] = s->mats[i].type;
         vstore(o + 1, s->mats[i].albedo); vstore(o + 4, s->mats[i].emit);
         o[7] = s->mats[i].ks[0]; o[8] = s->mats[i].ks[1]; o[9] = s->mats[i].ks[2];
         o[10] = s->mats[i].shininess; o[11] = s->mats[i].ior;
+        o[12] = s->mats[i].dist; o[13] = s->mats[i].alpha;
+        vstore(o + 14, s->mats[i].eta); vstore(o + 17, s->mats[i].k);
     }
     return s->nmats;
 }
@@ -1702,6 +2140,35 @@ void ora_kat_dielectric(const double *n, const double *wi, double ior, double u0
     out12[5] = dielectric_value(N, WI, ior, WO);
     vstore(out12 + 6, dielectric_eval(ks, ior, N, WI, d));
     vstore(out12 + 9, dielectric_eval(ks, ior, N, WI, WO));
+}
+void ora_kat_metal(const double *n, const double *wi, const double *albedo, const double *wo, double *out7)
+{
+    material m; memset(&m, 0, sizeof m);
+    m.type = MAT_METAL; m.albedo = vload(albedo);
+    const v3 N = vload(n), WI = vload(wi), WO = vload(wo);
+    double sp;
+    vstore(out7, spec_generate(&m, N, WI, vneg(WI), 0.0, 0.0, &sp));   /* r_in = ray(0, -wi) */
+    out7[3] = spec_value(&m, N, WI, WO);
+    vstore(out7 + 4, spec_eval(&m, N, WI, WO));
+}
+/* rough_conductor: out = generate() dir[3], sampled_pdf, value(unit(dir)), value(wo),
+ * eval_bsdf(unit(dir))[3], eval_bsdf(wo)[3] */
+void ora_kat_conductor(const double *n, const double *wi, int ggx, double alpha, const double *eta, const double *k,
+                       const double *spec, double s0, double s1, const double *wo, double *out12)
+{
+    material m; memset(&m, 0, sizeof m);
+    m.type = MAT_ROUGH; m.alpha = alpha; m.dist = ggx ? DIST_GGX : DIST_BECKMANN;
+    m.eta = vload(eta); m.k = vload(k); m.ks[0] = spec[0]; m.ks[1] = spec[1]; m.ks[2] = spec[2];
+    const v3 N = vload(n), WI = vload(wi), WO = vload(wo);
+    double sp;
+    const v3 d = rough_generate(N, WI, alpha, m.dist, s0, s1, &sp);
+    const v3 du = unit(d);
+    vstore(out12, d);
+    out12[3] = sp;
+    out12[4] = rough_value(N, WI, alpha, m.dist, du);
+    out12[5] = rough_value(N, WI, alpha, m.dist, WO);
+    vstore(out12 + 6, rough_eval(&m, N, WI, du));
+    vstore(out12 + 9, rough_eval(&m, N, WI, WO));
 }
 void ora_kat_tri_sample(const double *v9, const double *n9, int geo, int n_tris_in_mesh, const double *o,
                         const double *smp, double *out10)

@@ -54,6 +54,24 @@ int  ora_load_scene(const char *kind, const char *obj_path, double aspect, ora_s
 void ora_free_scene(ora_scene *s);
 void ora_scene_get_info(const ora_scene *s, ora_scene_info *info);
 
+/* Incremental construction (main.cpp's scene functions).  Materials are 20
+ * doubles: type (FRT_MAT_* values: 0 lambertian, 1 diffuse_light,
+ * 2 modified_phong, 3 metal, 4 dielectric, 5 rough_conductor), albedo[3],
+ * emit[3], ks[3] (specular reflectance), shininess, ior, distribution
+ * (0 GGX, 1 Beckmann), alpha, eta[3], k[3]. */
+int  ora_scene_new(ora_scene **out);
+/* create_triangle_mesh(file, toWorld, bsdf, lights, geo) (triangle.cpp:26-60);
+ * to_world16 row-major or NULL (identity), bsdf20 NULL = the file's MTL materials.
+ * Returns -1 on I/O error, -2 for a singular matrix. */
+int  ora_scene_add_obj(ora_scene *s, const char *obj_path, const double *to_world16, const double *bsdf20,
+                       int use_geometry_normals);
+/* where: 1 world list, 2 Scene::lights, 3 both */
+int  ora_scene_add_sphere(ora_scene *s, const double *c, double r, const double *mat20, int where);
+void ora_scene_set_camera(ora_scene *s, const double *from, const double *at, const double *vup, double vfov,
+                          double aspect, double aperture, double focus);
+/* world_kind 0: create_bvh over the world prims in insertion order, 1: hitable_list */
+int  ora_scene_finish(ora_scene *s, int world_kind);
+
 /* Flattened export of the reference-topology BVH in left-first DFS order:
  * node i: box lo[3],hi[3] (6 doubles), left, right (child >= 0 = node index,
  * child < 0 = ~prim_ref).  prim_ref: triangle t -> t, sphere k -> (1<<30)|k. */
@@ -63,7 +81,7 @@ int  ora_scene_export_tris(const ora_scene *s, double *v9, int32_t *mat);
 
 void ora_scene_export_camera(const ora_scene *s, double *out19);
 int  ora_scene_export_lights(const ora_scene *s, int32_t *refs);
-int  ora_scene_export_materials(const ora_scene *s, double *out12);   /* type, albedo, emit, ks, Ns, Ni */
+int  ora_scene_export_materials(const ora_scene *s, double *out20);   /* the 20-double description */
 
 /* Render pixels (linear index y*nx+x, y=0 bottom row) with `spp` samples each,
  * frame seed `seed`, on `nthreads` threads.  out_rgb[3*i..] = mean radiance
@@ -117,6 +135,12 @@ void ora_kat_phong(const double *n, const double *wi, double e, double s0, doubl
                    const double *kd, const double *ks, double *out11);
 void ora_kat_dielectric(const double *n, const double *wi, double ior, double u0, const double *wo, const double *ks,
                         double *out12);
+/* metal (material.h:110-130): out reflect dir[3], constant pdf value, eval_bsdf[3] */
+void ora_kat_metal(const double *n, const double *wi, const double *albedo, const double *wo, double *out7);
+/* rough_conductor + roughconductor_pdf (material.h:246-315, pdf.h:231-486): ggx = 1 GGX, 0 Beckmann;
+ * out: generate dir[3], sampled_pdf, value(unit dir), value(wo), eval(unit dir)[3], eval(wo)[3] */
+void ora_kat_conductor(const double *n, const double *wi, int ggx, double alpha, const double *eta, const double *k,
+                       const double *spec, double s0, double s1, const double *wo, double *out12);
 /* triangle sample_direct from o: out p[3], normal[3], to_light[3], pdf */
 void ora_kat_tri_sample(const double *v9, const double *n9, int geo, int n_tris_in_mesh, const double *o,
                         const double *smp, double *out10);

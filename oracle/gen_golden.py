@@ -26,6 +26,9 @@ def main():
     with tempfile.TemporaryDirectory() as home:
         env = dict(os.environ, HOME=home)
         out = subprocess.check_output([os.path.join(HERE, "_ref", "ref_kat"), str(n)], env=env, text=True)
+        # metal / rough_conductor: own program (util.h sincos, see ref_kat_conductor.cpp)
+        out += subprocess.check_output([os.path.join(HERE, "_ref", "ref_kat_conductor"), str(n)], env=env,
+                                       text=True, timeout=60)
         cases = {}
         pfm = None
         for line in out.splitlines():
@@ -43,7 +46,7 @@ def main():
             cases.setdefault(kind, []).append([ins, outs])
     cases["pfm"] = pfm
     cases["_meta"] = {
-        "generator": "oracle/ref_kat.cpp (built from /root/reference/first_ray sources by oracle/Makefile `ref`)",
+        "generator": "oracle/ref_kat.cpp + ref_kat_conductor.cpp (built from /root/reference/first_ray sources by oracle/Makefile `ref`)",
         "ncases": n,
         "format": "hex floats (float.fromhex); per kind: [inputs, outputs]",
     }

@@ -1,0 +1,45 @@
+"""Scene specs for HostScene.from_spec / OracleScene.from_spec (the
+frt_scene_new ... frt_scene_finish builder): CornellBox-Original plus the
+materials the reference builds only in hand-written scenes -- metal
+(random_scene, main.cpp:87-89) and rough_conductor with the constants of
+veach_ajar (main.cpp:340-344: POT2 GGX alpha 0.15, DOORHANDLE Beckmann 0.25)
+-- on a sphere and on a cube OBJ placed with a toWorld matrix and a bsdf
+override (create_triangle_mesh, triangle.cpp:26-60)."""
+import math
+import os
+
+SCENES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "scenes")
+CORNELL_OBJ = os.path.join(SCENES, "CornellBox-Original.obj")
+CUBE_OBJ = os.path.join(SCENES, "cube.obj")
+
+F32 = lambda x: float(__import__("numpy").float32(x))   # noqa: E731  (C++ float literals, e.g. 0.15f)
+CORNELL_CAM = {"lookfrom": (0.0, 1.0, F32(3.9)), "lookat": (0.0, 1.0, 0.0), "vup": (0.0, 1.0, 0.0),
+               "vfov": 40.0, "aperture": 0.0, "focus": 10.0}                       # main.cpp:236-242
+GOLD_ETA, GOLD_K = (1.65746, 0.880369, 0.521229), (9.22387, 6.26952, 4.837)      # main.cpp:340-344
+
+
+def rough(dist, alpha, spec=(1.0, 1.0, 1.0)):
+    return {"type": "rough_conductor", "distribution": dist, "alpha": F32(alpha), "eta": GOLD_ETA, "k": GOLD_K,
+            "specular": spec}
+
+
+METAL = {"type": "metal", "albedo": (0.9, 0.8, 0.6)}
+
+
+def to_world(scale, yaw_deg, t):
+    """Row-major Matrix4x4: translate * rotate_y * scale."""
+    c, s = math.cos(math.radians(yaw_deg)), math.sin(math.radians(yaw_deg))
+    return [c * scale, 0.0, s * scale, t[0],
+            0.0, scale, 0.0, t[1],
+            -s * scale, 0.0, c * scale, t[2],
+            0.0, 0.0, 0.0, 1.0]
+
+
+def cornell_conductors(sphere_dist="ggx", cube_dist="beckmann", world="bvh", metal=True):
+    objs = [{"obj": CORNELL_OBJ, "geo": True}]
+    if metal:
+        objs.append({"sphere": (0.33, 0.82, 0.37), "radius": 0.22, "material": METAL})      # on the short box
+    objs.append({"sphere": (-0.6, 0.25, 0.6), "radius": 0.25, "material": rough(sphere_dist, 0.15)})
+    objs.append({"obj": CUBE_OBJ, "to_world": to_world(0.15, 30.0, (-0.33, 1.35, -0.29)),     # on the tall box
+                 "bsdf": rough(cube_dist, 0.25), "geo": False})
+    return {"objects": objs, "camera": CORNELL_CAM, "world": world}

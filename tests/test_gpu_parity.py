@@ -253,11 +253,10 @@ def test_edge_cases(ctx, cornell_obj, nx, ny, spp, depth):
 
 
 def test_unsupported_material_rejected(ctx, cornell_obj):
-    """Materials outside the supported set (metal, rough_conductor: the
-    reference builds them only in hand-written scenes) fail loudly at upload."""
+    """Material types outside frt.h's FRT_MAT_* set fail loudly at upload."""
     import ctypes
     hs = frt.HostScene("cornell_box_obj", cornell_obj, 1.0)
     v = hs.view()
-    ctypes.cast(v.materials, ctypes.POINTER(frt.Material))[0].type = 3      # metal
+    ctypes.cast(v.materials, ctypes.POINTER(frt.Material))[0].type = 7      # no such material
     with pytest.raises(frt.FrtError, match="not supported"):
         ctx.upload(v)

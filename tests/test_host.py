@@ -21,7 +21,7 @@ def test_library_exports_every_declared_symbol():
     L = frt.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert L.frt_get_abi_version() == frt.ABI_VERSION == 3
+    assert L.frt_get_abi_version() == frt.ABI_VERSION == 4
 
 
 def test_create_without_device_fails_cleanly():
@@ -72,8 +72,9 @@ def test_cornell_scene_matches_oracle(cornell_obj, aspect):
     cam = np.concatenate([list(v.cam_origin), list(v.cam_lower_left), list(v.cam_horizontal),
                           list(v.cam_vertical), list(v.cam_u), list(v.cam_v), [v.cam_lens_radius]])
     assert np.array_equal(cam, osc.camera())
-    # materials: type, albedo, emit, specular, exponent, ior
-    mats = np.array([[m.type, *m.albedo, *m.emit, *m.specular, m.exponent, m.ior] for m in
+    # materials: the oracle's 20-double description
+    mats = np.array([[m.type, *m.albedo, *m.emit, *m.specular, m.exponent, m.ior, m.distribution, m.alpha,
+                      *m.eta, *m.k] for m in
                      (ctypes.cast(v.materials, ctypes.POINTER(frt.Material))[i] for i in range(v.n_materials))])
     assert np.array_equal(mats, osc.materials())
 
@@ -158,7 +159,8 @@ def test_specular_scene_materials_and_topology(objfix, request):
     hs = frt.HostScene("cornell_box_obj", obj, 1.0)
     osc = oracle.OracleScene("cornell_box_obj", obj, 1.0)
     v = hs.view()
-    mats = np.array([[m.type, *m.albedo, *m.emit, *m.specular, m.exponent, m.ior] for m in
+    mats = np.array([[m.type, *m.albedo, *m.emit, *m.specular, m.exponent, m.ior, m.distribution, m.alpha,
+                      *m.eta, *m.k] for m in
                      (ctypes.cast(v.materials, ctypes.POINTER(frt.Material))[i] for i in range(v.n_materials))])
     assert np.array_equal(mats, osc.materials())
     types = set(mats[:, 0].astype(int))

@@ -162,6 +162,38 @@ def test_list_hit_ties(kat):
         assert bits_equal(out, H(outs)), (ins, out, H(outs))
 
 
+def test_metal(kat):
+    """metal::scatter direction, constant_pdf value, eval_bsdf (material.h:110-130, pdf.h:186-201)."""
+    L = oracle.lib()
+    assert len(kat["metal"]) >= 100
+    for ins, outs in kat["metal"]:
+        x = H(ins); want = H(outs)
+        wo = [0.3, -0.2, 0.9]
+        out = np.zeros(7)
+        L.ora_kat_metal(darr(x[0:3])[1], darr(x[3:6])[1], darr(x[6:9])[1], darr(wo)[1],
+                        out.ctypes.data_as(darr([0])[1].__class__))
+        assert bits_equal(out[:3], want[:3]) and out[3] == want[3] and bits_equal(out[4:], x[6:9]), (ins, out, want)
+        assert bits_equal(want[4:], x[6:9])
+
+
+def test_rough_conductor(kat):
+    """roughconductor_pdf generate (visible normals, GGX + Beckmann) / sampled_pdf / value and
+    rough_conductor::eval_bsdf (pdf.h:231-486, pdf.cpp:5-12, material.h:246-315, microfacet.h)."""
+    L = oracle.lib()
+    cases = kat["conductor"]
+    assert len(cases) >= 100 and {int(float.fromhex(c[0][6])) for c in cases} == {0, 1}
+    nonzero = 0
+    for ins, outs in cases:
+        x = H(ins); want = H(outs)
+        out = np.zeros(12)
+        L.ora_kat_conductor(darr(x[0:3])[1], darr(x[3:6])[1], int(x[6]), x[7], darr(x[8:11])[1], darr(x[11:14])[1],
+                            darr(x[14:17])[1], x[17], x[18], darr(x[19:22])[1],
+                            out.ctypes.data_as(darr([0])[1].__class__))
+        assert bits_equal(out, want), (ins, out, want)
+        nonzero += want[6] != 0.0
+    assert nonzero > len(cases) // 4, "KAT set should exercise non-zero BSDF values"
+
+
 def test_pfm_bytes(kat, tmp_path):
     p = kat["pfm"]
     data = H(p["data"])
@@ -174,6 +206,7 @@ def test_kat_coverage(kat):
     # every component kind the reference harness emits is checked above
     assert {k for k in kat if not k.startswith("_")} == {
         "tri_hit", "sphere_hit", "aabb_hit", "camera", "cosine", "tri_sample", "sphere_sample",
-        "miweight", "fromsrgb", "pick", "sort", "list_hit", "pfm", "fresnel", "phong", "dielectric"}
+        "miweight", "fromsrgb", "pick", "sort", "list_hit", "pfm", "fresnel", "phong", "dielectric",
+        "metal", "conductor"}
     hits = sum(int(float.fromhex(o[0])) for _, o in kat["tri_hit"])
     assert 20 < hits < len(kat["tri_hit"]) - 20, "KAT set should mix hits and misses"

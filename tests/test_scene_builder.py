@@ -1,0 +1,114 @@
+"""The incremental scene builder (frt_scene_new ... frt_scene_finish: what
+main.cpp's scene functions do with create_triangle_mesh(file, toWorld, bsdf),
+spheres, the camera and create_bvh) against the oracle's builder, and the
+metal / rough_conductor shading code run on the host against the oracle.
+Scene arrays are bit-exact (fp64 host pipeline on both sides)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import first_raytracer_amd as frt
+import oracle
+import scene_specs as SS
+
+
+def both(spec, aspect=1.0):
+    return frt.HostScene.from_spec(spec, aspect), oracle.OracleScene.from_spec(spec, aspect)
+
+
+def host_materials(hs):
+    v = hs.view()
+    return np.array([[m.type, *m.albedo, *m.emit, *m.specular, m.exponent, m.ior, m.distribution, m.alpha,
+                      *m.eta, *m.k] for m in
+                     (ctypes.cast(v.materials, ctypes.POINTER(frt.Material))[i] for i in range(v.n_materials))])
+
+
+@pytest.mark.parametrize("world", ["bvh", "list"])
+def test_builder_scene_matches_oracle(world):
+    hs, osc = both(SS.cornell_conductors(world=world), 16 / 9)
+    assert (hs.info.n_tris, hs.info.n_spheres, hs.info.n_materials, hs.info.n_lights, hs.info.world_kind) == \
+        (osc.info.n_tris, osc.info.n_spheres, osc.info.n_materials, osc.info.n_lights, osc.info.world_kind)
+    a = hs.arrays()
+    tv, tm = osc.tris()
+    assert np.array_equal(a["tri_v"], tv) and np.array_equal(a["tri_material"], tm)
+    assert np.array_equal(host_materials(hs), osc.materials())
+    assert np.array_equal(a["lights"], osc.lights())
+    if world == "bvh":
+        b, l, r = osc.bvh()
+        assert np.array_equal(a["node_box"], b)
+        assert np.array_equal(a["node_child"][:, 0], l) and np.array_equal(a["node_child"][:, 1], r)
+    else:
+        # insertion order: the Cornell triangles, the two spheres, the cube's triangles
+        n = hs.info.n_tris
+        assert list(a["list"]) == list(range(n - 12)) + [frt.FRT_PRIM_SPHERE | k for k in range(2)] + \
+            list(range(n - 12, n))
+    v = hs.view()
+    cam = np.concatenate([list(v.cam_origin), list(v.cam_lower_left), list(v.cam_horizontal),
+                          list(v.cam_vertical), list(v.cam_u), list(v.cam_v), [v.cam_lens_radius]])
+    assert np.array_equal(cam, osc.camera())
+
+
+def test_builder_transform_and_override():
+    """toWorld moves the cube's vertices (point transform) and every cube
+    triangle takes the one override material (triangle.cpp:36-52)."""
+    spec = SS.cornell_conductors()
+    hs = frt.HostScene.from_spec(spec, 1.0)
+    a = hs.arrays()
+    cube = a["tri_v"][-12:].reshape(-1, 3)
+    M = np.array(spec["objects"][-1]["to_world"]).reshape(4, 4)
+    corners = np.array([[x, y, z] for x in (-1, 1) for y in (-1, 1) for z in (-1, 1)], float)
+    want = corners @ M[:3, :3].T + M[:3, 3]
+    assert all(np.abs(want - c).sum(1).min() < 1e-12 for c in cube)
+    mats = host_materials(hs)
+    cm = set(a["tri_material"][-12:])
+    assert len(cm) == 1 and mats[cm.pop()][0] == frt.MAT_TYPES["rough_conductor"]
+
+
+def test_builder_reproduces_named_scene(cornell_obj):
+    """The builder with CornellBox-Original alone is cornell_box_obj (main.cpp:222-252)."""
+    hs = frt.HostScene.from_spec({"objects": [{"obj": cornell_obj, "geo": True}], "camera": SS.CORNELL_CAM}, 1.0)
+    ref = frt.HostScene("cornell_box_obj", cornell_obj, 1.0)
+    a, b = hs.arrays(), ref.arrays()
+    for k in ("tri_v", "tri_material", "node_box", "node_child", "lights"):
+        assert np.array_equal(a[k], b[k]), k
+
+
+def test_builder_errors(cornell_obj):
+    singular = dict(SS.cornell_conductors())
+    singular["objects"] = [{"obj": SS.CUBE_OBJ, "to_world": [0.0] * 16}]
+    with pytest.raises(frt.FrtError):
+        frt.HostScene.from_spec(singular, 1.0)
+    bad = {"objects": [{"sphere": (0, 0, 0), "radius": 1.0, "material": SS.rough("ggx", 0.0)}], "camera": SS.CORNELL_CAM}
+    with pytest.raises(frt.FrtError):
+        frt.HostScene.from_spec(bad, 1.0)
+    missing = {"objects": [{"obj": "/nonexistent.obj"}], "camera": SS.CORNELL_CAM}
+    with pytest.raises(frt.FrtError):
+        frt.HostScene.from_spec(missing, 1.0)
+
+
+@pytest.mark.parametrize("sphere_dist,cube_dist", [("ggx", "beckmann"), ("beckmann", "ggx")])
+def test_conductor_shading_host_vs_oracle(sphere_dist, cube_dist):
+    """The megakernel's per-lane path code (fp32, frt_path.hpp: metal + rough
+    conductor specular branch, NEE with their pdfs) run on the host against the
+    fp64 oracle on the same streams."""
+    spec = SS.cornell_conductors(sphere_dist, cube_dist)
+    hs, osc = both(spec)
+    nx = ny = 48
+    pix = np.arange(nx * ny, dtype=np.int32)
+    g, st = frt.selftest_path_host(hs, frt.RenderParams.make(nx, ny, 8, seed=5), pix)
+    ref, cnt = osc.render(nx, ny, 8, seed=5)
+    g = g.reshape(-1, 3).astype(np.float64)
+    assert st.samples == cnt.samples and st.camera_rays == cnt.camera_rays
+    assert abs(st.rays - cnt.rays) / cnt.rays < 2e-3
+    assert float(np.sqrt(np.mean((g - ref) ** 2))) < 1e-3
+
+
+def test_ao_rejects_metal():
+    """ao::Li asks metal's constant_pdf to generate(), which throws (pdf.h:195-198)."""
+    hs, osc = both(SS.cornell_conductors())
+    with pytest.raises(frt.FrtError):
+        frt.selftest_path_host(hs, frt.RenderParams.make(8, 8, 1, integrator=frt.FRT_INTEGRATOR_AO),
+                               np.arange(64, dtype=np.int32))
+    with pytest.raises(RuntimeError):
+        osc.render(8, 8, 1, integrator=2)
