@@ -177,7 +177,10 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
     const int nl = S.n_lights;
     int idx = (int)(rnd0 * (float)nl);
     if (idx == nl) idx -= 1;
-    P.term = pdf == 0.0f;
+    // Lambertian-only kernels (MATS = false) never see pdf 0: the cosine lobe's
+    // z = sqrt(1 - r0) >= 2^-12 (r0 < 1 - 2^-24), far above the rounding of
+    // dot(n, wo); the constant lets the compiler drop the state.
+    P.term = MATS && pdf == 0.0f;
     if (P.term && !(idx >= 0 && !diel)) return true;
     const f3 nee_o = p + kEps * n;
     const f3 origin = (!MATS || lamb || dot(n, wo) > 0.0f) ? nee_o : p - kEps * n;   // hrec.p moved off (:243, :253)

@@ -594,11 +594,6 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
     if (!(lamb || spec) || P.depth > max_depth) return true;   // no scatter: Le (= 0)
     const bool diel = MATS && mtype == FRT_MAT_DIELECTRIC;
     const uint32_t base = dim_bounce(P.depth);
-    // NEE's light pick (path.cpp:39-40)
-    const int nl = S.n_lights;
-    int idx = (int)(rng_u(P.key, base + 3) * (float)nl);
-    if (idx == nl) idx -= 1;
-    const bool nee = idx >= 0 && !diel;
     // The scattered direction first: a zero pdf returns 0 for this vertex,
     // dropping its NEE too (path.cpp:84-86, 103-106) -- after the reference has
     // traced the shadow ray, so that ray is still traced (P.term).
@@ -621,7 +616,15 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
         const f3 bsdf = spec_eval(M, n, wi, wo);
         beta_next = P.beta * (rcp(pdf) * bsdf);
     }
-    P.term = pdf == 0.0f;
+    // Lambertian-only kernels (MATS = false) never see pdf 0: the cosine lobe's
+    // z = sqrt(1 - r0) >= 2^-12 (r0 < 1 - 2^-24), far above the rounding of
+    // dot(n, wo); the constant lets the compiler drop the state.
+    // NEE's light pick (path.cpp:39-40)
+    const int nl = S.n_lights;
+    int idx = (int)(rng_u(P.key, base + 3) * (float)nl);
+    if (idx == nl) idx -= 1;
+    const bool nee = idx >= 0 && !diel;
+    P.term = MATS && pdf == 0.0f;
     if (P.term && !nee) return true;
     // origin of the next ray: off the surface on the side it leaves (path.cpp:91-93, 99)
     const f3 nee_o = p + kEps * n;
