@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("FRT_LIB_PATH") or os.path.join(HERE, "libfrt.so")
 FRT_WORLD_BVH, FRT_WORLD_LIST = 0, 1
 FRT_MAT_LAMBERTIAN, FRT_MAT_DIFFUSE_LIGHT = 0, 1
 FRT_PRIM_SPHERE = 1 << 30
-ABI_VERSION = 4                 # include/frt.h FRT_ABI_VERSION (frt_stats / frt_material layout)
+ABI_VERSION = 5                 # include/frt.h FRT_ABI_VERSION (frt_stats / frt_material layout)
 FRT_MAT_LAMBERTIAN, FRT_MAT_DIFFUSE_LIGHT, FRT_MAT_MODIFIED_PHONG, FRT_MAT_METAL, FRT_MAT_DIELECTRIC = 0, 1, 2, 3, 4
 FRT_MAT_ROUGH_CONDUCTOR = 5
 FRT_DIST_GGX, FRT_DIST_BECKMANN = 0, 1
@@ -90,15 +90,16 @@ class SceneView(ctypes.Structure):
 class RenderParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in ("nx", "ny", "spp")] + [("seed", ctypes.c_uint32)] + [
         (n, ctypes.c_int32) for n in ("max_depth", "integrator", "tile_size", "shard_index", "shard_count",
-                                      "samples_per_item", "flags", "mlt_chains", "mlt_bootstrap")]
+                                      "samples_per_item", "flags", "mlt_chains", "mlt_bootstrap", "sample_offset")]
 
     @classmethod
     def make(cls, nx, ny, spp, seed=0, max_depth=33, tile_size=32, shard_index=0, shard_count=1,
-             samples_per_item=0, flags=0, integrator=0):
-        """integrator: FRT_INTEGRATOR_PATH (path.cpp), _AO (ao.cpp) or _NORMALS (debug_renderer.h)."""
+             samples_per_item=0, flags=0, integrator=0, sample_offset=0):
+        """integrator: FRT_INTEGRATOR_PATH (path.cpp), _AO (ao.cpp) or _NORMALS (debug_renderer.h);
+        sample_offset: first global sample index (progressive passes)."""
         return cls(nx=nx, ny=ny, spp=spp, seed=seed, max_depth=max_depth, integrator=integrator, tile_size=tile_size,
                    shard_index=shard_index, shard_count=shard_count, samples_per_item=samples_per_item, flags=flags,
-                   mlt_chains=0, mlt_bootstrap=0)
+                   mlt_chains=0, mlt_bootstrap=0, sample_offset=sample_offset)
 
     @classmethod
     def pssmlt(cls, nx, ny, mutations_per_pixel, chains, seed=0, bootstrap=10000, shard_index=0, shard_count=1,
@@ -140,7 +141,8 @@ EXPORTS = ("frt_get_abi_version", "frt_create", "frt_destroy", "frt_last_error",
            "frt_scene_create", "frt_scene_new", "frt_scene_add_obj", "frt_scene_add_sphere", "frt_scene_set_camera",
            "frt_scene_set_env", "frt_scene_finish",
            "frt_scene_view_get", "frt_scene_info", "frt_scene_destroy", "frt_write_tessellated_obj",
-           "frt_write_pfm", "frt_selftest_path_host", "frt_selftest_mlt_paths_host")
+           "frt_write_pfm", "frt_film_accumulate", "frt_tonemap_u8", "frt_write_image", "frt_selftest_path_host",
+           "frt_selftest_mlt_paths_host")
 
 
 def lib():
@@ -189,6 +191,9 @@ def lib():
     L.frt_scene_finish.argtypes = [vp, ctypes.c_int]
     L.frt_write_tessellated_obj.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p]
     L.frt_write_pfm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, vp]
+    L.frt_film_accumulate.argtypes = [vp, ctypes.c_int64, vp, ctypes.c_int64, ctypes.c_int64]
+    L.frt_tonemap_u8.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
+    L.frt_write_image.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int]
     L.frt_selftest_path_host.argtypes = [ctypes.POINTER(SceneView), ctypes.POINTER(RenderParams), vp,
                                          ctypes.c_int, vp, ctypes.POINTER(Stats)]
     L.frt_selftest_mlt_paths_host.argtypes = [ctypes.POINTER(SceneView), ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
@@ -394,6 +399,34 @@ def write_pfm(path, film):
     film = np.ascontiguousarray(film, dtype=np.float32)
     ny, nx = film.shape[0], film.shape[1]
     _check(lib().frt_write_pfm(path.encode(), nx, ny, film.ctypes.data), "frt_write_pfm")
+
+
+def film_accumulate(acc, acc_spp, film, spp):
+    """Progressive accumulation (frt_film_accumulate): acc <- mean over acc_spp + spp samples."""
+    acc = np.ascontiguousarray(acc, dtype=np.float32)
+    film = np.ascontiguousarray(film, dtype=np.float32)
+    _check(lib().frt_film_accumulate(acc.ctypes.data, int(acc_spp), film.ctypes.data, int(spp), film.size),
+           "frt_film_accumulate")
+    return acc
+
+
+def tonemap_u8(film):
+    """viewer::add_sample's display mapping (viewer.cpp:115-117) of a (ny, nx, 3) mean film."""
+    film = np.ascontiguousarray(film, dtype=np.float32)
+    ny, nx = film.shape[0], film.shape[1]
+    out = np.zeros((ny, nx, 3), np.uint8)
+    _check(lib().frt_tonemap_u8(film.ctypes.data, nx, ny, out.ctypes.data), "frt_tonemap_u8")
+    return out
+
+
+IMAGE_FORMATS = {"png": 0, "bmp": 1, "jpg": 2}
+
+
+def write_image(path, rgb_u8, fmt="png"):
+    """image::save_image (image.cpp:24-58) of a (ny, nx, 3) u8 image, y = 0 bottom."""
+    rgb_u8 = np.ascontiguousarray(rgb_u8, dtype=np.uint8)
+    ny, nx = rgb_u8.shape[0], rgb_u8.shape[1]
+    _check(lib().frt_write_image(path.encode(), nx, ny, rgb_u8.ctypes.data, IMAGE_FORMATS[fmt]), "frt_write_image")
 
 
 def write_tessellated_obj(src_obj, k, dst_obj):

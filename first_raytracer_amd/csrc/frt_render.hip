@@ -41,7 +41,7 @@ constexpr int kLdsMaxDepth = 16;                // LDS plan: binary stacks of 8 
 
 struct DevWork {
     int nx, ny, spp, max_depth;
-    uint32_t seed;
+    uint32_t seed, s_off;                // frame seed, first global sample index (progressive passes)
     int tile, ntx, shard_index, shard_count;
     int spi, n_chunks;
     uint32_t n_items, n_slots;
@@ -224,7 +224,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         // ---- next camera sample of the item ----
         const bool start = !active && have_item && s_cur < s_end;
         if (start) {
-            path_begin(P, S, px, py, W.nx, W.ny, W.seed, pix, (uint32_t)s_cur);
+            path_begin(P, S, px, py, W.nx, W.ny, W.seed, pix, (uint32_t)s_cur + W.s_off);
             ++s_cur;
             active = true;
             next_ray = true;
@@ -1106,7 +1106,7 @@ extern "C" int frt_selftest_path_host(const frt_scene_view *sv, const frt_render
         f3 acc = mk3(0, 0, 0);
         for (int smp = 0; smp < p->spp; ++smp) {
             PathState P;
-            path_begin(P, S, px, py, p->nx, p->ny, p->seed, (uint32_t)pix, (uint32_t)smp);
+            path_begin(P, S, px, py, p->nx, p->ny, p->seed, (uint32_t)pix, (uint32_t)(smp + p->sample_offset));
             ++n_cam;
             for (;;) {
                 Hit h;
@@ -1185,10 +1185,12 @@ static bool params_ok(const frt_render_params *p)
     if (!(p && p->nx > 0 && p->ny > 0 && p->spp > 0 && (T % 8) == 0 && T <= 256 && p->shard_count >= 1 &&
           p->shard_index >= 0 && p->shard_index < p->shard_count && p->max_depth >= -1 && p->max_depth < 100000))
         return false;
+    if (p->sample_offset < 0 || (int64_t)p->sample_offset + p->spp > (int64_t)0xffffffffLL) return false;
     if (p->integrator == FRT_INTEGRATOR_PATH || p->integrator == FRT_INTEGRATOR_AO ||
         p->integrator == FRT_INTEGRATOR_NORMALS)
         return true;
-    return p->integrator == FRT_INTEGRATOR_PSSMLT && p->mlt_chains > 0 && p->mlt_bootstrap > 0;
+    return p->integrator == FRT_INTEGRATOR_PSSMLT && p->mlt_chains > 0 && p->mlt_bootstrap > 0 &&
+           p->sample_offset == 0;
 }
 static int my_tiles(const frt_render_params *p)
 {
@@ -1504,6 +1506,7 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     }
     DevWork W{};
     W.nx = p->nx; W.ny = p->ny; W.spp = p->spp; W.max_depth = p->max_depth; W.seed = p->seed;
+    W.s_off = (uint32_t)p->sample_offset;
     W.tile = T; W.ntx = (p->nx + T - 1) / T; W.shard_index = p->shard_index; W.shard_count = p->shard_count;
     W.spi = spi; W.n_chunks = n_chunks; W.n_items = (uint32_t)n_items; W.n_slots = n_slots;
     W.partial = c->partial; W.counter = c->counter; W.wave_rays = c->wave_rays;

@@ -4,11 +4,12 @@
 //
 //   frt_render --scene cornell|veach|obj --obj FILE [--res 1920x1080] [--ns 512]
 //              [--seed 0] [--gpus 1] [--integrator path|pssmlt|ao|normals] [--chains 262144]
-//              [--env r,g,b] [--out out.pfm]
+//              [--env r,g,b] [--out out.pfm] [--png out.png]
 //
 // --integrator pssmlt: renderer<pssmlt_gpu>, --ns = mutations per pixel.
 // --integrator ao / normals: renderer<ao_gpu> / renderer<normals_gpu> (ao.h, debug_renderer.h).
 // --env: constant environment colour (the reference scenes' is black).
+// --png: also the tonemapped display image (viewer::add_sample bytes, image::save_image).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -18,7 +19,7 @@
 
 int main(int argc, char **argv)
 {
-    std::string scene = "cornell", obj, out = "out.pfm", integrator = "path";
+    std::string scene = "cornell", obj, out = "out.pfm", integrator = "path", png;
     int nx = 512, ny = 512, gpus = 1, chains = 1 << 18;
     long ns = 100;
     unsigned seed = 0;
@@ -37,6 +38,7 @@ int main(int argc, char **argv)
         else if (a == "--seed") seed = (unsigned)std::strtoul(next(), nullptr, 10);
         else if (a == "--gpus") gpus = std::atoi(next());
         else if (a == "--out") out = next();
+        else if (a == "--png") png = next();
         else if (a == "--integrator") integrator = next();
         else if (a == "--chains") chains = std::atoi(next());
         else if (a == "--env") {
@@ -79,6 +81,10 @@ int main(int argc, char **argv)
         }
         film.save_pfm(out);
         std::printf("Saved %s\n", out.c_str());
+        if (!png.empty()) {
+            film.save_image(png, FRT_IMAGE_PNG);
+            std::printf("Saved %s\n", png.c_str());
+        }
     } catch (const std::exception &e) {
         std::fprintf(stderr, "frt_render: %s\n", e.what());
         return 1;

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FRT_ABI_VERSION 4
+#define FRT_ABI_VERSION 5
 
 enum {
     FRT_OK = 0,
@@ -132,6 +132,11 @@ typedef struct frt_render_params {
      * mlt_bootstrap = paths for the normaliser b (pssmlt.h:12 N_Init = 10000). */
     int32_t mlt_chains;
     int32_t mlt_bootstrap;
+    /* progressive rendering (path / AO / normals): this call renders samples
+     * [sample_offset, sample_offset + spp) of every pixel -- the RNG streams
+     * are keyed by the global sample index, so passes of 64 + 64 + ... samples
+     * average to the film of one call with their total (frt_film_accumulate). */
+    int32_t sample_offset;
 } frt_render_params;
 
 typedef struct frt_stats {
@@ -238,6 +243,23 @@ int frt_write_tessellated_obj(const char *src_obj, int k, const char *dst_obj);
 
 /* image_pfm::save_image layout (image.h:89-118), path used as given. */
 int frt_write_pfm(const char *path, int nx, int ny, const float *rgb);
+
+/* ---- film / output side (viewer.cpp:109-132, image.cpp:24-58) ---- */
+/* Progressive accumulation: acc = (acc * acc_spp + pass * pass_spp) / (acc_spp + pass_spp),
+ * per element (n floats), so a film accumulated over passes is the mean over all of
+ * their samples (viewer.cpp:111 divides by the total ns). */
+int frt_film_accumulate(float *acc, int64_t acc_spp, const float *pass, int64_t pass_spp, int64_t n);
+/* viewer::add_sample's display mapping (viewer.cpp:115-117): per channel
+ * int(pow(1 - exp(-x), 1/2.2) * 255 + 0.5), stored as a byte, for a mean film
+ * (nx*ny*3 floats, y = 0 bottom row) -> u8 rgb in the same layout. */
+int frt_tonemap_u8(const float *rgb, int nx, int ny, uint8_t *out_u8);
+/* image::save_image (image.cpp:24-58): u8 rgb (y = 0 bottom row) flipped to
+ * top-down rows (stbi_flip_vertically_on_write) and written as PNG or BMP.  The
+ * extension is appended when missing, as the reference does.  The reference's
+ * switch writes BMP bytes for STBI_JPG and JPEG for STBI_BMP (image.cpp:40-52);
+ * FRT_IMAGE_JPG reproduces the first, and JPEG encoding is not provided. */
+enum { FRT_IMAGE_PNG = 0, FRT_IMAGE_BMP = 1, FRT_IMAGE_JPG = 2 };
+int frt_write_image(const char *path, int nx, int ny, const uint8_t *rgb_u8, int format);
 
 /* ---- self-test hook for CPU-only unit tests: runs the megakernel's per-lane
  *      path code (frt_path.hpp) on the host over the flattened fp32 scene for

@@ -97,6 +97,18 @@ struct viewer {
         std::vector<float> f(fout_image.begin(), fout_image.end());
         check(frt_write_pfm(path.c_str(), nx, ny, f.data()), "frt_write_pfm");
     }
+    // image::save_image of out_image (image.cpp:24-58): FRT_IMAGE_PNG / _BMP / _JPG (BMP bytes, as the
+    // reference's switch writes); path used as given, extension appended when missing
+    void save_image(const std::string &path, int format = FRT_IMAGE_PNG) const
+    {
+        check(frt_write_image(path.c_str(), nx, ny, out_image.data(), format), "frt_write_image");
+    }
+    // a whole mean film at once (the GPU path): linear film + display bytes (frt_tonemap_u8)
+    void store_film(const float *rgb)
+    {
+        for (size_t i = 0; i < fout_image.size(); ++i) fout_image[i] = rgb[i];
+        check(frt_tonemap_u8(rgb, nx, ny, out_image.data()), "frt_tonemap_u8");
+    }
     const int nx, ny;
     const uint64_t ns;
     const int num_channels;

@@ -91,6 +91,8 @@ def lib():
         L.ora_mlt_eye_path.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, dp, dp]
         L.ora_mlt_eye_path.restype = None
         L.ora_write_pfm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, dp]
+        L.ora_tonemap_u8.argtypes = [dp, ctypes.c_long, ctypes.c_void_p]
+        L.ora_tonemap_u8.restype = None
         L.ora_kat_metal.argtypes = [dp, dp, dp, dp, dp]
         L.ora_kat_metal.restype = None
         L.ora_kat_conductor.argtypes = [dp, dp, ctypes.c_int, ctypes.c_double, dp, dp, dp, ctypes.c_double,

@@ -2236,6 +2236,11 @@ void ora_kat_list_hit(int ntri, int nsph, const double *geom, const double *o, c
 }
 
 /* image_pfm::save_image (image.h:89-118): "PF\n<w> <h>\n-1\n" + float rows y=0..h-1 */
+/* viewer::add_sample's display bytes (viewer.cpp:115-117) */
+void ora_tonemap_u8(const double *rgb, long n, uint8_t *out)
+{
+    for (long i = 0; i < n; ++i) out[i] = (uint8_t)(int)(pow(1 - exp(-rgb[i]), 1 / 2.2) * 255 + .5);
+}
 int ora_write_pfm(const char *path, int nx, int ny, const double *rgb)
 {
     FILE *f = fopen(path, "wb");

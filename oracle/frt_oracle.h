@@ -155,6 +155,9 @@ void   ora_kat_sort(const double *keys, int n, int32_t *perm_out);
 
 void   ora_kat_list_hit(int ntri, int nsph, const double *geom, const double *o, const double *d, double *out3);
 
+/* viewer::add_sample's display bytes (viewer.cpp:115-117), n values */
+void ora_tonemap_u8(const double *rgb, long n, uint8_t *out);
+
 /* PFM writer with image_pfm::save_image byte layout (image.h:89-118). */
 int  ora_write_pfm(const char *path, int nx, int ny, const double *rgb);
 

@@ -25,11 +25,14 @@ def read_pfm(path):
 
 def test_cli_path_matches_binding(cornell_obj, tmp_path):
     out = str(tmp_path / "c.pfm")
+    png = str(tmp_path / "c.png")
     r = subprocess.run([CLI, "--scene", "cornell", "--obj", cornell_obj, "--res", "64x48", "--ns", "8",
-                        "--seed", "3", "--out", out], capture_output=True, text=True, timeout=300)
+                        "--seed", "3", "--out", out, "--png", png], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert "Rays/second" in r.stdout or "rays" in r.stdout.lower()
     img = read_pfm(out)
+    from test_film import read_png
+    assert np.array_equal(read_png(png), frt.tonemap_u8(img)[::-1])   # display bytes, top-down rows
     ctx = frt.Context(0)
     try:
         ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, 64 / 48))

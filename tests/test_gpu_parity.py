@@ -260,3 +260,17 @@ def test_unsupported_material_rejected(ctx, cornell_obj):
     ctypes.cast(v.materials, ctypes.POINTER(frt.Material))[0].type = 7      # no such material
     with pytest.raises(frt.FrtError, match="not supported"):
         ctx.upload(v)
+
+
+def test_progressive_passes(ctx, cornell_obj):
+    """frt_render_params.sample_offset: passes [0, 3) + [3, 8) accumulated
+    (frt_film_accumulate) equal one 8-spp call up to fp32 summation order."""
+    hs = frt.HostScene("cornell_box_obj", cornell_obj, 1.0)
+    ctx.upload(hs)
+    nx = ny = 64
+    full, st = ctx.render(frt.RenderParams.make(nx, ny, 8, seed=9))
+    p1, s1 = ctx.render(frt.RenderParams.make(nx, ny, 3, seed=9))
+    p2, s2 = ctx.render(frt.RenderParams.make(nx, ny, 5, seed=9, sample_offset=3))
+    acc = frt.film_accumulate(p1, 3, p2, 5)
+    assert s1.rays + s2.rays == st.rays
+    assert np.allclose(acc, full, rtol=1e-5, atol=1e-7)
