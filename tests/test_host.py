@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_library_exports_every_declared_symbol():
     hdr = open(os.path.join(ROOT, "include", "frt.h")).read()
-    declared = set(re.findall(r"\b(frt_[a-z_]+)\s*\(", hdr))
+    declared = set(re.findall(r"\b(frt_[a-z0-9_]+)\s*\(", hdr))
     assert declared == set(frt.EXPORTS)
     L = frt.lib()
     for name in declared:
