@@ -1,0 +1,15 @@
+// frt_lbvh.hpp -- GPU linear BVH builder (frt_lbvh.hip), internal to libfrt.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <string>
+
+namespace frt {
+// n >= 2 primitive boxes (box6: lo xyz, hi xyz per prim, fp32 rounded outward)
+// -> n-1 internal nodes: child2 (internal index >= 0 or ~sorted leaf position),
+// node_box6 (per internal node), order (sorted leaf position -> prim index),
+// ms = device time of the build passes.  Runs on `st` (current device).
+// Returns 0, or -1 with `err` set.
+int lbvh_build(hipStream_t st, int n, const float *box6, int32_t *child2, float *node_box6, int32_t *order, float *ms,
+               std::string &err);
+}  // namespace frt

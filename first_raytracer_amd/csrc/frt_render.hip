@@ -30,6 +30,7 @@
 #include "frt_device.hpp"
 #include "frt_path.hpp"
 #include "frt_mlt.hpp"
+#include "frt_lbvh.hpp"
 
 using namespace frt;
 
@@ -600,6 +601,21 @@ extern "C" int frt_destroy(frt_ctx *c)
 }
 
 extern "C" const char *frt_last_error(const frt_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+// GPU BVH build on this context's device and stream (frt_lbvh.hip); called
+// by frt_scene_build_bvh_gpu (csrc/host/scene.cpp).  Internal to libfrt.so.
+extern "C" int frt_internal_lbvh(frt_ctx *c, int n, const float *box6, int32_t *child2, float *node_box6,
+                                 int32_t *order, double *ms)
+{
+    if (!c || n < 2 || !box6 || !child2 || !node_box6 || !order) return FRT_E_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    float dev_ms = 0.0f;
+    std::string err;
+    if (frt::lbvh_build(c->stream, n, box6, child2, node_box6, order, &dev_ms, err) != 0)
+        return set_err(c, FRT_E_HIP, err);
+    if (ms) *ms = dev_ms;
+    return FRT_OK;
+}
 
 // ---- scene flattening: DFS order, fp32 conversion with outward-rounded boxes ----
 static inline float round_down(double x)

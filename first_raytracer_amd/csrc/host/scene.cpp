@@ -843,6 +843,93 @@ extern "C" int frt_scene_finish(frt_host_scene *s, int world_kind)
     return FRT_OK;
 }
 
+// ---- GPU BVH build (frt_lbvh.hip through the context's device) ----
+extern "C" int frt_internal_lbvh(frt_ctx *c, int n, const float *box6, int32_t *child2, float *node_box6,
+                                 int32_t *order, double *ms);
+
+static inline float f_down(double x)
+{
+    float f = (float)x;
+    if ((double)f > x) f = std::nextafter(f, -INFINITY);
+    return f;
+}
+static inline float f_up(double x)
+{
+    float f = (float)x;
+    if ((double)f < x) f = std::nextafter(f, INFINITY);
+    return f;
+}
+
+extern "C" int frt_scene_build_bvh_gpu(frt_host_scene *s, frt_ctx *ctx, double *device_ms)
+{
+    if (!s || !ctx || !s->finished) return FRT_E_INVALID;
+    const auto t0 = std::chrono::steady_clock::now();
+    const std::vector<int32_t> prims = (s->world_kind == FRT_WORLD_LIST) ? s->list : s->world;
+    const int n = (int)prims.size();
+    if (n == 0) return FRT_E_INVALID;
+    std::vector<double> nbox;
+    std::vector<int32_t> nchild;
+    int32_t root = 0;
+    double ms = 0.0;
+    if (n == 1) {
+        root = ~prims[0];
+    } else {
+        // fp32 boxes rounded outward: they contain the fp64 primitives, so the
+        // tree's boxes do too (flatten_scene pads them again for the fp32 rays)
+        std::vector<float> box6(6 * (size_t)n);
+        for (int i = 0; i < n; ++i) {
+            const int ref = prims[i];
+            double lo[3], hi[3];
+            if (ref & FRT_PRIM_SPHERE) {
+                const double *q = &s->sphere[4 * (ref & ~FRT_PRIM_SPHERE)];
+                for (int k = 0; k < 3; ++k) { lo[k] = q[k] - q[3]; hi[k] = q[k] + q[3]; }
+            } else {
+                const double *v = &s->tri_v[9 * ref];
+                for (int k = 0; k < 3; ++k) {
+                    lo[k] = std::fmin(std::fmin(v[k], v[3 + k]), v[6 + k]);
+                    hi[k] = std::fmax(std::fmax(v[k], v[3 + k]), v[6 + k]);
+                }
+            }
+            for (int k = 0; k < 3; ++k) { box6[6 * i + k] = f_down(lo[k]); box6[6 * i + 3 + k] = f_up(hi[k]); }
+        }
+        std::vector<int32_t> child2(2 * (size_t)(n - 1)), order(n);
+        std::vector<float> nb6(6 * (size_t)(n - 1));
+        const int rc = frt_internal_lbvh(ctx, n, box6.data(), child2.data(), nb6.data(), order.data(), &ms);
+        if (rc != FRT_OK) return rc;
+        nbox.assign(nb6.begin(), nb6.end());
+        nchild.resize(child2.size());
+        for (size_t i = 0; i < child2.size(); ++i) {
+            const int c = child2[i];
+            if (c < 0 && (~c >= n || order[~c] < 0 || order[~c] >= n)) return FRT_E_HIP;
+            if (c >= n - 1) return FRT_E_HIP;
+            nchild[i] = c >= 0 ? c : ~prims[order[~c]];
+        }
+    }
+    // depth of the new tree (levels of interior nodes on the longest path)
+    int depth = 0;
+    if (root >= 0 && !nchild.empty()) {
+        std::vector<std::pair<int, int>> st{{0, 1}};
+        size_t visited = 0;
+        while (!st.empty()) {
+            const auto [node, d] = st.back();
+            st.pop_back();
+            if (++visited > nchild.size()) return FRT_E_HIP;   // not a tree
+            depth = std::max(depth, d);
+            for (int side = 0; side < 2; ++side)
+                if (nchild[2 * node + side] >= 0) st.push_back({nchild[2 * node + side], d + 1});
+        }
+    }
+    s->node_box = std::move(nbox);
+    s->node_child = std::move(nchild);
+    s->root = root;
+    s->bvh_depth = depth;
+    s->world_kind = FRT_WORLD_BVH;
+    s->list.clear();
+    s->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (device_ms) *device_ms = ms;
+    return FRT_OK;
+}
+
 extern "C" int frt_scene_view_get(const frt_host_scene *s, frt_scene_view *v)
 {
     if (!s || !v || !s->finished) return FRT_E_INVALID;

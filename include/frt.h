@@ -234,6 +234,14 @@ int frt_scene_set_camera(frt_host_scene *s, const double *lookfrom, const double
 int frt_scene_set_env(frt_host_scene *s, const double *rgb);
 /* world_kind FRT_WORLD_BVH (create_bvh) or FRT_WORLD_LIST */
 int frt_scene_finish(frt_host_scene *s, int world_kind);
+/* GPU BVH builder: replaces the finished scene's world
+ * (BVH or list) with a linear BVH over the same world prims built on ctx's
+ * device -- Morton codes, radix sort, Karras hierarchy, atomic refit
+ * (csrc/frt_lbvh.hip) -- in place of parallel_bvh_node::create_bvh's SAH sweep.
+ * Finish with FRT_WORLD_LIST to skip the host build.  The topology differs
+ * from the reference's, so exact-t ties between primitives may resolve
+ * differently.  device_ms (optional) = device time of the build passes. */
+int frt_scene_build_bvh_gpu(frt_host_scene *s, frt_ctx *ctx, double *device_ms);
 int frt_scene_info(const frt_host_scene *s, frt_host_scene_info *info);
 void frt_scene_destroy(frt_host_scene *s);
 
