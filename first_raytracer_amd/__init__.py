@@ -59,6 +59,9 @@ class Material(ctypes.Structure):
         return r
 
 
+# cornell_box_obj's camera (main.cpp:236-242): lookfrom (0, 1, 3.9f), vfov 40, focus 10
+CORNELL_CAMERA = {"lookfrom": (0.0, 1.0, float(np.float32(3.9))), "lookat": (0.0, 1.0, 0.0), "vup": (0.0, 1.0, 0.0),
+                  "vfov": 40.0, "aperture": 0.0, "focus": 10.0}
 MAT_TYPES = {"lambertian": 0, "diffuse_light": 1, "modified_phong": 2, "metal": 3, "dielectric": 4,
              "rough_conductor": 5}                      # FRT_MAT_*
 DISTRIBUTIONS = {"ggx": 0, "beckmann": 1}               # FRT_DIST_*

@@ -15,6 +15,7 @@ CUBE_OBJ = os.path.join(SCENES, "cube.obj")
 F32 = lambda x: float(__import__("numpy").float32(x))   # noqa: E731  (C++ float literals, e.g. 0.15f)
 CORNELL_CAM = {"lookfrom": (0.0, 1.0, F32(3.9)), "lookat": (0.0, 1.0, 0.0), "vup": (0.0, 1.0, 0.0),
                "vfov": 40.0, "aperture": 0.0, "focus": 10.0}                       # main.cpp:236-242
+assert CORNELL_CAM == __import__("first_raytracer_amd").CORNELL_CAMERA
 GOLD_ETA, GOLD_K = (1.65746, 0.880369, 0.521229), (9.22387, 6.26952, 4.837)      # main.cpp:340-344
 
 
