@@ -138,8 +138,10 @@ def main():
     ap.add_argument("--spp", type=int, default=512)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--tile", type=int, default=32)
-    ap.add_argument("--bvh", default="host", choices=["host", "gpu"],
-                    help="host: reference-topology SAH build; gpu: linear BVH built on the GPU (frt_lbvh.hip)")
+    ap.add_argument("--bvh", default="sah", choices=["host", "gpu", "sah"],
+                    help="sah (default): binned SAH tree (host); host: the reference's create_bvh topology "
+                         "(exact-t ties resolved in its order); gpu: linear BVH built on the GPU (frt_lbvh.hip). "
+                         "List-world scenes (veach) ignore it")
     ap.add_argument("--cpu-pixels", type=int, default=0, help="pixels in the CPU-baseline sample (0: calibrated)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline duration when calibrated")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -189,9 +191,8 @@ def main():
     kind, obj, scene_name = scene_spec(args.scene, workdir, tag=f"_r{rank}")
     t0 = time.perf_counter()
     gpu_build_ms = None
-    if args.bvh == "gpu":                        # OBJ load only; the BVH is built on the GPU below
-        if kind != "cornell_box_obj":
-            raise SystemExit("--bvh gpu: cornell-camera OBJ scenes only")
+    bvh = args.bvh if kind == "cornell_box_obj" else "host"   # veach: list world, no BVH
+    if bvh in ("gpu", "sah"):                    # OBJ load only; the BVH is built below
         hs = frt.HostScene.from_spec({"objects": [{"obj": obj, "geo": True}], "camera": frt.CORNELL_CAMERA,
                                       "world": "list"}, nx / ny)
     else:
@@ -206,7 +207,9 @@ def main():
     integ = {"path": frt.FRT_INTEGRATOR_PATH, "ao": frt.FRT_INTEGRATOR_AO,
              "normals": frt.FRT_INTEGRATOR_NORMALS}.get(args.integrator, frt.FRT_INTEGRATOR_PSSMLT)
     ctx = frt.Context(local)
-    if args.bvh == "gpu":
+    if bvh == "sah":
+        hs.build_bvh_sah()                       # binned SAH on the host (in host_build_s)
+    if bvh == "gpu":
         hs.build_bvh_gpu(ctx)                    # warm-up build (hipcub kernels load on first use)
         tg = time.perf_counter()
         gpu_build_ms = hs.build_bvh_gpu(ctx)     # Morton + radix sort + Karras + refit (frt_lbvh.hip)
@@ -336,7 +339,7 @@ def main():
             "mutations_per_step": int(last.samples) if args.integrator == "pssmlt" else None,
             "rays_per_step": int(rays // args.steps),
             "setup_s": round(setup_s, 2), "host_build_s": round(build_s, 2), "upload_s": round(upload_s, 2),
-            "bvh": ("gpu-lbvh" if args.bvh == "gpu" else "host-sah (reference topology)"),
+            "bvh": {"gpu": "gpu-lbvh", "sah": "binned SAH (host)"}.get(bvh, "create_bvh (reference topology)"),
             "gpu_build_ms": None if gpu_build_ms is None else round(gpu_build_ms, 3),
             "value_per_gpu": round(value / world, 1),
             "image_mean": [round(float(x), 6) for x in film_np.reshape(-1, 3).mean(0)],

@@ -143,6 +143,7 @@ EXPORTS = ("frt_get_abi_version", "frt_create", "frt_destroy", "frt_last_error",
            "frt_shard_slot_count", "frt_shard_slots", "frt_render", "frt_render_multi", "frt_render_device",
            "frt_scene_create", "frt_scene_new", "frt_scene_add_obj", "frt_scene_add_sphere", "frt_scene_set_camera",
            "frt_scene_set_env", "frt_scene_finish", "frt_scene_build_bvh_gpu",
+           "frt_scene_build_bvh_sah",
            "frt_scene_view_get", "frt_scene_info", "frt_scene_destroy", "frt_write_tessellated_obj",
            "frt_write_pfm", "frt_film_accumulate", "frt_tonemap_u8", "frt_write_image", "frt_selftest_path_host",
            "frt_selftest_mlt_paths_host")
@@ -193,6 +194,7 @@ def lib():
     L.frt_scene_set_env.argtypes = [vp, dp]
     L.frt_scene_finish.argtypes = [vp, ctypes.c_int]
     L.frt_scene_build_bvh_gpu.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_double)]
+    L.frt_scene_build_bvh_sah.argtypes = [vp]
     L.frt_write_tessellated_obj.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p]
     L.frt_write_pfm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, vp]
     L.frt_film_accumulate.argtypes = [vp, ctypes.c_int64, vp, ctypes.c_int64, ctypes.c_int64]
@@ -304,6 +306,12 @@ class HostScene:
             "lights": arr(v.lights, v.n_lights, np.int32),
             "list": arr(v.list, v.n_list, np.int32),
         }
+
+    def build_bvh_sah(self):
+        """Replace the world by a binned-SAH tree (frt_scene_build_bvh_sah); returns build ms."""
+        _check(lib().frt_scene_build_bvh_sah(self.ptr), "frt_scene_build_bvh_sah")
+        lib().frt_scene_info(self.ptr, ctypes.byref(self.info))
+        return self.info.build_ms
 
     def build_bvh_gpu(self, ctx):
         """Replace the world by a GPU-built linear BVH (frt_scene_build_bvh_gpu);

@@ -4,12 +4,14 @@
 //
 //   frt_render --scene cornell|veach|obj --obj FILE [--res 1920x1080] [--ns 512]
 //              [--seed 0] [--gpus 1] [--integrator path|pssmlt|ao|normals] [--chains 262144]
-//              [--env r,g,b] [--out out.pfm] [--png out.png]
+//              [--env r,g,b] [--out out.pfm] [--png out.png] [--bvh reference|sah]
 //
 // --integrator pssmlt: renderer<pssmlt_gpu>, --ns = mutations per pixel.
 // --integrator ao / normals: renderer<ao_gpu> / renderer<normals_gpu> (ao.h, debug_renderer.h).
 // --env: constant environment colour (the reference scenes' is black).
 // --png: also the tonemapped display image (viewer::add_sample bytes, image::save_image).
+// --bvh sah: rebuild the scene's BVH with the binned SAH builder (faster traversal;
+//   exact-t ties then follow that tree's order instead of create_bvh's).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -19,7 +21,7 @@
 
 int main(int argc, char **argv)
 {
-    std::string scene = "cornell", obj, out = "out.pfm", integrator = "path", png;
+    std::string scene = "cornell", obj, out = "out.pfm", integrator = "path", png, bvh = "reference";
     int nx = 512, ny = 512, gpus = 1, chains = 1 << 18;
     long ns = 100;
     unsigned seed = 0;
@@ -39,6 +41,7 @@ int main(int argc, char **argv)
         else if (a == "--gpus") gpus = std::atoi(next());
         else if (a == "--out") out = next();
         else if (a == "--png") png = next();
+        else if (a == "--bvh") bvh = next();
         else if (a == "--integrator") integrator = next();
         else if (a == "--chains") chains = std::atoi(next());
         else if (a == "--env") {
@@ -53,6 +56,8 @@ int main(int argc, char **argv)
         const std::string kind = scene == "cornell" ? "cornell_box_obj" : scene == "veach" ? "veach_mis" : "obj_smooth";
         frt::Scene s(kind, obj, double(nx) / double(ny));
         if (has_env) s.set_env(env[0], env[1], env[2]);
+        if (bvh == "sah") s.build_bvh_sah();
+        else if (bvh != "reference") { std::fprintf(stderr, "unknown --bvh %s\n", bvh.c_str()); return 2; }
         std::printf("BVH construction took me %g seconds (%d triangles, depth %d).\n", s.info().build_ms * 1e-3,
                     s.info().n_tris, s.info().bvh_depth);
         frt::viewer film(nx, ny, (uint64_t)ns);

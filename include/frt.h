@@ -242,6 +242,10 @@ int frt_scene_finish(frt_host_scene *s, int world_kind);
  * from the reference's, so exact-t ties between primitives may resolve
  * differently.  device_ms (optional) = device time of the build passes. */
 int frt_scene_build_bvh_gpu(frt_host_scene *s, frt_ctx *ctx, double *device_ms);
+/* Binned SAH tree (32 centroid bins per axis, host threads) over the same
+ * world prims: better traversal than the reference's sweep on large meshes
+ * (same tie caveat as the GPU tree). */
+int frt_scene_build_bvh_sah(frt_host_scene *s);
 int frt_scene_info(const frt_host_scene *s, frt_host_scene_info *info);
 void frt_scene_destroy(frt_host_scene *s);
 

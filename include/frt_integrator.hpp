@@ -56,6 +56,18 @@ public:
     }
     // Scene::env_map with another constant colour (material.h:206-232)
     void set_env(double r, double g, double b) { env_[0] = r; env_[1] = g; env_[2] = b; has_env_ = true; }
+    // replace the reference-topology BVH: binned SAH on the host, or the GPU
+    // linear BVH on ctx's device (frt_scene_build_bvh_sah / _gpu)
+    void build_bvh_sah()
+    {
+        check(frt_scene_build_bvh_sah(scene_.get()), "frt_scene_build_bvh_sah");
+        check(frt_scene_info(scene_.get(), &info_), "frt_scene_info");
+    }
+    void build_bvh_gpu(frt_ctx *ctx)
+    {
+        check(frt_scene_build_bvh_gpu(scene_.get(), ctx, nullptr), "frt_scene_build_bvh_gpu", ctx);
+        check(frt_scene_info(scene_.get(), &info_), "frt_scene_info");
+    }
     const frt_host_scene_info &info() const { return info_; }
 
 private:

@@ -1,8 +1,9 @@
-"""GPU BVH builder (frt_scene_build_bvh_gpu, csrc/frt_lbvh.hip): Morton keys,
-device radix sort, Karras hierarchy, atomic refit.  The tree replaces the
-reference-topology SAH tree; hits can differ from the oracle's only at exact
-t ties between primitives, so renders meet the same RMSE gate and the ray
-counts agree within rounding-divergence noise."""
+"""Alternative BVHs: the GPU builder (frt_scene_build_bvh_gpu, csrc/frt_lbvh.hip:
+Morton keys, device radix sort, Karras hierarchy, atomic refit) and the binned
+SAH builder (frt_scene_build_bvh_sah).  Either tree replaces the
+reference-topology tree; hits can differ from the oracle's only at exact t ties
+between primitives, so renders meet the same RMSE gate and the ray counts agree
+within rounding-divergence noise."""
 import numpy as np
 import pytest
 
@@ -34,17 +35,22 @@ def check_tree(hs, n_prims):
     assert internal == list(range(1, n_prims - 1))                    # every node but the root has one parent
 
 
+def build(hs, ctx, how):
+    return hs.build_bvh_gpu(ctx) if how == "gpu" else hs.build_bvh_sah()
+
+
+@pytest.mark.parametrize("how", ["gpu", "sah"])
 @pytest.mark.parametrize("spec_name", ["cornell", "conductors"])
-def test_gpu_bvh_render_matches_oracle(ctx, cornell_obj, spec_name):
+def test_gpu_bvh_render_matches_oracle(ctx, cornell_obj, spec_name, how):
     spec = ({"objects": [{"obj": cornell_obj, "geo": True}], "camera": SS.CORNELL_CAM} if spec_name == "cornell"
             else SS.cornell_conductors())
     spec = dict(spec, world="list")                                      # skip the host SAH build
     nx, ny, spp = 96, 72, 16
     hs = frt.HostScene.from_spec(spec, nx / ny)
     n = hs.info.n_list
-    dev_ms = hs.build_bvh_gpu(ctx)
+    ms = build(hs, ctx, how)
     check_tree(hs, n)
-    print(spec_name, "gpu build", dev_ms, "ms depth", hs.info.bvh_depth)
+    print(spec_name, how, "build", ms, "ms depth", hs.info.bvh_depth)
     ctx.upload(hs)
     film, st = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=5))
     ref, cnt = oracle.OracleScene.from_spec(dict(spec, world="bvh"), nx / ny).render(nx, ny, spp, seed=5)
@@ -53,8 +59,9 @@ def test_gpu_bvh_render_matches_oracle(ctx, cornell_obj, spec_name):
     assert rmse(film, ref) <= 1e-3
 
 
+@pytest.mark.parametrize("how", ["gpu", "sah"])
 @pytest.mark.parametrize("flags", [0, frt.FRT_FLAG_BVH2])
-def test_gpu_bvh_large_scene_matches_host_tree(ctx, cornell_obj, tmp_path, flags):
+def test_gpu_bvh_large_scene_matches_host_tree(ctx, cornell_obj, tmp_path, flags, how):
     """~20k triangles (HBM plan: BVH4Q from the GPU-built binary tree, or binary
     with FRT_FLAG_BVH2): same image as the host SAH tree up to exact-tie noise."""
     dst = str(tmp_path / "t24.obj")
@@ -65,11 +72,11 @@ def test_gpu_bvh_large_scene_matches_host_tree(ctx, cornell_obj, tmp_path, flags
     ref, st0 = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=1, flags=flags))
     hs = frt.HostScene.from_spec({"objects": [{"obj": dst, "geo": True}], "camera": SS.CORNELL_CAM, "world": "list"},
                                  nx / ny)
-    dev_ms = hs.build_bvh_gpu(ctx)
+    ms = build(hs, ctx, how)
     check_tree(hs, sah.info.n_tris)
     ctx.upload(hs)
     film, st = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=1, flags=flags))
-    print("t24 gpu build", dev_ms, "ms; depth", hs.info.bvh_depth, "vs SAH", sah.info.bvh_depth)
+    print("t24", how, "build", ms, "ms; depth", hs.info.bvh_depth, "vs reference", sah.info.bvh_depth)
     assert st.scene_in_lds == 0 and st.camera_rays == st0.camera_rays
     assert abs(st.rays - st0.rays) / st0.rays < 1e-3
     assert rmse(film, ref) <= 1e-4

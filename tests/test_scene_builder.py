@@ -112,3 +112,25 @@ def test_ao_rejects_metal():
                                np.arange(64, dtype=np.int32))
     with pytest.raises(RuntimeError):
         osc.render(8, 8, 1, integrator=2)
+
+
+def test_binned_sah_tree_host(cornell_obj):
+    """frt_scene_build_bvh_sah: a valid tree over every world prim, and the
+    device path code over it (host replay) matches the oracle's render."""
+    spec = SS.cornell_conductors(world="list")
+    hs = frt.HostScene.from_spec(spec, 1.0)
+    n = hs.info.n_list
+    hs.build_bvh_sah()
+    a = hs.arrays()
+    assert hs.info.world_kind == 0 and hs.info.n_nodes == n - 1
+    child = a["node_child"].reshape(-1)
+    assert sorted(~c for c in child if c < 0) == sorted(list(range(hs.info.n_tris)) +
+                                                       [frt.FRT_PRIM_SPHERE | k for k in range(2)])
+    assert sorted(c for c in child if c >= 0) == [i for i in range(n - 1) if i != a["root"]]
+    boxes = a["node_box"]
+    assert np.all(boxes[:, :3] <= boxes[:, 3:])
+    nx = ny = 40
+    g, st = frt.selftest_path_host(hs, frt.RenderParams.make(nx, ny, 4, seed=8), np.arange(nx * ny, dtype=np.int32))
+    ref, cnt = oracle.OracleScene.from_spec(dict(spec, world="bvh"), 1.0).render(nx, ny, 4, seed=8)
+    assert st.camera_rays == cnt.camera_rays
+    assert float(np.sqrt(np.mean((g.reshape(-1, 3) - ref) ** 2))) < 1e-3
