@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--res", default="1920x1080")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variants", default="default,no_lds")
+    ap.add_argument("--bvh", default="sah", choices=["host", "sah"],
+                    help="sah: binned SAH tree (bench default); host: the reference topology")
     args = ap.parse_args()
     import torch  # noqa: F401  (single HIP runtime)
     import first_raytracer_amd as frt
@@ -47,7 +49,12 @@ def main():
     def opt(v, key):
         return next((o[len(key):] for o in v.split("/")[1:] if o.startswith(key)), "")
 
-    hs = frt.HostScene(kind, obj, nx / ny)
+    if args.bvh == "sah" and kind == "cornell_box_obj":
+        hs = frt.HostScene.from_spec({"objects": [{"obj": obj, "geo": True}], "camera": frt.CORNELL_CAMERA,
+                                      "world": "list"}, nx / ny)
+        hs.build_bvh_sah()
+    else:
+        hs = frt.HostScene(kind, obj, nx / ny)
     ctxs = {}
     for v in chosen:
         leaf = opt(v, "leaf")
