@@ -80,3 +80,28 @@ def test_gpu_bvh_large_scene_matches_host_tree(ctx, cornell_obj, tmp_path, flags
     assert st.scene_in_lds == 0 and st.camera_rays == st0.camera_rays
     assert abs(st.rays - st0.rays) / st0.rays < 1e-3
     assert rmse(film, ref) <= 1e-4
+
+
+def test_bench_default_tree_all_integrators(ctx, cornell_obj):
+    """The bench's default scene build (binned SAH tree) against the oracle
+    (reference topology) for every integrator: path, PSS-MLT short chains,
+    AO, normals."""
+    nx, ny = 64, 48
+    hs = frt.HostScene.from_spec({"objects": [{"obj": cornell_obj, "geo": True}], "camera": frt.CORNELL_CAMERA,
+                                  "world": "list"}, nx / ny)
+    hs.build_bvh_sah()
+    hs.set_env((1.0, 1.0, 1.0))
+    ctx.upload(hs)
+    osc = oracle.OracleScene("cornell_box_obj", cornell_obj, nx / ny)
+    osc.set_env((1.0, 1.0, 1.0))
+    for integ in (frt.FRT_INTEGRATOR_PATH, frt.FRT_INTEGRATOR_AO, frt.FRT_INTEGRATOR_NORMALS):
+        film, st = ctx.render(frt.RenderParams.make(nx, ny, 16, seed=6, integrator=integ))
+        ref, cnt = osc.render(nx, ny, 16, seed=6, integrator=integ)
+        assert st.camera_rays == cnt.camera_rays and abs(st.rays - cnt.rays) / cnt.rays < 2e-3
+        assert rmse(film, ref) <= 1e-3, integ
+    chains, mpp = 1536, 4
+    film = np.zeros((ny, nx, 3), np.float32)
+    film, st = ctx.render(frt.RenderParams.pssmlt(nx, ny, mpp, chains, seed=3, bootstrap=2000), film)
+    ref, b, cnt = osc.mlt_render(nx, ny, chains, mpp * nx * ny // chains, seed=3, n_init=2000)
+    assert abs(st.rays - cnt.rays) / cnt.rays < 2e-3
+    assert rmse(film, ref) <= 1e-3 * max(1.0, float(np.abs(ref).max()))
