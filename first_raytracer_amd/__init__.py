@@ -18,10 +18,11 @@ LIB_PATH = os.environ.get("FRT_LIB_PATH") or os.path.join(HERE, "libfrt.so")
 FRT_WORLD_BVH, FRT_WORLD_LIST = 0, 1
 FRT_MAT_LAMBERTIAN, FRT_MAT_DIFFUSE_LIGHT = 0, 1
 FRT_PRIM_SPHERE = 1 << 30
-ABI_VERSION = 5                 # include/frt.h FRT_ABI_VERSION (frt_stats / frt_material layout)
+ABI_VERSION = 6                 # include/frt.h FRT_ABI_VERSION (frt_stats / frt_material layout)
 FRT_MAT_LAMBERTIAN, FRT_MAT_DIFFUSE_LIGHT, FRT_MAT_MODIFIED_PHONG, FRT_MAT_METAL, FRT_MAT_DIELECTRIC = 0, 1, 2, 3, 4
 FRT_MAT_ROUGH_CONDUCTOR = 5
 FRT_DIST_GGX, FRT_DIST_BECKMANN = 0, 1
+FRT_TEX_CONSTANT, FRT_TEX_CHECKER = 0, 1
 FRT_FLAG_NO_LDS_SCENE = 1
 FRT_FLAG_WAVES5 = 2
 FRT_FLAG_WAVES6 = 4
@@ -43,7 +44,9 @@ class Material(ctypes.Structure):
     _fields_ = [("type", ctypes.c_int32), ("distribution", ctypes.c_int32),
                 ("albedo", ctypes.c_double * 3), ("emit", ctypes.c_double * 3),
                 ("specular", ctypes.c_double * 3), ("exponent", ctypes.c_double), ("ior", ctypes.c_double),
-                ("alpha", ctypes.c_double), ("eta", ctypes.c_double * 3), ("k", ctypes.c_double * 3)]
+                ("alpha", ctypes.c_double), ("eta", ctypes.c_double * 3), ("k", ctypes.c_double * 3),
+                ("texture", ctypes.c_int32), ("reserved", ctypes.c_int32), ("tex_odd", ctypes.c_double * 3),
+                ("tex_scale", ctypes.c_double * 2)]
 
     @classmethod
     def from_spec(cls, m):
@@ -56,6 +59,11 @@ class Material(ctypes.Structure):
         r.exponent = float(m.get("exponent", 0.0))
         r.ior = float(m.get("ior", 0.0))
         r.alpha = float(m.get("alpha", 0.0))
+        tex = m.get("checker")               # {"odd": rgb, "scale": (u_scale, v_scale)}
+        if tex is not None:
+            r.texture = FRT_TEX_CHECKER
+            r.tex_odd[:] = [float(x) for x in tex["odd"]]
+            r.tex_scale[:] = [float(x) for x in tex["scale"]]
         return r
 
 
@@ -87,6 +95,7 @@ class SceneView(ctypes.Structure):
         ("env_color", ctypes.c_double * 3),
         ("cam_w", ctypes.c_double * 3),
         ("cam_half_height", ctypes.c_double),
+        ("tri_uv", ctypes.c_void_p),
     ]
 
 

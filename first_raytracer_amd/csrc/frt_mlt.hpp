@@ -129,8 +129,9 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
     f3 n;
     int mat;
     prim_shade(S, h.prim, P.ro, p, h.u, h.v, n, mat);
-    const float4 m0 = S.mats[kMatStride * mat], m1 = S.mats[kMatStride * mat + 1];
+    float4 m0 = S.mats[kMatStride * mat], m1 = S.mats[kMatStride * mat + 1];
     const int mtype = f2i(m0.w);
+    if constexpr (MATS) apply_texture(S, mat, mtype, h.prim, p, h.u, h.v, m0, m1);
     const float sc0 = src.get(M.off), sc1 = src.get(M.off + 1);   // scatter rnd (pssmlt.cpp:159-163)
     M.off += 3;                                         // consumed at every hit
     if (mtype == FRT_MAT_DIFFUSE_LIGHT && dot(n, P.rd) < 0.0f) {

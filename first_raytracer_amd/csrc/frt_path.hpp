@@ -18,8 +18,9 @@ FRT_HD int f2i(float f) { return __builtin_bit_cast(int, f); }
 FRT_HD float i2f(int i) { return __builtin_bit_cast(float, i); }
 // materials: kMatStride float4 per material (frt_upload_scene packs them):
 // m0 = (albedo | kd | metal albedo | rough eta, type), m1 = (emit | ks,
-// exponent | ior | alpha), m2 = (rough k, distribution)
-constexpr int kMatStride = 3;
+// exponent | ior | alpha), m2 = (rough k, distribution), m3 = (checker tex1
+// colour, texture kind), m4 = (u_scale, v_scale, -, -)
+constexpr int kMatStride = 5;
 FRT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
 // true if the predicate holds on any active lane of the wave (the host self-test is one lane)
 FRT_HD bool wave_any(bool x)
@@ -45,7 +46,8 @@ struct DevScene {
     const float4 *tnorm;     // 3 x float4 per triangle: vertex normals (smooth shading only)
     const float4 *spheres;   // (centre, radius)
     const int *sphere_mat;
-    const float4 *mats;      // 2 x float4 per material: (albedo, type) | (emit, -)
+    const float4 *mats;      // kMatStride x float4 per material (see kMatStride)
+    const float4 *tuv;       // 2 x float4 per triangle: (uv0, uv1) | (uv2, -): texture coordinates (textured scenes)
     const int *lights;       // device prim refs
     const int *list;         // device prim refs (list worlds)
     const uint4 *nodes4;     // 4 x uint4 per 4-wide node (HBM-resident scenes; DESIGN.md "BVH4Q")
@@ -430,6 +432,49 @@ FRT_HD f3 prim_sample(const DevScene &S, int ref, f3 o, float u0, float u1, f3 &
     return lp - o;
 }
 
+// ---- textures (texture.h:30-49), MATS kernels only ----
+// (int)x as the reference's x86-64 build computes it (cvttsd2si): NaN and
+// out-of-range give INT_MIN
+FRT_HD int x86_trunc(float x)
+{
+    if (!(x > -2147483649.0f && x < 2147483648.0f)) return (int)0x80000000;
+    return (int)x;
+}
+FRT_HD int imodulo2(int a) { const int r = a % 2; return r < 0 ? r + 2 : r; }   // util.h:125-128
+// hit texture coordinates: get_sphere_uv(p - centre) (hitable.h:15-21; the
+// offset is not normalised, as in sphere.h:52) or the OBJ vt interpolated
+// with the barycentrics (triangle.h:105-107)
+FRT_HD void prim_uv(const DevScene &S, int ref, f3 p, float u, float v, float &tu, float &tv)
+{
+    if (ref & FRT_PRIM_SPHERE) {
+        const f3 q = p - xyz(S.spheres[ref & ~FRT_PRIM_SPHERE]);
+        const float phi = atan2f(q.z, q.x), theta = asinf(q.y);
+        tu = 1.0f - (phi + kPi) / (2.0f * kPi);
+        tv = (theta + 0.5f * kPi) / kPi;
+        return;
+    }
+    const float4 a = S.tuv[2 * ref], b = S.tuv[2 * ref + 1];
+    const float w = 1.0f - u - v;
+    tu = (w * a.x + u * a.z) + v * b.x;
+    tv = (w * a.y + u * a.w) + v * b.y;
+}
+// checker_texture::value: the material's textured colour (m0 for lambertian /
+// modified_phong, m1 for dielectric / rough_conductor) becomes tex1 where
+// x * y == 1 (texture.h:37-41)
+FRT_HD void apply_texture(const DevScene &S, int mat, int mtype, int ref, f3 p, float u, float v, float4 &m0,
+                          float4 &m1)
+{
+    const float4 m3 = S.mats[kMatStride * mat + 3];
+    if (f2i(m3.w) != FRT_TEX_CHECKER) return;
+    const float4 m4 = S.mats[kMatStride * mat + 4];
+    float tu, tv;
+    prim_uv(S, ref, p, u, v, tu, tv);
+    const int x = 2 * imodulo2(x86_trunc(tu * m4.x * 2.0f)) - 1, y = 2 * imodulo2(x86_trunc(tv * m4.y * 2.0f)) - 1;
+    if (x * y != 1) return;
+    if (mtype == FRT_MAT_LAMBERTIAN || mtype == FRT_MAT_MODIFIED_PHONG) { m0.x = m3.x; m0.y = m3.y; m0.z = m3.z; }
+    else { m1.x = m3.x; m1.y = m3.y; m1.z = m3.z; }
+}
+
 // ---------------------------------------------------------------------------
 // one path as a state machine: begin() makes the camera ray, shade() consumes
 // the hit of the ray just traced and sets up the next one (shadow first,
@@ -574,8 +619,9 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
     f3 n;
     int mat;
     prim_shade(S, h.prim, P.ro, p, h.u, h.v, n, mat);
-    const float4 m0 = S.mats[kMatStride * mat], m1 = S.mats[kMatStride * mat + 1];
+    float4 m0 = S.mats[kMatStride * mat], m1 = S.mats[kMatStride * mat + 1];
     const int mtype = f2i(m0.w);
+    if constexpr (MATS) apply_texture(S, mat, mtype, h.prim, p, h.u, h.v, m0, m1);
     // diffuse_light::emitted is one-sided (material.h:184-190)
     if (mtype == FRT_MAT_DIFFUSE_LIGHT && dot(n, P.rd) < 0.0f) {
         const f3 Le = xyz(m1);

@@ -633,7 +633,7 @@ static inline float round_up(double x)
 
 // host image of the device scene (DESIGN.md "Data layout")
 struct FlatScene {
-    std::vector<float4> nodes, tris, tshade, tnorm, spheres, mats;
+    std::vector<float4> nodes, tris, tshade, tnorm, spheres, mats, tuv;
     std::vector<uint4> nodes4;   // 4-wide quantized BVH
     bool has4 = false;           // nodes4 / root4 usable
     int root4 = 0, depth4 = 0;
@@ -828,6 +828,12 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
         if (t != FRT_MAT_LAMBERTIAN && t != FRT_MAT_DIFFUSE_LIGHT && t != FRT_MAT_MODIFIED_PHONG &&
             t != FRT_MAT_METAL && t != FRT_MAT_DIELECTRIC && t != FRT_MAT_ROUGH_CONDUCTOR)
             return fail(FRT_E_UNSUPPORTED, "material type " + std::to_string(t) + " is not supported");
+        const int tex = sv->materials[i].texture;
+        if (tex != FRT_TEX_CONSTANT && tex != FRT_TEX_CHECKER)
+            return fail(FRT_E_INVALID, "material texture must be FRT_TEX_CONSTANT or FRT_TEX_CHECKER");
+        if (tex == FRT_TEX_CHECKER && (t == FRT_MAT_DIFFUSE_LIGHT || t == FRT_MAT_METAL))
+            return fail(FRT_E_UNSUPPORTED, "checker textures apply to lambertian / modified_phong / dielectric / "
+                                           "rough_conductor colours");
         if (t == FRT_MAT_ROUGH_CONDUCTOR &&
             (!(sv->materials[i].alpha > 0.0) || (sv->materials[i].distribution != FRT_DIST_GGX &&
                                                   sv->materials[i].distribution != FRT_DIST_BECKMANN)))
@@ -981,6 +987,18 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
                 F.tnorm[3 * d + k] = make_float4((float)sv->tri_n[9 * i + 3 * k], (float)sv->tri_n[9 * i + 3 * k + 1],
                                                  (float)sv->tri_n[9 * i + 3 * k + 2], 0.0f);
     }
+    // texture coordinates, only when a material is textured (in HBM; read at textured hits)
+    bool any_tex = false;
+    for (int i = 0; i < nm; ++i) any_tex |= sv->materials[i].texture == FRT_TEX_CHECKER;
+    if (any_tex) {
+        F.tuv.assign(2 * (size_t)std::max(nt, 1), make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+        if (sv->tri_uv)
+            for (int d = 0; d < nt; ++d) {
+                const double *q = &sv->tri_uv[6 * tri_order[d]];
+                F.tuv[2 * d] = make_float4((float)q[0], (float)q[1], (float)q[2], (float)q[3]);
+                F.tuv[2 * d + 1] = make_float4((float)q[4], (float)q[5], 0.0f, 0.0f);
+            }
+    }
     F.spheres.resize(ns);
     F.smat.resize(ns);
     for (int k = 0; k < ns; ++k) {
@@ -1001,6 +1019,8 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
         else d[1] = f4(m.specular, (float)(m.type == FRT_MAT_MODIFIED_PHONG ? m.exponent
                                            : m.type == FRT_MAT_DIELECTRIC ? m.ior : m.alpha));
         d[2] = f4(m.k, i2f(m.distribution));
+        d[3] = f4(m.tex_odd, i2f(m.texture));
+        d[4] = make_float4((float)m.tex_scale[0], (float)m.tex_scale[1], 0.0f, 0.0f);
     }
     if (sv->n_lights < 0 || (sv->n_lights > 0 && !sv->lights)) return fail(FRT_E_INVALID, "scene view: bad lights");
     F.lights.resize(sv->n_lights);
@@ -1064,6 +1084,7 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
     if ((rc = upload_vec(c, F.nodes, &S.nodes)) || (rc = upload_vec(c, F.nodes4, &S.nodes4)) ||
         (rc = upload_vec(c, F.tris, &S.tris)) ||
         (rc = upload_vec(c, F.tshade, &S.tshade)) || (rc = upload_vec(c, F.tnorm, &S.tnorm)) ||
+        (rc = upload_vec(c, F.tuv, &S.tuv)) ||
         (rc = upload_vec(c, F.spheres, &S.spheres)) || (rc = upload_vec(c, F.smat, &S.sphere_mat)) ||
         (rc = upload_vec(c, F.mats, &S.mats)) || (rc = upload_vec(c, F.lights, &S.lights)) ||
         (rc = upload_vec(c, F.list, &S.list)))
@@ -1078,6 +1099,7 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
     for (int i = 0; i < sv->n_materials; ++i) {
         const int t = sv->materials[i].type;
         if (t != FRT_MAT_LAMBERTIAN && t != FRT_MAT_DIFFUSE_LIGHT) c->has_spec_mats = true;
+        if (sv->materials[i].texture == FRT_TEX_CHECKER) c->has_spec_mats = true;   // textures: MATS kernels
         if (t == FRT_MAT_METAL) c->has_metal = true;
     }
     c->depth4 = F.depth4;
@@ -1107,6 +1129,7 @@ extern "C" int frt_selftest_path_host(const frt_scene_view *sv, const frt_render
             if (sv->materials[i].type == FRT_MAT_METAL) return FRT_E_UNSUPPORTED;
     DevScene S = F.meta;
     S.nodes = F.nodes.data(); S.nodes4 = F.nodes4.data(); S.tris = F.tris.data(); S.tshade = F.tshade.data(); S.tnorm = F.tnorm.data();
+    S.tuv = F.tuv.data();
     S.spheres = F.spheres.data(); S.sphere_mat = F.smat.data(); S.mats = F.mats.data();
     S.lights = F.lights.data(); S.list = F.list.data();
     std::vector<int> stack(std::max(F.depth + 1, kSelftestStack));
@@ -1171,6 +1194,7 @@ extern "C" int frt_selftest_mlt_paths_host(const frt_scene_view *sv, int nx, int
     if (rc != FRT_OK) return rc;
     DevScene S = F.meta;
     S.nodes = F.nodes.data(); S.nodes4 = F.nodes4.data(); S.tris = F.tris.data(); S.tshade = F.tshade.data(); S.tnorm = F.tnorm.data();
+    S.tuv = F.tuv.data();
     S.spheres = F.spheres.data(); S.sphere_mat = F.smat.data(); S.mats = F.mats.data();
     S.lights = F.lights.data(); S.list = F.list.data();
     std::vector<int> stack(std::max(F.depth + 1, 1));

@@ -120,9 +120,10 @@ struct ObjMesh {
     int mtl = -2;  // -2: no material
     std::vector<int> v;   // 3 per face
     std::vector<int> vn;  // 3 per face (-1 = none)
+    std::vector<int> vt;  // 3 per face (-1 = none)
 };
 struct ObjData {
-    std::vector<float> v, vn;
+    std::vector<float> v, vn, vt;   // vt: 2 per texture vertex (u, v)
     std::vector<Mtl> mats;
     std::vector<ObjMesh> meshes;
 };
@@ -236,6 +237,13 @@ bool parse_obj(const std::string &path, ObjData &od)
                 q = parse_float(skip_ws(q), x);
                 od.vn.push_back(x);
             }
+        } else if (p[0] == 'v' && p[1] == 't') {
+            const char *q = p + 2;
+            for (int k = 0; k < 2; ++k) {       // u, v (Assimp keeps a third component; uv uses two)
+                float x;
+                q = parse_float(skip_ws(q), x);
+                od.vt.push_back(x);
+            }
         } else if (!strncmp(p, "mtllib", 6)) {
             load_mtl(dir_of(path) + rstrip(skip_ws(p + 6)), od);
         } else if ((p[0] == 'g' || p[0] == 'o') && (p[1] == ' ' || p[1] == '\t' || p[1] == 0 || p[1] == '\r')) {
@@ -265,29 +273,31 @@ bool parse_obj(const std::string &path, ObjData &od)
             else cur->mtl = idx;
         } else if (p[0] == 'f' && (p[1] == ' ' || p[1] == '\t')) {
             if (!cur) cur = new_mesh(cur_mtl);
-            int vi[64], ni[64], nv = 0;
+            int vi[64], ni[64], ti[64], nv = 0;
             const char *q = p + 1;
-            const int nverts = (int)(od.v.size() / 3), nnorm = (int)(od.vn.size() / 3);
+            const int nverts = (int)(od.v.size() / 3), nnorm = (int)(od.vn.size() / 3), ntex = (int)(od.vt.size() / 2);
             while (*q && nv < 64) {
                 q = skip_ws(q);
                 if (!*q || *q == '\r' || *q == '\n') break;
                 char *e;
                 long a = strtol(q, &e, 10);
                 q = e;
-                long nn = 0;
+                long nn = 0, tt = 0;
                 if (*q == '/') {
                     ++q;
-                    if (*q != '/') { strtol(q, &e, 10); q = e; }
+                    if (*q != '/') { tt = strtol(q, &e, 10); q = e; }
                     if (*q == '/') { ++q; nn = strtol(q, &e, 10); q = e; }
                 }
                 while (*q && *q != ' ' && *q != '\t') ++q;
                 vi[nv] = (int)(a < 0 ? nverts + a : a - 1);
                 ni[nv] = nn == 0 ? -1 : (int)(nn < 0 ? nnorm + nn : nn - 1);
+                ti[nv] = tt == 0 ? -1 : (int)(tt < 0 ? ntex + tt : tt - 1);
                 ++nv;
             }
             auto push = [&](int a, int b, int c) {
                 cur->v.insert(cur->v.end(), {vi[a], vi[b], vi[c]});
                 cur->vn.insert(cur->vn.end(), {ni[a], ni[b], ni[c]});
+                cur->vt.insert(cur->vt.end(), {ti[a], ti[b], ti[c]});
             };
             if (nv == 3) {
                 push(0, 1, 2);
@@ -384,7 +394,7 @@ inline double from_srgb(double v)  // util.h:62-66
 // host scene
 // ---------------------------------------------------------------------------
 struct frt_host_scene {
-    std::vector<double> tri_v, tri_n, tri_inv_area;
+    std::vector<double> tri_v, tri_n, tri_inv_area, tri_uv;
     std::vector<int32_t> tri_mat;
     std::vector<uint8_t> tri_geo;
     std::vector<double> sphere;
@@ -558,8 +568,14 @@ int add_obj(frt_host_scene &s, const std::string &path, bool geo, const double *
         } else {
             cn.assign(3 * m.v.size(), 0.0f);
         }
+        // texture coordinates (mesh_loader.cpp:34-38) when every corner has a vt;
+        // without them the reference leaves uv uninitialised -- here 0
+        bool has_vt = !od.vt.empty();
+        for (int x : m.vt) if (x < 0 || 2 * (size_t)x + 1 >= od.vt.size()) { has_vt = false; break; }
         const int base = (int)s.tri_mat.size();
         for (size_t f = 0; f < nf; ++f) {
+            for (int k = 0; k < 3; ++k)
+                for (int d = 0; d < 2; ++d) s.tri_uv.push_back(has_vt ? (double)od.vt[2 * m.vt[3 * f + k] + d] : 0.0);
             double v[9], n[9];
             for (int k = 0; k < 3; ++k)
                 for (int d = 0; d < 3; ++d) {
@@ -884,6 +900,7 @@ extern "C" int frt_scene_new(frt_host_scene **out)
 static bool material_ok(const frt_material *m)
 {
     if (!m) return false;
+    if (m->texture != FRT_TEX_CONSTANT && m->texture != FRT_TEX_CHECKER) return false;
     switch (m->type) {
     case FRT_MAT_LAMBERTIAN: case FRT_MAT_DIFFUSE_LIGHT: case FRT_MAT_MODIFIED_PHONG: case FRT_MAT_METAL:
     case FRT_MAT_DIELECTRIC: return true;
@@ -1081,6 +1098,7 @@ extern "C" int frt_scene_view_get(const frt_host_scene *s, frt_scene_view *v)
     v->tri_material = s->tri_mat.data();
     v->tri_geometry_normal = s->tri_geo.data();
     v->tri_inv_area = s->tri_inv_area.data();
+    v->tri_uv = s->tri_uv.empty() ? nullptr : s->tri_uv.data();
     v->n_spheres = (int32_t)s->sphere_mat.size();
     v->sphere = s->sphere.data();
     v->sphere_material = s->sphere_mat.data();

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FRT_ABI_VERSION 5
+#define FRT_ABI_VERSION 6
 
 enum {
     FRT_OK = 0,
@@ -75,7 +75,18 @@ typedef struct frt_material {
     double ior;              /* dielectric: ref_idx                                       */
     double alpha;            /* rough_conductor: roughness (alphaU = alphaV)              */
     double eta[3], k[3];     /* rough_conductor: complex IOR (fresnelConductorExact)      */
+    /* The material's texture (lambertian albedo, modified_phong diffuse_reflectance,
+     * dielectric / rough_conductor specular_reflectance): FRT_TEX_CONSTANT uses the
+     * colour field above; FRT_TEX_CHECKER (checker_texture, texture.h:30-49) of two
+     * constants -- that field as tex0 and tex_odd as tex1 -- at u_scale, v_scale,
+     * looked up at the hit's uv (sphere: get_sphere_uv, hitable.h:15-21; triangle:
+     * interpolated OBJ vt, triangle.h:105-107). */
+    int32_t texture;
+    int32_t reserved;
+    double tex_odd[3];
+    double tex_scale[2];
 } frt_material;
+enum { FRT_TEX_CONSTANT = 0, FRT_TEX_CHECKER = 1 };
 
 typedef struct frt_scene_view {
     int32_t world_kind;                 /* FRT_WORLD_BVH or FRT_WORLD_LIST              */
@@ -114,6 +125,8 @@ typedef struct frt_scene_view {
      * (pssmlt.cpp:134-138) needs them; half_height = 256 / camera::dist */
     double cam_w[3];
     double cam_half_height;
+    /* texture coordinates: 6 per tri (uv of v0, v1, v2, the OBJ's vt), or NULL = 0 */
+    const double *tri_uv;
 } frt_scene_view;
 
 typedef struct frt_render_params {

@@ -65,6 +65,8 @@ def lib():
         L.ora_rng_uniform.restype = ctypes.c_double
         L.ora_kat_tri_hit.argtypes = [dp, dp, ctypes.c_int, dp, dp, ctypes.c_double, ctypes.c_double, dp]
         L.ora_kat_sphere_hit.argtypes = [dp, ctypes.c_double, dp, dp, ctypes.c_double, ctypes.c_double, dp]
+        L.ora_kat_texture_sphere.argtypes = [dp, ctypes.c_double, dp, dp, ctypes.c_double, ctypes.c_double, dp]
+        L.ora_kat_texture_tri.argtypes = [dp, dp, dp, dp, ctypes.c_double, ctypes.c_double, dp]
         L.ora_kat_aabb_hit.argtypes = [dp, dp, dp, dp, ctypes.c_double, ctypes.c_double]
         L.ora_kat_camera.argtypes = [dp, dp, dp, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                      ctypes.c_double, ctypes.c_double, dp, dp]
@@ -121,9 +123,9 @@ SPHERE_WHERE = {"world": 1, "lights": 2, "both": 3}
 
 
 def material_desc(m):
-    """The 20-double material description of frt_oracle.h from a scene-spec
+    """The 26-double material description of frt_oracle.h from a scene-spec
     material dict (first_raytracer_amd.scene_spec documents the keys)."""
-    d = np.zeros(20)
+    d = np.zeros(26)
     d[0] = MAT_TYPES[m["type"]]
     d[1:4] = m.get("albedo", (0, 0, 0))
     d[4:7] = m.get("emit", (0, 0, 0))
@@ -134,6 +136,10 @@ def material_desc(m):
     d[13] = m.get("alpha", 0.0)
     d[14:17] = m.get("eta", (0, 0, 0))
     d[17:20] = m.get("k", (0, 0, 0))
+    if m.get("checker") is not None:
+        d[20] = 1
+        d[21:24] = m["checker"]["odd"]
+        d[24:26] = m["checker"]["scale"]
     return d
 
 
@@ -214,7 +220,7 @@ class OracleScene:
         return out[:self.info.n_lights]
 
     def materials(self):
-        out = np.zeros((max(self.info.n_materials, 1), 20))
+        out = np.zeros((max(self.info.n_materials, 1), 26))
         lib().ora_scene_export_materials(self.ptr, out.ctypes.data)
         return out[:self.info.n_materials]
 

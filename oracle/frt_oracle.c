@@ -209,7 +209,11 @@ enum { MAT_LAMBERT = 0, MAT_LIGHT = 1, MAT_PHONG = 2, MAT_METAL = 3, MAT_DIELECT
 enum { DIST_GGX = 0, DIST_BECKMANN = 1 };                                     /* util.h:48-52 */
 /* albedo: lambertian / modified_phong diffuse / metal albedo; ks: specular
  * reflectance (phong, dielectric, rough_conductor's constant texture) */
-typedef struct { int type; v3 albedo; v3 emit; double ks[3], ior, shininess; int dist; double alpha; v3 eta, k; } material;
+typedef struct {
+    int type; v3 albedo; v3 emit; double ks[3], ior, shininess; int dist; double alpha; v3 eta, k;
+    int tex; v3 tex_odd; double tex_scale[2];   /* checker_texture (texture.h:30-49) of the textured colour */
+} material;
+enum { TEX_CONSTANT = 0, TEX_CHECKER = 1 };
 
 /* ---- specular materials (material.h:75-171, pdf.h:99-184, util.h:73-117) ---- */
 static const double DELTA_EPSILON = 1e-3f;                                   /* util.h:12 */
@@ -630,6 +634,7 @@ static inline ray camera_get_ray(const camera *c, double s, double t, double l0,
 typedef struct {
     v3 v0, v1, v2, e1, e2;      /* triangle.h:58-66 (edges from the fp64 vertices) */
     v3 n0, n1, n2;              /* vertex normals (mesh->normals)                  */
+    double uv[6];               /* mesh->uv of v0, v1, v2 (0 without vt)            */
     double inv_area;            /* 1/(0.5 |e1 x e2| nTriangles_of_mesh)            */
     int mat, geo;               /* material, use_geometry_normals                  */
 } tri;
@@ -658,7 +663,38 @@ typedef struct {
     v3 p, normal;
     int32_t obj;     /* prim ref */
     int mat;
+    double tu, tv;   /* hrec.u, hrec.v: texture coordinates (triangle.h:105-107, sphere.h:52) */
 } hit_record;
+
+/* (int)x as x86-64's cvttsd2si computes it: NaN and out-of-range give INT_MIN
+ * (the C++ conversion is undefined there; checker_texture hits it through
+ * get_sphere_uv's NaN on large spheres) */
+static inline int x86_trunc(double x)
+{
+    if (!(x > -2147483649.0 && x < 2147483648.0)) return INT32_MIN;
+    return (int)x;
+}
+static inline int imodulo(int a, int b) { int r = a % b; return (r < 0) ? r + b : r; }   /* util.h:125-128 */
+/* checker_texture::value (texture.h:35-44): 1 -> tex1 (odd), 0 -> tex0 */
+static inline int checker_odd(double u, double v, double us, double vs)
+{
+    const int x = 2 * imodulo(x86_trunc(u * us * 2), 2) - 1, y = 2 * imodulo(x86_trunc(v * vs * 2), 2) - 1;
+    return x * y == 1;
+}
+/* the hit's material with its texture evaluated: lambertian albedo,
+ * modified_phong diffuse_reflectance, dielectric / rough_conductor specular */
+static const material *mat_at(const ora_scene *s, const hit_record *h, material *tmp)
+{
+    const material *m = &s->mats[h->mat];
+    if (m->tex != TEX_CHECKER) return m;
+    *tmp = *m;
+    if (checker_odd(h->tu, h->tv, m->tex_scale[0], m->tex_scale[1])) {
+        if (m->type == MAT_LAMBERT || m->type == MAT_PHONG) tmp->albedo = m->tex_odd;
+        else vstore(tmp->ks, m->tex_odd);
+    }
+    return tmp;
+}
+
 
 /* triangle::hit (triangle.h:69-118) */
 static int tri_hit(const tri *tr, const ray *r, double t_min, double t_max, hit_record *hrec, double *uo, double *vo)
@@ -683,6 +719,9 @@ static int tri_hit(const tri *tr, const ray *r, double t_min, double t_max, hit_
             else
                 hrec->normal = unit(vadd(vadd(smul((1 - u - v), tr->n0), smul(u, tr->n1)), smul(v, tr->n2)));
             hrec->mat = tr->mat;
+            /* uvhit = (1-u-v) uv0 + u uv1 + v uv2 (triangle.h:105) */
+            hrec->tu = ((1 - u - v) * tr->uv[0] + u * tr->uv[2]) + v * tr->uv[4];
+            hrec->tv = ((1 - u - v) * tr->uv[1] + u * tr->uv[3]) + v * tr->uv[5];
             if (uo) { *uo = u; *vo = v; }
             return 1;
         }
@@ -707,6 +746,12 @@ static int sphere_hit(const sphere *sp, const ray *r, double t_min, double t_max
         rec->normal = sdiv(vsub(rec->p, sp->c), sp->r);
         if (vlen2(vsub(r->o, sp->c)) < sp->r * sp->r) rec->normal = vneg(rec->normal);
         rec->mat = sp->mat;
+        /* get_sphere_uv(rec.p - center) (hitable.h:15-21): the offset is not
+         * normalised, so asin sees |y| > 1 (NaN) on spheres of radius > 1 */
+        const v3 q = vsub(rec->p, sp->c);
+        const double phi = atan2(q.e[2], q.e[0]), theta = asin(q.e[1]);
+        rec->tu = 1 - (phi + M_PI) / (2 * M_PI);
+        rec->tv = (theta + M_PI / 2) / M_PI;
         return 1;
     }
     return 0;
@@ -876,7 +921,8 @@ static v3 Li(li_ctx *c, const ray *r, int depth, const hit_record *prev, double 
             const double weight = miWeight(surface_bsdf_pdf, light_pdf);
             return smul(weight, Le);
         }
-        const material *m = &s->mats[hrec.mat];
+        material mtex;
+        const material *m = mat_at(s, &hrec, &mtex);
         /* lambertian / modified_phong / dielectric::scatter succeed; diffuse_light's fails (material.h) */
         if (depth <= 33 && mat_scatters(m->type)) {
             const uint32_t base = DIM_BOUNCE(depth);
@@ -1124,7 +1170,8 @@ static v3 mlt_Li(const ora_scene *s, const ray *r, mlt_state *st)
             const double weight = miWeight(st->prev_pdf, light_pdf);
             return smul(weight, Le);
         }
-        const material *m = &s->mats[hrec.mat];
+        material mtex;
+        const material *m = mat_at(s, &hrec, &mtex);
         if (mat_scatters(m->type)) {
             const int specular = m->type != MAT_LAMBERT;
             const v3 wi = vneg(unit(r->d));
@@ -1470,11 +1517,12 @@ static const char *fast_atof_float(const char *c, float *outv)
 float ora_kat_atof(const char *s) { float f; fast_atof_float(s, &f); return f; }
 
 typedef struct { char name[128]; float kd[3], ks[3], ke[3]; float d, ni, ns; int has_kd; } mtl;
-typedef struct { int mtl; int nfaces; int *faces; int cap; } omesh;   /* faces: triangles, vertex idx */
+typedef struct { int mtl; int nfaces; int *faces; int cap; int *tfaces; } omesh;   /* faces: v idx + vn idx; tfaces: vt idx */
 
 typedef struct {
     float *v; int nv, capv;              /* positions */
     float *vn; int nvn, capvn;           /* normals (vn) */
+    float *vt; int nvt, capvt;           /* texture coordinates (vt: u, v) */
     mtl *mats; int nmats;
     omesh *meshes; int nmeshes, capm;
     int *fv_n;                            /* per triangle corner: normal index or -1 (parallel to faces) */
@@ -1538,11 +1586,17 @@ static omesh *new_mesh(objdata *od, int mtl_idx)
     m->mtl = mtl_idx;
     return m;
 }
-static void mesh_push(omesh *m, int a, int b, int c, int na, int nb, int nc)
+static void mesh_push(omesh *m, int a, int b, int c, int na, int nb, int nc, int ta, int tb, int tc)
 {
-    if (m->nfaces == m->cap) { m->cap = m->cap ? 2 * m->cap : 64; m->faces = (int *)realloc(m->faces, sizeof(int) * 6 * (size_t)m->cap); }
+    if (m->nfaces == m->cap) {
+        m->cap = m->cap ? 2 * m->cap : 64;
+        m->faces = (int *)realloc(m->faces, sizeof(int) * 6 * (size_t)m->cap);
+        m->tfaces = (int *)realloc(m->tfaces, sizeof(int) * 3 * (size_t)m->cap);
+    }
+    int *t = &m->tfaces[3 * m->nfaces];
     int *f = &m->faces[6 * m->nfaces++];
     f[0] = a; f[1] = b; f[2] = c; f[3] = na; f[4] = nb; f[5] = nc;
+    t[0] = ta; t[1] = tb; t[2] = tc;
 }
 static inline void fsub3(const float *a, const float *b, float *o) { o[0] = a[0] - b[0]; o[1] = a[1] - b[1]; o[2] = a[2] - b[2]; }
 static inline void fdivs3(float *v, float f)   /* aiVector3t::operator/= */
@@ -1595,6 +1649,11 @@ static int parse_obj(const char *path, objdata *od)
             const char *q = p + 2;
             for (int k = 0; k < 3; ++k) { while (*q == ' ' || *q == '\t') ++q; q = fast_atof_float(q, &od->vn[3 * od->nvn + k]); }
             od->nvn++;
+        } else if (p[0] == 'v' && p[1] == 't') {
+            if (od->nvt == od->capvt) { od->capvt = od->capvt ? 2 * od->capvt : 1024; od->vt = (float *)realloc(od->vt, sizeof(float) * 2 * (size_t)od->capvt); }
+            const char *q = p + 2;
+            for (int k = 0; k < 2; ++k) { while (*q == ' ' || *q == '\t') ++q; q = fast_atof_float(q, &od->vt[2 * od->nvt + k]); }
+            od->nvt++;
         } else if (!strncmp(p, "mtllib", 6)) {
             const char *nm = p + 6; while (*nm == ' ' || *nm == '\t') ++nm;
             char dir[2048]; snprintf(dir, sizeof dir, "%s", path);
@@ -1628,31 +1687,32 @@ static int parse_obj(const char *path, objdata *od)
             else cur->mtl = idx;
         } else if (p[0] == 'f' && (p[1] == ' ' || p[1] == '\t')) {
             if (!cur) { cur = new_mesh(od, cur_mtl); cur_has_obj = 1; }
-            int vi[64], ni[64], nvtx = 0;
+            int vi[64], ni[64], ti[64], nvtx = 0;
             const char *q = p + 1;
             while (*q && nvtx < 64) {
                 while (*q == ' ' || *q == '\t') ++q;
                 if (!*q) break;
-                long a = strtol(q, (char **)&q, 10), nn = 0;
+                long a = strtol(q, (char **)&q, 10), nn = 0, tt = 0;
                 if (*q == '/') {
                     ++q;
-                    if (*q != '/') strtol(q, (char **)&q, 10);
+                    if (*q != '/') tt = strtol(q, (char **)&q, 10);
                     if (*q == '/') { ++q; nn = strtol(q, (char **)&q, 10); }
                 }
                 while (*q && *q != ' ' && *q != '\t') ++q;
                 vi[nvtx] = (int)(a < 0 ? od->nv + a : a - 1);
                 ni[nvtx] = nn == 0 ? -1 : (int)(nn < 0 ? od->nvn + nn : nn - 1);
+                ti[nvtx] = tt == 0 ? -1 : (int)(tt < 0 ? od->nvt + tt : tt - 1);
                 nvtx++;
             }
-            if (nvtx == 3) mesh_push(cur, vi[0], vi[1], vi[2], ni[0], ni[1], ni[2]);
+            if (nvtx == 3) mesh_push(cur, vi[0], vi[1], vi[2], ni[0], ni[1], ni[2], ti[0], ti[1], ti[2]);
             else if (nvtx == 4) {
                 int s0 = quad_start(od, vi);
-                int t[4] = {vi[s0], vi[(s0 + 1) % 4], vi[(s0 + 2) % 4], vi[(s0 + 3) % 4]};
-                int tn[4] = {ni[s0], ni[(s0 + 1) % 4], ni[(s0 + 2) % 4], ni[(s0 + 3) % 4]};
-                mesh_push(cur, t[0], t[1], t[2], tn[0], tn[1], tn[2]);
-                mesh_push(cur, t[0], t[2], t[3], tn[0], tn[2], tn[3]);
+                int o[4] = {s0, (s0 + 1) % 4, (s0 + 2) % 4, (s0 + 3) % 4};
+                mesh_push(cur, vi[o[0]], vi[o[1]], vi[o[2]], ni[o[0]], ni[o[1]], ni[o[2]], ti[o[0]], ti[o[1]], ti[o[2]]);
+                mesh_push(cur, vi[o[0]], vi[o[2]], vi[o[3]], ni[o[0]], ni[o[2]], ni[o[3]], ti[o[0]], ti[o[2]], ti[o[3]]);
             } else if (nvtx > 4) {
-                for (int k = 1; k + 1 < nvtx; ++k) mesh_push(cur, vi[0], vi[k], vi[k + 1], ni[0], ni[k], ni[k + 1]);
+                for (int k = 1; k + 1 < nvtx; ++k)
+                    mesh_push(cur, vi[0], vi[k], vi[k + 1], ni[0], ni[k], ni[k + 1], ti[0], ti[k], ti[k + 1]);
             }
         }
     }
@@ -1763,7 +1823,7 @@ static int mat4_invert(const double *src, double *t)
     return 1;
 }
 
-/* material from the 20-double description of ora_scene_add_obj / _add_sphere */
+/* material from the 26-double description of ora_scene_add_obj / _add_sphere */
 static material material_from_desc(const double *d)
 {
     material m; memset(&m, 0, sizeof(m));
@@ -1772,6 +1832,7 @@ static material material_from_desc(const double *d)
     m.ks[0] = d[7]; m.ks[1] = d[8]; m.ks[2] = d[9];
     m.shininess = d[10]; m.ior = d[11]; m.dist = (int)d[12]; m.alpha = d[13];
     m.eta = vload(d + 14); m.k = vload(d + 17);
+    m.tex = (int)d[20]; m.tex_odd = vload(d + 21); m.tex_scale[0] = d[24]; m.tex_scale[1] = d[25];
     return m;
 }
 
@@ -1839,10 +1900,17 @@ static int add_obj_x(ora_scene *s, const char *path, int geo, int32_t **lights, 
         } else {
             memset(cn, 0, sizeof(float) * 9 * (size_t)m->nfaces);
         }
+        /* texture coordinates (mesh_loader.cpp:34-38) when every corner has a vt;
+         * without them the reference leaves uv uninitialised -- here 0 */
+        int has_vt = od.nvt > 0;
+        for (int c = 0; c < 3 * m->nfaces && has_vt; ++c)
+            if (m->tfaces[c] < 0 || m->tfaces[c] >= od.nvt) has_vt = 0;
         s->tris = (tri *)realloc(s->tris, sizeof(tri) * (size_t)(s->ntris + m->nfaces));
         for (int fi = 0; fi < m->nfaces; ++fi) {
             tri *t = &s->tris[s->ntris + fi];
             const int *f = &m->faces[6 * fi];
+            for (int k = 0; k < 3; ++k)
+                for (int d = 0; d < 2; ++d) t->uv[2 * k + d] = has_vt ? (double)od.vt[2 * m->tfaces[3 * fi + k] + d] : 0.0;
             t->v0 = mk(od.v[3 * f[0]], od.v[3 * f[0] + 1], od.v[3 * f[0] + 2]);
             t->v1 = mk(od.v[3 * f[1]], od.v[3 * f[1] + 1], od.v[3 * f[1] + 2]);
             t->v2 = mk(od.v[3 * f[2]], od.v[3 * f[2] + 1], od.v[3 * f[2] + 2]);
@@ -1866,8 +1934,8 @@ static int add_obj_x(ora_scene *s, const char *path, int geo, int32_t **lights, 
         s->ntris += m->nfaces;
         free(cn);
     }
-    for (int i = 0; i < od.nmeshes; ++i) free(od.meshes[i].faces);
-    free(od.meshes); free(od.v); free(od.vn); free(od.mats);
+    for (int i = 0; i < od.nmeshes; ++i) { free(od.meshes[i].faces); free(od.meshes[i].tfaces); }
+    free(od.meshes); free(od.v); free(od.vn); free(od.vt); free(od.mats);
     return 0;
 }
 
@@ -2037,16 +2105,18 @@ int ora_scene_export_lights(const ora_scene *s, int32_t *refs)
     for (int i = 0; i < s->nlights; ++i) refs[i] = s->lights[i];
     return s->nlights;
 }
-int ora_scene_export_materials(const ora_scene *s, double *out20)
+int ora_scene_export_materials(const ora_scene *s, double *out26)
 {
     for (int i = 0; i < s->nmats; ++i) {
-        double *o = out20 + 20 * i;
+        double *o = out26 + 26 * i;
         o[0] = s->mats[i].type;
         vstore(o + 1, s->mats[i].albedo); vstore(o + 4, s->mats[i].emit);
         o[7] = s->mats[i].ks[0]; o[8] = s->mats[i].ks[1]; o[9] = s->mats[i].ks[2];
         o[10] = s->mats[i].shininess; o[11] = s->mats[i].ior;
         o[12] = s->mats[i].dist; o[13] = s->mats[i].alpha;
         vstore(o + 14, s->mats[i].eta); vstore(o + 17, s->mats[i].k);
+        o[20] = s->mats[i].tex; vstore(o + 21, s->mats[i].tex_odd);
+        o[24] = s->mats[i].tex_scale[0]; o[25] = s->mats[i].tex_scale[1];
     }
     return s->nmats;
 }
@@ -2085,6 +2155,33 @@ int ora_kat_sphere_hit(const double *c, double r, const double *o, const double 
     memset(out, 0, sizeof(double) * 8);
     out[0] = ok;
     if (ok) { out[1] = h.t; vstore(out + 2, h.p); vstore(out + 5, h.normal); }
+    return ok;
+}
+/* KAT: hit texture coordinates and checker_texture::value's pick (texture.h:35-44):
+ * out4 = ok, u, v, odd; t_max = (double)FLT_MAX as in the reference harness */
+int ora_kat_texture_sphere(const double *c, double r, const double *o, const double *d, double us, double vs,
+                           double *out4)
+{
+    sphere sp; sp.c = vload(c); sp.r = r; sp.mat = 0;
+    ray ry; ry.o = vload(o); ry.d = vload(d);
+    hit_record h;
+    const int ok = sphere_hit(&sp, &ry, 1e-4, (double)3.40282347e+38f, &h);
+    memset(out4, 0, sizeof(double) * 4);
+    out4[0] = ok;
+    if (ok) { out4[1] = h.tu; out4[2] = h.tv; out4[3] = checker_odd(h.tu, h.tv, us, vs); }
+    return ok;
+}
+int ora_kat_texture_tri(const double *v9, const double *uv6, const double *o, const double *d, double us, double vs,
+                        double *out4)
+{
+    tri t = kat_tri(v9, NULL, 1, 1);
+    memcpy(t.uv, uv6, sizeof(double) * 6);
+    ray r; r.o = vload(o); r.d = vload(d);
+    hit_record h;
+    const int ok = tri_hit(&t, &r, 1e-4, (double)3.40282347e+38f, &h, NULL, NULL);
+    memset(out4, 0, sizeof(double) * 4);
+    out4[0] = ok;
+    if (ok) { out4[1] = h.tu; out4[2] = h.tv; out4[3] = checker_odd(h.tu, h.tv, us, vs); }
     return ok;
 }
 int ora_kat_aabb_hit(const double *lo, const double *hi, const double *o, const double *d, double tmin, double tmax)

@@ -54,19 +54,20 @@ int  ora_load_scene(const char *kind, const char *obj_path, double aspect, ora_s
 void ora_free_scene(ora_scene *s);
 void ora_scene_get_info(const ora_scene *s, ora_scene_info *info);
 
-/* Incremental construction (main.cpp's scene functions).  Materials are 20
+/* Incremental construction (main.cpp's scene functions).  Materials are 26
  * doubles: type (FRT_MAT_* values: 0 lambertian, 1 diffuse_light,
  * 2 modified_phong, 3 metal, 4 dielectric, 5 rough_conductor), albedo[3],
  * emit[3], ks[3] (specular reflectance), shininess, ior, distribution
- * (0 GGX, 1 Beckmann), alpha, eta[3], k[3]. */
+ * (0 GGX, 1 Beckmann), alpha, eta[3], k[3], texture (0 constant, 1 checker
+ * of the textured colour and tex_odd), tex_odd[3], u_scale, v_scale. */
 int  ora_scene_new(ora_scene **out);
 /* create_triangle_mesh(file, toWorld, bsdf, lights, geo) (triangle.cpp:26-60);
  * to_world16 row-major or NULL (identity), bsdf20 NULL = the file's MTL materials.
  * Returns -1 on I/O error, -2 for a singular matrix. */
-int  ora_scene_add_obj(ora_scene *s, const char *obj_path, const double *to_world16, const double *bsdf20,
+int  ora_scene_add_obj(ora_scene *s, const char *obj_path, const double *to_world16, const double *bsdf26,
                        int use_geometry_normals);
 /* where: 1 world list, 2 Scene::lights, 3 both */
-int  ora_scene_add_sphere(ora_scene *s, const double *c, double r, const double *mat20, int where);
+int  ora_scene_add_sphere(ora_scene *s, const double *c, double r, const double *mat26, int where);
 void ora_scene_set_camera(ora_scene *s, const double *from, const double *at, const double *vup, double vfov,
                           double aspect, double aperture, double focus);
 /* world_kind 0: create_bvh over the world prims in insertion order, 1: hitable_list */
@@ -81,7 +82,7 @@ int  ora_scene_export_tris(const ora_scene *s, double *v9, int32_t *mat);
 
 void ora_scene_export_camera(const ora_scene *s, double *out19);
 int  ora_scene_export_lights(const ora_scene *s, int32_t *refs);
-int  ora_scene_export_materials(const ora_scene *s, double *out20);   /* the 20-double description */
+int  ora_scene_export_materials(const ora_scene *s, double *out26);   /* the 26-double description */
 
 /* Render pixels (linear index y*nx+x, y=0 bottom row) with `spp` samples each,
  * frame seed `seed`, on `nthreads` threads.  out_rgb[3*i..] = mean radiance
@@ -122,6 +123,11 @@ int  ora_kat_tri_hit(const double *v9, const double *n9, int geo, const double *
 /* sphere c[3], r; out: hit, t, p[3], normal[3] */
 int  ora_kat_sphere_hit(const double *c, double r, const double *o, const double *d,
                         double tmin, double tmax, double *out);
+/* hit texture coordinates + checker_texture::value's pick; out4: ok, u, v, odd */
+int  ora_kat_texture_sphere(const double *c, double r, const double *o, const double *d, double us, double vs,
+                            double *out4);
+int  ora_kat_texture_tri(const double *v9, const double *uv6, const double *o, const double *d, double us,
+                         double vs, double *out4);
 /* out: 1/0 */
 int  ora_kat_aabb_hit(const double *lo, const double *hi, const double *o, const double *d,
                       double tmin, double tmax);

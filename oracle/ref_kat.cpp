@@ -356,6 +356,60 @@ static void kat_specular(int ncases)
     }
 }
 
+// checker_texture::value at sphere and triangle hits: the hit's texture
+// coordinates (get_sphere_uv, the interpolated OBJ vt) and the colour picked
+static void kat_texture(int ncases)
+{
+    const Vector3f c0(0.125, 0.25, 0.375), c1(0.625, 0.75, 0.875);
+    for (int c = 0; c < ncases; ++c) {
+        const double scales[5] = {1, 2, 5, 10, (double)(float)(0.5 + 20 * urand())};
+        const double us = scales[c % 5], vs = scales[(c / 5) % 5];
+        checker_texture tex(new constant_texture(c0), new constant_texture(c1), us, vs);
+        hit_record h;
+        bool ok;
+        if (c % 2 == 0) {
+            Vector3f cen(fgrid(3), fgrid(3), fgrid(3));
+            // radii above 1 put |p - centre|.y past 1: asin's NaN, (int)NaN
+            double r = (double)(float)(c % 8 == 0 ? 1.0 + 2 * urand() : 0.05 + 0.95 * urand());
+            sphere sp(cen, r, nullptr);
+            Vector3f o(fgrid(6), fgrid(6), fgrid(6));
+            Vector3f d = cen + Vector3f(srand2(r), srand2(r), srand2(r)) - o;
+            ok = sp.hit(ray(o, d), 1e-4, (double)FLT_MAX, h);
+            printf("tex_sphere"); pv(cen); p(r); pv(o); pv(d); p(us); p(vs); bar();
+        } else {
+            double v9[9], uv6[6];
+            rand_tri(v9);
+            for (double &x : uv6) x = fgrid(2);
+            Vector3f *vv = new Vector3f[3];
+            Vector3f *nn = new Vector3f[3];
+            Vector2f *uv = new Vector2f[3];
+            int idx[3] = {0, 1, 2};
+            for (int k = 0; k < 3; ++k) {
+                vv[k] = Vector3f(v9[3 * k], v9[3 * k + 1], v9[3 * k + 2]);
+                nn[k] = Vector3f(0, 0, 1);
+                uv[k] = Vector2f(uv6[2 * k], uv6[2 * k + 1]);
+            }
+            auto mesh = std::make_shared<triangle_mesh>(1, 3, vv, idx, nn, uv,
+                std::make_unique<lambertian>(new constant_texture(c0)), true, "kat", true);
+            triangle tr(mesh, 0);
+            double a = urand() * 0.9 + 0.05, b = urand() * (0.95 - a);
+            Vector3f target = (1 - a - b) * vv[0] + a * vv[1] + b * vv[2];
+            Vector3f o(fgrid(4), fgrid(4), fgrid(4));
+            ok = tr.hit(ray(o, target - o), 1e-4, (double)FLT_MAX, h);
+            printf("tex_tri");
+            for (double x : v9) p(x);
+            for (double x : uv6) p(x);
+            pv(o); pv(target - o); p(us); p(vs); bar();
+        }
+        p(ok ? 1 : 0);
+        if (ok) {
+            const Vector3f col = tex.value(h);
+            p(h.u); p(h.v); p(col[0] == c1[0] ? 1 : 0);
+        } else for (int i = 0; i < 3; ++i) p(0);
+        printf("\n");
+    }
+}
+
 static void kat_pfm()
 {
     const int nx = 3, ny = 2, nn = 3;
@@ -379,6 +433,7 @@ int main(int argc, char **argv)
     kat_sort(n / 4);
     kat_list_hit(n / 2);
     kat_specular(n);
+    kat_texture(n);
     kat_pfm();
     return 0;
 }

@@ -36,6 +36,29 @@ def to_world(scale, yaw_deg, t):
             0.0, 0.0, 0.0, 1.0]
 
 
+QUAD_UV_OBJ = os.path.join(SCENES, "quad_uv.obj")
+
+
+def checker(material, odd, scale):
+    """checker_texture(constant(material's colour), constant(odd), u_scale, v_scale) (texture.h:30-49)."""
+    return dict(material, checker={"odd": odd, "scale": scale})
+
+
+def cornell_textured(world="bvh"):
+    """Checker textures on a vt-mapped quad over the floor (lambertian, random_scene's colours,
+    main.cpp:62), on a rough conductor sphere (veach_ajar's FLOOR_MATERIAL, main.cpp:341-342:
+    GGX alpha 0.1f, 0.8 / 0.2 at 20 x 80) and on a dielectric's specular reflectance."""
+    floor = checker({"type": "lambertian", "albedo": (F32(0.2), F32(0.3), F32(0.1))}, (F32(0.99),) * 3, (4.0, 4.0))
+    objs = [{"obj": CORNELL_OBJ, "geo": True},
+            {"obj": QUAD_UV_OBJ, "bsdf": floor, "geo": True},
+            {"sphere": (-0.6, 0.25, 0.6), "radius": 0.25,
+             "material": checker(rough("ggx", 0.1, (0.8, 0.8, 0.8)), (0.2, 0.2, 0.2), (20.0, 80.0))},
+            {"sphere": (0.33, 0.82, 0.37), "radius": 0.22,
+             "material": checker({"type": "dielectric", "ior": 1.5, "specular": (1.0, 1.0, 1.0)}, (0.3, 0.6, 0.9),
+                                 (3.0, 3.0))}]
+    return {"objects": objs, "camera": CORNELL_CAM, "world": world}
+
+
 def cornell_conductors(sphere_dist="ggx", cube_dist="beckmann", world="bvh", metal=True):
     objs = [{"obj": CORNELL_OBJ, "geo": True}]
     if metal:

@@ -1,0 +1,64 @@
+"""checker_texture (texture.h:30-49) on the GPU against the fp64 oracle: a
+vt-mapped OBJ quad (lambertian), a rough conductor sphere with veach_ajar's
+floor checker and a dielectric with a checkered specular reflectance
+(tests/scene_specs.py cornell_textured), in path::Li and pssmlt::Li.
+Tolerance as in test_gpu_parity.py: image RMSE <= 1e-3 on linear radiance."""
+import numpy as np
+import pytest
+
+import first_raytracer_amd as frt
+import oracle
+import scene_specs as SS
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = frt.Context(0)
+    yield c
+    c.close()
+
+
+def rmse(a, b):
+    return float(np.sqrt(np.mean((np.asarray(a, np.float64).reshape(-1, 3) - np.asarray(b, np.float64).reshape(-1, 3)) ** 2)))
+
+
+@pytest.mark.parametrize("world,flags", [
+    ("bvh", 0),                               # LDS-resident binary BVH
+    ("bvh", frt.FRT_FLAG_NO_LDS_SCENE),       # HBM 4-wide BVH
+    ("list", 0)])                             # hitable_list world
+def test_path_textures(ctx, world, flags):
+    spec = SS.cornell_textured(world)
+    nx, ny, spp = 96, 72, 32
+    ctx.upload(frt.HostScene.from_spec(spec, nx / ny))
+    film, st = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=11, flags=flags))
+    ref, cnt = oracle.OracleScene.from_spec(spec, nx / ny).render(nx, ny, spp, seed=11)
+    e = rmse(film, ref)
+    print(world, flags, "rmse", e, "rays", st.rays, cnt.rays)
+    assert st.samples == cnt.samples and st.camera_rays == cnt.camera_rays
+    assert abs(st.rays - cnt.rays) / cnt.rays < 2e-3
+    assert np.isfinite(film).all()
+    assert e <= 1e-3
+
+
+def test_pssmlt_textures(ctx):
+    spec = SS.cornell_textured()
+    nx, ny, mpp, chains = 48, 48, 4, 2304
+    ctx.upload(frt.HostScene.from_spec(spec, 1.0))
+    film = np.zeros((ny, nx, 3), np.float32)
+    film, st = ctx.render(frt.RenderParams.pssmlt(nx, ny, mpp, chains, seed=4, bootstrap=2000), film)
+    steps = mpp * nx * ny // chains
+    ref, b, cnt = oracle.OracleScene.from_spec(spec, 1.0).mlt_render(nx, ny, chains, steps, seed=4, n_init=2000)
+    assert st.samples == chains * steps == cnt.samples
+    assert abs(st.rays - cnt.rays) / cnt.rays < 5e-3
+    assert rmse(film, ref) <= 2e-3 * max(1.0, float(np.abs(ref).max()))
+
+
+def test_checker_light_rejected(ctx):
+    spec = {"objects": [{"obj": SS.CORNELL_OBJ, "geo": True},
+                        {"sphere": (0, 1, 0), "radius": 0.1, "where": "both",
+                         "material": SS.checker({"type": "diffuse_light", "emit": (4, 4, 4)}, (1, 1, 1), (2, 2))}],
+            "camera": SS.CORNELL_CAM}
+    with pytest.raises(frt.FrtError, match="checker"):
+        ctx.upload(frt.HostScene.from_spec(spec, 1.0))

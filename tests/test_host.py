@@ -21,7 +21,7 @@ def test_library_exports_every_declared_symbol():
     L = frt.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert L.frt_get_abi_version() == frt.ABI_VERSION == 5
+    assert L.frt_get_abi_version() == frt.ABI_VERSION == 6
 
 
 def test_create_without_device_fails_cleanly():
@@ -74,7 +74,7 @@ def test_cornell_scene_matches_oracle(cornell_obj, aspect):
     assert np.array_equal(cam, osc.camera())
     # materials: the oracle's 20-double description
     mats = np.array([[m.type, *m.albedo, *m.emit, *m.specular, m.exponent, m.ior, m.distribution, m.alpha,
-                      *m.eta, *m.k] for m in
+                      *m.eta, *m.k, m.texture, *m.tex_odd, *m.tex_scale] for m in
                      (ctypes.cast(v.materials, ctypes.POINTER(frt.Material))[i] for i in range(v.n_materials))])
     assert np.array_equal(mats, osc.materials())
 
@@ -160,7 +160,7 @@ def test_specular_scene_materials_and_topology(objfix, request):
     osc = oracle.OracleScene("cornell_box_obj", obj, 1.0)
     v = hs.view()
     mats = np.array([[m.type, *m.albedo, *m.emit, *m.specular, m.exponent, m.ior, m.distribution, m.alpha,
-                      *m.eta, *m.k] for m in
+                      *m.eta, *m.k, m.texture, *m.tex_odd, *m.tex_scale] for m in
                      (ctypes.cast(v.materials, ctypes.POINTER(frt.Material))[i] for i in range(v.n_materials))])
     assert np.array_equal(mats, osc.materials())
     types = set(mats[:, 0].astype(int))

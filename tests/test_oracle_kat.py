@@ -194,6 +194,34 @@ def test_rough_conductor(kat):
     assert nonzero > len(cases) // 4, "KAT set should exercise non-zero BSDF values"
 
 
+def nan_equal(a, b):
+    """bit-equal, NaN == NaN (get_sphere_uv's asin of |y| > 1)"""
+    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    return a.shape == b.shape and bool(np.all((np.isnan(a) & np.isnan(b)) | (a.view(np.uint64) == b.view(np.uint64))))
+
+
+def test_checker_texture(kat):
+    """checker_texture::value (texture.h:35-44) at sphere hits -- get_sphere_uv of the
+    unnormalised offset (hitable.h:15-21, sphere.h:52), NaN on spheres of radius > 1, which
+    (int) turns into INT_MIN on x86-64 -- and at triangle hits (interpolated vt, triangle.h:105-107)."""
+    L = oracle.lib()
+    n = odd = nan = 0
+    for ins, outs in kat["tex_sphere"]:
+        x = H(ins); want = H(outs); out = np.zeros(4)
+        L.ora_kat_texture_sphere(darr(x[0:3])[1], x[3], darr(x[4:7])[1], darr(x[7:10])[1], x[10], x[11],
+                                 out.ctypes.data_as(darr([0])[1].__class__))
+        assert nan_equal(out, want), (ins, out, want)
+        n += want[0]; odd += want[3]; nan += bool(np.isnan(want[2]))
+    for ins, outs in kat["tex_tri"]:
+        x = H(ins); want = H(outs); out = np.zeros(4)
+        L.ora_kat_texture_tri(darr(x[0:9])[1], darr(x[9:15])[1], darr(x[15:18])[1], darr(x[18:21])[1], x[21], x[22],
+                              out.ctypes.data_as(darr([0])[1].__class__))
+        assert nan_equal(out, want), (ins, out, want)
+        n += want[0]; odd += want[3]
+    assert len(kat["tex_sphere"]) + len(kat["tex_tri"]) >= 100
+    assert 0 < odd < n and nan > 0, (n, odd, nan)
+
+
 def test_pfm_bytes(kat, tmp_path):
     p = kat["pfm"]
     data = H(p["data"])
@@ -207,6 +235,6 @@ def test_kat_coverage(kat):
     assert {k for k in kat if not k.startswith("_")} == {
         "tri_hit", "sphere_hit", "aabb_hit", "camera", "cosine", "tri_sample", "sphere_sample",
         "miweight", "fromsrgb", "pick", "sort", "list_hit", "pfm", "fresnel", "phong", "dielectric",
-        "metal", "conductor"}
+        "metal", "conductor", "tex_sphere", "tex_tri"}
     hits = sum(int(float.fromhex(o[0])) for _, o in kat["tri_hit"])
     assert 20 < hits < len(kat["tri_hit"]) - 20, "KAT set should mix hits and misses"

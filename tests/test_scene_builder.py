@@ -20,7 +20,7 @@ def both(spec, aspect=1.0):
 def host_materials(hs):
     v = hs.view()
     return np.array([[m.type, *m.albedo, *m.emit, *m.specular, m.exponent, m.ior, m.distribution, m.alpha,
-                      *m.eta, *m.k] for m in
+                      *m.eta, *m.k, m.texture, *m.tex_odd, *m.tex_scale] for m in
                      (ctypes.cast(v.materials, ctypes.POINTER(frt.Material))[i] for i in range(v.n_materials))])
 
 
@@ -102,6 +102,50 @@ def test_conductor_shading_host_vs_oracle(sphere_dist, cube_dist):
     assert st.samples == cnt.samples and st.camera_rays == cnt.camera_rays
     assert abs(st.rays - cnt.rays) / cnt.rays < 2e-3
     assert float(np.sqrt(np.mean((g - ref) ** 2))) < 1e-3
+
+
+@pytest.mark.parametrize("world", ["bvh", "list"])
+def test_textured_scene_host_vs_oracle(world):
+    """checker textures (texture.h:30-49) at OBJ-vt and sphere uv: the builder keeps the
+    vt (mesh_loader.cpp:34-38; 0 for meshes without), and the device path code run on the
+    host matches the oracle; without the textures the image differs."""
+    spec = SS.cornell_textured(world)
+    hs, osc = both(spec)
+    assert np.array_equal(host_materials(hs), osc.materials())
+    v = hs.view()
+    uv = np.ctypeslib.as_array(ctypes.cast(v.tri_uv, ctypes.POINTER(ctypes.c_double)), shape=(v.n_tris * 6,))
+    assert not uv[:-12].any()                                           # CornellBox-Original has no vt
+    assert sorted(set(uv[-12:])) == [0.0, 1.0] and uv[-12:].sum() == 6.0  # the quad's two triangles
+    nx = ny = 48
+    g, st = frt.selftest_path_host(hs, frt.RenderParams.make(nx, ny, 8, seed=5), np.arange(nx * ny, dtype=np.int32))
+    ref, cnt = osc.render(nx, ny, 8, seed=5)
+    assert st.camera_rays == cnt.camera_rays
+    assert abs(st.rays - cnt.rays) / cnt.rays < 2e-3
+    assert float(np.sqrt(np.mean((g.reshape(-1, 3) - ref) ** 2))) < 1e-3
+    plain = dict(spec, objects=[{k: ({kk: vv for kk, vv in x.items() if kk != "checker"} if isinstance(x, dict) else x)
+                                 for k, x in o.items()} for o in spec["objects"]])
+    ref0, _ = oracle.OracleScene.from_spec(plain, 1.0).render(nx, ny, 8, seed=5)
+    assert float(np.sqrt(np.mean((ref0 - ref) ** 2))) > 1e-2
+
+
+def test_texture_rejections():
+    """checker on a light's emission or on metal's albedo is not mapped: upload refuses it
+    loudly; an unknown texture kind fails in the builder."""
+    light = {"objects": [{"obj": SS.CORNELL_OBJ, "geo": True},
+                         {"sphere": (0, 1, 0), "radius": 0.1, "where": "both",
+                          "material": SS.checker({"type": "diffuse_light", "emit": (4, 4, 4)}, (1, 1, 1), (2, 2))}],
+             "camera": SS.CORNELL_CAM}
+    hs = frt.HostScene.from_spec(light, 1.0)
+    with pytest.raises(frt.FrtError):
+        frt.selftest_path_host(hs, frt.RenderParams.make(4, 4, 1), np.arange(16, dtype=np.int32))
+    m = frt.Material.from_spec({"type": "lambertian", "albedo": (0.5, 0.5, 0.5)})
+    m.texture = 7
+    s = ctypes.c_void_p()
+    L = frt.lib()
+    assert L.frt_scene_new(ctypes.byref(s)) == 0
+    c = (ctypes.c_double * 3)(0, 0, 0)
+    assert L.frt_scene_add_sphere(s, c, ctypes.c_double(1.0), ctypes.byref(m), 1) != 0
+    L.frt_scene_destroy(s)
 
 
 def test_ao_rejects_metal():
