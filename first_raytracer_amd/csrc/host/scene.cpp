@@ -18,6 +18,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <map>
@@ -752,9 +753,12 @@ struct SahBuilder {
     std::vector<double> node_box;
     std::vector<int32_t> node_child;
     std::atomic<int> n_nodes{0}, max_depth{0};
+    static constexpr int kMaxBins = 128;
+    int bins = 32;                           // FRT_SAH_BINS overrides (tuning experiments)
 
     explicit SahBuilder(const std::vector<Box> &b) : box(b), cen(3 * b.size()), idx(b.size())
     {
+        if (const char *e = std::getenv("FRT_SAH_BINS")) bins = std::max(2, std::min(kMaxBins, std::atoi(e)));
         for (size_t i = 0; i < b.size(); ++i) {
             idx[i] = (int32_t)i;
             for (int k = 0; k < 3; ++k) cen[3 * i + k] = 0.5 * (b[i].lo[k] + b[i].hi[k]);
@@ -781,21 +785,21 @@ struct SahBuilder {
         const int n = e - b;
         int mid = b + n / 2;
         if (n > 2) {
-            constexpr int kBins = 32;
+            const int kBins = bins;
             double best = INFINITY;
             int best_axis = -1, best_bin = 0;
             for (int axis = 0; axis < 3; ++axis) {
                 const double ext = chi[axis] - clo[axis];
                 if (!(ext > 0)) continue;
-                Box bb[kBins];
-                int cnt[kBins] = {};
+                Box bb[kMaxBins];
+                int cnt[kMaxBins] = {};
                 const double sc = kBins / ext;
                 for (int i = b; i < e; ++i) {
                     const int bi = std::min(kBins - 1, (int)((cen[3 * idx[i] + axis] - clo[axis]) * sc));
                     bb[bi] = cnt[bi]++ ? surround(bb[bi], box[idx[i]]) : box[idx[i]];
                 }
-                double right_area[kBins];
-                int right_cnt[kBins];
+                double right_area[kMaxBins];
+                int right_cnt[kMaxBins];
                 Box acc{};
                 int c = 0;
                 for (int i = kBins - 1; i > 0; --i) {
