@@ -1309,8 +1309,10 @@ static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
     const bool lds = d < kLdsMaxDepth && sb <= kLdsSceneBytes && !(flags & FRT_FLAG_NO_LDS_SCENE);
     // register cap: waves/SIMD the compiler must fit (its spills land in the
     // shading code, not the traversal loops).  Measured (profiles/r01_ab_perf3.jsonl):
-    // 5 waves best for LDS-resident scenes, 6 for HBM-resident ones.
-    int waves = lds ? 5 : 6;
+    // 5 waves best for LDS-resident scenes, 6 for HBM-resident ones.  The
+    // material kernels (MATS) in LDS run 15-21 % faster on the compiler's own
+    // allocation than under the 5-wave cap (profiles/r01d_perf_mats.jsonl).
+    int waves = (MATS && lds) ? 0 : lds ? 5 : 6;
     if (flags & FRT_FLAG_WAVES4) waves = 0;   // the compiler's own allocation (~120 VGPRs, 4 waves)
     if (flags & FRT_FLAG_WAVES5) waves = 5;
     if (flags & FRT_FLAG_WAVES6) waves = 6;
