@@ -2,9 +2,12 @@
 
 Tile t of the frame belongs to rank t mod N (frt_render_params.shard_index /
 shard_count).  Each rank renders its tiles into a slot buffer in HBM; the
-buffers (padded to the largest shard) are all-gathered with torch.distributed
--- RCCL over xGMI with the "nccl" backend, gloo in the CPU tests -- and rank 0
-scatters the slots into the film (viewer::fout_image order, y = 0 bottom).
+buffers (padded to the largest shard) are gathered to rank 0 with
+torch.distributed -- RCCL grouped send/recv over xGMI with the "nccl"
+backend, gloo in the CPU tests -- and rank 0 scatters the slots into the film
+(viewer::fout_image order, y = 0 bottom).  Only rank 0 receives: N-1 buffers
+cross the links once (SURVEY.md §8(e) "gather to rank 0"), not N(N-1) as an
+all-gather would move.
 """
 import numpy as np
 import torch
@@ -25,7 +28,7 @@ def shard_layout(nx, ny, tile, world):
 
 
 class TileGather:
-    """All-gather of per-rank slot buffers + scatter into rank 0's film."""
+    """Gather of per-rank slot buffers to rank 0 + scatter into rank 0's film."""
 
     def __init__(self, nx, ny, tile, world, rank, device, stage_cpu=False):
         """stage_cpu: gather through host copies (a gloo rehearsal of the GPU
@@ -36,23 +39,27 @@ class TileGather:
         self.max_slots = max(counts)
         self.my_slots = torch.zeros(self.max_slots * 3, dtype=torch.float32, device=device)
         self.gathered = (torch.zeros(world * self.max_slots * 3, dtype=torch.float32, device=device)
-                         if world > 1 else None)
+                         if world > 1 and rank == 0 else None)
         self.film = torch.zeros(nx * ny * 3, dtype=torch.float32, device=device) if rank == 0 else None
         if rank == 0:
             sp = torch.from_numpy(slot_pix).to(device)
             self.valid = sp >= 0
             self.dst = sp[self.valid]
 
+    def _gather_list(self, buf):
+        return list(buf.view(self.world, -1).unbind(0)) if self.rank == 0 else None
+
     def gather(self):
         """Collective: every rank calls it after rendering into self.my_slots."""
         src = self.my_slots
         if self.world > 1:
             if self.stage_cpu:
-                g = torch.empty(self.gathered.numel(), dtype=torch.float32)
-                dist.all_gather_into_tensor(g, self.my_slots.cpu())
-                self.gathered.copy_(g)
+                g = torch.empty(self.world * self.max_slots * 3, dtype=torch.float32) if self.rank == 0 else None
+                dist.gather(self.my_slots.cpu(), self._gather_list(g) if g is not None else None, dst=0)
+                if self.rank == 0:
+                    self.gathered.copy_(g)
             else:
-                dist.all_gather_into_tensor(self.gathered, self.my_slots)
+                dist.gather(self.my_slots, self._gather_list(self.gathered), dst=0)
             src = self.gathered
         if self.rank == 0:
             self.film.view(-1, 3)[self.dst] = src.view(-1, 3)[self.valid]
