@@ -1,21 +1,27 @@
 #!/usr/bin/env python3
 """Benchmark: Mrays/s of the MI355X path integrator on the BASELINE.json config
 (CornellBox-Original, 1920x1080, 512 spp, path + NEE + MIS), with the image
-tiles sharded over N GPUs (one process per GPU, RCCL all-gather of the tile
-radiance over xGMI), plus the roofline of the path megakernel and the CPU
-baseline (the fp64 C restatement, oracle/, timed on this host's cores).
+tiles sharded over N GPUs (one process per GPU, RCCL gather of the tile
+radiance to rank 0 over xGMI), plus the roofline of the path megakernel and
+the CPU baseline (the fp64 C restatement, oracle/, timed on this host's cores).
+
+The same JSON line carries the north-star run (BASELINE.json north_star, SURVEY
+§8(d) C4): the 1,005,858-triangle tessellated Cornell box at 1920x1080 / 512
+spp, sharded the same way, timed the same way, with its own RMSE against the
+oracle and its own roofline ("north_star": {...}).
 
 One "step" = one full frame: every rank renders its tiles (tile t -> rank
-t mod N) into HBM, then the per-rank slot buffers are all-gathered and rank 0
-scatters them into the film.  Scene upload and BVH build happen before the
+t mod N) into HBM, then the per-rank slot buffers are gathered to rank 0,
+which scatters them into the film.  Scene build and upload happen before the
 timed region.
 
-    python bench.py [--gpus N --steps K --warmup W] [--scene cornell|cornell_1m|veach]
+    python bench.py [--gpus N --steps K --warmup W] [--scene cornell|cornell_1m|veach|sphere]
 
 Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -27,13 +33,34 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mrays/sec + RMSE vs CPU ref, CornellBox 1080p 512spp, 1/2/4/8 MI355X"
 SCENES = os.path.join(ROOT, "tests", "golden", "scenes")
-LDS_PEAK_GBS = 150000.0   # ds_read_b128 aggregate, MI355X_MICROARCH.md §LDS
-HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+# MI355X_MICROARCH.md: HBM3E 8.0 TB/s; 256 CUs x 4 SIMD-32 at 2.4 GHz, a wave64
+# VALU instruction issues over 2 cycles -> 1228.8 G wave-instructions/s; LDS
+# aggregate ~150 TB/s for ds_read_b64/b128
+HBM_PEAK_GBS = 8000.0
+VALU_PEAK_GINST = 256 * 4 * 2.4 / 2.0
+LDS_PEAK_GBS = 150000.0
 NODE_BYTES, TRI_BYTES, RAY_BYTES = 32, 48, 32   # B_ray = 32 V + 48 T + 32
+NS_TARGET_MRAYS = 1000.0                        # north_star: >= 1 Gray/s on one MI355X
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def host_cpus():
+    """CPUs this process may use: its affinity mask, capped by the cgroup CPU
+    quota (a GPU box shares a large host; nproc reports the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, math.ceil(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def scene_spec(name, workdir, tag=""):
@@ -54,8 +81,8 @@ def scene_spec(name, workdir, tag=""):
     raise ValueError(name)
 
 
-def load_traversal_stats(key):
-    path = os.path.join(ROOT, "profiles", "traversal_stats.json")
+def load_profile(fname, key):
+    path = os.path.join(ROOT, "profiles", fname)
     if os.path.exists(path):
         with open(path) as f:
             return json.load(f).get(key)
@@ -128,6 +155,205 @@ def cpu_baseline_mlt(kind, obj, nx, ny, seed, threads, seconds):
             "rmse": None, "sample": f"{chains} chains x {steps} mutations"}
 
 
+def roofline(integrator, key, world, res, V, T):
+    """Roofline of the dominant kernel (the megakernel) for this config.
+
+    The bound follows where the scene lives (DESIGN.md §7 "Roofline"):
+    * scene in LDS (Cornell, 5 KiB): the kernel issues divergent VALU work and
+      reads its scene from LDS; HBM carries only the per-(chunk, slot) partial
+      sums.  bound "valu": achieved = VALU wave-instructions per launch (PMC
+      SQ_INSTS_VALU per ray x rays per launch) / launch time, peak = 1228.8 G/s.
+    * scene in HBM (cornell_1m, ~150 MB): bound "hbm": achieved = HBM bytes per
+      launch from the PMC passes (2 x FETCH_SIZE + WRITE_SIZE per ray, the
+      gfx950 correction of MI355X_MICROARCH.md) x rays per launch / launch time.
+    The per-ray PMC figures come from profiles/roofline_pmc.json (made by
+    tools/roofline_pmc.py from the rocprofv3 CSVs named there); the launch time
+    and ray count are this run's.  The SURVEY §8(d) algorithmic bytes
+    (B_ray = 32 V + 48 T + 32 on the reference's tree) are reported beside it."""
+    launch_s = res["avg_kernel_ms"] * 1e-3
+    rays = res["rays_per_launch"]
+    pmc = load_profile("roofline_pmc.json", f"{integrator}:{key}")
+    out = {"kernel": "mlt_megakernel" if integrator == "pssmlt" else "path_megakernel",
+           "rays_per_launch": int(rays), "avg_launch_ms": round(res["avg_kernel_ms"], 3),
+           "scene_residency": "lds" if res["scene_in_lds"] else "hbm",
+           "scene_bytes": int(res["scene_bytes"]), "launch": res["launch"]}
+    algo = None
+    if V is not None:
+        b_ray = NODE_BYTES * V + TRI_BYTES * T + RAY_BYTES
+        algo = rays * b_ray / launch_s / 1e9
+        out.update({"algorithmic_bytes_per_ray": round(b_ray, 1), "V_node": round(V, 3), "T_tri": round(T, 3),
+                    "algorithmic_GBps": round(algo, 1)})
+    if pmc is not None:
+        out["pmc_source"] = pmc.get("source")
+        if pmc.get("valu_lane_util") is not None:
+            out["valu_lane_util"] = round(pmc["valu_lane_util"], 4)
+        hbm = pmc.get("hbm_bytes_per_ray")
+        hbm_gbs = rays * hbm / launch_s / 1e9 if hbm is not None else None
+        if res["scene_in_lds"] and pmc.get("valu_insts_per_ray") is not None:
+            ach = rays * pmc["valu_insts_per_ray"] / launch_s / 1e9
+            out.update({"bound": "valu", "achieved": round(ach, 1), "peak": VALU_PEAK_GINST, "unit": "Ginst/s",
+                        "frac": round(ach / VALU_PEAK_GINST, 4),
+                        "traffic": None if hbm is None else int(rays * hbm),
+                        "hbm_GBps": None if hbm_gbs is None else round(hbm_gbs, 1),
+                        "lds_frac": None if algo is None else round(algo / LDS_PEAK_GBS, 4)})
+        elif hbm is not None:
+            out.update({"bound": "hbm", "achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(hbm_gbs / HBM_PEAK_GBS, 4), "traffic": int(rays * hbm),
+                        "algorithmic_over_traffic": None if algo is None else round(algo / hbm_gbs, 3)})
+            if pmc.get("valu_insts_per_ray") is not None:
+                out["valu_issue_frac"] = round(rays * pmc["valu_insts_per_ray"] / launch_s / 1e9 / VALU_PEAK_GINST, 4)
+    if "bound" not in out:
+        # no counter profile for this config: the algorithmic model alone (it can
+        # exceed 1 when L2 / the Infinity Cache / LDS serve the node reads)
+        out.update({"bound": "hbm", "achieved": None if algo is None else round(algo, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": None if algo is None else round(algo / HBM_PEAK_GBS, 4),
+                    "traffic": None, "basis": "algorithmic bytes, no PMC profile for this config"})
+    return out
+
+
+class Runner:
+    """Per-process GPU state: the rank, the device, the collectives."""
+
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != args.gpus:
+            log(f"note: --gpus {args.gpus} but WORLD_SIZE {self.world}; using WORLD_SIZE")
+        self.gloo = args.backend == "gloo"
+        if self.gloo:
+            local = local % torch.cuda.device_count()
+        if self.world > 1:
+            torch.cuda.set_device(local)
+            if self.gloo:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        self.local = local
+        self.dev = torch.device("cuda", local)
+        import first_raytracer_amd as frt
+        self.frt = frt
+        self.ctx = frt.Context(local)
+
+    def all_reduce(self, t, op=None):
+        """RCCL on device tensors; the gloo rehearsal stages through the host."""
+        kw = {} if op is None else {"op": op}
+        if self.gloo:
+            h = t.cpu()
+            self.dist.all_reduce(h, **kw)
+            t.copy_(h)
+        else:
+            self.dist.all_reduce(t, **kw)
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def measure(self, args, scene, spp, steps, warmup, bvh_arg):
+        """Build + upload `scene`, then W warmup and K timed frames (barrier +
+        synchronize on both sides, max over ranks)."""
+        torch, frt = self.torch, self.frt
+        nx, ny = (int(x) for x in args.res.lower().split("x"))
+        workdir = os.path.join(ROOT, "gpurun_out") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else "/tmp"
+        kind, obj, scene_name = scene_spec(scene, workdir, tag=f"_r{self.rank}")
+        t0 = time.perf_counter()
+        gpu_build_ms = None
+        bvh = bvh_arg if kind == "cornell_box_obj" else "host"   # veach: list world, no BVH
+        if bvh in ("gpu", "sah"):                    # OBJ load only; the BVH is built below
+            hs = frt.HostScene.from_spec({"objects": [{"obj": obj, "geo": True}], "camera": frt.CORNELL_CAMERA,
+                                          "world": "list"}, nx / ny)
+        else:
+            hs = frt.HostScene(kind, obj, nx / ny)   # OBJ load + reference-topology BVH build (host)
+        env = None
+        if args.env:
+            env = tuple(float(x) for x in args.env.split(","))
+        elif args.integrator == "ao":
+            env = (1.0, 1.0, 1.0)                    # the scenes' black environment would make every AO sample 0
+        if env is not None:
+            hs.set_env(env)
+        integ = {"path": frt.FRT_INTEGRATOR_PATH, "ao": frt.FRT_INTEGRATOR_AO,
+                 "normals": frt.FRT_INTEGRATOR_NORMALS}.get(args.integrator, frt.FRT_INTEGRATOR_PSSMLT)
+        ctx = self.ctx
+        if bvh == "sah":
+            hs.build_bvh_sah()                       # binned SAH on the host (in host_build_s)
+        if bvh == "gpu":
+            hs.build_bvh_gpu(ctx)                    # warm-up build (hipcub kernels load on first use)
+            tg = time.perf_counter()
+            gpu_build_ms = hs.build_bvh_gpu(ctx)     # Morton + radix sort + Karras + refit (frt_lbvh.hip)
+            t0 += time.perf_counter() - tg           # count one build in host_build_s
+        t1 = time.perf_counter()
+        ctx.upload(hs)                               # flatten + leaf collapse + BVH4Q + copy to HBM
+        t2 = time.perf_counter()
+        world, rank = self.world, self.rank
+        if args.integrator == "pssmlt":
+            # chains shard over ranks (chain c -> rank c mod N); splat films are summed
+            params = frt.RenderParams.pssmlt(nx, ny, spp, args.chains, seed=args.seed,
+                                             shard_index=rank, shard_count=world)
+            mlt_film = torch.zeros(nx * ny * 3, dtype=torch.float32, device=self.dev)
+        else:
+            params = frt.RenderParams.make(nx, ny, spp, seed=args.seed, tile_size=args.tile,
+                                           shard_index=rank, shard_count=world, integrator=integ)
+            from first_raytracer_amd.dist import TileGather
+            tgather = TileGather(nx, ny, args.tile, world, rank, self.dev, stage_cpu=self.gloo)
+        stream = torch.cuda.current_stream(self.dev)
+
+        def step():
+            if args.integrator == "pssmlt":
+                st = ctx.render_device(params, mlt_film.data_ptr(), stream.cuda_stream)
+                if world > 1:
+                    self.all_reduce(mlt_film)        # RCCL sum of the per-rank splat films
+                return st
+            st = ctx.render_device(params, tgather.my_slots.data_ptr(), stream.cuda_stream)
+            tgather.gather()       # RCCL gather of the tile slots to rank 0, which scatters them into its film
+            return st
+
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize(self.dev)
+        self.barrier()
+        t_start = time.perf_counter()
+        rays = 0
+        kernel_ms = []
+        last = None
+        for k in range(steps):
+            st = step()
+            rays += st.rays
+            kernel_ms.append(st.kernel_ms)
+            last = st
+            log(f"rank {rank} {scene} step {k}: {st.rays / 1e9:.3f} Grays, kernel {st.kernel_ms:.1f} ms")
+        torch.cuda.synchronize(self.dev)
+        self.barrier()
+        elapsed = time.perf_counter() - t_start
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=self.dev)
+            self.all_reduce(t, op=self.dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+            r = torch.tensor([float(rays)], dtype=torch.float64, device=self.dev)
+            self.all_reduce(r, op=self.dist.ReduceOp.SUM)
+            rays = int(r.item())
+        film = None
+        if rank == 0:
+            film = (mlt_film if args.integrator == "pssmlt" else tgather.film).cpu().numpy()
+        return {
+            "scene": scene, "scene_name": scene_name, "kind": kind, "obj": obj, "nx": nx, "ny": ny, "spp": spp,
+            "steps": steps, "warmup": warmup, "elapsed": elapsed, "rays": rays, "value": rays / elapsed / 1e6,
+            "integ": integ, "env": env, "bvh": bvh, "gpu_build_ms": gpu_build_ms,
+            "setup_s": t2 - t0, "build_s": t1 - t0, "upload_s": t2 - t1,
+            "avg_kernel_ms": float(np.mean(kernel_ms)), "rays_per_launch": last.rays,
+            "samples_per_launch": last.samples, "scene_in_lds": last.scene_in_lds,
+            "scene_bytes": last.scene_bytes,
+            "launch": {"waves_cap": int(last.waves_cap), "stack": int(last.stack_entries),
+                       "bvh_depth": int(last.bvh_depth)},
+            "film": film,
+        }
+
+
+BVH_NAMES = {"gpu": "gpu-lbvh", "sah": "binned SAH (host)", "host": "create_bvh (reference topology)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -144,8 +370,12 @@ def main():
                          "List-world scenes (veach) ignore it")
     ap.add_argument("--cpu-pixels", type=int, default=0, help="pixels in the CPU-baseline sample (0: calibrated)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline duration when calibrated")
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every CPU this process may use (host_cpus)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--north-star", default="auto", choices=["auto", "on", "off"],
+                    help="auto: with the default config (cornell, path) also run cornell_1m 1080p/512spp")
+    ap.add_argument("--ns-steps", type=int, default=3, help="timed frames of the north-star run")
+    ap.add_argument("--ns-pixels", type=int, default=4096, help="oracle pixel sample for the north-star RMSE")
     ap.add_argument("--pfm", default="", help="write the rank-0 film here")
     ap.add_argument("--integrator", default="path", choices=["path", "pssmlt", "ao", "normals"],
                     help="pssmlt: C5 config, --spp = mutations per pixel; ao (ao.cpp), normals (debug_renderer.h)")
@@ -154,212 +384,105 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the N-rank path with host-staged collectives (e.g. ranks sharing one GPU)")
     args = ap.parse_args()
-    nx, ny = (int(x) for x in args.res.lower().split("x"))
 
-    import torch
-    import torch.distributed as dist
-
-    import first_raytracer_amd as frt
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
-    gloo = args.backend == "gloo"
-    if gloo:
-        local = local % torch.cuda.device_count()
-    if world > 1:
-        torch.cuda.set_device(local)
-        if gloo:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-
-    def all_reduce(t, op=None):
-        """RCCL on device tensors; the gloo rehearsal stages through the host."""
-        kw = {} if op is None else {"op": op}
-        if gloo:
-            h = t.cpu()
-            dist.all_reduce(h, **kw)
-            t.copy_(h)
-        else:
-            dist.all_reduce(t, **kw)
-
-    workdir = os.path.join(ROOT, "gpurun_out") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else "/tmp"
-    kind, obj, scene_name = scene_spec(args.scene, workdir, tag=f"_r{rank}")
-    t0 = time.perf_counter()
-    gpu_build_ms = None
-    bvh = args.bvh if kind == "cornell_box_obj" else "host"   # veach: list world, no BVH
-    if bvh in ("gpu", "sah"):                    # OBJ load only; the BVH is built below
-        hs = frt.HostScene.from_spec({"objects": [{"obj": obj, "geo": True}], "camera": frt.CORNELL_CAMERA,
-                                      "world": "list"}, nx / ny)
-    else:
-        hs = frt.HostScene(kind, obj, nx / ny)   # OBJ load + reference-topology BVH build (host)
-    env = None
-    if args.env:
-        env = tuple(float(x) for x in args.env.split(","))
-    elif args.integrator == "ao":
-        env = (1.0, 1.0, 1.0)                    # the scenes' black environment would make every AO sample 0
-    if env is not None:
-        hs.set_env(env)
-    integ = {"path": frt.FRT_INTEGRATOR_PATH, "ao": frt.FRT_INTEGRATOR_AO,
-             "normals": frt.FRT_INTEGRATOR_NORMALS}.get(args.integrator, frt.FRT_INTEGRATOR_PSSMLT)
-    ctx = frt.Context(local)
-    if bvh == "sah":
-        hs.build_bvh_sah()                       # binned SAH on the host (in host_build_s)
-    if bvh == "gpu":
-        hs.build_bvh_gpu(ctx)                    # warm-up build (hipcub kernels load on first use)
-        tg = time.perf_counter()
-        gpu_build_ms = hs.build_bvh_gpu(ctx)     # Morton + radix sort + Karras + refit (frt_lbvh.hip)
-        t0 += time.perf_counter() - tg           # count one build in host_build_s
-    t1 = time.perf_counter()
-    ctx.upload(hs)                               # flatten + leaf collapse + BVH4Q + copy to HBM
-    t2 = time.perf_counter()
-    build_s, upload_s, setup_s = t1 - t0, t2 - t1, t2 - t0
-
-    if args.integrator == "pssmlt":
-        # chains shard over ranks (chain c -> rank c mod N); splat films are summed
-        params = frt.RenderParams.pssmlt(nx, ny, args.spp, args.chains, seed=args.seed,
-                                         shard_index=rank, shard_count=world)
-        mlt_film = torch.zeros(nx * ny * 3, dtype=torch.float32, device=dev)
-
-        class _Film:
-            film = mlt_film
-        tg = _Film()
-    else:
-        params = frt.RenderParams.make(nx, ny, args.spp, seed=args.seed, tile_size=args.tile,
-                                       shard_index=rank, shard_count=world, integrator=integ)
-        from first_raytracer_amd.dist import TileGather
-        tg = TileGather(nx, ny, args.tile, world, rank, dev, stage_cpu=gloo)
-    stream = torch.cuda.current_stream(dev)
-
-    def step():
-        if args.integrator == "pssmlt":
-            st = ctx.render_device(params, mlt_film.data_ptr(), stream.cuda_stream)
-            if world > 1:
-                all_reduce(mlt_film)        # RCCL sum of the per-rank splat films
-            return st
-        st = ctx.render_device(params, tg.my_slots.data_ptr(), stream.cuda_stream)
-        tg.gather()       # RCCL all-gather of the tile slots, rank 0 scatters into its film
-        return st
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t_start = time.perf_counter()
-    rays = 0
-    kernel_ms = []
-    last = None
-    for k in range(args.steps):
-        st = step()
-        rays += st.rays
-        kernel_ms.append(st.kernel_ms)
-        last = st
-        log(f"rank {rank} step {k}: {st.rays / 1e9:.3f} Grays, kernel {st.kernel_ms:.1f} ms")
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        r = torch.tensor([float(rays)], dtype=torch.float64, device=dev)
-        all_reduce(r, op=dist.ReduceOp.SUM)
-        rays = int(r.item())
+    R = Runner(args)
+    world, rank = R.world, R.rank
+    res = R.measure(args, args.scene, args.spp, args.steps, args.warmup, args.bvh)
+    do_ns = args.north_star == "on" or (args.north_star == "auto" and args.scene == "cornell"
+                                        and args.integrator == "path" and args.res == "1920x1080"
+                                        and args.spp == 512)
+    ns = R.measure(args, "cornell_1m", 512, args.ns_steps, 1, args.bvh) if do_ns else None
 
     if rank == 0:
-        value = rays / elapsed / 1e6
-        film_np = tg.film.cpu().numpy()
+        nx, ny = res["nx"], res["ny"]
         key = f"{args.scene}:{nx}x{ny}"
+        threads = args.cpu_threads or host_cpus()
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
             if args.integrator == "pssmlt":
-                cpu = cpu_baseline_mlt(kind, obj, nx, ny, args.seed, threads, args.cpu_seconds)
+                cpu = cpu_baseline_mlt(res["kind"], res["obj"], nx, ny, args.seed, threads, args.cpu_seconds)
             else:
-                cpu = cpu_baseline(kind, obj, nx, ny, args.spp, args.seed, args.cpu_pixels, threads, film_np,
-                                   args.cpu_seconds, integrator=integ, env=env)
-            cpu["threads"] = threads
-        ts = load_traversal_stats(key)
-        if cpu is not None:
-            V, T = cpu["V"], cpu["T"]
-        elif ts is not None:
-            V, T = ts["V"], ts["T"]
-        else:
-            V = T = None
-        avg_kernel_s = float(np.mean(kernel_ms)) * 1e-3
-        rays_per_launch = last.rays
-        roofline = None
-        if V is not None:
-            b_ray = NODE_BYTES * V + TRI_BYTES * T + RAY_BYTES
-            achieved = rays_per_launch * b_ray / avg_kernel_s / 1e9
-            traffic = None
-            pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-            if os.path.exists(pmc):
-                with open(pmc) as f:
-                    traffic = json.load(f).get(f"{args.integrator}:{key}:n{world}")
-            roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "kernel": "mlt_megakernel" if args.integrator == "pssmlt" else "path_megakernel",
-                        "bytes_per_ray": round(b_ray, 1),
-                        "V_node": round(V, 3), "T_tri": round(T, 3), "rays_per_launch": int(rays_per_launch),
-                        "avg_launch_ms": round(avg_kernel_s * 1e3, 3),
-                        # where the algorithmic bytes are served from: an LDS-resident scene is not
-                        # HBM-bound (frac can exceed 1); its LDS-read peak is ~150 TB/s (MI355X_MICROARCH.md §LDS)
-                        "scene_residency": "lds" if last.scene_in_lds else "hbm",
-                        "scene_bytes": int(last.scene_bytes),
-                        "lds_frac": round(achieved / LDS_PEAK_GBS, 4) if last.scene_in_lds else None,
-                        "launch": {"waves_cap": int(last.waves_cap), "stack": int(last.stack_entries),
-                                   "bvh_depth": int(last.bvh_depth)}}
+                cpu = cpu_baseline(res["kind"], res["obj"], nx, ny, args.spp, args.seed, args.cpu_pixels, threads,
+                                    res["film"], args.cpu_seconds, integrator=res["integ"], env=res["env"])
+        ts = load_profile("traversal_stats.json", key)
+        V, T = (cpu["V"], cpu["T"]) if cpu is not None else (ts["V"], ts["T"]) if ts is not None else (None, None)
         li_name = {"path": "path::Li", "ao": "ao::Li", "normals": "normals_renderer::Li"}.get(args.integrator)
-        workload = {"path": f"{scene_name} {nx}x{ny} {args.spp}spp path+NEE+MIS",
-                    "ao": f"{scene_name} {nx}x{ny} {args.spp}spp ambient occlusion (ao.cpp)",
-                    "normals": f"{scene_name} {nx}x{ny} {args.spp}spp shading normals (debug_renderer.h)",
-                    "pssmlt": f"{scene_name} {nx}x{ny} PSS-MLT {args.spp} mutations/pixel, {args.chains} chains"
+        sname = res["scene_name"]
+        workload = {"path": f"{sname} {nx}x{ny} {args.spp}spp path+NEE+MIS",
+                    "ao": f"{sname} {nx}x{ny} {args.spp}spp ambient occlusion (ao.cpp)",
+                    "normals": f"{sname} {nx}x{ny} {args.spp}spp shading normals (debug_renderer.h)",
+                    "pssmlt": f"{sname} {nx}x{ny} PSS-MLT {args.spp} mutations/pixel, {args.chains} chains"
                     }[args.integrator]
+        film_np = res["film"]
+        nproc = os.cpu_count()
         line = {
-            "metric": METRIC, "value": round(value, 1), "unit": "Mrays/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+            "metric": METRIC, "value": round(res["value"], 1), "unit": "Mrays/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(res["elapsed"] / args.steps * 1e3, 2),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": workload,
                        "integrator": args.integrator, "scene": args.scene,
                        "nx": nx, "ny": ny, "spp": args.spp, "seed": args.seed, "tile": args.tile,
-                       "env": env,
+                       "env": res["env"],
                        "parallelism": (f"chains-interleaved x{world} + rccl all-reduce" if args.integrator == "pssmlt"
-                                       else f"tiles-interleaved x{world} + rccl all-gather")},
+                                       else f"tiles-interleaved x{world} + rccl gather to rank 0")},
             "rmse": None if cpu is None else cpu["rmse"],
             "rmse_detail": None if cpu is None or "diverged_pixels" not in cpu else {
                 "pixels": cpu["npix"], "diverged_pixels": cpu["diverged_pixels"],
                 "rmse_converged": cpu["rmse_converged"], "diverged_threshold": 1e-3},
-            "mutations_per_step": int(last.samples) if args.integrator == "pssmlt" else None,
-            "rays_per_step": int(rays // args.steps),
-            "setup_s": round(setup_s, 2), "host_build_s": round(build_s, 2), "upload_s": round(upload_s, 2),
-            "bvh": {"gpu": "gpu-lbvh", "sah": "binned SAH (host)"}.get(bvh, "create_bvh (reference topology)"),
-            "gpu_build_ms": None if gpu_build_ms is None else round(gpu_build_ms, 3),
-            "value_per_gpu": round(value / world, 1),
+            "mutations_per_step": int(res["samples_per_launch"]) if args.integrator == "pssmlt" else None,
+            "rays_per_step": int(res["rays"] // args.steps),
+            "setup_s": round(res["setup_s"], 2), "host_build_s": round(res["build_s"], 2),
+            "upload_s": round(res["upload_s"], 2),
+            "bvh": BVH_NAMES[res["bvh"]],
+            "gpu_build_ms": None if res["gpu_build_ms"] is None else round(res["gpu_build_ms"], 3),
+            "value_per_gpu": round(res["value"] / world, 1),
             "image_mean": [round(float(x), 6) for x in film_np.reshape(-1, 3).mean(0)],
-            "roofline": roofline,
+            "roofline": roofline(args.integrator, key, world, res, V, T),
             "cpu_baseline": None if cpu is None else {
-                "value": round(cpu["mrays"], 3), "unit": "Mrays/s", "cores": cpu["threads"], "kind": "port",
+                "value": round(cpu["mrays"], 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+                "host_nproc": nproc,
                 "sample": (f"{cpu['npix']} evenly spaced pixels of the same {nx}x{ny} frame at {args.spp} spp "
-                           f"({cpu['rays']} rays, {cpu['seconds']:.1f} s); fp64 C restatement of {li_name}")
+                           f"({cpu['rays']} rays, {cpu['seconds']:.1f} s) on {threads} threads (every CPU this "
+                           f"process may use; the host reports {nproc}); fp64 C restatement of {li_name}. "
+                           f"first_ray itself (path.cpp + cpp-taskflow + GLFW) cannot be built here")
                 if args.integrator != "pssmlt" else
                           (f"PSS-MLT {cpu['sample']} on the same {nx}x{ny} frame ({cpu['rays']} rays, "
-                           f"{cpu['seconds']:.1f} s); fp64 C restatement of pssmlt.cpp")},
+                           f"{cpu['seconds']:.1f} s) on {threads} threads; fp64 C restatement of pssmlt.cpp")},
         }
-        if gloo:
+        if ns is not None:
+            nkey = f"cornell_1m:{ns['nx']}x{ns['ny']}"
+            ncpu = None
+            if world == 1 and not args.no_cpu_baseline:
+                ncpu = cpu_baseline(ns["kind"], ns["obj"], ns["nx"], ns["ny"], 512, args.seed, args.ns_pixels,
+                                     threads, ns["film"], 0.0)
+            nts = load_profile("traversal_stats.json", nkey)
+            nV, nT = ((ncpu["V"], ncpu["T"]) if ncpu is not None else (nts["V"], nts["T"]) if nts is not None
+                      else (None, None))
+            line["north_star"] = {
+                "workload": f"{ns['scene_name']} {ns['nx']}x{ns['ny']} 512spp path+NEE+MIS",
+                "value": round(ns["value"], 1), "unit": "Mrays/s", "n_gpus": world,
+                "steps": ns["steps"], "warmup": ns["warmup"],
+                "ms_per_step": round(ns["elapsed"] / ns["steps"] * 1e3, 2),
+                "target": f">= {NS_TARGET_MRAYS:.0f} Mrays/s on one MI355X",
+                "target_met": bool(ns["value"] / world >= NS_TARGET_MRAYS),
+                "rays_per_step": int(ns["rays"] // ns["steps"]),
+                "bvh": BVH_NAMES[ns["bvh"]], "setup_s": round(ns["setup_s"], 2),
+                "rmse": None if ncpu is None else ncpu["rmse"],
+                "rmse_detail": None if ncpu is None else {
+                    "pixels": ncpu["npix"], "diverged_pixels": ncpu["diverged_pixels"],
+                    "rmse_converged": ncpu["rmse_converged"], "diverged_threshold": 1e-3,
+                    "oracle_mrays": round(ncpu["mrays"], 3), "oracle_threads": threads},
+                "image_mean": [round(float(x), 6) for x in ns["film"].reshape(-1, 3).mean(0)],
+                "roofline": roofline("path", nkey, world, ns, nV, nT),
+            }
+        if R.gloo:
             line["config"]["parallelism"] += " (gloo host-staged rehearsal)"
         if args.pfm:
-            frt.write_pfm(args.pfm, film_np.reshape(ny, nx, 3))
+            R.frt.write_pfm(args.pfm, film_np.reshape(ny, nx, 3))
         print(json.dumps(line), flush=True)
-    ctx.close()
+    R.ctx.close()
     if world > 1:
-        dist.destroy_process_group()
+        R.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

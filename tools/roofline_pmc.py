@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Per-ray PMC figures of the megakernel for bench.py's roofline, from
+rocprofv3 --pmc passes of ONE bench command (each pass its own run):
+
+  python tools/roofline_pmc.py KEY --sq DIR --fetch DIR --write DIR --bench BENCH.json [--copy-to profiles/r02]
+
+KEY is "<integrator>:<scene>:<nx>x<ny>" (bench.py's key).  From the LAST
+*_megakernel dispatch of each pass (counters summed over dimensions):
+  valu_insts_per_ray  = SQ_INSTS_VALU / rays per launch
+  valu_lane_util      = SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU)
+  hbm_bytes_per_ray   = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 / rays per launch
+FETCH_SIZE / WRITE_SIZE are KiB; FETCH_SIZE is doubled as MI355X_MICROARCH.md
+"HBM [CDNA4]" prescribes for gfx950 (it tallies 128-B requests at 64 B).
+The rays per launch come from the bench JSON the passes printed (every pass
+renders the same frame; the ray count is deterministic).  Updates
+profiles/roofline_pmc.json[KEY]; --copy-to keeps the CSVs under profiles/.
+"""
+import argparse
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def last_megakernel(d):
+    path = os.path.join(d, "run_counter_collection.csv")
+    per = defaultdict(lambda: defaultdict(float))
+    names = {}
+    for r in csv.DictReader(open(path)):
+        if "megakernel" not in r["Kernel_Name"]:
+            continue
+        did = int(r["Dispatch_Id"])
+        per[did][r["Counter_Name"]] += float(r["Counter_Value"])
+        names[did] = r["Kernel_Name"]
+    if not per:
+        sys.exit(f"no megakernel dispatch in {path}")
+    last = max(per)
+    return names[last], dict(per[last]), path
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("key")
+    ap.add_argument("--sq", required=True)
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--bench", required=True)
+    ap.add_argument("--copy-to", default="")
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "roofline_pmc.json"))
+    a = ap.parse_args()
+    line = [l for l in open(a.bench) if l.startswith("{")][-1]
+    b = json.loads(line)
+    rays = b["roofline"]["rays_per_launch"]
+    kname, sq, p_sq = last_megakernel(a.sq)
+    _, fe, p_fe = last_megakernel(a.fetch)
+    _, wr, p_wr = last_megakernel(a.write)
+    fetch_b = 2.0 * fe["FETCH_SIZE"] * 1024.0
+    write_b = wr["WRITE_SIZE"] * 1024.0
+    rec = {
+        "kernel": kname.replace("(anonymous namespace)::", "").split("(")[0],
+        "rays_per_launch": rays,
+        "SQ": sq, "FETCH_SIZE_KiB": fe["FETCH_SIZE"], "WRITE_SIZE_KiB": wr["WRITE_SIZE"],
+        "valu_insts_per_ray": sq["SQ_INSTS_VALU"] / rays,
+        "valu_lane_util": sq["SQ_THREAD_CYCLES_VALU"] / (64.0 * sq["SQ_ACTIVE_INST_VALU"]),
+        "hbm_bytes_per_ray": (fetch_b + write_b) / rays,
+        "read_bytes_per_ray": fetch_b / rays, "write_bytes_per_ray": write_b / rays,
+        "correction": "hbm = 2 x FETCH_SIZE + WRITE_SIZE (KiB x 1024), MI355X_MICROARCH.md HBM [CDNA4]",
+    }
+    srcs = []
+    for tag, p in (("sq", p_sq), ("fetch", p_fe), ("write", p_wr)):
+        if a.copy_to:
+            os.makedirs(a.copy_to, exist_ok=True)
+            dst = os.path.join(a.copy_to, f"pmc_{a.key.replace(':', '_')}_{tag}.csv")
+            shutil.copy(p, dst)
+            p = os.path.relpath(dst, ROOT)
+        srcs.append(p)
+    rec["source"] = ", ".join(srcs)
+    t = json.load(open(a.out)) if os.path.exists(a.out) else {}
+    t[a.key] = rec
+    json.dump(t, open(a.out, "w"), indent=1, sort_keys=True)
+    print(json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    main()
