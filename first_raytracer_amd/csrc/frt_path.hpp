@@ -32,6 +32,51 @@ FRT_HD bool wave_any(bool x)
 #endif
 }
 
+// number of active lanes of the wave for which x holds (host self-test: one lane)
+FRT_HD int wave_count(bool x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __popcll(__ballot(x));
+#else
+    return x ? 1 : 0;
+#endif
+}
+
+// Diagnostic build only (`make exp NAME=diag DEFS=-DFRT_DIAG`): per-phase
+// lane occupancy.  FRT_DIAG_TICK(k) adds, for the executing wave, one trip and
+// the number of active lanes to counter pair k of the wave's slot in
+// frt_diag (read back by frt_diag_read); FRT_DIAG_CYC(k, c) adds cycles.
+// Compiled out of every product build.
+#if defined(FRT_DIAG)
+constexpr int kDiagSlots = 24;
+extern __device__ unsigned long long *frt_diag;
+#endif
+#if defined(FRT_DIAG) && defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ unsigned long long *diag_slot()
+{
+    return frt_diag + (size_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * kDiagSlots;
+}
+#define FRT_DIAG_TICK(k)                                                                \
+    do {                                                                                \
+        const uint64_t m_ = __ballot(1);                                                \
+        if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)m_) - 1) {           \
+            unsigned long long *d_ = diag_slot();                                       \
+            d_[2 * (k)] += 1;                                                           \
+            d_[2 * (k) + 1] += __popcll(m_);                                            \
+        }                                                                               \
+    } while (0)
+#define FRT_DIAG_CYC(k, c)                                                              \
+    do {                                                                                \
+        const uint64_t m_ = __ballot(1);                                                \
+        if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)m_) - 1) diag_slot()[k] += (c); \
+    } while (0)
+#define FRT_DIAG_CLOCK() ((unsigned long long)clock64())
+#else
+#define FRT_DIAG_TICK(k) do {} while (0)
+#define FRT_DIAG_CYC(k, c) do {} while (0)
+#define FRT_DIAG_CLOCK() 0ull
+#endif
+
 constexpr int kSentinel = 0x7fffffff;   // "stack empty"; never a node index
 constexpr int kEmptyChild = kSentinel;  // unused slot of a 4-wide node (never pushed)
 constexpr int kWorldBvh4 = 2;           // internal world kind: 4-wide quantized BVH
@@ -77,7 +122,8 @@ struct Hit {
 // (count - 1 in bits 27..29 below the sphere flag: up to 8 triangles, 2^27 triangles per scene)
 constexpr int kLeafCountShift = 27, kLeafIndexMask = (1 << kLeafCountShift) - 1, kLeafIndexLimit = 1 << kLeafCountShift;
 constexpr int kLeafMax = 8, kLeafDefault = 4, kLeafSmallScene = 2;
-constexpr int kTravMinLds = 12, kTravMinHbm = 32;   // path_megakernel: see trav_min()
+constexpr int kTravMinLds = 12, kTravMinHbm = 24;   // path_megakernel: see trav_min()
+constexpr int kMinDescLds = 0, kMinDescHbm = 8;     // leaf postponing: see min_desc()
 
 FRT_HD float4 node_part(const DevScene &S, int i, int k) { return S.nodes[i * S.node_es + k * S.node_ps]; }
 FRT_HD uint4 node4_part(const DevScene &S, int i, int k) { return S.nodes4[i * S.node4_es + k * S.node4_ps]; }
@@ -104,6 +150,7 @@ FRT_HD bool leaf_hit(const DevScene &S, int lref, f3 o, f3 d, float tmin, bool a
     const int first = is_sph ? lref : (lref & kLeafIndexMask);
     const int count = is_sph ? 1 : (lref >> kLeafCountShift) + 1;
     for (int k = 0; k < count; ++k) {
+        FRT_DIAG_TICK(1);
         const int ref = first + k;
         float u, v;
         const float t = prim_t(S, ref, o, d, tmin, h.t, u, v);
@@ -152,13 +199,19 @@ FRT_HD bool trav_begin(Trav &T, const DevScene &S, int root, f3 o, f3 d, float t
 }
 
 // binary nodes: descend to a leaf, test it.  True when the query is finished.
+// min_desc > 0 (the megakernel's leaf postponing): the descent stops for the
+// whole wave once fewer than min_desc of its lanes are still descending; those
+// lanes keep their node and stack and resume on the next step, while the lanes
+// that reached a leaf test it now.  A wave then no longer runs its node loop
+// for as many trips as its slowest lane needs to reach a leaf.
 template <int STRIDE>
-FRT_HD bool bvh2_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk)
+FRT_HD bool bvh2_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int min_desc = 0)
 {
     int node = T.node, sp = T.sp;
     // (a branch-free body -- speculative stack-top read, predicated push -- was
     // 4.5 % slower on Cornell: profiles/r01_exp1_branchy.txt)
     while ((unsigned)node < (unsigned)kSentinel) {   // interior node
+        FRT_DIAG_TICK(2);
         const float4 n0 = node_part(S, node, 0), n1 = node_part(S, node, 1);
         const float4 n2 = node_part(S, node, 2), n3 = node_part(S, node, 3);
         const float t0 = slab_entry(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, T.tmin, T.h.t);
@@ -177,8 +230,13 @@ FRT_HD bool bvh2_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *
         } else {
             node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel;
         }
+        if (min_desc > 0 && wave_count((unsigned)node < (unsigned)kSentinel) < min_desc) break;
     }
-
+    if ((unsigned)node < (unsigned)kSentinel) {          // postponed: still descending
+        T.node = node;
+        T.sp = sp;
+        return false;
+    }
     bool done = node == kSentinel || leaf_hit(S, ~node, o, d, T.tmin, anyhit, T.h);
     if (!done) {
         node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel;
@@ -202,57 +260,86 @@ FRT_HD bool bvh2_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *
 // for one; then every lane tests its parked leaf at once.  Visits more nodes
 // with a stale t_best (still conservative), keeps lanes busy.
 template <int STRIDE, int LSTACK, bool SPEC = false>
-FRT_HD bool bvh4_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int *ovf)
+FRT_HD bool bvh4_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int *ovf, int min_desc = 0)
 {
     int node = T.node, sp = T.sp;
     int parked = 0;                                     // leaf refs are negative; 0 = none
+    // Entries below LSTACK live in the lane's LDS column, deeper ones in `ovf`
+    // (scratch).  A wave-uniform test keeps the common case on plain LDS
+    // accesses: a per-lane select between the two would make the compiler
+    // branch per push and pop through a generic (flat) pointer.
     auto push = [&](int v) {
-        if (sp < LSTACK) stk[sp * STRIDE] = v;
-        else ovf[sp - LSTACK] = v;
+        if (!wave_any(sp >= LSTACK)) {
+            stk[sp * STRIDE] = v;
+        } else {
+            if (sp < LSTACK) stk[sp * STRIDE] = v;
+            else ovf[sp - LSTACK] = v;
+        }
         ++sp;
     };
     auto pop = [&]() -> int {
         if (sp == 0) return kSentinel;
         --sp;
+        if (!wave_any(sp >= LSTACK)) return stk[sp * STRIDE];
         return sp < LSTACK ? stk[sp * STRIDE] : ovf[sp - LSTACK];
     };
     if (SPEC && node < 0) { parked = node; node = pop(); }
     while ((unsigned)node < (unsigned)kSentinel) {
+        FRT_DIAG_TICK(0);
         const uint4 w0 = node4_part(S, node, 0), w1 = node4_part(S, node, 1);
         const uint4 w2 = node4_part(S, node, 2), w3 = node4_part(S, node, 3);
         const SlabRay &sr = T.sr;
         const float ax = u2f((w0.w & 0xffu) << 23) * sr.invd.x, bx = fmaf(u2f(w0.x), sr.invd.x, sr.oinv.x);
         const float ay = u2f(((w0.w >> 8) & 0xffu) << 23) * sr.invd.y, by = fmaf(u2f(w0.y), sr.invd.y, sr.oinv.y);
         const float az = u2f(((w0.w >> 16) & 0xffu) << 23) * sr.invd.z, bz = fmaf(u2f(w0.z), sr.invd.z, sr.oinv.z);
+        // near / far plane words per axis by the ray's direction sign: a
+        // negative 1/d turns the hi plane into the entry plane.  Per child this
+        // replaces the per-axis min / max of the two plane distances (the same
+        // values: q_lo <= q_hi and the scale a has the sign of 1/d), and empty
+        // slots, stored as the inverted box q_lo = 255 > q_hi = 0, miss by
+        // themselves (build_bvh4).
+        const bool sx = sr.invd.x < 0.0f, sy = sr.invd.y < 0.0f, sz = sr.invd.z < 0.0f;
+        const uint32_t xn = sx ? w2.y : w2.x, xf = sx ? w2.x : w2.y;
+        const uint32_t yn = sy ? w2.w : w2.z, yf = sy ? w2.z : w2.w;
+        const uint32_t zn = sz ? w3.y : w3.x, zf = sz ? w3.x : w3.y;
         float t[4];
         int c[4] = {(int)w1.x, (int)w1.y, (int)w1.z, (int)w1.w};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int sh = 8 * i;
-            const float tx0 = fmaf((float)((w2.x >> sh) & 0xffu), ax, bx), tx1 = fmaf((float)((w2.y >> sh) & 0xffu), ax, bx);
-            const float ty0 = fmaf((float)((w2.z >> sh) & 0xffu), ay, by), ty1 = fmaf((float)((w2.w >> sh) & 0xffu), ay, by);
-            const float tz0 = fmaf((float)((w3.x >> sh) & 0xffu), az, bz), tz1 = fmaf((float)((w3.y >> sh) & 0xffu), az, bz);
-            const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), T.tmin));
-            const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), T.h.t));
-            t[i] = (tf < tn || c[i] == kEmptyChild) ? __builtin_inff() : tn;
+            const float txn = fmaf((float)((xn >> sh) & 0xffu), ax, bx), txf = fmaf((float)((xf >> sh) & 0xffu), ax, bx);
+            const float tyn = fmaf((float)((yn >> sh) & 0xffu), ay, by), tyf = fmaf((float)((yf >> sh) & 0xffu), ay, by);
+            const float tzn = fmaf((float)((zn >> sh) & 0xffu), az, bz), tzf = fmaf((float)((zf >> sh) & 0xffu), az, bz);
+            const float tn = fmaxf(fmaxf(txn, tyn), fmaxf(tzn, T.tmin));
+            const float tf = fminf(fminf(txf, tyf), fminf(tzf, T.h.t));
+            t[i] = (tf < tn) ? __builtin_inff() : tn;
         }
-        // nearest first: sorting network on (t, child)
+        // nearest first: sorting network on (t, child), as selects (no branches)
         auto cx = [&](int i, int j) {
-            if (t[j] < t[i]) {
-                const float tt = t[i]; t[i] = t[j]; t[j] = tt;
-                const int cc = c[i]; c[i] = c[j]; c[j] = cc;
-            }
+            const bool sw = t[j] < t[i];
+            const float ti = sw ? t[j] : t[i], tj = sw ? t[i] : t[j];
+            const int ci = sw ? c[j] : c[i], cj = sw ? c[i] : c[j];
+            t[i] = ti; t[j] = tj; c[i] = ci; c[j] = cj;
         };
         // (nearest-only ordering, the rest unsorted, was 5.6 % slower on 1M: profiles/r01_exp2.txt)
         cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
-        if (t[3] != __builtin_inff()) push(c[3]);
-        if (t[2] != __builtin_inff()) push(c[2]);
-        if (t[1] != __builtin_inff()) push(c[1]);
+        // hit children are sorted first; the far ones go on the stack, farthest first
+        if (!wave_any(sp > LSTACK - 3)) {               // wave-uniform: every push stays in LDS
+            if (t[3] != __builtin_inff()) stk[sp++ * STRIDE] = c[3];
+            if (t[2] != __builtin_inff()) stk[sp++ * STRIDE] = c[2];
+            if (t[1] != __builtin_inff()) stk[sp++ * STRIDE] = c[1];
+        } else {
+            if (t[3] != __builtin_inff()) push(c[3]);
+            if (t[2] != __builtin_inff()) push(c[2]);
+            if (t[1] != __builtin_inff()) push(c[1]);
+        }
         node = (t[0] != __builtin_inff()) ? c[0] : pop();
         if constexpr (SPEC) {
             if (parked == 0 && node < 0) { parked = node; node = pop(); }
             // keep going while some lane of the wave still has no leaf to test
             if (!wave_any(parked == 0 && (unsigned)node < (unsigned)kSentinel)) break;
+        } else {
+            if (min_desc > 0 && wave_count((unsigned)node < (unsigned)kSentinel) < min_desc) break;
         }
     }
     if constexpr (SPEC) {
@@ -263,6 +350,11 @@ FRT_HD bool bvh4_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *
         T.node = node;
         T.sp = sp;
         return node == kSentinel;
+    }
+    if ((unsigned)node < (unsigned)kSentinel) {          // postponed (min_desc): still descending
+        T.node = node;
+        T.sp = sp;
+        return false;
     }
     bool done = node == kSentinel || leaf_hit(S, ~node, o, d, T.tmin, anyhit, T.h);
     if (!done) {
@@ -346,7 +438,8 @@ FRT_HD bool brute_all(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit)
 }
 
 template <int WORLD, int STRIDE, int STACK, bool SPEC = false>
-FRT_HD bool trav_step_world(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int *ovf)
+FRT_HD bool trav_step_world(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int *ovf,
+                            int min_desc = 0)
 {
     if constexpr (WORLD == kWorldBrute) {
         return brute_all(T, S, o, d, anyhit);
@@ -354,9 +447,9 @@ FRT_HD bool trav_step_world(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit,
         T.h = trace_list(S, o, d, T.h.t, anyhit);
         return true;
     } else if constexpr (WORLD == kWorldBvh4) {
-        return bvh4_step<STRIDE, STACK, SPEC>(T, S, o, d, anyhit, stk, ovf);
+        return bvh4_step<STRIDE, STACK, SPEC>(T, S, o, d, anyhit, stk, ovf, min_desc);
     } else {
-        return bvh2_step<STRIDE>(T, S, o, d, anyhit, stk);
+        return bvh2_step<STRIDE>(T, S, o, d, anyhit, stk, min_desc);
     }
 }
 

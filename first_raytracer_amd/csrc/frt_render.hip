@@ -47,6 +47,7 @@ struct DevWork {
     int spi, n_chunks;
     uint32_t n_items, n_slots;
     int trav_min;                        // shade when at most this many lanes of a wave still traverse
+    int min_desc;                        // leaf postponing: see bvh2_step
     float *partial;                      // [n_chunks][n_slots][3]
     unsigned *counter;                   // work-queue head
     unsigned long long *wave_rays;       // [n_waves][4]: camera, extension, shadow, samples
@@ -144,14 +145,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     // ray counters are wave-uniform (SGPRs): popcounts of per-iteration ballots
     unsigned long long n_cam = 0, n_ext = 0, n_sh = 0, n_smp = 0;
 
+    unsigned long long diag_t0 = FRT_DIAG_CLOCK();
     for (;;) {
+        FRT_DIAG_TICK(6);
         // ---- traversal: steps (descend to a leaf, test it) of every lane's ray,
         // until at most trav_min lanes are still traversing.  Lanes whose ray is
         // done wait here only while the rest of the wave needs few more steps;
         // then they shade together while the stragglers keep their state.
         for (;;) {
             bool shadow_done = false;
-            if (tracing && trav_step_world<WORLD, kBlock, STACK, SPEC>(T, S, P.ro, P.rd, P.shadow, stk, ovf)) {
+            if (tracing) FRT_DIAG_TICK(3);
+            if (tracing && trav_step_world<WORLD, kBlock, STACK, SPEC>(T, S, P.ro, P.rd, P.shadow, stk, ovf,
+                                                                       W.min_desc)) {
                 if (KIND == FRT_INTEGRATOR_PATH && P.shadow) {   // finish the shadow ray here, keep traversing
                     if (path_after_shadow<MATS>(P, T.h.prim < 0)) {
                         shadow_done = true;
@@ -170,9 +175,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             if (__popcll(__ballot(tracing)) <= W.trav_min) break;
         }
         // ---- shade the finished rays ----
+        const unsigned long long diag_t1 = FRT_DIAG_CLOCK();
+        FRT_DIAG_CYC(16, diag_t1 - diag_t0);
         uint32_t ne = 0, ns = 0;
         bool next_ray = false;
         if (pending) {
+            FRT_DIAG_TICK(4);
             pending = false;
             if (shade_kind<KIND, MATS>(P, S, T.h, W.max_depth, ne, ns)) {
                 acc = acc + P.L;
@@ -183,6 +191,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         }
         n_ext += __popcll(__ballot(ne != 0));
         n_sh += __popcll(__ballot(ns != 0));
+        const unsigned long long diag_t2 = FRT_DIAG_CLOCK();
+        FRT_DIAG_CYC(17, diag_t2 - diag_t1);
         // ---- retire a finished item: its chunk sum goes to its own slot ----
         if (!active && have_item && s_cur >= s_end) {
             float *dst = W.partial + 3ull * ((size_t)chunk * W.n_slots + slot);
@@ -238,6 +248,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             tracing = trav_begin_world<WORLD>(T, S, P.ro, P.rd, P.rtmax);
             pending = !tracing;
         }
+        diag_t0 = FRT_DIAG_CLOCK();
+        FRT_DIAG_CYC(18, diag_t0 - diag_t2);
         if (__ballot(active || !exhausted) == 0) break;
     }
     // per-wave ray counters, no atomics: lane 0 writes the wave's sums
@@ -286,6 +298,7 @@ struct MltWork {
     uint64_t steps;                      // mutations per chain
     float b, scale, s2p, logp;           // normaliser, nx*ny/ns, pixel-dim perturb constants
     int trav_min;                        // see path_megakernel / trav_min()
+    int min_desc;                        // leaf postponing: see bvh2_step
     float *U;                            // [kMltDims][n_local] current primary samples
     float *film;                         // [nx*ny*3] splat accumulation
     unsigned *counter;
@@ -370,7 +383,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
         // ---- traversal steps until at most trav_min lanes still traverse ----
         for (;;) {
             bool ext = false;
-            if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, M.P.ro, M.P.rd, M.P.shadow, stk, ovf)) {
+            if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, M.P.ro, M.P.rd, M.P.shadow, stk, ovf,
+                                                                 W.min_desc)) {
                 if (M.P.shadow) {               // finish the shadow ray here (mlt_shade's shadow branch)
                     if (!path_after_shadow<MATS>(M.P, T.h.prim < 0)) {   // path ended (P.term)
                         tracing = false;
@@ -505,6 +519,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
 }
 
 }  // namespace
+
+#if defined(FRT_DIAG)
+__device__ unsigned long long *frt::frt_diag;
+#endif
 
 // ==========================================================================
 // host side
@@ -654,6 +672,16 @@ static int trav_min(bool lds_scene)
     return std::min(std::max(v, 0), 63);
 }
 
+// Leaf postponing (bvh2_step): a wave's descent stops once fewer than this
+// many of its lanes still descend.  0 = every lane reaches its leaf first.
+// FRT_MIN_DESC overrides (tuning knob, not part of the C-ABI).
+static int min_desc(bool lds_scene)
+{
+    const char *e = std::getenv("FRT_MIN_DESC");
+    const int v = e ? std::atoi(e) : (lds_scene ? kMinDescLds : kMinDescHbm);
+    return std::min(std::max(v, 0), 64);
+}
+
 // Triangles per leaf: FRT_LEAF_SIZE overrides (1 = the reference's one-prim
 // leaves), else 0 = by plan (see flatten_scene).  A tuning knob of this
 // library, not part of the C-ABI.
@@ -787,6 +815,8 @@ static bool build_bvh4(FlatScene &F, int root_ref)
                 while (e > -126 && std::ldexp(255.0, e - 1) >= ext) --e;
             }
             if (e > 20) return false;                  // 2^e / |d| must stay finite (|1/d| <= 1e30)
+            if (e < -100) return false;                // 2^e / |d| must stay a normal float for the empty-slot
+                                                       // test (padded boxes are never this thin)
             ex[a] = e;
             for (int k = 0; k < n; ++k) {
                 double ql = std::floor(((double)ch[k].lo[a] - lo) / std::ldexp(1.0, e));
@@ -800,6 +830,10 @@ static bool build_bvh4(FlatScene &F, int root_ref)
                 qhi[a] |= (uint32_t)qh << (8 * k);
             }
         }
+        // empty slots: the inverted box q_lo = 255 > q_hi = 0 on every axis,
+        // which the near / far slab test of bvh4_step rejects by itself
+        for (int k = n; k < 4; ++k)
+            for (int a = 0; a < 3; ++a) qlo[a] |= 0xffu << (8 * k);
         uint4 w0, w1, w2, w3;
         w0.x = (uint32_t)f2i(org[0]); w0.y = (uint32_t)f2i(org[1]); w0.z = (uint32_t)f2i(org[2]);
         w0.w = (uint32_t)(ex[0] + 127) | ((uint32_t)(ex[1] + 127) << 8) | ((uint32_t)(ex[2] + 127) << 16);
@@ -1296,7 +1330,10 @@ static Launcher bvh_launcher(int waves, size_t sb)
     if (waves == 5) return make_launcher<STACK, WORLD, LDS, 5, SPEC, MATS>(sb);
     return make_launcher<STACK, WORLD, LDS, 1, SPEC, MATS>(sb);
 }
-constexpr int kBvh4LdsStack = 16;   // 16 KiB of LDS per block; deeper entries go to scratch
+#ifndef FRT_EXP_BVH4_LSTACK
+#define FRT_EXP_BVH4_LSTACK 16
+#endif
+constexpr int kBvh4LdsStack = FRT_EXP_BVH4_LSTACK;   // 16 KiB of LDS per block; deeper entries go to scratch
 constexpr int kBvh4LdsStackSmall = 8;   // LDS-resident scenes (shallow trees)
 constexpr int kBruteMaxTris = 128;
 // MATS: the scene has modified_phong / dielectric materials (specular branch compiled in)
@@ -1466,6 +1503,7 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
     W.logp = (float)std::log((double)0.1f / (2.0 / (double)(p->nx + p->ny)));
     W.U = c->partial; W.film = dev_film; W.counter = c->counter; W.wave_rays = c->wave_rays;
     W.trav_min = trav_min(lds_scene);
+    W.min_desc = min_desc(lds_scene);
     HIPCHK(c, hipMemsetAsync(dev_film, 0, (size_t)p->nx * p->ny * 3 * sizeof(float), st));
     HIPCHK(c, hipMemsetAsync(c->counter, 0, 64, st));
     HIPCHK(c, hipEventRecord(c->ev0, st));
@@ -1499,6 +1537,16 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
     c->last_mlt_b = b;
     return FRT_OK;
 }
+
+#if defined(FRT_DIAG)
+static unsigned long long g_diag_sum[kDiagSlots];
+// diagnostic builds only: the per-phase counters of the last path render, summed over waves
+extern "C" int frt_diag_read(unsigned long long *out)
+{
+    for (int k = 0; k < kDiagSlots; ++k) out[k] = g_diag_sum[k];
+    return kDiagSlots;
+}
+#endif
 
 static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots, hipStream_t st, frt_stats *stats)
 {
@@ -1553,8 +1601,21 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     W.spi = spi; W.n_chunks = n_chunks; W.n_items = (uint32_t)n_items; W.n_slots = n_slots;
     W.partial = c->partial; W.counter = c->counter; W.wave_rays = c->wave_rays;
     W.trav_min = trav_min(L.lds_scene);
+    W.min_desc = min_desc(L.lds_scene);
 
     HIPCHK(c, hipMemsetAsync(c->counter, 0, 64, st));
+#if defined(FRT_DIAG)
+    static unsigned long long *diag_buf = nullptr;
+    static size_t diag_n = 0;
+    if (diag_n < n_waves * kDiagSlots) {
+        if (diag_buf) HIPCHK(c, hipFree(diag_buf));
+        diag_n = n_waves * kDiagSlots;
+        HIPCHK(c, hipMalloc(&diag_buf, diag_n * sizeof(unsigned long long)));
+    }
+    HIPCHK(c, hipMemsetAsync(diag_buf, 0, diag_n * sizeof(unsigned long long), st));
+    HIPCHK(c, hipMemcpyToSymbolAsync(HIP_SYMBOL(frt::frt_diag), &diag_buf, sizeof(diag_buf), 0,
+                                     hipMemcpyHostToDevice, st));
+#endif
     HIPCHK(c, hipEventRecord(c->ev0, st));
     DevScene Sarg = c->S;
     void *args[] = {&Sarg, &W};
@@ -1571,6 +1632,15 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     HIPCHK(c, hipStreamSynchronize(st));
     float ms = 0.0f;
     HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+#if defined(FRT_DIAG)
+    {
+        std::vector<unsigned long long> dv(n_waves * kDiagSlots);
+        HIPCHK(c, hipMemcpy(dv.data(), diag_buf, dv.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        for (int k = 0; k < kDiagSlots; ++k) g_diag_sum[k] = 0;
+        for (size_t w = 0; w < n_waves; ++w)
+            for (int k = 0; k < kDiagSlots; ++k) g_diag_sum[k] += dv[w * kDiagSlots + k];
+    }
+#endif
     if (stats) {
         memset(stats, 0, sizeof(*stats));
         for (size_t w = 0; w < n_waves; ++w) {

@@ -6,8 +6,8 @@ kernel ms and Grays/s as JSON lines.
   python tools/perf_ab.py [--scene cornell|cornell_1m|veach] [--spp 64] [--rounds 5]
                           [--variants default,waves5,default/leaf1]
 
-A variant is FLAG[+FLAG...][/leafN][/travN]: render flags (travN sets
-FRT_TRAV_MIN=N for its renders), on a scene uploaded with
+A variant is FLAG[+FLAG...][/leafN][/travN][/descN]: render flags (travN sets
+FRT_TRAV_MIN=N, descN FRT_MIN_DESC=N for its renders), on a scene uploaded with
 FRT_LEAF_SIZE=N (one context per leaf size; default = the library default).
 """
 import argparse
@@ -72,10 +72,11 @@ def main():
     for r in range(args.rounds + 1):
         for v in chosen:
             leaf = opt(v, "leaf")
-            if opt(v, "trav"):
-                os.environ["FRT_TRAV_MIN"] = opt(v, "trav")
-            else:
-                os.environ.pop("FRT_TRAV_MIN", None)
+            for key, env in (("trav", "FRT_TRAV_MIN"), ("desc", "FRT_MIN_DESC")):
+                if opt(v, key):
+                    os.environ[env] = opt(v, key)
+                else:
+                    os.environ.pop(env, None)
             p = frt.RenderParams.make(nx, ny, args.spp, seed=0, flags=flags[v.split("/")[0]])
             films[leaf], st = ctxs[leaf].render(p, films.get(leaf))
             if r > 0:
