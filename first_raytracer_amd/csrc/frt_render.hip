@@ -16,12 +16,14 @@
 // hitable_list.cpp:4-21, camera::get_ray camera.h:30-35, viewer::add_sample
 // viewer.cpp:109-132.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -286,6 +288,26 @@ __global__ void film_reduce(const float *__restrict__ partial, float *__restrict
     out[3ull * s + 2] = b;
 }
 
+// frt_render_multi: the gathered slot buffers of n shards (shard r at
+// gathered[r * max_slots * 3]) into the device film, (y*nx+x)*3
+__global__ void scatter_shards(const float *__restrict__ gathered, float *__restrict__ film, uint32_t max_slots,
+                               int n, int tile, int ntx, int nx, int ny)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (uint64_t)max_slots * (uint64_t)n) return;
+    const int r = (int)(i / max_slots);
+    const uint32_t s = (uint32_t)(i % max_slots);
+    const int T2 = tile * tile;
+    const int tile_id = r + (int)(s / (uint32_t)T2) * n;
+    int lx, ly;
+    slot_to_local((int)(s % (uint32_t)T2), tile, lx, ly);
+    const int px = (tile_id % ntx) * tile + lx, py = (tile_id / ntx) * tile + ly;
+    if (px >= nx || py >= ny) return;                // padding slots, slots past a short shard's end
+    const size_t d = 3 * ((size_t)py * nx + px);
+    film[d + 0] = gathered[3 * i + 0];
+    film[d + 1] = gathered[3 * i + 1];
+    film[d + 2] = gathered[3 * i + 2];
+}
 
 // ------------------------------------------------------------------------
 // PSS-MLT (pssmlt.cpp:301-365)
@@ -550,7 +572,21 @@ struct frt_ctx {
     unsigned *counter = nullptr;
     unsigned long long *wave_rays = nullptr; size_t wave_rays_n = 0;
     float *slots_out = nullptr; size_t slots_out_bytes = 0;
+    // frt_render_multi on this context as shard 0: RCCL communicators over the
+    // member devices (one per member, cached while the device list is the
+    // same), the gather buffer and the device film
+    std::vector<int> comm_devs;
+    std::vector<ncclComm_t> comms;
+    float *gather = nullptr; size_t gather_bytes = 0;
+    float *film_dev = nullptr; size_t film_dev_bytes = 0;
 };
+
+static void free_comms(frt_ctx *c)
+{
+    for (ncclComm_t m : c->comms) (void)ncclCommDestroy(m);
+    c->comms.clear();
+    c->comm_devs.clear();
+}
 
 static int set_err(frt_ctx *c, int code, const std::string &m)
 {
@@ -611,6 +647,9 @@ extern "C" int frt_destroy(frt_ctx *c)
     if (c->counter) (void)hipFree(c->counter);
     if (c->wave_rays) (void)hipFree(c->wave_rays);
     if (c->slots_out) (void)hipFree(c->slots_out);
+    free_comms(c);
+    if (c->gather) (void)hipFree(c->gather);
+    if (c->film_dev) (void)hipFree(c->film_dev);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1323,10 +1362,13 @@ static Launcher make_launcher(size_t scene_bytes)
     L.wide = WORLD == kWorldBvh4;
     return L;
 }
+#ifndef FRT_EXP_W6
+#define FRT_EXP_W6 6   // experiment builds: the register cap behind the "6 waves" plans
+#endif
 template <int STACK, bool LDS, int WORLD = FRT_WORLD_BVH, bool SPEC = false, bool MATS = false>
 static Launcher bvh_launcher(int waves, size_t sb)
 {
-    if (waves == 6) return make_launcher<STACK, WORLD, LDS, 6, SPEC, MATS>(sb);
+    if (waves == 6) return make_launcher<STACK, WORLD, LDS, FRT_EXP_W6, SPEC, MATS>(sb);
     if (waves == 5) return make_launcher<STACK, WORLD, LDS, 5, SPEC, MATS>(sb);
     return make_launcher<STACK, WORLD, LDS, 1, SPEC, MATS>(sb);
 }
@@ -1705,28 +1747,79 @@ extern "C" int frt_render(frt_ctx *c, const frt_render_params *p, float *film_rg
     return FRT_OK;
 }
 
+// device buffer of at least `bytes` (grown, never shrunk)
+static int ensure_buf(frt_ctx *c, float **buf, size_t *have, size_t bytes)
+{
+    if (bytes <= *have) return FRT_OK;
+    if (*buf) HIPCHK(c, hipFree(*buf));
+    *buf = nullptr;
+    *have = 0;
+    HIPCHK(c, hipMalloc(buf, bytes));
+    *have = bytes;
+    return FRT_OK;
+}
+
+#define NCCLCHK(ctx, x)                                                                            \
+    do {                                                                                           \
+        ncclResult_t r_ = (x);                                                                     \
+        if (r_ != ncclSuccess)                                                                     \
+            return set_err(ctx, FRT_E_HIP, std::string(#x) + ": " + ncclGetErrorString(r_));      \
+    } while (0)
+
 // One process, n GPUs (SURVEY 8(b) frt_render_multi; what frt::path_gpu does
-// in C++): context i renders shard (i, n) of the request on its own host
-// thread.  Path shards write disjoint pixels of film_rgb; PSS-MLT shard films
-// are summed into film_rgb in the fixed order 0..n-1.  Stats: ray and sample
-// counts summed, kernel_ms / total_ms the slowest shard's.
+// in C++; the reference's task graph over rows, path.cpp:118-148).  Context i
+// renders shard (i, n) -- tiles i, i + n, ... -- into its own HBM slot buffer
+// on its own host thread (frt_render_device), then the buffers move device to
+// device to context 0's GPU:
+//   * every context on its own device: RCCL, one communicator per device
+//     (ncclCommInitAll, cached on ctxs[0]), a grouped ncclSend / ncclRecv of
+//     each shard's slots to rank 0 over xGMI (PSS-MLT: ncclReduce, sum);
+//   * contexts sharing a device (RCCL takes one rank per device):
+//     hipMemcpyPeerAsync into the same gather buffer (PSS-MLT: summed in
+//     order 0..n-1 by film_add).
+// Context 0 scatters the gathered slots into a device film and copies it to
+// film_rgb once.  Path shards cover every pixel, so film_rgb is overwritten;
+// PSS-MLT adds the summed splat film to film_rgb (as frt_render does).
+// Stats: ray and sample counts summed, kernel_ms / total_ms the slowest shard's.
+__global__ void film_add(float *__restrict__ dst, const float *__restrict__ src, size_t n)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] += src[i];
+}
+
 extern "C" int frt_render_multi(frt_ctx **ctxs, int n, const frt_render_params *p, float *film_rgb, frt_stats *st)
 {
     if (!ctxs || n <= 0 || !p || !film_rgb) return FRT_E_INVALID;
     for (int i = 0; i < n; ++i)
         if (!ctxs[i]) return FRT_E_INVALID;
+    frt_ctx *c0 = ctxs[0];
     if (!params_ok(p) || p->shard_count != 1 || p->shard_index != 0)
-        return set_err(ctxs[0], FRT_E_INVALID, "frt_render_multi: params must describe the whole frame (shard 0 of 1)");
+        return set_err(c0, FRT_E_INVALID, "frt_render_multi: params must describe the whole frame (shard 0 of 1)");
+    const auto t_start = std::chrono::steady_clock::now();
     const bool mlt = p->integrator == FRT_INTEGRATOR_PSSMLT;
     const size_t film_n = (size_t)p->nx * p->ny * 3;
-    std::vector<std::vector<float>> part(mlt ? n : 0, std::vector<float>(mlt ? film_n : 0, 0.0f));
+    // per-shard slot buffers (the largest shard's size: RCCL moves equal counts)
+    int64_t max_slots = 0;
+    for (int i = 0; i < n; ++i) {
+        frt_render_params q = *p;
+        q.shard_index = i;
+        q.shard_count = n;
+        max_slots = std::max<int64_t>(max_slots, frt_shard_slot_count(&q));
+    }
+    const size_t shard_floats = (size_t)max_slots * 3;
+    for (int i = 0; i < n; ++i) {
+        HIPCHK(ctxs[i], hipSetDevice(ctxs[i]->device));
+        const int rc = ensure_buf(ctxs[i], &ctxs[i]->slots_out, &ctxs[i]->slots_out_bytes,
+                                  std::max<size_t>(shard_floats * sizeof(float), 16));
+        if (rc != FRT_OK) return rc;
+    }
     std::vector<frt_stats> sts(n);
     std::vector<int> rcs(n, FRT_OK);
     auto work = [&](int i) {
         frt_render_params q = *p;
         q.shard_index = i;
         q.shard_count = n;
-        rcs[i] = frt_render(ctxs[i], &q, mlt ? part[i].data() : film_rgb, &sts[i]);
+        rcs[i] = render_impl(ctxs[i], &q, ctxs[i]->slots_out, ctxs[i]->stream, &sts[i]);
     };
     std::vector<std::thread> th;
     for (int i = 1; i < n; ++i) th.emplace_back(work, i);
@@ -1734,12 +1827,74 @@ extern "C" int frt_render_multi(frt_ctx **ctxs, int n, const frt_render_params *
     for (auto &t : th) t.join();
     for (int i = 0; i < n; ++i)
         if (rcs[i] != FRT_OK) {
-            if (i != 0) set_err(ctxs[0], rcs[i], std::string("shard ") + std::to_string(i) + ": " + ctxs[i]->err);
+            if (i != 0) set_err(c0, rcs[i], std::string("shard ") + std::to_string(i) + ": " + ctxs[i]->err);
             return rcs[i];
         }
-    if (mlt)
-        for (int i = 0; i < n; ++i)
-            for (size_t k = 0; k < film_n; ++k) film_rgb[k] += part[i][k];
+    // ---- device-to-device exchange to context 0 ----
+    std::vector<int> devs(n);
+    bool distinct = true;
+    for (int i = 0; i < n; ++i) {
+        devs[i] = ctxs[i]->device;
+        for (int j = 0; j < i; ++j) distinct &= devs[j] != devs[i];
+    }
+    HIPCHK(c0, hipSetDevice(c0->device));
+    int rc = ensure_buf(c0, &c0->gather, &c0->gather_bytes, std::max<size_t>((size_t)n * shard_floats * sizeof(float), 16));
+    if (rc == FRT_OK) rc = ensure_buf(c0, &c0->film_dev, &c0->film_dev_bytes, std::max<size_t>(film_n * sizeof(float), 16));
+    if (rc != FRT_OK) return rc;
+    if (distinct) {
+        if (c0->comm_devs != devs) {
+            free_comms(c0);
+            c0->comms.resize(n);
+            NCCLCHK(c0, ncclCommInitAll(c0->comms.data(), n, devs.data()));
+            c0->comm_devs = devs;
+        }
+        NCCLCHK(c0, ncclGroupStart());
+        for (int i = 0; i < n; ++i) {
+            if (mlt) {          // the shard films summed on rank 0
+                NCCLCHK(c0, ncclReduce(ctxs[i]->slots_out, i == 0 ? c0->film_dev : ctxs[i]->slots_out, film_n,
+                                       ncclFloat, ncclSum, 0, c0->comms[i], ctxs[i]->stream));
+            } else {            // shard i's slots -> gather[i]
+                NCCLCHK(c0, ncclSend(ctxs[i]->slots_out, shard_floats, ncclFloat, 0, c0->comms[i], ctxs[i]->stream));
+                NCCLCHK(c0, ncclRecv(c0->gather + (size_t)i * shard_floats, shard_floats, ncclFloat, i, c0->comms[0],
+                                     c0->stream));
+            }
+        }
+        NCCLCHK(c0, ncclGroupEnd());
+        for (int i = 1; i < n; ++i) {   // rank 0's stream waits for the senders' streams
+            HIPCHK(ctxs[i], hipSetDevice(ctxs[i]->device));
+            HIPCHK(ctxs[i], hipStreamSynchronize(ctxs[i]->stream));
+        }
+        HIPCHK(c0, hipSetDevice(c0->device));
+    } else {
+        for (int i = 0; i < n; ++i) {
+            HIPCHK(c0, hipMemcpyPeerAsync(c0->gather + (size_t)i * shard_floats, c0->device, ctxs[i]->slots_out,
+                                          ctxs[i]->device, shard_floats * sizeof(float), c0->stream));
+        }
+        if (mlt) {
+            HIPCHK(c0, hipMemsetAsync(c0->film_dev, 0, film_n * sizeof(float), c0->stream));
+            for (int i = 0; i < n; ++i) {
+                hipLaunchKernelGGL(film_add, dim3((unsigned)((film_n + 255) / 256)), dim3(256), 0, c0->stream,
+                                   c0->film_dev, c0->gather + (size_t)i * shard_floats, film_n);
+                HIPCHK(c0, hipGetLastError());
+            }
+        }
+    }
+    if (!mlt) {
+        const int T = eff_tile(p);
+        const uint64_t total = (uint64_t)n * (uint64_t)max_slots;
+        hipLaunchKernelGGL(scatter_shards, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, c0->stream,
+                           c0->gather, c0->film_dev, (uint32_t)max_slots, n, T, (p->nx + T - 1) / T, p->nx, p->ny);
+        HIPCHK(c0, hipGetLastError());
+    }
+    if (mlt) {
+        std::vector<float> host(film_n);
+        HIPCHK(c0, hipMemcpyAsync(host.data(), c0->film_dev, film_n * sizeof(float), hipMemcpyDeviceToHost, c0->stream));
+        HIPCHK(c0, hipStreamSynchronize(c0->stream));
+        for (size_t k = 0; k < film_n; ++k) film_rgb[k] += host[k];
+    } else {
+        HIPCHK(c0, hipMemcpyAsync(film_rgb, c0->film_dev, film_n * sizeof(float), hipMemcpyDeviceToHost, c0->stream));
+        HIPCHK(c0, hipStreamSynchronize(c0->stream));
+    }
     if (st) {
         frt_stats a = sts[0];
         for (int i = 1; i < n; ++i) {
@@ -1747,8 +1902,8 @@ extern "C" int frt_render_multi(frt_ctx **ctxs, int n, const frt_render_params *
             a.shadow_rays += sts[i].shadow_rays; a.samples += sts[i].samples;
             a.pixels += mlt ? 0 : sts[i].pixels; a.work_items += sts[i].work_items;
             a.kernel_ms = std::max(a.kernel_ms, sts[i].kernel_ms);
-            a.total_ms = std::max(a.total_ms, sts[i].total_ms);
         }
+        a.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
         *st = a;
     }
     return FRT_OK;

@@ -171,16 +171,17 @@ def test_bvh4_matches_binary(ctx, cornell_obj, tmp_path):
 
 @pytest.mark.parametrize("flags", [0, frt.FRT_FLAG_NO_LDS_SCENE, frt.FRT_FLAG_NO_LDS_SCENE | frt.FRT_FLAG_BVH2])
 def test_trav_min_invariance(ctx, cornell_obj, tmp_path, monkeypatch, flags):
-    """When finished rays get shaded (FRT_TRAV_MIN) changes scheduling only:
-    every ray's hit and every item's sum order are the same, so films are
-    bit-identical."""
+    """When finished rays get shaded (FRT_TRAV_MIN) and when a wave's descent
+    stops for leaf tests (FRT_MIN_DESC) change scheduling only: every ray's hit
+    and every item's sum order are the same, so films are bit-identical."""
     dst = str(tmp_path / "tess.obj")
     frt.write_tessellated_obj(cornell_obj, 6, dst)
     nx, ny, spp = 48, 40, 8
     ctx.upload(frt.HostScene("cornell_box_obj", dst, nx / ny))
     res = []
-    for tm in ("0", "16", "48"):
+    for tm, desc in (("0", "0"), ("16", "0"), ("48", "0"), ("24", "8"), ("16", "40")):
         monkeypatch.setenv("FRT_TRAV_MIN", tm)
+        monkeypatch.setenv("FRT_MIN_DESC", desc)      # leaf postponing (bvh2_step / bvh4_step)
         f, st = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=17, flags=flags))
         res.append((f, st.rays))
     for f, r in res[1:]:
@@ -220,9 +221,10 @@ def test_deterministic_and_shard_invariant(ctx, cornell_obj):
 
 
 def test_render_multi_matches_single(ctx, cornell_obj):
-    """frt_render_multi over 3 contexts (all on device 0 here; one per GPU in
-    production) gives the single-context film bit for bit, and PSS-MLT shard
-    films sum to the single-context film within fp32 atomic-order noise."""
+    """frt_render_multi over 3 contexts sharing device 0 (RCCL takes one rank
+    per device, so shards move with hipMemcpyPeerAsync here) gives the
+    single-context film bit for bit, and PSS-MLT shard films sum to the
+    single-context film within fp32 atomic-order noise."""
     nx, ny, spp = 80, 60, 8
     hs = frt.HostScene("cornell_box_obj", cornell_obj, nx / ny)
     ctx.upload(hs)
@@ -240,6 +242,35 @@ def test_render_multi_matches_single(ctx, cornell_obj):
         assert np.allclose(m1, mm, rtol=1e-4, atol=1e-5)
     finally:
         for c in extra:
+            c.close()
+
+
+def test_render_multi_rccl_path(ctx, cornell_obj):
+    """frt_render_multi with every context on its own device moves the shard
+    slots to context 0 with RCCL (ncclCommInitAll + grouped ncclSend / ncclRecv,
+    ncclReduce for PSS-MLT).  One context = one rank sending to itself, the
+    path a one-GPU box can run; every GPU of the box when it has more.  The
+    film equals the single-context render bit for bit (the RNG is keyed by
+    the global pixel, the sums are per slot)."""
+    import torch
+    nx, ny, spp = 72, 40, 8
+    hs = frt.HostScene("cornell_box_obj", cornell_obj, nx / ny)
+    ctx.upload(hs)
+    one, st1 = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=33, tile_size=16))
+    ctxs = [ctx] + [frt.Context(d) for d in range(1, torch.cuda.device_count())]
+    try:
+        for c in ctxs[1:]:
+            c.upload(hs)
+        for _ in range(2):                      # the second call reuses the cached communicators
+            many, stm = frt.render_multi(ctxs, frt.RenderParams.make(nx, ny, spp, seed=33, tile_size=16))
+            assert np.array_equal(one, many)
+            assert stm.rays == st1.rays and stm.pixels == nx * ny
+        p = frt.RenderParams.pssmlt(nx, ny, 4, 1000, seed=6, bootstrap=1000)
+        m1, _ = ctx.render(p)
+        mm, _ = frt.render_multi(ctxs, p)
+        assert np.allclose(m1, mm, rtol=1e-4, atol=1e-5)
+    finally:
+        for c in ctxs[1:]:
             c.close()
 
 
