@@ -441,6 +441,14 @@ template <int WORLD, int STRIDE, int STACK, bool SPEC = false>
 FRT_HD bool trav_step_world(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int *ovf,
                             int min_desc = 0)
 {
+    // 4-wide (HBM-resident scenes): the slab ray and t_min again from (o, d)
+    // (the values trav_begin set), so that they are not live across the
+    // megakernel's shading phases (spilled VGPRs 81 -> 36 at the 6-wave cap;
+    // cornell_1m +2.8 %, same-call A/B).  The binary LDS plan keeps them.
+    if constexpr (WORLD == kWorldBvh4) {
+        T.sr = slab_ray(o, d);
+        T.tmin = kEps * fmaxf(1.0f, fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z))));
+    }
     if constexpr (WORLD == kWorldBrute) {
         return brute_all(T, S, o, d, anyhit);
     } else if constexpr (WORLD == FRT_WORLD_LIST) {

@@ -119,26 +119,39 @@ __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
 // ------------------------------------------------------------------------
 // the persistent path megakernel
 // ------------------------------------------------------------------------
-// KIND = FRT_INTEGRATOR_PATH, _AO or _NORMALS: the per-sample integrator (shade_kind)
+// Work-item state of a lane: sample range, slot, chunk, pixel and the chunk's
+// radiance sum, in an LDS column (kItemWords x kBlock ints after the traversal
+// stack).  It is touched once per sample; as VGPRs it stayed live -- and
+// spilled to scratch -- across every traversal and shading phase (spilled
+// VGPRs at the register cap: cornell_1m 51 -> 24, Cornell 31 -> 6; same-call
+// A/B +4.5 % / +1 %).
+constexpr int kItemWords = 10;
+enum { kIsCur, kIsEnd, kIsSlot, kIsChunk, kIsPix, kIsPx, kIsPy, kIsAcc };   // kIsAcc..+2: r, g, b
+struct ItemState {
+    int *b;      // the lane's column
+    __device__ int get(int k) const { return b[k * kBlock]; }
+    __device__ void set(int k, int x) const { b[k * kBlock] = x; }
+};
+
 template <int STACK, int WORLD, bool LDS_SCENE, int WAVES = 1, bool SPEC = false, bool MATS = false,
           int KIND = FRT_INTEGRATOR_PATH>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void path_megakernel(
     const DevScene S0, const DevWork W)
 {
-    extern __shared__ __attribute__((aligned(16))) int lds_mem[];   // [STACK][kBlock] stack, then the scene
+    // [STACK][kBlock] stack, [kItemWords][kBlock] item state, then the scene
+    extern __shared__ __attribute__((aligned(16))) int lds_mem[];
     int *stk = lds_mem + threadIdx.x;                                 // one LDS column per lane
+    constexpr int kStackInts = WORLD != FRT_WORLD_LIST ? STACK * kBlock : 0;
+    constexpr int kItemInts = kItemWords * kBlock;
     DevScene S = S0;
-    if constexpr (LDS_SCENE) scene_to_lds<WORLD == kWorldBvh4>(S, lds_mem + STACK * kBlock);
+    if constexpr (LDS_SCENE) scene_to_lds<WORLD == kWorldBvh4>(S, lds_mem + kStackInts + kItemInts);
     else scene_strides_hbm(S);
     const int lane = threadIdx.x & 63;
     const int T2 = W.tile * W.tile;
 
     // work-item state
     bool have_item = false, exhausted = false, active = false;
-    int s_cur = 0, s_end = 0;
-    uint32_t slot = 0, chunk = 0, pix = 0;
-    int px = 0, py = 0;
-    f3 acc = mk3(0, 0, 0);
+    const ItemState I{lds_mem + kStackInts + (int)threadIdx.x};
     PathState P;
     // ray in flight: tracing = traversal steps remain; pending = finished, not yet shaded
     Trav T;
@@ -157,8 +170,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         for (;;) {
             bool shadow_done = false;
             if (tracing) FRT_DIAG_TICK(3);
+            // (LDS-resident binary plans: no leaf postponing, compiled out)
             if (tracing && trav_step_world<WORLD, kBlock, STACK, SPEC>(T, S, P.ro, P.rd, P.shadow, stk, ovf,
-                                                                       W.min_desc)) {
+                                                                       LDS_SCENE && WORLD == FRT_WORLD_BVH
+                                                                           ? 0 : W.min_desc)) {
                 if (KIND == FRT_INTEGRATOR_PATH && P.shadow) {   // finish the shadow ray here, keep traversing
                     if (path_after_shadow<MATS>(P, T.h.prim < 0)) {
                         shadow_done = true;
@@ -185,7 +200,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             FRT_DIAG_TICK(4);
             pending = false;
             if (shade_kind<KIND, MATS>(P, S, T.h, W.max_depth, ne, ns)) {
-                acc = acc + P.L;
+                I.set(kIsAcc + 0, f2i(i2f(I.get(kIsAcc + 0)) + P.L.x));
+                I.set(kIsAcc + 1, f2i(i2f(I.get(kIsAcc + 1)) + P.L.y));
+                I.set(kIsAcc + 2, f2i(i2f(I.get(kIsAcc + 2)) + P.L.z));
                 active = false;
             } else {
                 next_ray = true;
@@ -196,9 +213,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         const unsigned long long diag_t2 = FRT_DIAG_CLOCK();
         FRT_DIAG_CYC(17, diag_t2 - diag_t1);
         // ---- retire a finished item: its chunk sum goes to its own slot ----
-        if (!active && have_item && s_cur >= s_end) {
-            float *dst = W.partial + 3ull * ((size_t)chunk * W.n_slots + slot);
-            dst[0] = acc.x; dst[1] = acc.y; dst[2] = acc.z;
+        if (!active && have_item && I.get(kIsCur) >= I.get(kIsEnd)) {
+            float *dst = W.partial + 3ull * ((size_t)(uint32_t)I.get(kIsChunk) * W.n_slots + (uint32_t)I.get(kIsSlot));
+            dst[0] = i2f(I.get(kIsAcc + 0)); dst[1] = i2f(I.get(kIsAcc + 1)); dst[2] = i2f(I.get(kIsAcc + 2));
             have_item = false;
         }
         // ---- wave-aggregated refill: one atomic per wave, lanes ranked by mbcnt ----
@@ -216,29 +233,35 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
                 } else {
                     const uint32_t s = w % (uint32_t)T2;
                     const uint32_t q = w / (uint32_t)T2;
-                    chunk = q % (uint32_t)W.n_chunks;
+                    const uint32_t chunk = q % (uint32_t)W.n_chunks;
                     const uint32_t t_ord = q / (uint32_t)W.n_chunks;
                     const int tile_id = W.shard_index + (int)t_ord * W.shard_count;
                     int lx, ly;
                     slot_to_local((int)s, W.tile, lx, ly);
-                    px = (tile_id % W.ntx) * W.tile + lx;
-                    py = (tile_id / W.ntx) * W.tile + ly;
-                    slot = t_ord * (uint32_t)T2 + s;
+                    const int px = (tile_id % W.ntx) * W.tile + lx;
+                    const int py = (tile_id / W.ntx) * W.tile + ly;
                     if (px < W.nx && py < W.ny) {   // padding slots of edge tiles carry no work
                         have_item = true;
-                        pix = (uint32_t)py * (uint32_t)W.nx + (uint32_t)px;
-                        s_cur = (int)chunk * W.spi;
-                        s_end = min(W.spp, s_cur + W.spi);
-                        acc = mk3(0, 0, 0);
+                        const int s_cur = (int)chunk * W.spi;
+                        I.set(kIsCur, s_cur);
+                        I.set(kIsEnd, min(W.spp, s_cur + W.spi));
+                        I.set(kIsSlot, (int)(t_ord * (uint32_t)T2 + s));
+                        I.set(kIsChunk, (int)chunk);
+                        I.set(kIsPix, py * W.nx + px);
+                        I.set(kIsPx, px);
+                        I.set(kIsPy, py);
+                        I.set(kIsAcc + 0, 0); I.set(kIsAcc + 1, 0); I.set(kIsAcc + 2, 0);
                     }
                 }
             }
         }
         // ---- next camera sample of the item ----
-        const bool start = !active && have_item && s_cur < s_end;
+        const bool start = !active && have_item && I.get(kIsCur) < I.get(kIsEnd);
         if (start) {
-            path_begin(P, S, px, py, W.nx, W.ny, W.seed, pix, (uint32_t)s_cur + W.s_off);
-            ++s_cur;
+            const int s_cur = I.get(kIsCur);
+            path_begin(P, S, I.get(kIsPx), I.get(kIsPy), W.nx, W.ny, W.seed, (uint32_t)I.get(kIsPix),
+                       (uint32_t)s_cur + W.s_off);
+            I.set(kIsCur, s_cur + 1);
             active = true;
             next_ray = true;
         }
@@ -1355,7 +1378,8 @@ static Launcher make_launcher(size_t scene_bytes)
 {
     Launcher L;
     L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES, SPEC, MATS, KIND>);
-    L.lds = (WORLD != FRT_WORLD_LIST ? (size_t)STACK * kBlock * sizeof(int) : 0) + (LDS ? scene_bytes : 0);
+    L.lds = (WORLD != FRT_WORLD_LIST ? (size_t)STACK * kBlock * sizeof(int) : 0) +
+            (size_t)kItemWords * kBlock * sizeof(int) + (LDS ? scene_bytes : 0);
     L.stack = STACK;
     L.waves = WAVES > 1 ? WAVES : 0;
     L.lds_scene = LDS;
