@@ -31,6 +31,7 @@ FRT_FLAG_BVH2 = 16
 FRT_FLAG_BVH4 = 32
 FRT_FLAG_BRUTE = 64
 FRT_FLAG_SPEC = 128
+FRT_FLAG_NO_OCT = 256
 FRT_INTEGRATOR_PATH, FRT_INTEGRATOR_PSSMLT, FRT_INTEGRATOR_AO, FRT_INTEGRATOR_NORMALS = 0, 1, 2, 3
 
 ERRORS = {0: "ok", -1: "invalid", -2: "hip", -3: "no scene", -4: "unsupported", -5: "io", -6: "no gfx950 device"}

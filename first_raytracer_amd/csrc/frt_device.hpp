@@ -151,6 +151,18 @@ FRT_HD float slab_entry(float lox, float loy, float loz, float hix, float hiy, f
     return (tf < tn) ? __builtin_inff() : tn;
 }
 
+// the same test on a box stored as (near, far) planes for the ray's octant
+// (bvh2_step OCT): bit-identical to slab_entry on the (lo, hi) box
+FRT_HD float slab_entry_nf(float nx, float ny, float nz, float fx, float fy, float fz, const SlabRay &r,
+                           float tmin, float tmax)
+{
+    const float tn = fmaxf(fmaxf(fmaf(nx, r.invd.x, r.oinv.x), fmaf(ny, r.invd.y, r.oinv.y)),
+                           fmaxf(fmaf(nz, r.invd.z, r.oinv.z), tmin));
+    const float tf = fminf(fminf(fmaf(fx, r.invd.x, r.oinv.x), fmaf(fy, r.invd.y, r.oinv.y)),
+                           fminf(fmaf(fz, r.invd.z, r.oinv.z), tmax));
+    return (tf < tn) ? __builtin_inff() : tn;
+}
+
 // Moller-Trumbore (triangle.h:69-118): returns t, or -1 on miss.  Accepts
 // t in (tmin, tmax] -- the caller resolves t == tmax with the DFS rank tie rule.
 FRT_HD float tri_intersect(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float tmin, float tmax, float &u, float &v)

@@ -81,6 +81,7 @@ constexpr int kSentinel = 0x7fffffff;   // "stack empty"; never a node index
 constexpr int kEmptyChild = kSentinel;  // unused slot of a 4-wide node (never pushed)
 constexpr int kWorldBvh4 = 2;           // internal world kind: 4-wide quantized BVH
 constexpr int kWorldBrute = 3;          // internal world kind: every triangle, in lockstep (tiny scenes)
+constexpr int kWorldBvh2Oct = 4;        // internal world kind: binary nodes from LDS, one copy per ray octant
 constexpr int kBvh4Overflow = 40;       // private stack entries after the LDS ones
 
 // device scene (fp32, HBM-resident; DESIGN.md "Data layout")
@@ -96,6 +97,8 @@ struct DevScene {
     const int *lights;       // device prim refs
     const int *list;         // device prim refs (list worlds)
     const uint4 *nodes4;     // 4 x uint4 per 4-wide node (HBM-resident scenes; DESIGN.md "BVH4Q")
+    const float4 *nodes_oct; // 8 copies of `nodes`, copy o with each child box as (near xyz, far xyz) for
+                             // rays of octant o (bit a set: 1/d_a < 0); LDS plans copy them (kWorldBvh2Oct)
     int root;                // node index, or ~prim for a single-leaf world
     int root4;               // 4-wide root node, or the same leaf ref as root
     int n_lights, n_list, world_kind;
@@ -204,18 +207,34 @@ FRT_HD bool trav_begin(Trav &T, const DevScene &S, int root, f3 o, f3 d, float t
 // lanes keep their node and stack and resume on the next step, while the lanes
 // that reached a leaf test it now.  A wave then no longer runs its node loop
 // for as many trips as its slowest lane needs to reach a leaf.
-template <int STRIDE>
+// OCT (kWorldBvh2Oct): S.nodes holds the 8 octant copies; the ray's copy
+// stores every child box as (near xyz, far xyz) for its direction signs, so a
+// box costs 6 FMAs and two 3-way max / min instead of also sorting each
+// slab's two distances (the same values: lo <= hi and 1/d has the octant's
+// sign, so the near plane's distance is the smaller one).
+template <int STRIDE, bool OCT = false>
 FRT_HD bool bvh2_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int min_desc = 0)
 {
     int node = T.node, sp = T.sp;
+    DevScene Sn = S;
+    if constexpr (OCT) {
+        const int oct = (T.sr.invd.x < 0.0f ? 1 : 0) | (T.sr.invd.y < 0.0f ? 2 : 0) | (T.sr.invd.z < 0.0f ? 4 : 0);
+        Sn.nodes = S.nodes + oct * 4 * S.node_ps;
+    }
     // (a branch-free body -- speculative stack-top read, predicated push -- was
     // 4.5 % slower on Cornell: profiles/r01_exp1_branchy.txt)
     while ((unsigned)node < (unsigned)kSentinel) {   // interior node
         FRT_DIAG_TICK(2);
-        const float4 n0 = node_part(S, node, 0), n1 = node_part(S, node, 1);
-        const float4 n2 = node_part(S, node, 2), n3 = node_part(S, node, 3);
-        const float t0 = slab_entry(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, T.tmin, T.h.t);
-        const float t1 = slab_entry(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, T.sr, T.tmin, T.h.t);
+        const float4 n0 = node_part(Sn, node, 0), n1 = node_part(Sn, node, 1);
+        const float4 n2 = node_part(Sn, node, 2), n3 = node_part(Sn, node, 3);
+        float t0, t1;
+        if constexpr (OCT) {
+            t0 = slab_entry_nf(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, T.tmin, T.h.t);
+            t1 = slab_entry_nf(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, T.sr, T.tmin, T.h.t);
+        } else {
+            t0 = slab_entry(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, T.tmin, T.h.t);
+            t1 = slab_entry(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, T.sr, T.tmin, T.h.t);
+        }
         const int c0 = f2i(n3.x), c1 = f2i(n3.y);
         const bool h0 = t0 != __builtin_inff(), h1 = t1 != __builtin_inff();
         if (h0 && h1) {
@@ -457,7 +476,7 @@ FRT_HD bool trav_step_world(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit,
     } else if constexpr (WORLD == kWorldBvh4) {
         return bvh4_step<STRIDE, STACK, SPEC>(T, S, o, d, anyhit, stk, ovf, min_desc);
     } else {
-        return bvh2_step<STRIDE>(T, S, o, d, anyhit, stk, min_desc);
+        return bvh2_step<STRIDE, WORLD == kWorldBvh2Oct>(T, S, o, d, anyhit, stk, min_desc);
     }
 }
 

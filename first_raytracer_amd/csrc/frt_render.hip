@@ -40,6 +40,7 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr size_t kLdsSceneBytes = 16 * 1024;   // LDS plan: 5-6 blocks/CU x (stack + scene) must fit 160 KiB
+constexpr size_t kLdsOctBytes = 14 * 1024;     // ... with the octant node copies: 5 x (8 + 10 + 14) KiB
 constexpr int kLdsMaxDepth = 16;                // LDS plan: binary stacks of 8 or 16 entries
 
 struct DevWork {
@@ -85,16 +86,22 @@ __device__ __forceinline__ void scene_strides_hbm(DevScene &S)
     S.sh_es = 2; S.sh_ps = 1;
 }
 
-template <bool WIDE>
+template <int WORLD>
 __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
 {
+    constexpr bool WIDE = WORLD == kWorldBvh4, OCT = WORLD == kWorldBvh2Oct;
     float4 *l4 = reinterpret_cast<float4 *>(lds_base);
     const DevScene S0 = S;
-    const int nn = WIDE ? 4 * S0.n_nodes4 : 4 * S0.n_nodes;
+    const int nn = WIDE ? 4 * S0.n_nodes4 : OCT ? 32 * S0.n_nodes : 4 * S0.n_nodes;
     const int nt = 3 * S0.n_tris, ns = 2 * S0.n_tris, nm = kMatStride * S0.n_mats;
     if constexpr (WIDE) {
         const float4 *src = reinterpret_cast<const float4 *>(S0.nodes4);
         for (int i = threadIdx.x; i < nn; i += kBlock) l4[(i & 3) * S0.n_nodes4 + (i >> 2)] = src[i];
+    } else if constexpr (OCT) {   // copy o, node j, part k -> [(4 o + k) * n_nodes + j]
+        for (int i = threadIdx.x; i < nn; i += kBlock) {
+            const int e = i >> 2, o = e / S0.n_nodes, j = e - o * S0.n_nodes;
+            l4[(4 * o + (i & 3)) * S0.n_nodes + j] = S0.nodes_oct[i];
+        }
     } else {
         for (int i = threadIdx.x; i < nn; i += kBlock) l4[(i & 3) * S0.n_nodes + (i >> 2)] = S0.nodes[i];
     }
@@ -144,7 +151,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     constexpr int kStackInts = WORLD != FRT_WORLD_LIST ? STACK * kBlock : 0;
     constexpr int kItemInts = kItemWords * kBlock;
     DevScene S = S0;
-    if constexpr (LDS_SCENE) scene_to_lds<WORLD == kWorldBvh4>(S, lds_mem + kStackInts + kItemInts);
+    if constexpr (LDS_SCENE) scene_to_lds<WORLD>(S, lds_mem + kStackInts + kItemInts);
     else scene_strides_hbm(S);
     const int lane = threadIdx.x & 63;
     const int T2 = W.tile * W.tile;
@@ -403,7 +410,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
     extern __shared__ __attribute__((aligned(16))) int lds_mem[];
     int *stk = lds_mem + threadIdx.x;
     DevScene S = S0;
-    if constexpr (LDS_SCENE) scene_to_lds<WORLD == kWorldBvh4>(S, lds_mem + STACK * kBlock);
+    if constexpr (LDS_SCENE) scene_to_lds<WORLD>(S, lds_mem + STACK * kBlock);
     else scene_strides_hbm(S);
     const int lane = threadIdx.x & 63;
     bool have = false, exhausted = false, init = false, large = false;
@@ -588,6 +595,7 @@ struct frt_ctx {
     bool has_spec_mats = false;   // a non-lambertian scattering material: kernels with the specular branch
     bool has_metal = false;       // ao::Li cannot sample metal (constant_pdf::generate throws, pdf.h:195-198)
     size_t scene_lds_bytes = 0, scene_lds_bytes4 = 0;   // LDS copy with binary / 4-wide nodes
+    size_t scene_lds_bytes_oct = 0;                     // ... with the 8 octant copies of the binary nodes
     double last_mlt_b = 0.0;
     std::vector<void *> scene_bufs;
     // workspace
@@ -715,6 +723,7 @@ static inline float round_up(double x)
 struct FlatScene {
     std::vector<float4> nodes, tris, tshade, tnorm, spheres, mats, tuv;
     std::vector<uint4> nodes4;   // 4-wide quantized BVH
+    std::vector<float4> nodes_oct;   // 8 octant copies of `nodes` (DevScene::nodes_oct)
     bool has4 = false;           // nodes4 / root4 usable
     int root4 = 0, depth4 = 0;
     std::vector<int> smat, lights, list;
@@ -1127,6 +1136,27 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     F.list.resize(sv->world_kind == FRT_WORLD_LIST ? sv->n_list : 0);
     for (size_t i = 0; i < F.list.size(); ++i) F.list[i] = dev_ref(sv->list[i]);
 
+    // octant copies of the binary nodes: child boxes as (near xyz, far xyz)
+    F.nodes_oct.resize(8 * F.nodes.size());
+    for (int o = 0; o < 8; ++o)
+        for (size_t i = 0; i < F.nodes.size() / 4; ++i) {
+            const float4 *n = &F.nodes[4 * i];
+            const float b0[6] = {n[0].x, n[0].y, n[0].z, n[0].w, n[1].x, n[1].y};
+            const float b1[6] = {n[1].z, n[1].w, n[2].x, n[2].y, n[2].z, n[2].w};
+            float q[12];
+            for (int a = 0; a < 3; ++a) {
+                const bool neg = (o >> a) & 1;
+                q[a] = neg ? b0[3 + a] : b0[a];
+                q[3 + a] = neg ? b0[a] : b0[3 + a];
+                q[6 + a] = neg ? b1[3 + a] : b1[a];
+                q[9 + a] = neg ? b1[a] : b1[3 + a];
+            }
+            float4 *d = &F.nodes_oct[(size_t)o * F.nodes.size() + 4 * i];
+            d[0] = make_float4(q[0], q[1], q[2], q[3]);
+            d[1] = make_float4(q[4], q[5], q[6], q[7]);
+            d[2] = make_float4(q[8], q[9], q[10], q[11]);
+            d[3] = n[3];
+        }
     S.root = (sv->world_kind == FRT_WORLD_BVH) ? ((sv->root >= 0) ? 0 : ~dev_ref(~sv->root)) : 0;
     F.has4 = sv->world_kind == FRT_WORLD_BVH && build_bvh4(F, S.root);
     if (!F.has4) F.nodes4.clear();
@@ -1178,6 +1208,7 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
     DevScene &S = c->S;
     int rc;
     if ((rc = upload_vec(c, F.nodes, &S.nodes)) || (rc = upload_vec(c, F.nodes4, &S.nodes4)) ||
+        (rc = upload_vec(c, F.nodes_oct, &S.nodes_oct)) ||
         (rc = upload_vec(c, F.tris, &S.tris)) ||
         (rc = upload_vec(c, F.tshade, &S.tshade)) || (rc = upload_vec(c, F.tnorm, &S.tnorm)) ||
         (rc = upload_vec(c, F.tuv, &S.tuv)) ||
@@ -1201,6 +1232,7 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
     c->depth4 = F.depth4;
     c->scene_lds_bytes = sizeof(float4) * (F.nodes.size() + F.tris.size() + F.tshade.size() + F.mats.size());
     c->scene_lds_bytes4 = sizeof(float4) * (F.nodes4.size() + F.tris.size() + F.tshade.size() + F.mats.size());
+    c->scene_lds_bytes_oct = sizeof(float4) * (F.nodes_oct.size() + F.tris.size() + F.tshade.size() + F.mats.size());
     c->have_scene = true;
     return FRT_OK;
 }
@@ -1224,7 +1256,8 @@ extern "C" int frt_selftest_path_host(const frt_scene_view *sv, const frt_render
         for (int i = 0; i < sv->n_materials; ++i)
             if (sv->materials[i].type == FRT_MAT_METAL) return FRT_E_UNSUPPORTED;
     DevScene S = F.meta;
-    S.nodes = F.nodes.data(); S.nodes4 = F.nodes4.data(); S.tris = F.tris.data(); S.tshade = F.tshade.data(); S.tnorm = F.tnorm.data();
+    S.nodes = F.nodes.data(); S.nodes4 = F.nodes4.data(); S.nodes_oct = F.nodes_oct.data();
+    S.tris = F.tris.data(); S.tshade = F.tshade.data(); S.tnorm = F.tnorm.data();
     S.tuv = F.tuv.data();
     S.spheres = F.spheres.data(); S.sphere_mat = F.smat.data(); S.mats = F.mats.data();
     S.lights = F.lights.data(); S.list = F.list.data();
@@ -1289,7 +1322,8 @@ extern "C" int frt_selftest_mlt_paths_host(const frt_scene_view *sv, int nx, int
     const int rc = flatten_scene(sv, F, err);
     if (rc != FRT_OK) return rc;
     DevScene S = F.meta;
-    S.nodes = F.nodes.data(); S.nodes4 = F.nodes4.data(); S.tris = F.tris.data(); S.tshade = F.tshade.data(); S.tnorm = F.tnorm.data();
+    S.nodes = F.nodes.data(); S.nodes4 = F.nodes4.data(); S.nodes_oct = F.nodes_oct.data();
+    S.tris = F.tris.data(); S.tshade = F.tshade.data(); S.tnorm = F.tnorm.data();
     S.tuv = F.tuv.data();
     S.spheres = F.spheres.data(); S.sphere_mat = F.smat.data(); S.mats = F.mats.data();
     S.lights = F.lights.data(); S.list = F.list.data();
@@ -1443,6 +1477,13 @@ static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
         L = bvh_launcher<kBvh4LdsStack, false, kWorldBvh4, false, MATS>(waves, 0);
         return FRT_OK;
     }
+    // LDS-resident binary tree: the per-octant node copies when they fit
+    const bool oct = lds && !(flags & FRT_FLAG_NO_OCT) && c->scene_lds_bytes_oct <= kLdsOctBytes;
+    if (oct) {
+        L = d < 8 ? bvh_launcher<8, true, kWorldBvh2Oct, false, MATS>(waves, c->scene_lds_bytes_oct)
+                  : bvh_launcher<16, true, kWorldBvh2Oct, false, MATS>(waves, c->scene_lds_bytes_oct);
+        return FRT_OK;
+    }
     if (d < 8) L = lds ? bvh_launcher<8, true, FRT_WORLD_BVH, false, MATS>(waves, sb)
                        : bvh_launcher<8, false, FRT_WORLD_BVH, false, MATS>(waves, 0);
     else if (d < 16) L = lds ? bvh_launcher<16, true, FRT_WORLD_BVH, false, MATS>(waves, sb)
@@ -1463,7 +1504,11 @@ static int pick_launcher_kind(const frt_ctx *c, int flags, Launcher &L)
     const int d = c->stack_needed;
     const size_t sb = c->scene_lds_bytes;
     const bool lds = d < kLdsMaxDepth && sb <= kLdsSceneBytes && !(flags & FRT_FLAG_NO_LDS_SCENE);
-    if (lds) {
+    const bool oct = lds && !(flags & FRT_FLAG_NO_OCT) && c->scene_lds_bytes_oct <= kLdsOctBytes;
+    if (oct) {
+        L = d < 8 ? make_launcher<8, kWorldBvh2Oct, true, 5, false, M, KIND>(c->scene_lds_bytes_oct)
+                  : make_launcher<16, kWorldBvh2Oct, true, 5, false, M, KIND>(c->scene_lds_bytes_oct);
+    } else if (lds) {
         L = d < 8 ? make_launcher<8, FRT_WORLD_BVH, true, 5, false, M, KIND>(sb)
                   : make_launcher<16, FRT_WORLD_BVH, true, 5, false, M, KIND>(sb);
     } else if (c->has_bvh4 && !(flags & FRT_FLAG_BVH2) && bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {

@@ -164,6 +164,9 @@ def test_bvh4_matches_binary(ctx, cornell_obj, tmp_path):
     b_lds, stb = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21))
     assert stw.scene_in_lds == 1 and stb.scene_in_lds == 1 and stw.stack_entries == 8
     assert np.array_equal(w_lds, b_lds)
+    # LDS binary plan: the per-octant node copies (default) vs the (lo, hi) boxes
+    noct, stn = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21, flags=frt.FRT_FLAG_NO_OCT))
+    assert stn.scene_in_lds == 1 and np.array_equal(noct, b_lds) and stn.rays == stb.rays
     # tiny scene: every triangle in lockstep (FRT_FLAG_BRUTE)
     br, stbr = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21, flags=frt.FRT_FLAG_BRUTE))
     assert stbr.scene_in_lds == 1 and np.array_equal(br, b_lds) and stbr.rays == stb.rays
@@ -188,12 +191,21 @@ def test_trav_min_invariance(ctx, cornell_obj, tmp_path, monkeypatch, flags):
         assert np.array_equal(f, res[0][0]) and r == res[0][1]
 
 
-def test_launch_plan(ctx, cornell_obj, tmp_path):
+def test_launch_plan(ctx, cornell_obj, mirror_obj, sphere_obj, tmp_path):
     """The launcher picks the planned kernel: small scenes from LDS with the
-    binary BVH at 5 waves/SIMD, HBM-resident scenes on the 4-wide BVH at 6."""
+    binary BVH at 5 waves/SIMD, HBM-resident scenes on the 4-wide BVH at 6;
+    small scenes with specular materials (MATS kernels) from LDS on the
+    compiler's own register allocation (waves_cap 0)."""
     ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, 1.0))
     _, st = ctx.render(frt.RenderParams.make(16, 16, 1))
     assert (st.scene_in_lds, st.waves_cap, st.stack_entries) == (1, 5, 8)
+    ctx.upload(frt.HostScene("cornell_box_obj", mirror_obj, 1.0))            # modified_phong, 36 triangles
+    _, st = ctx.render(frt.RenderParams.make(16, 16, 1))
+    assert (st.scene_in_lds, st.waves_cap) == (1, 0)
+    ctx.upload(frt.HostScene("cornell_box_obj", sphere_obj, 1.0))            # 2,188 triangles: HBM, 4-wide
+    _, st = ctx.render(frt.RenderParams.make(16, 16, 1))
+    assert (st.scene_in_lds, st.waves_cap, st.stack_entries) == (0, 6, 16)
+    ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, 1.0))
     _, st = ctx.render(frt.RenderParams.make(16, 16, 1, flags=frt.FRT_FLAG_NO_LDS_SCENE))
     assert (st.scene_in_lds, st.waves_cap, st.stack_entries) == (0, 6, 16)
     _, st = ctx.render(frt.RenderParams.make(16, 16, 1, flags=frt.FRT_FLAG_NO_LDS_SCENE | frt.FRT_FLAG_BVH2))

@@ -38,7 +38,8 @@ def main():
     kind, obj, name = scene_spec(args.scene, "/tmp")
     names = {"default": 0, "no_lds": frt.FRT_FLAG_NO_LDS_SCENE, "waves4": frt.FRT_FLAG_WAVES4,
              "waves5": frt.FRT_FLAG_WAVES5, "waves6": frt.FRT_FLAG_WAVES6, "bvh2": frt.FRT_FLAG_BVH2,
-             "bvh4": frt.FRT_FLAG_BVH4, "brute": frt.FRT_FLAG_BRUTE, "spec": frt.FRT_FLAG_SPEC}
+             "bvh4": frt.FRT_FLAG_BVH4, "brute": frt.FRT_FLAG_BRUTE, "spec": frt.FRT_FLAG_SPEC,
+             "no_oct": frt.FRT_FLAG_NO_OCT}
     flags = {}
     for v in args.variants.split(","):
         parts = v.split("/")[0].split("+")
