@@ -351,7 +351,7 @@ class Runner:
         }
 
 
-BVH_NAMES = {"gpu": "gpu-lbvh", "sah": "binned SAH (host)", "host": "create_bvh (reference topology)"}
+BVH_NAMES = {"gpu": "gpu-lbvh", "sah": "binned SAH (host, 32 bins per axis)", "host": "create_bvh (reference topology)"}
 
 
 def main():

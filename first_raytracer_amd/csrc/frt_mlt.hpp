@@ -116,7 +116,7 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
 {
     PathState &P = M.P;
     if (P.shadow) {
-        if (!path_after_shadow<MATS>(P, h.prim < 0)) return true;
+        if (!path_after_shadow<(MATS ? kMatsAll : kMatsNone)>(P, h.prim < 0)) return true;
         if (P.depth <= kMltMaxPath) ++n_ext;
         return false;
     }
@@ -168,10 +168,10 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
     } else {                                            // pssmlt.cpp:232-249
         SM = spec_mat(S, mat, mtype, m0, m1);
         float sampled;
-        wo = spec_generate(SM, n, wi, sc0, sc1, sampled);
-        pdf = spec_value(SM, n, wi, wo);
+        wo = spec_generate<kMatsAll>(SM, n, wi, sc0, sc1, sampled);
+        pdf = spec_value<kMatsAll>(SM, n, wi, wo);
         if (sampled > 0.0f) pdf = sampled;
-        const f3 bsdf = spec_eval(SM, n, wi, wo);
+        const f3 bsdf = spec_eval<kMatsAll>(SM, n, wi, wo);
         beta_next = P.beta * (rcp(pdf) * bsdf);
     }
     // a zero pdf ends the path after the shadow ray the reference traces first (P.term)
@@ -200,8 +200,8 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
         if (cos_lo != 0.0f) {
             const float light_pdf = fdiv(prim_pdf(S, lref, p, h.t, n, tu) * dist2, fabsf(cos_lo));
             const bool l = !MATS || lamb;
-            const f3 f = l ? cos_wi * (kInvPi * xyz(m0)) : spec_eval(SM, n, wi, tu);
-            const float bsdf_pdf = l ? fmaxf(cos_wi, 0.0f) * kInvPi : spec_value(SM, n, wi, tu);
+            const f3 f = l ? cos_wi * (kInvPi * xyz(m0)) : spec_eval<kMatsAll>(SM, n, wi, tu);
+            const float bsdf_pdf = l ? fmaxf(cos_wi, 0.0f) * kInvPi : spec_value<kMatsAll>(SM, n, wi, tu);
             const float wgt = mi_weight(light_pdf, bsdf_pdf);
             const float4 lm0 = S.mats[kMatStride * lmat], lm1 = S.mats[kMatStride * lmat + 1];
             if (f2i(lm0.w) == FRT_MAT_DIFFUSE_LIGHT && dot(ln, tu) < 0.0f)

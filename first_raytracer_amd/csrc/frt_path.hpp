@@ -552,6 +552,15 @@ FRT_HD f3 prim_sample(const DevScene &S, int ref, f3 o, float u0, float u1, f3 &
     return lp - o;
 }
 
+// Material sets a kernel is compiled for (the MATS template mask): the
+// lambertian / diffuse_light core is always there; kMatsTex adds checker
+// textures, kMatsSpec the specular branch for modified_phong, metal and
+// dielectric, kMatsRough the rough conductor lobes (erf / erfinv, GGX slopes,
+// conductor Fresnel) -- the register-hungry part.  A scene runs the smallest
+// kernel covering its materials (frt_upload_scene).
+constexpr int kMatsNone = 0, kMatsTex = 1, kMatsSpec = 2, kMatsRough = 4, kMatsAll = 7;
+constexpr int kMatsSpecAny = kMatsSpec | kMatsRough;
+
 // ---- textures (texture.h:30-49), MATS kernels only ----
 // (int)x as the reference's x86-64 build computes it (cvttsd2si): NaN and
 // out-of-range give INT_MIN
@@ -657,13 +666,13 @@ FRT_HD void path_begin(PathState &P, const DevScene &S, int px, int py, int nx, 
 // so the reference returns 0 for the vertex after tracing the shadow ray
 // (path.cpp:45-77 run before :87-90 / :103-106) -- the ray is traced and
 // counted like the reference's, its NEE term dropped.
-template <bool MATS = true>
+template <int MATS = kMatsAll>
 FRT_HD bool path_after_shadow(PathState &P, bool unoccluded)
 {
     P.shadow = false;
     if (P.term) return false;
     if (unoccluded) P.L = P.L + P.nee;
-    if constexpr (MATS) P.ro = P.nxt_o;
+    if constexpr ((MATS & kMatsSpecAny) != 0) P.ro = P.nxt_o;
     P.rd = P.nxt_d; P.rtmax = kTMaxClosest;
     ++P.depth;
     return true;
@@ -684,6 +693,9 @@ FRT_HD SpecMat spec_mat(const DevScene &S, int mat, int type, float4 m0, float4 
 }
 // scatter's direction from the get3d sample (material.h:83-88, 117-119, 139-145,
 // 262-268) and srec.sampled_pdf (-1 unless the rough conductor sets it)
+// MATS without kMatsRough: the scene has no rough conductor, its lobes are
+// not compiled (the switch's default is then metal's).
+template <int MATS = kMatsAll>
 FRT_HD f3 spec_generate(const SpecMat &M, f3 n, f3 wi, float s0, float s1, float &sampled_pdf)
 {
     sampled_pdf = -1.0f;
@@ -691,25 +703,35 @@ FRT_HD f3 spec_generate(const SpecMat &M, f3 n, f3 wi, float s0, float s1, float
     case FRT_MAT_MODIFIED_PHONG: return cosine_power_generate(n, wi, M.m1.w, s0, s1);
     case FRT_MAT_DIELECTRIC: return dielectric_generate(n, wi, M.m1.w, s0);
     case FRT_MAT_METAL: return reflect(-wi, n);          // reflect(unit(r_in.d), n); -wi = unit(r_in.d)
-    default: return normalize(rough_generate(n, wi, M.m1.w, f2i(M.m2.w), s0, s1, sampled_pdf));
+    default:
+        if constexpr ((MATS & kMatsRough) != 0)
+            return normalize(rough_generate(n, wi, M.m1.w, f2i(M.m2.w), s0, s1, sampled_pdf));
+        return reflect(-wi, n);
     }
 }
+template <int MATS = kMatsAll>
 FRT_HD float spec_value(const SpecMat &M, f3 n, f3 wi, f3 wo)     // srec.pdf_ptr->value
 {
     switch (M.type) {
     case FRT_MAT_MODIFIED_PHONG: return cosine_power_value(n, wi, M.m1.w, wo);
     case FRT_MAT_DIELECTRIC: return dielectric_value(n, wi, M.m1.w, wo);
     case FRT_MAT_METAL: return 1.0f;                     // constant_pdf(1) (pdf.h:186-201)
-    default: return rough_value(n, wi, M.m1.w, f2i(M.m2.w), wo);
+    default:
+        if constexpr ((MATS & kMatsRough) != 0) return rough_value(n, wi, M.m1.w, f2i(M.m2.w), wo);
+        return 1.0f;
     }
 }
+template <int MATS = kMatsAll>
 FRT_HD f3 spec_eval(const SpecMat &M, f3 n, f3 wi, f3 wo)          // eval_bsdf
 {
     switch (M.type) {
     case FRT_MAT_MODIFIED_PHONG: return phong_eval(xyz(M.m0), xyz(M.m1), M.m1.w, n, wi, wo);
     case FRT_MAT_DIELECTRIC: return dielectric_eval(xyz(M.m1), M.m1.w, n, wi, wo);
     case FRT_MAT_METAL: return xyz(M.m0);
-    default: return rough_eval(xyz(M.m0), xyz(M.m2), xyz(M.m1), M.m1.w, f2i(M.m2.w), n, wi, wo);
+    default:
+        if constexpr ((MATS & kMatsRough) != 0)
+            return rough_eval(xyz(M.m0), xyz(M.m2), xyz(M.m1), M.m1.w, f2i(M.m2.w), n, wi, wo);
+        return xyz(M.m0);
     }
 }
 FRT_HD bool mat_is_specular(int t)
@@ -722,7 +744,7 @@ FRT_HD bool mat_no_mis(int t) { return t == FRT_MAT_MODIFIED_PHONG || t == FRT_M
 // Returns true when the path is finished (P.L is the sample's radiance).
 // MATS = false compiles the lambertian / diffuse_light scenes' kernel: the
 // specular branch is dead code there (it would cost registers and code size).
-template <bool MATS = true>
+template <int MATS = kMatsAll>
 FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_depth, uint32_t &n_ext, uint32_t &n_sh)
 {
     if (P.shadow) {
@@ -741,7 +763,7 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
     prim_shade(S, h.prim, P.ro, p, h.u, h.v, n, mat);
     float4 m0 = S.mats[kMatStride * mat], m1 = S.mats[kMatStride * mat + 1];
     const int mtype = f2i(m0.w);
-    if constexpr (MATS) apply_texture(S, mat, mtype, h.prim, p, h.u, h.v, m0, m1);
+    if constexpr ((MATS & kMatsTex) != 0) apply_texture(S, mat, mtype, h.prim, p, h.u, h.v, m0, m1);
     // diffuse_light::emitted is one-sided (material.h:184-190)
     if (mtype == FRT_MAT_DIFFUSE_LIGHT && dot(n, P.rd) < 0.0f) {
         const f3 Le = xyz(m1);
@@ -756,9 +778,9 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
         }
         return true;
     }
-    const bool lamb = mtype == FRT_MAT_LAMBERTIAN, spec = MATS && mat_is_specular(mtype);
+    const bool lamb = mtype == FRT_MAT_LAMBERTIAN, spec = (MATS & kMatsSpecAny) && mat_is_specular(mtype);
     if (!(lamb || spec) || P.depth > max_depth) return true;   // no scatter: Le (= 0)
-    const bool diel = MATS && mtype == FRT_MAT_DIELECTRIC;
+    const bool diel = (MATS & kMatsSpec) && mtype == FRT_MAT_DIELECTRIC;
     const uint32_t base = dim_bounce(P.depth);
     // The scattered direction first: a zero pdf returns 0 for this vertex,
     // dropping its NEE too (path.cpp:84-86, 103-106) -- after the reference has
@@ -767,7 +789,7 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
     float pdf;
     const f3 wi = -normalize(P.rd);                     // hrec.wi (triangle.h:108, sphere.h:47)
     SpecMat M{};
-    if (!MATS || lamb) {                                // cosine_pdf (path.cpp:96-110)
+    if (!(MATS & kMatsSpecAny) || lamb) {               // cosine_pdf (path.cpp:96-110)
         const Onb uvw = onb_from_w(n);
         wo = onb_local(uvw, cosine_direction(rng_u(P.key, base + 6), rng_u(P.key, base + 7)));
         const float cw = dot(n, normalize(wo));
@@ -776,10 +798,10 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
     } else {                                            // specular branch (path.cpp:78-95); the
         M = spec_mat(S, mat, mtype, m0, m1);            // scatter sample is get3d's (base + 0, 1)
         float sampled;
-        wo = spec_generate(M, n, wi, rng_u(P.key, base + 0), rng_u(P.key, base + 1), sampled);
-        pdf = spec_value(M, n, wi, wo);
+        wo = spec_generate<MATS>(M, n, wi, rng_u(P.key, base + 0), rng_u(P.key, base + 1), sampled);
+        pdf = spec_value<MATS>(M, n, wi, wo);
         if (sampled > 0.0f) pdf = sampled;              // path.cpp:82
-        const f3 bsdf = spec_eval(M, n, wi, wo);
+        const f3 bsdf = spec_eval<MATS>(M, n, wi, wo);
         beta_next = P.beta * (rcp(pdf) * bsdf);
     }
     // Lambertian-only kernels (MATS = false) never see pdf 0: the cosine lobe's
@@ -790,13 +812,13 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
     int idx = (int)(rng_u(P.key, base + 3) * (float)nl);
     if (idx == nl) idx -= 1;
     const bool nee = idx >= 0 && !diel;
-    P.term = MATS && pdf == 0.0f;
+    P.term = (MATS & kMatsSpecAny) && pdf == 0.0f;
     if (P.term && !nee) return true;
     // origin of the next ray: off the surface on the side it leaves (path.cpp:91-93, 99)
     const f3 nee_o = p + kEps * n;
-    const f3 origin = (!MATS || lamb || dot(n, wo) > 0.0f) ? nee_o : p - kEps * n;
+    const f3 origin = (!(MATS & kMatsSpecAny) || lamb || dot(n, wo) > 0.0f) ? nee_o : p - kEps * n;
     P.nxt_d = wo;
-    if constexpr (MATS) P.nxt_o = origin;
+    if constexpr ((MATS & kMatsSpecAny) != 0) P.nxt_o = origin;
     // next-event estimation (path.cpp:38-77); not from dielectrics (path.cpp:40)
     if (nee) {
         const int lref = S.lights[idx];
@@ -811,9 +833,9 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
         if (cos_lo != 0.0f) {
             const float light_pdf = fdiv(prim_pdf(S, lref, p, h.t, n, tu) * dist2, fabsf(cos_lo));
             // eval_bsdf toward the light; only the non-specular bsdf gets the cosine (path.cpp:61-62)
-            const bool l = !MATS || lamb;
-            const f3 f = l ? cos_wi * (kInvPi * xyz(m0)) : spec_eval(M, n, wi, tu);
-            const float bsdf_pdf = l ? fmaxf(cos_wi, 0.0f) * kInvPi : spec_value(M, n, wi, tu);
+            const bool l = !(MATS & kMatsSpecAny) || lamb;
+            const f3 f = l ? cos_wi * (kInvPi * xyz(m0)) : spec_eval<MATS>(M, n, wi, tu);
+            const float bsdf_pdf = l ? fmaxf(cos_wi, 0.0f) * kInvPi : spec_value<MATS>(M, n, wi, tu);
             const float wgt = mi_weight(light_pdf, bsdf_pdf);
             const float4 lm0 = S.mats[kMatStride * lmat], lm1 = S.mats[kMatStride * lmat + 1];
             if (f2i(lm0.w) == FRT_MAT_DIFFUSE_LIGHT && dot(ln, tu) < 0.0f)
@@ -823,7 +845,7 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
         P.shadow = true;
         ++n_sh;
     }
-    P.prev_spec = MATS && mat_no_mis(mtype);
+    P.prev_spec = (MATS & kMatsSpec) && mat_no_mis(mtype);
     P.beta = beta_next;
     P.prev_p = p;
     P.prev_pdf = pdf;
@@ -846,7 +868,7 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
 // hitable_list.cpp:27-29: t_max is NaN): only spheres can occlude there
 // (sphere.h's `t > t_max` test passes NaN, triangle.h's `t < t_max` does
 // not), answered here with a loop over the list's spheres.
-template <bool MATS = true>
+template <int MATS = kMatsAll>
 FRT_HD bool ao_shade(PathState &P, const DevScene &S, const Hit &h, uint32_t &n_sh)
 {
     if (P.shadow) {                                     // visibility ray done
@@ -866,14 +888,14 @@ FRT_HD bool ao_shade(PathState &P, const DevScene &S, const Hit &h, uint32_t &n_
     f3 wo;
     if (mtype == FRT_MAT_LAMBERTIAN) {
         wo = onb_local(onb_from_w(n), cosine_direction(u0, u1));
-    } else if (MATS && mtype == FRT_MAT_MODIFIED_PHONG) {
+    } else if ((MATS & kMatsSpec) && mtype == FRT_MAT_MODIFIED_PHONG) {
         wo = cosine_power_generate(n, -normalize(P.rd), m1.w, u0, u1);
-    } else if (MATS && mtype == FRT_MAT_DIELECTRIC) {
+    } else if ((MATS & kMatsSpec) && mtype == FRT_MAT_DIELECTRIC) {
         wo = dielectric_generate(n, -normalize(P.rd), m1.w, u0);
-    } else if (MATS && mtype == FRT_MAT_ROUGH_CONDUCTOR) {   // pdf.h:465-482 (metal is refused at launch)
+    } else if ((MATS & kMatsRough) && mtype == FRT_MAT_ROUGH_CONDUCTOR) {   // pdf.h:465-482 (metal: refused at launch)
         const float4 m2 = S.mats[kMatStride * mat + 2];
         float unused;
-        wo = rough_generate(n, -normalize(P.rd), m1.w, f2i(m2.w), u0, u1, unused);
+        if constexpr ((MATS & kMatsRough) != 0) wo = rough_generate(n, -normalize(P.rd), m1.w, f2i(m2.w), u0, u1, unused);
     } else {
         return true;                                    // no scatter (diffuse_light)
     }
@@ -912,7 +934,7 @@ FRT_HD bool normals_shade(PathState &P, const DevScene &S, const Hit &h)
 }
 
 // integrator dispatch of the megakernel / self-test (KIND = FRT_INTEGRATOR_*)
-template <int KIND, bool MATS>
+template <int KIND, int MATS>
 FRT_HD bool shade_kind(PathState &P, const DevScene &S, const Hit &h, int max_depth, uint32_t &n_ext, uint32_t &n_sh)
 {
     if constexpr (KIND == FRT_INTEGRATOR_AO) return ao_shade<MATS>(P, S, h, n_sh);

@@ -140,7 +140,7 @@ struct ItemState {
     __device__ void set(int k, int x) const { b[k * kBlock] = x; }
 };
 
-template <int STACK, int WORLD, bool LDS_SCENE, int WAVES = 1, bool SPEC = false, bool MATS = false,
+template <int STACK, int WORLD, bool LDS_SCENE, int WAVES = 1, bool SPEC = false, int MATS = kMatsNone,
           int KIND = FRT_INTEGRATOR_PATH>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void path_megakernel(
     const DevScene S0, const DevWork W)
@@ -438,7 +438,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
             if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, M.P.ro, M.P.rd, M.P.shadow, stk, ovf,
                                                                  W.min_desc)) {
                 if (M.P.shadow) {               // finish the shadow ray here (mlt_shade's shadow branch)
-                    if (!path_after_shadow<MATS>(M.P, T.h.prim < 0)) {   // path ended (P.term)
+                    if (!path_after_shadow<(MATS ? kMatsAll : kMatsNone)>(M.P, T.h.prim < 0)) {   // path ended (P.term)
                         tracing = false;
                         pending = true;
                     } else if (mlt_beyond(M)) {
@@ -592,7 +592,8 @@ struct frt_ctx {
     bool has_bvh4 = false;
     int depth4 = 0;
     int n_tris = 0, n_spheres = 0;
-    bool has_spec_mats = false;   // a non-lambertian scattering material: kernels with the specular branch
+    bool has_spec_mats = false;   // a non-lambertian scattering material or a texture: MATS kernels
+    int mats = kMatsNone;         // kMats* mask of the scene's material set (pick_launcher)
     bool has_metal = false;       // ao::Li cannot sample metal (constant_pdf::generate throws, pdf.h:195-198)
     size_t scene_lds_bytes = 0, scene_lds_bytes4 = 0;   // LDS copy with binary / 4-wide nodes
     size_t scene_lds_bytes_oct = 0;                     // ... with the 8 octant copies of the binary nodes
@@ -1223,12 +1224,15 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
     c->n_spheres = (int)F.spheres.size();
     c->has_spec_mats = false;
     c->has_metal = false;
+    c->mats = kMatsNone;
     for (int i = 0; i < sv->n_materials; ++i) {
         const int t = sv->materials[i].type;
-        if (t != FRT_MAT_LAMBERTIAN && t != FRT_MAT_DIFFUSE_LIGHT) c->has_spec_mats = true;
-        if (sv->materials[i].texture == FRT_TEX_CHECKER) c->has_spec_mats = true;   // textures: MATS kernels
+        if (t == FRT_MAT_MODIFIED_PHONG || t == FRT_MAT_METAL || t == FRT_MAT_DIELECTRIC) c->mats |= kMatsSpec;
+        if (t == FRT_MAT_ROUGH_CONDUCTOR) c->mats |= kMatsRough;
+        if (sv->materials[i].texture == FRT_TEX_CHECKER) c->mats |= kMatsTex;
         if (t == FRT_MAT_METAL) c->has_metal = true;
     }
+    c->has_spec_mats = c->mats != kMatsNone;
     c->depth4 = F.depth4;
     c->scene_lds_bytes = sizeof(float4) * (F.nodes.size() + F.tris.size() + F.tshade.size() + F.mats.size());
     c->scene_lds_bytes4 = sizeof(float4) * (F.nodes4.size() + F.tris.size() + F.tshade.size() + F.mats.size());
@@ -1406,7 +1410,7 @@ struct Launcher {
     bool lds_scene = false;
     bool wide = false;      // 4-wide quantized BVH
 };
-template <int STACK, int WORLD, bool LDS, int WAVES = 1, bool SPEC = false, bool MATS = false,
+template <int STACK, int WORLD, bool LDS, int WAVES = 1, bool SPEC = false, int MATS = kMatsNone,
           int KIND = FRT_INTEGRATOR_PATH>
 static Launcher make_launcher(size_t scene_bytes)
 {
@@ -1423,11 +1427,15 @@ static Launcher make_launcher(size_t scene_bytes)
 #ifndef FRT_EXP_W6
 #define FRT_EXP_W6 6   // experiment builds: the register cap behind the "6 waves" plans
 #endif
-template <int STACK, bool LDS, int WORLD = FRT_WORLD_BVH, bool SPEC = false, bool MATS = false>
+template <int STACK, bool LDS, int WORLD = FRT_WORLD_BVH, bool SPEC = false, int MATS = kMatsNone>
 static Launcher bvh_launcher(int waves, size_t sb)
 {
     if (waves == 6) return make_launcher<STACK, WORLD, LDS, FRT_EXP_W6, SPEC, MATS>(sb);
     if (waves == 5) return make_launcher<STACK, WORLD, LDS, 5, SPEC, MATS>(sb);
+    if constexpr (MATS != kMatsNone) {
+        if (waves == 4) return make_launcher<STACK, WORLD, LDS, 4, SPEC, MATS>(sb);
+        if (waves == 3) return make_launcher<STACK, WORLD, LDS, 3, SPEC, MATS>(sb);
+    }
     return make_launcher<STACK, WORLD, LDS, 1, SPEC, MATS>(sb);
 }
 #ifndef FRT_EXP_BVH4_LSTACK
@@ -1436,8 +1444,8 @@ static Launcher bvh_launcher(int waves, size_t sb)
 constexpr int kBvh4LdsStack = FRT_EXP_BVH4_LSTACK;   // 16 KiB of LDS per block; deeper entries go to scratch
 constexpr int kBvh4LdsStackSmall = 8;   // LDS-resident scenes (shallow trees)
 constexpr int kBruteMaxTris = 128;
-// MATS: the scene has modified_phong / dielectric materials (specular branch compiled in)
-template <bool MATS>
+// MATS: the material set the kernel is compiled for (kMats* mask, frt_path.hpp)
+template <int MATS>
 static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
 {
     if (c->world_kind == FRT_WORLD_LIST) { L = make_launcher<16, FRT_WORLD_LIST, false, 1, false, MATS>(0); return FRT_OK; }
@@ -1449,11 +1457,21 @@ static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
     // 5 waves best for LDS-resident scenes, 6 for HBM-resident ones.  The
     // material kernels (MATS) in LDS run 15-21 % faster on the compiler's own
     // allocation than under the 5-wave cap (profiles/r01d_perf_mats.jsonl).
-    int waves = (MATS && lds) ? 0 : lds ? 5 : 6;
+    // Material kernels: textures alone cost about the lambertian kernel's
+    // registers (117 vs 111 VGPRs uncapped; the compiler's 4 waves are best),
+    // the specular branch 152, the rough conductor lobes 170 -- capped at 4
+    // waves/SIMD (128 VGPRs; a few spills in the specular shading) they run
+    // +40 % over the compiler's 2-wave allocation (same-call A/B,
+    // profiles/r02/r02_mats*.jsonl).
+    int waves = (MATS & kMatsSpecAny) ? (lds ? 4 : 5) : MATS == kMatsTex && lds ? 0 : lds ? 5 : 6;
+    if constexpr (MATS != kMatsNone) {   // FRT_MATS_WAVES: register cap of the material kernels (tuning knob, not part of the C-ABI)
+        const char *e = std::getenv("FRT_MATS_WAVES");
+        if (e) waves = std::atoi(e);
+    }
     if (flags & FRT_FLAG_WAVES4) waves = 0;   // the compiler's own allocation (~120 VGPRs, 4 waves)
     if (flags & FRT_FLAG_WAVES5) waves = 5;
     if (flags & FRT_FLAG_WAVES6) waves = 6;
-    if constexpr (!MATS) {   // A/B plans, lambertian scenes only
+    if constexpr (MATS == kMatsNone) {   // A/B plans, lambertian scenes only
         // tiny triangle-only scenes from LDS, every triangle in lockstep (FRT_FLAG_BRUTE)
         if (lds && (flags & FRT_FLAG_BRUTE) && c->n_spheres == 0 && c->n_tris <= kBruteMaxTris) {
             L = bvh_launcher<8, true, kWorldBrute>(waves, sb);
@@ -1499,7 +1517,7 @@ static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
 template <int KIND>
 static int pick_launcher_kind(const frt_ctx *c, int flags, Launcher &L)
 {
-    constexpr bool M = KIND == FRT_INTEGRATOR_AO;
+    constexpr int M = KIND == FRT_INTEGRATOR_AO ? kMatsAll : kMatsNone;
     if (c->world_kind == FRT_WORLD_LIST) { L = make_launcher<16, FRT_WORLD_LIST, false, 1, false, M, KIND>(0); return FRT_OK; }
     const int d = c->stack_needed;
     const size_t sb = c->scene_lds_bytes;
@@ -1528,7 +1546,13 @@ static int pick_launcher(const frt_ctx *c, int integrator, int flags, Launcher &
 {
     if (integrator == FRT_INTEGRATOR_AO) return pick_launcher_kind<FRT_INTEGRATOR_AO>(c, flags, L);
     if (integrator == FRT_INTEGRATOR_NORMALS) return pick_launcher_kind<FRT_INTEGRATOR_NORMALS>(c, flags, L);
-    return c->has_spec_mats ? pick_launcher_t<true>(c, flags, L) : pick_launcher_t<false>(c, flags, L);
+    switch (c->mats) {   // the smallest kernel covering the scene's materials
+    case kMatsNone: return pick_launcher_t<kMatsNone>(c, flags, L);
+    case kMatsTex: return pick_launcher_t<kMatsTex>(c, flags, L);
+    case kMatsSpec:
+    case kMatsSpec | kMatsTex: return pick_launcher_t<kMatsSpec | kMatsTex>(c, flags, L);
+    default: return pick_launcher_t<kMatsAll>(c, flags, L);
+    }
 }
 
 

@@ -753,12 +753,18 @@ struct SahBuilder {
     std::vector<double> node_box;
     std::vector<int32_t> node_child;
     std::atomic<int> n_nodes{0}, max_depth{0};
-    static constexpr int kMaxBins = 128;
-    int bins = 32;                           // FRT_SAH_BINS overrides (tuning experiments)
+    // centroid bins per axis: 32 (8-128 measured 1-2 % apart on the GPU,
+    // profiles/r01d_ab_sah_bins.txt).  A build-time constant, so no stray
+    // environment can change the tree (and with it which of two exactly tied
+    // hits a ray reports); experiment builds set FRT_EXP_SAH_BINS.
+#ifndef FRT_EXP_SAH_BINS
+#define FRT_EXP_SAH_BINS 32
+#endif
+    static constexpr int kMaxBins = FRT_EXP_SAH_BINS;
+    static constexpr int bins = FRT_EXP_SAH_BINS;
 
     explicit SahBuilder(const std::vector<Box> &b) : box(b), cen(3 * b.size()), idx(b.size())
     {
-        if (const char *e = std::getenv("FRT_SAH_BINS")) bins = std::max(2, std::min(kMaxBins, std::atoi(e)));
         for (size_t i = 0; i < b.size(); ++i) {
             idx[i] = (int32_t)i;
             for (int k = 0; k < 3; ++k) cen[3 * i + k] = 0.5 * (b[i].lo[k] + b[i].hi[k]);

@@ -41,6 +41,29 @@ def test_path_conductors(ctx, sphere_dist, cube_dist, world, flags):
     assert e <= 1e-3
 
 
+def test_register_caps_agree(ctx, monkeypatch):
+    """The material kernels give the same film under every register cap and
+    plan (FRT_MATS_WAVES 0 / 4 / 5 / 6; LDS binary, HBM 4-wide, HBM binary).
+    A source restructuring of the specular dispatch once compiled to kernels
+    that were right uncapped and wrong (RMSE 0.04-0.18) under some caps, with
+    unchanged ray counts; this pins every cap against the oracle."""
+    spec = SS.cornell_conductors("beckmann", "ggx", "bvh")
+    nx, ny, spp = 64, 48, 16
+    ctx.upload(frt.HostScene.from_spec(spec, nx / ny))
+    ref, cnt = oracle.OracleScene.from_spec(spec, nx / ny).render(nx, ny, spp, seed=12)
+    films = []
+    for flags in (0, frt.FRT_FLAG_NO_LDS_SCENE, frt.FRT_FLAG_NO_LDS_SCENE | frt.FRT_FLAG_BVH2):
+        for w in ("0", "4", "5", "6"):
+            monkeypatch.setenv("FRT_MATS_WAVES", w)
+            film, st = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=12, flags=flags))
+            assert st.waves_cap == int(w)
+            e = rmse(film, ref)
+            assert e <= 1e-3, (flags, w, e)
+            films.append(film)
+    for f in films[1:]:                                   # the same hits and sums: bit-identical
+        assert np.array_equal(f, films[0])
+
+
 def test_pssmlt_conductors(ctx):
     """pssmlt::Li's specular branch with metal + rough conductors: short chains vs the oracle's."""
     spec = SS.cornell_conductors()

@@ -194,17 +194,17 @@ def test_trav_min_invariance(ctx, cornell_obj, tmp_path, monkeypatch, flags):
 def test_launch_plan(ctx, cornell_obj, mirror_obj, sphere_obj, tmp_path):
     """The launcher picks the planned kernel: small scenes from LDS with the
     binary BVH at 5 waves/SIMD, HBM-resident scenes on the 4-wide BVH at 6;
-    small scenes with specular materials (MATS kernels) from LDS on the
-    compiler's own register allocation (waves_cap 0)."""
+    scenes with specular materials (the kMatsSpec kernel) at 4 waves from LDS,
+    5 from HBM."""
     ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, 1.0))
     _, st = ctx.render(frt.RenderParams.make(16, 16, 1))
     assert (st.scene_in_lds, st.waves_cap, st.stack_entries) == (1, 5, 8)
     ctx.upload(frt.HostScene("cornell_box_obj", mirror_obj, 1.0))            # modified_phong, 36 triangles
     _, st = ctx.render(frt.RenderParams.make(16, 16, 1))
-    assert (st.scene_in_lds, st.waves_cap) == (1, 0)
+    assert (st.scene_in_lds, st.waves_cap) == (1, 4)
     ctx.upload(frt.HostScene("cornell_box_obj", sphere_obj, 1.0))            # 2,188 triangles: HBM, 4-wide
     _, st = ctx.render(frt.RenderParams.make(16, 16, 1))
-    assert (st.scene_in_lds, st.waves_cap, st.stack_entries) == (0, 6, 16)
+    assert (st.scene_in_lds, st.waves_cap, st.stack_entries) == (0, 5, 16)
     ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, 1.0))
     _, st = ctx.render(frt.RenderParams.make(16, 16, 1, flags=frt.FRT_FLAG_NO_LDS_SCENE))
     assert (st.scene_in_lds, st.waves_cap, st.stack_entries) == (0, 6, 16)

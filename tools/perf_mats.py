@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Throughput of the material kernels (MATS = true: metal, rough conductor,
-dielectric, checker textures) next to the lambertian-only kernel, on the
+"""Throughput of the material kernels (MATS mask: textures, phong / metal /
+dielectric, rough conductor) next to the lambertian-only kernel, on the
 builder scenes of tests/scene_specs.py at 1080p.  One JSON line per scene:
 rays / kernel time (HIP events inside libfrt.so), best of --rounds.
 
@@ -30,6 +30,10 @@ def main():
         "cornell_lambertian": {"objects": [{"obj": SS.CORNELL_OBJ, "geo": True}], "camera": SS.CORNELL_CAM},
         "cornell_conductors": SS.cornell_conductors(),
         "cornell_textured": SS.cornell_textured(),
+        # one material set each (the kernel the launcher picks: kMatsTex / kMatsSpec)
+        "cornell_checker_floor": {"objects": SS.cornell_textured()["objects"][:2], "camera": SS.CORNELL_CAM},
+        "cornell_mirror": {"objects": [{"obj": os.path.join(ROOT, "tests", "golden", "scenes", "CornellBox-Mirror.obj"),
+                                        "geo": True}], "camera": SS.CORNELL_CAM},
     }
     ctx = frt.Context(0)
     for name, spec in scenes.items():
