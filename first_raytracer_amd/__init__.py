@@ -32,6 +32,8 @@ FRT_FLAG_BVH4 = 32
 FRT_FLAG_BRUTE = 64
 FRT_FLAG_SPEC = 128
 FRT_FLAG_NO_OCT = 256
+FRT_GPU_BVH_PLOC = 0
+FRT_GPU_BVH_LBVH = 1
 FRT_INTEGRATOR_PATH, FRT_INTEGRATOR_PSSMLT, FRT_INTEGRATOR_AO, FRT_INTEGRATOR_NORMALS = 0, 1, 2, 3
 
 ERRORS = {0: "ok", -1: "invalid", -2: "hip", -3: "no scene", -4: "unsupported", -5: "io", -6: "no gfx950 device"}
@@ -153,7 +155,7 @@ EXPORTS = ("frt_get_abi_version", "frt_create", "frt_destroy", "frt_last_error",
            "frt_shard_slot_count", "frt_shard_slots", "frt_render", "frt_render_multi", "frt_render_device",
            "frt_scene_create", "frt_scene_new", "frt_scene_add_obj", "frt_scene_add_sphere", "frt_scene_set_camera",
            "frt_scene_set_env", "frt_scene_finish", "frt_scene_build_bvh_gpu",
-           "frt_scene_build_bvh_sah",
+           "frt_scene_build_bvh_sah", "frt_scene_build_bvh_gpu_algo",
            "frt_scene_view_get", "frt_scene_info", "frt_scene_destroy", "frt_write_tessellated_obj",
            "frt_write_pfm", "frt_film_accumulate", "frt_tonemap_u8", "frt_write_image", "frt_selftest_path_host",
            "frt_selftest_mlt_paths_host")
@@ -205,6 +207,7 @@ def lib():
     L.frt_scene_finish.argtypes = [vp, ctypes.c_int]
     L.frt_scene_build_bvh_gpu.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_double)]
     L.frt_scene_build_bvh_sah.argtypes = [vp]
+    L.frt_scene_build_bvh_gpu_algo.argtypes = [vp, vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
     L.frt_write_tessellated_obj.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p]
     L.frt_write_pfm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, vp]
     L.frt_film_accumulate.argtypes = [vp, ctypes.c_int64, vp, ctypes.c_int64, ctypes.c_int64]
@@ -323,11 +326,14 @@ class HostScene:
         lib().frt_scene_info(self.ptr, ctypes.byref(self.info))
         return self.info.build_ms
 
-    def build_bvh_gpu(self, ctx):
-        """Replace the world by a GPU-built linear BVH (frt_scene_build_bvh_gpu);
-        returns the device time of the build passes in ms."""
+    def build_bvh_gpu(self, ctx, algo="ploc"):
+        """Replace the world by a GPU-built BVH (frt_scene_build_bvh_gpu_algo): "ploc"
+        (PLOC clustering, the default) or "lbvh" (Karras linear BVH); returns the
+        device time of the build passes in ms."""
         ms = ctypes.c_double()
-        _check(lib().frt_scene_build_bvh_gpu(self.ptr, ctx.ptr, ctypes.byref(ms)), "frt_scene_build_bvh_gpu", ctx.ptr)
+        a = {"ploc": FRT_GPU_BVH_PLOC, "lbvh": FRT_GPU_BVH_LBVH}[algo]
+        _check(lib().frt_scene_build_bvh_gpu_algo(self.ptr, ctx.ptr, a, ctypes.byref(ms)),
+               "frt_scene_build_bvh_gpu_algo", ctx.ptr)
         lib().frt_scene_info(self.ptr, ctypes.byref(self.info))
         return ms.value
 

@@ -1,7 +1,8 @@
-// frt_lbvh.hip -- GPU BVH builder: a linear BVH over the
-// world primitives' boxes, built on the device in four passes, as a fast
-// alternative to the reference-topology SAH build (parallel_bvh_node::create_bvh,
-// parallel_bvh.h:67-175; host: csrc/host/scene.cpp).
+// frt_lbvh.hip -- GPU BVH builders over the world
+// primitives' boxes, on the device, as fast alternatives to the host SAH builds
+// (parallel_bvh_node::create_bvh, parallel_bvh.h:67-175; host: csrc/host/scene.cpp):
+// a linear BVH (steps 1-5 below) and PLOC clustering on the same Morton order
+// (steps 1-3, then k_ploc_*; SAH-like quality, the default).
 //
 //   1. centroid bounds       one block reduction + atomics on order-preserving uints
 //   2. Morton keys           30-bit (10 bits / axis) centroid code << 32 | prim index
@@ -170,6 +171,105 @@ __global__ __launch_bounds__(kBlock) void k_refit(const float4 *__restrict__ box
     }
 }
 
+// ---- PLOC (Meister & Bittner 2018, "Parallel Locally-Ordered Clustering for
+// Bounding Volume Hierarchy Construction") over the Morton-sorted leaves ----
+// A cluster = (box, id): id ~p for the leaf at sorted position p, >= 0 for an
+// internal node.  Per iteration: every cluster finds, among the kPlocRadius
+// clusters on either side in Morton order, the one whose union box has the
+// smallest surface area (ties: the lower index); mutual nearest neighbours
+// merge into a new internal node (the lower index creates it and keeps the
+// slot), and the survivors are compacted in order.  Internal nodes are
+// numbered downwards from n-2, so the root (the last merge) is node 0.
+#ifndef FRT_EXP_PLOC_R
+#define FRT_EXP_PLOC_R 16
+#endif
+constexpr int kPlocRadius = FRT_EXP_PLOC_R;
+
+__device__ __forceinline__ float union_area(float4 alo, float4 ahi, float4 blo, float4 bhi)
+{
+    const float dx = fmaxf(ahi.x, bhi.x) - fminf(alo.x, blo.x);
+    const float dy = fmaxf(ahi.y, bhi.y) - fminf(alo.y, blo.y);
+    const float dz = fmaxf(ahi.z, bhi.z) - fminf(alo.z, blo.z);
+    return dx * dy + dy * dz + dz * dx;
+}
+
+__global__ __launch_bounds__(kBlock) void k_ploc_init(const float4 *__restrict__ box, const unsigned long long *__restrict__ k,
+                                                       int n, float4 *cbox, int *cid)
+{
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const int prim = (int)(uint32_t)k[i];
+    cbox[2 * i] = box[2 * prim];
+    cbox[2 * i + 1] = box[2 * prim + 1];
+    cid[i] = ~i;
+}
+
+// nearest neighbour within the window; the block's clusters +- radius staged in LDS
+__global__ __launch_bounds__(kBlock) void k_ploc_nn(const float4 *__restrict__ cbox, int c, int *__restrict__ nn)
+{
+    __shared__ float4 slo[kBlock + 2 * kPlocRadius], shi[kBlock + 2 * kPlocRadius];
+    const int base = blockIdx.x * kBlock - kPlocRadius;
+    for (int t = threadIdx.x; t < kBlock + 2 * kPlocRadius; t += kBlock) {
+        const int j = base + t;
+        if (j >= 0 && j < c) { slo[t] = cbox[2 * j]; shi[t] = cbox[2 * j + 1]; }
+    }
+    __syncthreads();
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= c) return;
+    const int li = i - base;
+    const float4 alo = slo[li], ahi = shi[li];
+    float best = INFINITY;
+    int bj = -1;
+    const int j0 = max(0, i - kPlocRadius), j1 = min(c - 1, i + kPlocRadius);
+    for (int j = j0; j <= j1; ++j) {
+        if (j == i) continue;
+        const float a = union_area(alo, ahi, slo[j - base], shi[j - base]);
+        if (a < best) { best = a; bj = j; }           // ascending j: ties keep the lower index
+    }
+    nn[i] = bj;
+}
+
+// survivor / creator flags: mutual pairs merge at the lower index
+__global__ __launch_bounds__(kBlock) void k_ploc_flags(const int *__restrict__ nn, int c, int *keep, int *create)
+{
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= c) return;
+    const int j = nn[i];
+    const bool mutual = j >= 0 && nn[j] == i;
+    keep[i] = (mutual && i > j) ? 0 : 1;
+    create[i] = (mutual && i < j) ? 1 : 0;
+}
+
+__global__ __launch_bounds__(kBlock) void k_ploc_merge(const float4 *__restrict__ cbox, const int *__restrict__ cid,
+                                                        const int *__restrict__ nn, const int *__restrict__ keep_pos,
+                                                        const int *__restrict__ create_pos, const int *__restrict__ keep,
+                                                        const int *__restrict__ create, int c, int next_node,
+                                                        float4 *__restrict__ obox, int *__restrict__ oid,
+                                                        int *__restrict__ child, float4 *__restrict__ node_box)
+{
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= c || !keep[i]) return;
+    const int o = keep_pos[i];
+    if (!create[i]) {
+        obox[2 * o] = cbox[2 * i];
+        obox[2 * o + 1] = cbox[2 * i + 1];
+        oid[o] = cid[i];
+        return;
+    }
+    const int j = nn[i];
+    const float4 alo = cbox[2 * i], ahi = cbox[2 * i + 1], blo = cbox[2 * j], bhi = cbox[2 * j + 1];
+    const float4 lo = make_float4(fminf(alo.x, blo.x), fminf(alo.y, blo.y), fminf(alo.z, blo.z), 0.0f);
+    const float4 hi = make_float4(fmaxf(ahi.x, bhi.x), fmaxf(ahi.y, bhi.y), fmaxf(ahi.z, bhi.z), 0.0f);
+    const int node = next_node - create_pos[i];       // numbered downwards: the root is node 0
+    child[2 * node] = cid[i];                          // Morton order: the lower index on the left
+    child[2 * node + 1] = cid[j];
+    node_box[2 * node] = lo;
+    node_box[2 * node + 1] = hi;
+    obox[2 * o] = lo;
+    obox[2 * o + 1] = hi;
+    oid[o] = node;
+}
+
 }  // namespace
 
 namespace frt {
@@ -181,7 +281,7 @@ namespace frt {
     } while (0)
 
 int lbvh_build(hipStream_t st, int n, const float *box6, int32_t *child2, float *node_box6, int32_t *order,
-               float *ms, std::string &err)
+               float *ms, std::string &err, int algo)
 {
     int rc = -1;
     float4 *d_box = nullptr, *d_nbox = nullptr;
@@ -224,9 +324,67 @@ int lbvh_build(hipStream_t st, int n, const float *box6, int32_t *child2, float 
     k_morton<<<grid_n, kBlock, 0, st>>>(d_box, n, d_bounds, d_keys);
     LCHK(hipGetLastError());
     LCHK(hipcub::DeviceRadixSort::SortKeys(d_tmp, tmp_bytes, d_keys, d_sorted, n, 0, 64, st));
-    k_hierarchy<<<(n - 1 + kBlock - 1) / kBlock, kBlock, 0, st>>>(d_sorted, n, d_child, d_pint, d_pleaf);
-    k_refit<<<grid_n, kBlock, 0, st>>>(d_box, d_sorted, n, d_child, d_pint, d_pleaf, d_arrive, d_nbox);
-    LCHK(hipGetLastError());
+    if (algo == kGpuBvhLbvh) {
+        k_hierarchy<<<(n - 1 + kBlock - 1) / kBlock, kBlock, 0, st>>>(d_sorted, n, d_child, d_pint, d_pleaf);
+        k_refit<<<grid_n, kBlock, 0, st>>>(d_box, d_sorted, n, d_child, d_pint, d_pleaf, d_arrive, d_nbox);
+        LCHK(hipGetLastError());
+    } else {
+        // PLOC: ping-pong cluster arrays; flags and their exclusive scans per iteration
+#define PCHK(x)                                                                                     \
+    do {                                                                                            \
+        const hipError_t e_ = (x);                                                                  \
+        if (e_ != hipSuccess) { err = std::string(#x) + ": " + hipGetErrorString(e_); goto ploc_done; } \
+    } while (0)
+        float4 *cb[2] = {nullptr, nullptr};
+        int *ci[2] = {nullptr, nullptr};
+        int *nn = nullptr, *keep = nullptr, *create = nullptr, *kpos = nullptr, *cpos = nullptr;
+        void *stmp = nullptr;
+        size_t stmp_bytes = 0;
+        int tail[4];
+        int c = n, cur = 0, made = 0;
+        PCHK(hipMalloc(&cb[0], sizeof(float4) * 2 * (size_t)n));
+        PCHK(hipMalloc(&cb[1], sizeof(float4) * 2 * (size_t)n));
+        PCHK(hipMalloc(&ci[0], sizeof(int) * (size_t)n));
+        PCHK(hipMalloc(&ci[1], sizeof(int) * (size_t)n));
+        PCHK(hipMalloc(&nn, sizeof(int) * (size_t)n));
+        PCHK(hipMalloc(&keep, sizeof(int) * (size_t)n));
+        PCHK(hipMalloc(&create, sizeof(int) * (size_t)n));
+        PCHK(hipMalloc(&kpos, sizeof(int) * (size_t)n));
+        PCHK(hipMalloc(&cpos, sizeof(int) * (size_t)n));
+        PCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, stmp_bytes, keep, kpos, n, st));
+        PCHK(hipMalloc(&stmp, stmp_bytes));
+        k_ploc_init<<<grid_n, kBlock, 0, st>>>(d_box, d_sorted, n, cb[0], ci[0]);
+        PCHK(hipGetLastError());
+        while (c > 1) {
+            const int g = (c + kBlock - 1) / kBlock;
+            k_ploc_nn<<<g, kBlock, 0, st>>>(cb[cur], c, nn);
+            k_ploc_flags<<<g, kBlock, 0, st>>>(nn, c, keep, create);
+            PCHK(hipGetLastError());
+            PCHK(hipcub::DeviceScan::ExclusiveSum(stmp, stmp_bytes, keep, kpos, c, st));
+            PCHK(hipcub::DeviceScan::ExclusiveSum(stmp, stmp_bytes, create, cpos, c, st));
+            // survivors and merges of this pass (last element + its flag)
+            PCHK(hipMemcpyAsync(&tail[0], kpos + c - 1, sizeof(int), hipMemcpyDeviceToHost, st));
+            PCHK(hipMemcpyAsync(&tail[1], keep + c - 1, sizeof(int), hipMemcpyDeviceToHost, st));
+            PCHK(hipMemcpyAsync(&tail[2], cpos + c - 1, sizeof(int), hipMemcpyDeviceToHost, st));
+            PCHK(hipMemcpyAsync(&tail[3], create + c - 1, sizeof(int), hipMemcpyDeviceToHost, st));
+            k_ploc_merge<<<g, kBlock, 0, st>>>(cb[cur], ci[cur], nn, kpos, cpos, keep, create, c, n - 2 - made,
+                                               cb[cur ^ 1], ci[cur ^ 1], d_child, d_nbox);
+            PCHK(hipGetLastError());
+            PCHK(hipStreamSynchronize(st));
+            const int c_new = tail[0] + tail[1], merged = tail[2] + tail[3];
+            if (merged <= 0 || c_new != c - merged) { err = "ploc: no merge progress"; goto ploc_done; }
+            made += merged;
+            c = c_new;
+            cur ^= 1;
+        }
+        if (made != n - 1) err = "ploc: wrong node count";
+    ploc_done:
+        (void)hipFree(cb[0]); (void)hipFree(cb[1]); (void)hipFree(ci[0]); (void)hipFree(ci[1]);
+        (void)hipFree(nn); (void)hipFree(keep); (void)hipFree(create); (void)hipFree(kpos); (void)hipFree(cpos);
+        (void)hipFree(stmp);
+        if (!err.empty()) goto done;
+#undef PCHK
+    }
     LCHK(hipEventRecord(e1, st));
     {
         std::vector<float4> nb(2 * (size_t)(n - 1));

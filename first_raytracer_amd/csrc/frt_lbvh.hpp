@@ -1,4 +1,4 @@
-// frt_lbvh.hpp -- GPU linear BVH builder (frt_lbvh.hip), internal to libfrt.so.
+// frt_lbvh.hpp -- GPU BVH builders (frt_lbvh.hip: PLOC, linear BVH), internal to libfrt.so.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -10,6 +10,8 @@ namespace frt {
 // node_box6 (per internal node), order (sorted leaf position -> prim index),
 // ms = device time of the build passes.  Runs on `st` (current device).
 // Returns 0, or -1 with `err` set.
+// algo: kGpuBvhPloc (PLOC clustering, the default) or kGpuBvhLbvh (Karras).
+constexpr int kGpuBvhPloc = 0, kGpuBvhLbvh = 1;
 int lbvh_build(hipStream_t st, int n, const float *box6, int32_t *child2, float *node_box6, int32_t *order, float *ms,
-               std::string &err);
+               std::string &err, int algo = kGpuBvhPloc);
 }  // namespace frt

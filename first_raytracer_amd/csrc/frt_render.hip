@@ -694,13 +694,15 @@ extern "C" const char *frt_last_error(const frt_ctx *c) { return c ? c->err.c_st
 // GPU BVH build on this context's device and stream (frt_lbvh.hip); called
 // by frt_scene_build_bvh_gpu (csrc/host/scene.cpp).  Internal to libfrt.so.
 extern "C" int frt_internal_lbvh(frt_ctx *c, int n, const float *box6, int32_t *child2, float *node_box6,
-                                 int32_t *order, double *ms)
+                                 int32_t *order, double *ms, int algo)
 {
     if (!c || n < 2 || !box6 || !child2 || !node_box6 || !order) return FRT_E_INVALID;
+    if (algo != FRT_GPU_BVH_PLOC && algo != FRT_GPU_BVH_LBVH) return set_err(c, FRT_E_INVALID, "unknown GPU BVH builder");
     HIPCHK(c, hipSetDevice(c->device));
     float dev_ms = 0.0f;
     std::string err;
-    if (frt::lbvh_build(c->stream, n, box6, child2, node_box6, order, &dev_ms, err) != 0)
+    if (frt::lbvh_build(c->stream, n, box6, child2, node_box6, order, &dev_ms, err,
+                        algo == FRT_GPU_BVH_LBVH ? frt::kGpuBvhLbvh : frt::kGpuBvhPloc) != 0)
         return set_err(c, FRT_E_HIP, err);
     if (ms) *ms = dev_ms;
     return FRT_OK;

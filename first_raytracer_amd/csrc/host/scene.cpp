@@ -1012,7 +1012,7 @@ extern "C" int frt_scene_build_bvh_sah(frt_host_scene *s)
 
 // ---- GPU BVH build (frt_lbvh.hip through the context's device) ----
 extern "C" int frt_internal_lbvh(frt_ctx *c, int n, const float *box6, int32_t *child2, float *node_box6,
-                                 int32_t *order, double *ms);
+                                 int32_t *order, double *ms, int algo);
 
 static inline float f_down(double x)
 {
@@ -1028,6 +1028,11 @@ static inline float f_up(double x)
 }
 
 extern "C" int frt_scene_build_bvh_gpu(frt_host_scene *s, frt_ctx *ctx, double *device_ms)
+{
+    return frt_scene_build_bvh_gpu_algo(s, ctx, FRT_GPU_BVH_PLOC, device_ms);
+}
+
+extern "C" int frt_scene_build_bvh_gpu_algo(frt_host_scene *s, frt_ctx *ctx, int algo, double *device_ms)
 {
     if (!s || !ctx || !s->finished) return FRT_E_INVALID;
     const auto t0 = std::chrono::steady_clock::now();
@@ -1061,7 +1066,7 @@ extern "C" int frt_scene_build_bvh_gpu(frt_host_scene *s, frt_ctx *ctx, double *
         }
         std::vector<int32_t> child2(2 * (size_t)(n - 1)), order(n);
         std::vector<float> nb6(6 * (size_t)(n - 1));
-        const int rc = frt_internal_lbvh(ctx, n, box6.data(), child2.data(), nb6.data(), order.data(), &ms);
+        const int rc = frt_internal_lbvh(ctx, n, box6.data(), child2.data(), nb6.data(), order.data(), &ms, algo);
         if (rc != FRT_OK) return rc;
         nbox.assign(nb6.begin(), nb6.end());
         nchild.resize(child2.size());

@@ -248,14 +248,20 @@ int frt_scene_set_camera(frt_host_scene *s, const double *lookfrom, const double
 int frt_scene_set_env(frt_host_scene *s, const double *rgb);
 /* world_kind FRT_WORLD_BVH (create_bvh) or FRT_WORLD_LIST */
 int frt_scene_finish(frt_host_scene *s, int world_kind);
-/* GPU BVH builder: replaces the finished scene's world
- * (BVH or list) with a linear BVH over the same world prims built on ctx's
- * device -- Morton codes, radix sort, Karras hierarchy, atomic refit
- * (csrc/frt_lbvh.hip) -- in place of parallel_bvh_node::create_bvh's SAH sweep.
- * Finish with FRT_WORLD_LIST to skip the host build.  The topology differs
- * from the reference's, so exact-t ties between primitives may resolve
- * differently.  device_ms (optional) = device time of the build passes. */
+/* GPU BVH builders: replace the finished scene's world
+ * (BVH or list) with a BVH over the same world prims built on ctx's device
+ * (csrc/frt_lbvh.hip), in place of parallel_bvh_node::create_bvh's SAH sweep:
+ *   FRT_GPU_BVH_PLOC  Morton codes, radix sort, then PLOC clustering (mutual
+ *                     nearest neighbours by union surface area within 16
+ *                     clusters in Morton order) -- SAH-like quality;
+ *   FRT_GPU_BVH_LBVH  Morton codes, radix sort, Karras hierarchy, atomic refit.
+ * frt_scene_build_bvh_gpu = the PLOC builder.  Finish with FRT_WORLD_LIST to
+ * skip the host build.  The topology differs from the reference's, so exact-t
+ * ties between primitives may resolve differently.  device_ms (optional) =
+ * device time of the build passes. */
+enum { FRT_GPU_BVH_PLOC = 0, FRT_GPU_BVH_LBVH = 1 };
 int frt_scene_build_bvh_gpu(frt_host_scene *s, frt_ctx *ctx, double *device_ms);
+int frt_scene_build_bvh_gpu_algo(frt_host_scene *s, frt_ctx *ctx, int algo, double *device_ms);
 /* Binned SAH tree (32 centroid bins per axis, host threads) over the same
  * world prims: better traversal than the reference's sweep on large meshes
  * (same tie caveat as the GPU tree). */

@@ -27,8 +27,9 @@ def main():
     ap.add_argument("--res", default="1920x1080")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variants", default="default,no_lds")
-    ap.add_argument("--bvh", default="sah", choices=["host", "sah"],
-                    help="sah: binned SAH tree (bench default); host: the reference topology")
+    ap.add_argument("--bvh", default="sah", choices=["host", "sah", "ploc", "lbvh"],
+                    help="sah: binned SAH tree (bench default); host: the reference topology; "
+                         "ploc / lbvh: the GPU builders")
     args = ap.parse_args()
     import torch  # noqa: F401  (single HIP runtime)
     import first_raytracer_amd as frt
@@ -50,10 +51,15 @@ def main():
     def opt(v, key):
         return next((o[len(key):] for o in v.split("/")[1:] if o.startswith(key)), "")
 
-    if args.bvh == "sah" and kind == "cornell_box_obj":
+    if args.bvh != "host" and kind == "cornell_box_obj":
         hs = frt.HostScene.from_spec({"objects": [{"obj": obj, "geo": True}], "camera": frt.CORNELL_CAMERA,
                                       "world": "list"}, nx / ny)
-        hs.build_bvh_sah()
+        if args.bvh == "sah":
+            hs.build_bvh_sah()
+        else:
+            bctx = frt.Context(0)
+            print(json.dumps({"bvh": args.bvh, "build_ms": hs.build_bvh_gpu(bctx, args.bvh),
+                              "depth": hs.info.bvh_depth}), file=sys.stderr, flush=True)
     else:
         hs = frt.HostScene(kind, obj, nx / ny)
     ctxs = {}
