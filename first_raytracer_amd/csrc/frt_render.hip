@@ -1465,6 +1465,10 @@ static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
     // waves/SIMD (128 VGPRs; a few spills in the specular shading) they run
     // +40 % over the compiler's 2-wave allocation (same-call A/B,
     // profiles/r02/r02_mats*.jsonl).
+    // (The lambertian LDS kernel fits 111 VGPRs without spills since its work-
+    // item state moved to LDS; the compiler's 4 waves win 2 % at 64 spp but lose
+    // 10 % at the bench's 512 spp -- 337 vs 307 ms, same call --, so the cap stays:
+    // profiles/r02/r02_ab_cornell_knobs.jsonl, r02_ab_cornell_512spp.jsonl.)
     int waves = (MATS & kMatsSpecAny) ? (lds ? 4 : 5) : MATS == kMatsTex && lds ? 0 : lds ? 5 : 6;
     if constexpr (MATS != kMatsNone) {   // FRT_MATS_WAVES: register cap of the material kernels (tuning knob, not part of the C-ABI)
         const char *e = std::getenv("FRT_MATS_WAVES");
