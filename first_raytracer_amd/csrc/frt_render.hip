@@ -342,6 +342,11 @@ __global__ void scatter_shards(const float *__restrict__ gathered, float *__rest
 // ------------------------------------------------------------------------
 // PSS-MLT (pssmlt.cpp:301-365)
 // ------------------------------------------------------------------------
+// chain state columns (ItemState over kChainWords words): step count, chain
+// index, the current state's film position, scalar contribution, pending
+// weight and colour
+constexpr int kChainWords = 9;
+enum { kCsT, kCsC, kCsX, kCsY, kCsSc, kCsW, kCsCc };   // kCsCc..+2: r, g, b
 struct MltWork {
     int nx, ny;
     uint32_t seed;
@@ -407,17 +412,19 @@ template <int STACK, int WORLD, bool LDS_SCENE, bool MATS>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_MLT_WAVES))) void mlt_megakernel(
     const DevScene S0, const MltWork W)
 {
+    // [STACK][kBlock] stack, [kChainWords][kBlock] chain state, then the scene
     extern __shared__ __attribute__((aligned(16))) int lds_mem[];
     int *stk = lds_mem + threadIdx.x;
+    constexpr int kStackInts = WORLD != FRT_WORLD_LIST ? STACK * kBlock : 0;
     DevScene S = S0;
-    if constexpr (LDS_SCENE) scene_to_lds<WORLD>(S, lds_mem + STACK * kBlock);
+    if constexpr (LDS_SCENE) scene_to_lds<WORLD>(S, lds_mem + kStackInts + kChainWords * kBlock);
     else scene_strides_hbm(S);
     const int lane = threadIdx.x & 63;
     bool have = false, exhausted = false, init = false, large = false;
-    uint32_t j = 0, c = 0;
-    uint64_t t = 0;
-    float cx = 0, cy = 0, csc = 0, cw = 0;
-    f3 cc = mk3(0, 0, 0);
+    // the chain's current state (touched once per proposal) in an LDS column,
+    // as the path kernel's work item (ItemState)
+    const ItemState C{lds_mem + kStackInts + (int)threadIdx.x};
+    uint32_t j = 0;
     RngKey key{0, 0};
     MltPath M;
     uint32_t n_cam = 0, n_ext = 0, n_sh = 0, n_smp = 0;
@@ -478,9 +485,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
         if (done) {
             const f3 L = M.P.L;
             const float sc = fmaxf(fmaxf(L.x, L.y), L.z);
+            float cx = i2f(C.get(kCsX)), cy = i2f(C.get(kCsY)), csc = i2f(C.get(kCsSc)), cw = i2f(C.get(kCsW));
+            f3 cc = mk3(i2f(C.get(kCsCc)), i2f(C.get(kCsCc + 1)), i2f(C.get(kCsCc + 2)));
+            uint32_t t = (uint32_t)C.get(kCsT);
+            bool moved = false;
             if (init) {                                 // current = initial state, materialised
                 mat = true; mat_fresh = true;
                 cx = M.x; cy = M.y; cc = L; csc = sc;
+                moved = true;
                 init = false;
             } else {                                    // pssmlt.cpp:200-209
                 float a = 1.0f;
@@ -492,15 +504,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
                     cw = 0.0f;
                     mat = true; mat_fresh = large;
                     cx = M.x; cy = M.y; cc = L; csc = sc;
+                    moved = true;
                 }
                 ++t;
                 ++n_smp;
             }
-            if (t >= W.steps) {                         // chain finished
+            if ((uint64_t)t >= W.steps) {               // chain finished
                 if (csc > 0.0f && cw != 0.0f) mlt_splat(W, cx, cy, cc, cw);
                 have = false;
             } else {
                 setup_next = true;
+                C.set(kCsT, (int)t);
+                C.set(kCsW, f2i(cw));
+                if (moved) {
+                    C.set(kCsX, f2i(cx)); C.set(kCsY, f2i(cy)); C.set(kCsSc, f2i(csc));
+                    C.set(kCsCc, f2i(cc.x)); C.set(kCsCc + 1, f2i(cc.y)); C.set(kCsCc + 2, f2i(cc.z));
+                }
             }
         }
         // ---- materialise accepted proposals: the whole wave writes one chain's
@@ -517,7 +536,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
             }
         }
         if (setup_next) {                               // next proposal reads the new state
-            key = rng_key(W.seed ^ kMltChainSalt, c, (uint32_t)(t + 1));
+            key = rng_key(W.seed ^ kMltChainSalt, (uint32_t)C.get(kCsC), (uint32_t)C.get(kCsT) + 1u);
             large = rng_u(key, 0) < kMltLargeStep;      // large_step vs mutate (pssmlt.cpp:187-196)
             mlt_begin(M, S, source(), W.nx, W.ny);
             ++n_cam;
@@ -539,9 +558,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
                     have = true;
                     init = true;
                     j = w;
-                    c = (uint32_t)W.shard_index + w * (uint32_t)W.shard_count;
-                    t = 0;
-                    cw = 0.0f;
+                    const uint32_t c = (uint32_t)W.shard_index + w * (uint32_t)W.shard_count;
+                    C.set(kCsC, (int)c);
+                    C.set(kCsT, 0);
+                    C.set(kCsW, 0);
+                    C.set(kCsSc, 0);
                     key = rng_key(W.seed ^ kMltChainSalt, c, 0u);   // initial state: TMarkovChain(s)
                     mlt_begin(M, S, source(), W.nx, W.ny);
                     ++n_cam;
@@ -1595,12 +1616,13 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
     else if (d < 64) { stack = 64; mlt_kernels<64, FRT_WORLD_BVH>(c->has_spec_mats, &kboot, &kchain); }
     else return set_err(c, FRT_E_UNSUPPORTED, "BVH deeper than 63 levels");
     const size_t lds_boot = (size_t)stack * kBlock * sizeof(int);
-    const size_t lds = lds_boot + (lds_scene ? c->scene_lds_bytes : 0);
+    const size_t lds = lds_boot + (size_t)kChainWords * kBlock * sizeof(int) + (lds_scene ? c->scene_lds_bytes : 0);
     const uint32_t n_chains = (uint32_t)p->mlt_chains;
     const uint32_t n_local = (n_chains > (uint32_t)p->shard_index)
                                  ? (n_chains - 1 - (uint32_t)p->shard_index) / (uint32_t)p->shard_count + 1 : 0;
     const uint64_t total = (uint64_t)p->spp * (uint64_t)p->nx * (uint64_t)p->ny;   // viewer ns
     const uint64_t steps = total / n_chains;                                       // samples_per_thread
+    if (steps >= 0xffffffffULL) return set_err(c, FRT_E_UNSUPPORTED, "pssmlt: more than 2^32 - 1 mutations per chain");
     // bootstrap normaliser (identical on every shard: same streams, fixed-order host sum)
     const int n_init = p->mlt_bootstrap;
     const size_t need = std::max<size_t>((size_t)n_init * sizeof(float), (size_t)kMltDims * n_local * sizeof(float));
