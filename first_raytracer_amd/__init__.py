@@ -34,6 +34,7 @@ FRT_FLAG_SPEC = 128
 FRT_FLAG_NO_OCT = 256
 FRT_GPU_BVH_PLOC = 0
 FRT_GPU_BVH_LBVH = 1
+FRT_GPU_BVH_SAH = 2
 FRT_INTEGRATOR_PATH, FRT_INTEGRATOR_PSSMLT, FRT_INTEGRATOR_AO, FRT_INTEGRATOR_NORMALS = 0, 1, 2, 3
 
 ERRORS = {0: "ok", -1: "invalid", -2: "hip", -3: "no scene", -4: "unsupported", -5: "io", -6: "no gfx950 device"}
@@ -328,10 +329,10 @@ class HostScene:
 
     def build_bvh_gpu(self, ctx, algo="ploc"):
         """Replace the world by a GPU-built BVH (frt_scene_build_bvh_gpu_algo): "ploc"
-        (PLOC clustering, the default) or "lbvh" (Karras linear BVH); returns the
-        device time of the build passes in ms."""
+        (PLOC clustering, the default), "lbvh" (Karras linear BVH) or "gsah" (top-down
+        binned SAH); returns the device time of the build passes in ms."""
         ms = ctypes.c_double()
-        a = {"ploc": FRT_GPU_BVH_PLOC, "lbvh": FRT_GPU_BVH_LBVH}[algo]
+        a = {"ploc": FRT_GPU_BVH_PLOC, "lbvh": FRT_GPU_BVH_LBVH, "gsah": FRT_GPU_BVH_SAH}[algo]
         _check(lib().frt_scene_build_bvh_gpu_algo(self.ptr, ctx.ptr, a, ctypes.byref(ms)),
                "frt_scene_build_bvh_gpu_algo", ctx.ptr)
         lib().frt_scene_info(self.ptr, ctypes.byref(self.info))

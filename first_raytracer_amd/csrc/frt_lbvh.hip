@@ -270,6 +270,213 @@ __global__ __launch_bounds__(kBlock) void k_ploc_merge(const float4 *__restrict_
     oid[o] = node;
 }
 
+// ---- binned SAH, top down, one level of the tree per launch ----
+// A task is a node over idx[b, e) (sizes >= 2).  One block per task: box and
+// centroid bounds, 32 centroid bins per axis in LDS (ordered-uint min / max
+// atomics), the cheapest split N_L A_L + N_R A_R (the host builder's rule,
+// csrc/host/scene.cpp SahBuilder), then a stable block-wide partition of the
+// range into idx_out.  Children of two or more prims become next-level tasks;
+// single prims become leaves (~prim).  Node ids are handed out by an atomic
+// counter (their numbering varies, the tree does not).
+constexpr int kSahBins = 32;
+struct SahTask { int b, e, node; };
+
+__device__ __forceinline__ float4 fmin4(float4 a, float4 b)
+{
+    return make_float4(fminf(a.x, b.x), fminf(a.y, b.y), fminf(a.z, b.z), 0.0f);
+}
+__device__ __forceinline__ float4 fmax4(float4 a, float4 b)
+{
+    return make_float4(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), 0.0f);
+}
+__device__ __forceinline__ float area3(float4 lo, float4 hi)
+{
+    const float dx = hi.x - lo.x, dy = hi.y - lo.y, dz = hi.z - lo.z;
+    return 2.0f * (dx * dy + dy * dz + dz * dx);
+}
+__device__ __forceinline__ float comp(float4 v, int k) { return k == 0 ? v.x : k == 1 ? v.y : v.z; }
+
+__global__ __launch_bounds__(kBlock) void k_sah_level(const float4 *__restrict__ box, const int *__restrict__ idx_in,
+                                                       int *__restrict__ idx_out, const SahTask *__restrict__ tasks,
+                                                       SahTask *__restrict__ next, int *__restrict__ next_count,
+                                                       int *__restrict__ node_counter, int *__restrict__ child,
+                                                       float4 *__restrict__ node_box)
+{
+    __shared__ uint32_t red[6][kBlock];
+    __shared__ uint32_t bcnt[3][kSahBins], blo[3][kSahBins][3], bhi[3][kSahBins][3];
+    __shared__ uint32_t cmn[3], cmx[3];
+    __shared__ float best_cost[3];
+    __shared__ int best_bin[3];
+    __shared__ int s_axis, s_bin, s_left;
+    __shared__ int scan[kBlock];
+    const SahTask T = tasks[blockIdx.x];
+    const int b = T.b, e = T.e, n = e - b, tid = threadIdx.x;
+    // ---- bounds: prims' box union and centroid range ----
+    float4 lo = make_float4(INFINITY, INFINITY, INFINITY, 0.0f), hi = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.0f);
+    float4 clo = lo, chi = hi;
+    for (int i = b + tid; i < e; i += kBlock) {
+        const int p = idx_in[i];
+        const float4 a = box[2 * p], z = box[2 * p + 1];
+        const float4 c = make_float4(0.5f * (a.x + z.x), 0.5f * (a.y + z.y), 0.5f * (a.z + z.z), 0.0f);
+        lo = fmin4(lo, a); hi = fmax4(hi, z); clo = fmin4(clo, c); chi = fmax4(chi, c);
+    }
+    if (tid < 3) { cmn[tid] = 0xffffffffu; cmx[tid] = 0u; }
+    for (int k = 0; k < 3; ++k) { red[k][tid] = f2ord(comp(lo, k)); red[3 + k][tid] = f2ord(comp(hi, k)); }
+    __syncthreads();
+    for (int k = 0; k < 3; ++k) { atomicMin(&cmn[k], f2ord(comp(clo, k))); atomicMax(&cmx[k], f2ord(comp(chi, k))); }
+    for (int st = kBlock / 2; st > 0; st >>= 1) {
+        if (tid < st)
+            for (int k = 0; k < 3; ++k) {
+                red[k][tid] = min(red[k][tid], red[k][tid + st]);
+                red[3 + k][tid] = max(red[3 + k][tid], red[3 + k][tid + st]);
+            }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        node_box[2 * T.node] = make_float4(ord2f(red[0][0]), ord2f(red[1][0]), ord2f(red[2][0]), 0.0f);
+        node_box[2 * T.node + 1] = make_float4(ord2f(red[3][0]), ord2f(red[4][0]), ord2f(red[5][0]), 0.0f);
+    }
+    float cl[3], sc[3];
+    for (int k = 0; k < 3; ++k) {
+        cl[k] = ord2f(cmn[k]);
+        const float ext = ord2f(cmx[k]) - cl[k];
+        sc[k] = ext > 0.0f ? (float)kSahBins / ext : 0.0f;
+    }
+    // ---- bins ----
+    if (n > 2) {
+        for (int t = tid; t < 3 * kSahBins; t += kBlock) {
+            const int k = t / kSahBins, j = t % kSahBins;
+            bcnt[k][j] = 0u;
+            for (int a = 0; a < 3; ++a) { blo[k][j][a] = 0xffffffffu; bhi[k][j][a] = 0u; }
+        }
+        __syncthreads();
+        for (int i = b + tid; i < e; i += kBlock) {
+            const int p = idx_in[i];
+            const float4 a = box[2 * p], z = box[2 * p + 1];
+            const float c[3] = {0.5f * (a.x + z.x), 0.5f * (a.y + z.y), 0.5f * (a.z + z.z)};
+            for (int k = 0; k < 3; ++k) {
+                if (sc[k] == 0.0f) continue;
+                const int j = min(kSahBins - 1, (int)((c[k] - cl[k]) * sc[k]));
+                atomicAdd(&bcnt[k][j], 1u);
+                for (int q = 0; q < 3; ++q) {
+                    atomicMin(&blo[k][j][q], f2ord(comp(a, q)));
+                    atomicMax(&bhi[k][j][q], f2ord(comp(z, q)));
+                }
+            }
+        }
+        __syncthreads();
+        // ---- the cheapest split per axis (thread k), then over the axes ----
+        if (tid < 3) {
+            const int k = tid;
+            float bc = INFINITY;
+            int bj = -1;
+            if (sc[k] != 0.0f) {
+                float rarea[kSahBins];
+                int rcnt[kSahBins];
+                float4 rl = make_float4(INFINITY, INFINITY, INFINITY, 0.0f), rh = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.0f);
+                int c = 0;
+                for (int j = kSahBins - 1; j > 0; --j) {
+                    if (bcnt[k][j]) {
+                        rl = fmin4(rl, make_float4(ord2f(blo[k][j][0]), ord2f(blo[k][j][1]), ord2f(blo[k][j][2]), 0.0f));
+                        rh = fmax4(rh, make_float4(ord2f(bhi[k][j][0]), ord2f(bhi[k][j][1]), ord2f(bhi[k][j][2]), 0.0f));
+                        c += (int)bcnt[k][j];
+                    }
+                    rarea[j] = c ? area3(rl, rh) : 0.0f;
+                    rcnt[j] = c;
+                }
+                float4 ll = make_float4(INFINITY, INFINITY, INFINITY, 0.0f), lh = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.0f);
+                c = 0;
+                for (int j = 0; j < kSahBins - 1; ++j) {
+                    if (bcnt[k][j]) {
+                        ll = fmin4(ll, make_float4(ord2f(blo[k][j][0]), ord2f(blo[k][j][1]), ord2f(blo[k][j][2]), 0.0f));
+                        lh = fmax4(lh, make_float4(ord2f(bhi[k][j][0]), ord2f(bhi[k][j][1]), ord2f(bhi[k][j][2]), 0.0f));
+                        c += (int)bcnt[k][j];
+                    }
+                    if (c == 0 || rcnt[j + 1] == 0) continue;
+                    const float cost = (float)c * area3(ll, lh) + (float)rcnt[j + 1] * rarea[j + 1];
+                    if (cost < bc) { bc = cost; bj = j; }
+                }
+            }
+            best_cost[k] = bc;
+            best_bin[k] = bj;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int ax = -1;
+            for (int k = 0; k < 3; ++k)
+                if (best_bin[k] >= 0 && (ax < 0 || best_cost[k] < best_cost[ax])) ax = k;
+            s_axis = ax;
+            s_bin = ax >= 0 ? best_bin[ax] : 0;
+        }
+        __syncthreads();
+    } else if (tid == 0) {
+        s_axis = -1;
+    }
+    if (tid == 0) s_left = 0;
+    __syncthreads();
+    const int ax = s_axis, bin = s_bin;
+    // ---- stable partition of [b, e) into idx_out (left: bin <= best bin) ----
+    int mid;
+    if (ax >= 0) {
+        int nl = 0;
+        for (int i = b + tid; i < e; i += kBlock) {
+            const int p = idx_in[i];
+            const float c = 0.5f * (comp(box[2 * p], ax) + comp(box[2 * p + 1], ax));
+            nl += min(kSahBins - 1, (int)((c - cl[ax]) * sc[ax])) <= bin ? 1 : 0;
+        }
+        atomicAdd(&s_left, nl);
+        __syncthreads();
+        mid = b + s_left;
+    } else {
+        mid = b + n / 2;
+    }
+    if (ax >= 0 && mid > b && mid < e) {
+        int base_l = b, base_r = mid;
+        for (int c0 = b; c0 < e; c0 += kBlock) {
+            const int i = c0 + tid;
+            int p = 0, f = 0;
+            if (i < e) {
+                p = idx_in[i];
+                const float c = 0.5f * (comp(box[2 * p], ax) + comp(box[2 * p + 1], ax));
+                f = min(kSahBins - 1, (int)((c - cl[ax]) * sc[ax])) <= bin ? 1 : 0;
+            }
+            scan[tid] = f;
+            __syncthreads();
+            for (int off = 1; off < kBlock; off <<= 1) {          // inclusive scan (Hillis-Steele)
+                const int v = tid >= off ? scan[tid - off] : 0;
+                __syncthreads();
+                scan[tid] += v;
+                __syncthreads();
+            }
+            const int incl = scan[tid], tot = scan[kBlock - 1];
+            if (i < e) {
+                if (f) idx_out[base_l + incl - 1] = p;
+                else idx_out[base_r + (tid - incl)] = p;
+            }
+            base_l += tot;
+            base_r += min(kBlock, e - c0) - tot;
+            __syncthreads();
+        }
+    } else {                                                 // one bin or n <= 2: median split in order
+        mid = b + n / 2;
+        for (int i = b + tid; i < e; i += kBlock) idx_out[i] = idx_in[i];
+    }
+    __syncthreads();
+    // ---- children ----
+    if (tid < 2) {
+        const int cb = tid == 0 ? b : mid, ce = tid == 0 ? mid : e;
+        int ref;
+        if (ce - cb == 1) {
+            ref = ~idx_out[cb];
+        } else {
+            ref = atomicAdd(node_counter, 1);
+            const int slot = atomicAdd(next_count, 1);
+            next[slot] = SahTask{cb, ce, ref};
+        }
+        child[2 * T.node + tid] = ref;
+    }
+}
+
 }  // namespace
 
 namespace frt {
@@ -320,6 +527,50 @@ int lbvh_build(hipStream_t st, int n, const float *box6, int32_t *child2, float 
     LCHK(hipEventCreate(&e0));
     LCHK(hipEventCreate(&e1));
     LCHK(hipEventRecord(e0, st));
+    if (algo == kGpuBvhSah) {
+        // top-down binned SAH; leaves are ~prim, order = identity
+        int *ia = nullptr, *ib = nullptr, *d_cnt = nullptr;
+        SahTask *ta = nullptr, *tb = nullptr;
+        int k = 1, level = 0;
+        const SahTask root{0, n, 0};
+        std::vector<int> iota(n);
+        for (int i = 0; i < n; ++i) iota[i] = i;
+#define SCHK(x)                                                                                     \
+    do {                                                                                            \
+        const hipError_t e_ = (x);                                                                  \
+        if (e_ != hipSuccess) { err = std::string(#x) + ": " + hipGetErrorString(e_); goto sah_done; } \
+    } while (0)
+        SCHK(hipMalloc(&ia, sizeof(int) * (size_t)n));
+        SCHK(hipMalloc(&ib, sizeof(int) * (size_t)n));
+        SCHK(hipMalloc(&ta, sizeof(SahTask) * (size_t)n));
+        SCHK(hipMalloc(&tb, sizeof(SahTask) * (size_t)n));
+        SCHK(hipMalloc(&d_cnt, sizeof(int) * 2));
+        SCHK(hipMemcpyAsync(ia, iota.data(), sizeof(int) * (size_t)n, hipMemcpyHostToDevice, st));
+        SCHK(hipMemcpyAsync(ta, &root, sizeof(SahTask), hipMemcpyHostToDevice, st));
+        {
+            const int one = 1;                                    // node 0 = root, already allocated
+            SCHK(hipMemcpyAsync(d_cnt + 1, &one, sizeof(int), hipMemcpyHostToDevice, st));
+        }
+        while (k > 0) {
+            int nk = 0;
+            SCHK(hipMemsetAsync(d_cnt, 0, sizeof(int), st));
+            k_sah_level<<<k, kBlock, 0, st>>>(d_box, ia, ib, ta, tb, d_cnt, d_cnt + 1, d_child, d_nbox);
+            SCHK(hipGetLastError());
+            SCHK(hipMemcpyAsync(&nk, d_cnt, sizeof(int), hipMemcpyDeviceToHost, st));
+            SCHK(hipStreamSynchronize(st));
+            // ranges not split further keep their (final) order in ib; carry them over
+            std::swap(ia, ib);
+            std::swap(ta, tb);
+            k = nk;
+            if (++level > 4096) { err = "sah: no progress"; goto sah_done; }
+        }
+        for (int i = 0; i < n; ++i) order[i] = i;
+    sah_done:
+        (void)hipFree(ia); (void)hipFree(ib); (void)hipFree(ta); (void)hipFree(tb); (void)hipFree(d_cnt);
+#undef SCHK
+        if (!err.empty()) goto done;
+        goto finished;
+    }
     k_centroid_bounds<<<std::min(grid_n, 1024), kBlock, 0, st>>>(d_box, n, d_bounds);
     k_morton<<<grid_n, kBlock, 0, st>>>(d_box, n, d_bounds, d_keys);
     LCHK(hipGetLastError());
@@ -385,6 +636,7 @@ int lbvh_build(hipStream_t st, int n, const float *box6, int32_t *child2, float 
         if (!err.empty()) goto done;
 #undef PCHK
     }
+finished:
     LCHK(hipEventRecord(e1, st));
     {
         std::vector<float4> nb(2 * (size_t)(n - 1));
@@ -399,7 +651,8 @@ int lbvh_build(hipStream_t st, int n, const float *box6, int32_t *child2, float 
             const float v[6] = {a.x, a.y, a.z, b.x, b.y, b.z};
             for (int k = 0; k < 6; ++k) node_box6[6 * i + k] = v[k];
         }
-        for (int i = 0; i < n; ++i) order[i] = (int32_t)(uint32_t)hkeys[i];
+        if (algo != kGpuBvhSah)
+            for (int i = 0; i < n; ++i) order[i] = (int32_t)(uint32_t)hkeys[i];
     }
     rc = 0;
 done:

@@ -10,8 +10,9 @@ namespace frt {
 // node_box6 (per internal node), order (sorted leaf position -> prim index),
 // ms = device time of the build passes.  Runs on `st` (current device).
 // Returns 0, or -1 with `err` set.
-// algo: kGpuBvhPloc (PLOC clustering, the default) or kGpuBvhLbvh (Karras).
-constexpr int kGpuBvhPloc = 0, kGpuBvhLbvh = 1;
+// algo: kGpuBvhPloc (PLOC clustering, the default), kGpuBvhLbvh (Karras) or
+// kGpuBvhSah (top-down binned SAH; leaves are prims, `order` the identity).
+constexpr int kGpuBvhPloc = 0, kGpuBvhLbvh = 1, kGpuBvhSah = 2;
 int lbvh_build(hipStream_t st, int n, const float *box6, int32_t *child2, float *node_box6, int32_t *order, float *ms,
                std::string &err, int algo = kGpuBvhPloc);
 }  // namespace frt

@@ -718,12 +718,14 @@ extern "C" int frt_internal_lbvh(frt_ctx *c, int n, const float *box6, int32_t *
                                  int32_t *order, double *ms, int algo)
 {
     if (!c || n < 2 || !box6 || !child2 || !node_box6 || !order) return FRT_E_INVALID;
-    if (algo != FRT_GPU_BVH_PLOC && algo != FRT_GPU_BVH_LBVH) return set_err(c, FRT_E_INVALID, "unknown GPU BVH builder");
+    if (algo != FRT_GPU_BVH_PLOC && algo != FRT_GPU_BVH_LBVH && algo != FRT_GPU_BVH_SAH)
+        return set_err(c, FRT_E_INVALID, "unknown GPU BVH builder");
     HIPCHK(c, hipSetDevice(c->device));
     float dev_ms = 0.0f;
     std::string err;
     if (frt::lbvh_build(c->stream, n, box6, child2, node_box6, order, &dev_ms, err,
-                        algo == FRT_GPU_BVH_LBVH ? frt::kGpuBvhLbvh : frt::kGpuBvhPloc) != 0)
+                        algo == FRT_GPU_BVH_LBVH ? frt::kGpuBvhLbvh
+                        : algo == FRT_GPU_BVH_SAH ? frt::kGpuBvhSah : frt::kGpuBvhPloc) != 0)
         return set_err(c, FRT_E_HIP, err);
     if (ms) *ms = dev_ms;
     return FRT_OK;

@@ -254,12 +254,15 @@ int frt_scene_finish(frt_host_scene *s, int world_kind);
  *   FRT_GPU_BVH_PLOC  Morton codes, radix sort, then PLOC clustering (mutual
  *                     nearest neighbours by union surface area within 16
  *                     clusters in Morton order) -- SAH-like quality;
- *   FRT_GPU_BVH_LBVH  Morton codes, radix sort, Karras hierarchy, atomic refit.
+ *   FRT_GPU_BVH_LBVH  Morton codes, radix sort, Karras hierarchy, atomic refit;
+ *   FRT_GPU_BVH_SAH   top-down binned SAH, one tree level per launch, one
+ *                     workgroup per node (32 centroid bins per axis in LDS,
+ *                     cost N_L A_L + N_R A_R: frt_scene_build_bvh_sah's rule).
  * frt_scene_build_bvh_gpu = the PLOC builder.  Finish with FRT_WORLD_LIST to
  * skip the host build.  The topology differs from the reference's, so exact-t
  * ties between primitives may resolve differently.  device_ms (optional) =
  * device time of the build passes. */
-enum { FRT_GPU_BVH_PLOC = 0, FRT_GPU_BVH_LBVH = 1 };
+enum { FRT_GPU_BVH_PLOC = 0, FRT_GPU_BVH_LBVH = 1, FRT_GPU_BVH_SAH = 2 };
 int frt_scene_build_bvh_gpu(frt_host_scene *s, frt_ctx *ctx, double *device_ms);
 int frt_scene_build_bvh_gpu_algo(frt_host_scene *s, frt_ctx *ctx, int algo, double *device_ms);
 /* Binned SAH tree (32 centroid bins per axis, host threads) over the same

@@ -1,6 +1,7 @@
 """Alternative BVHs: the GPU builders (frt_scene_build_bvh_gpu_algo, csrc/frt_lbvh.hip:
 Morton keys and a device radix sort, then PLOC clustering or the Karras
-hierarchy with atomic refit) and the binned SAH builder (frt_scene_build_bvh_sah).  Either tree replaces the
+hierarchy with atomic refit, or a top-down binned SAH on the device) and the
+host binned SAH builder (frt_scene_build_bvh_sah).  Either tree replaces the
 reference-topology tree; hits can differ from the oracle's only at exact t ties
 between primitives, so renders meet the same RMSE gate and the ray counts agree
 within rounding-divergence noise."""
@@ -36,10 +37,10 @@ def check_tree(hs, n_prims):
 
 
 def build(hs, ctx, how):
-    return hs.build_bvh_gpu(ctx, how) if how in ("ploc", "lbvh") else hs.build_bvh_sah()
+    return hs.build_bvh_gpu(ctx, how) if how in ("ploc", "lbvh", "gsah") else hs.build_bvh_sah()
 
 
-@pytest.mark.parametrize("how", ["ploc", "lbvh", "sah"])
+@pytest.mark.parametrize("how", ["ploc", "lbvh", "gsah", "sah"])
 @pytest.mark.parametrize("spec_name", ["cornell", "conductors"])
 def test_gpu_bvh_render_matches_oracle(ctx, cornell_obj, spec_name, how):
     spec = ({"objects": [{"obj": cornell_obj, "geo": True}], "camera": SS.CORNELL_CAM} if spec_name == "cornell"
@@ -59,7 +60,7 @@ def test_gpu_bvh_render_matches_oracle(ctx, cornell_obj, spec_name, how):
     assert rmse(film, ref) <= 1e-3
 
 
-@pytest.mark.parametrize("how", ["ploc", "lbvh", "sah"])
+@pytest.mark.parametrize("how", ["ploc", "lbvh", "gsah", "sah"])
 @pytest.mark.parametrize("flags", [0, frt.FRT_FLAG_BVH2])
 def test_gpu_bvh_large_scene_matches_host_tree(ctx, cornell_obj, tmp_path, flags, how):
     """~20k triangles (HBM plan: BVH4Q from the GPU-built binary tree, or binary

@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--res", default="1920x1080")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variants", default="default,no_lds")
-    ap.add_argument("--bvh", default="sah", choices=["host", "sah", "ploc", "lbvh"],
+    ap.add_argument("--bvh", default="sah", choices=["host", "sah", "ploc", "lbvh", "gsah"],
                     help="sah: binned SAH tree (bench default); host: the reference topology; "
                          "ploc / lbvh: the GPU builders")
     args = ap.parse_args()
