@@ -262,7 +262,7 @@ class Runner:
         t0 = time.perf_counter()
         gpu_build_ms = None
         bvh = bvh_arg if kind == "cornell_box_obj" else "host"   # veach: list world, no BVH
-        if bvh in ("gpu", "lbvh", "gsah", "sah"):    # OBJ load only; the BVH is built below
+        if bvh in ("gpu", "ploc", "lbvh", "sah"):    # OBJ load only; the BVH is built below
             hs = frt.HostScene.from_spec({"objects": [{"obj": obj, "geo": True}], "camera": frt.CORNELL_CAMERA,
                                           "world": "list"}, nx / ny)
         else:
@@ -279,11 +279,11 @@ class Runner:
         ctx = self.ctx
         if bvh == "sah":
             hs.build_bvh_sah()                       # binned SAH on the host (in host_build_s)
-        if bvh in ("gpu", "lbvh", "gsah"):
-            algo = "ploc" if bvh == "gpu" else bvh
-            hs.build_bvh_gpu(ctx, algo)              # warm-up build (hipcub kernels load on first use)
+        if bvh in ("gpu", "ploc", "lbvh"):
+            algo = "gsah" if bvh == "gpu" else bvh
+            hs.build_bvh_gpu(ctx, algo)              # warm-up build (kernels load on first use)
             tg = time.perf_counter()
-            gpu_build_ms = hs.build_bvh_gpu(ctx, algo)   # Morton + radix sort + PLOC / Karras (frt_lbvh.hip)
+            gpu_build_ms = hs.build_bvh_gpu(ctx, algo)   # binned SAH / PLOC / Karras on the device (frt_lbvh.hip)
             t0 += time.perf_counter() - tg           # count one build in host_build_s
         t1 = time.perf_counter()
         ctx.upload(hs)                               # flatten + leaf collapse + BVH4Q + copy to HBM
@@ -352,7 +352,8 @@ class Runner:
         }
 
 
-BVH_NAMES = {"gpu": "PLOC (GPU)", "lbvh": "linear BVH (GPU)", "gsah": "binned SAH (GPU, 32 bins per axis)", "sah": "binned SAH (host, 32 bins per axis)",
+BVH_NAMES = {"gpu": "binned SAH (GPU, 32 bins per axis)", "ploc": "PLOC (GPU)", "lbvh": "linear BVH (GPU)",
+             "sah": "binned SAH (host, 32 bins per axis)",
              "host": "create_bvh (reference topology)"}
 
 
@@ -366,11 +367,11 @@ def main():
     ap.add_argument("--spp", type=int, default=512)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--tile", type=int, default=32)
-    ap.add_argument("--bvh", default="sah", choices=["host", "gpu", "lbvh", "gsah", "sah"],
-                    help="sah (default): binned SAH tree (host); host: the reference's create_bvh topology "
-                         "(exact-t ties resolved in its order); gpu: PLOC clustering on the GPU; lbvh: the Karras "
-                         "linear BVH on the GPU; gsah: binned SAH on the GPU (frt_lbvh.hip). List-world scenes "
-                         "(veach) ignore it")
+    ap.add_argument("--bvh", default="gpu", choices=["gpu", "sah", "host", "ploc", "lbvh"],
+                    help="gpu (default): binned SAH tree built on the GPU (frt_lbvh.hip); sah: the same rule on "
+                         "the host; host: the reference's create_bvh topology (exact-t ties resolved in its "
+                         "order); ploc / lbvh: PLOC clustering / the Karras linear BVH on the GPU. List-world "
+                         "scenes (veach) ignore it")
     ap.add_argument("--cpu-pixels", type=int, default=0, help="pixels in the CPU-baseline sample (0: calibrated)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline duration when calibrated")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every CPU this process may use (host_cpus)")

@@ -327,10 +327,10 @@ class HostScene:
         lib().frt_scene_info(self.ptr, ctypes.byref(self.info))
         return self.info.build_ms
 
-    def build_bvh_gpu(self, ctx, algo="ploc"):
-        """Replace the world by a GPU-built BVH (frt_scene_build_bvh_gpu_algo): "ploc"
-        (PLOC clustering, the default), "lbvh" (Karras linear BVH) or "gsah" (top-down
-        binned SAH); returns the device time of the build passes in ms."""
+    def build_bvh_gpu(self, ctx, algo="gsah"):
+        """Replace the world by a GPU-built BVH (frt_scene_build_bvh_gpu_algo): "gsah"
+        (top-down binned SAH, the default), "ploc" (PLOC clustering) or "lbvh" (Karras
+        linear BVH); returns the device time of the build passes in ms."""
         ms = ctypes.c_double()
         a = {"ploc": FRT_GPU_BVH_PLOC, "lbvh": FRT_GPU_BVH_LBVH, "gsah": FRT_GPU_BVH_SAH}[algo]
         _check(lib().frt_scene_build_bvh_gpu_algo(self.ptr, ctx.ptr, a, ctypes.byref(ms)),

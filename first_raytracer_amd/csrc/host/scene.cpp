@@ -1029,7 +1029,7 @@ static inline float f_up(double x)
 
 extern "C" int frt_scene_build_bvh_gpu(frt_host_scene *s, frt_ctx *ctx, double *device_ms)
 {
-    return frt_scene_build_bvh_gpu_algo(s, ctx, FRT_GPU_BVH_PLOC, device_ms);
+    return frt_scene_build_bvh_gpu_algo(s, ctx, FRT_GPU_BVH_SAH, device_ms);
 }
 
 extern "C" int frt_scene_build_bvh_gpu_algo(frt_host_scene *s, frt_ctx *ctx, int algo, double *device_ms)

@@ -253,12 +253,12 @@ int frt_scene_finish(frt_host_scene *s, int world_kind);
  * (csrc/frt_lbvh.hip), in place of parallel_bvh_node::create_bvh's SAH sweep:
  *   FRT_GPU_BVH_PLOC  Morton codes, radix sort, then PLOC clustering (mutual
  *                     nearest neighbours by union surface area within 16
- *                     clusters in Morton order) -- SAH-like quality;
+ *                     clusters in Morton order);
  *   FRT_GPU_BVH_LBVH  Morton codes, radix sort, Karras hierarchy, atomic refit;
  *   FRT_GPU_BVH_SAH   top-down binned SAH, one tree level per launch, one
  *                     workgroup per node (32 centroid bins per axis in LDS,
  *                     cost N_L A_L + N_R A_R: frt_scene_build_bvh_sah's rule).
- * frt_scene_build_bvh_gpu = the PLOC builder.  Finish with FRT_WORLD_LIST to
+ * frt_scene_build_bvh_gpu = the binned SAH builder.  Finish with FRT_WORLD_LIST to
  * skip the host build.  The topology differs from the reference's, so exact-t
  * ties between primitives may resolve differently.  device_ms (optional) =
  * device time of the build passes. */

@@ -3,8 +3,9 @@ north-star scene; cornell_box_obj main.cpp:222-252 on the mesh
 frt.write_tessellated_obj(k=172) writes) through frt_render, against the fp64
 oracle on the same counter-RNG streams.
 
-Two trees: the bench default (binned SAH, frt_scene_build_bvh_sah) and the
-reference's create_bvh topology (parallel_bvh.h:67-175).  Both run the
+Three trees: the bench default (binned SAH built on the GPU,
+frt_scene_build_bvh_gpu), the same rule on the host (frt_scene_build_bvh_sah)
+and the reference's create_bvh topology (parallel_bvh.h:67-175).  Both run the
 HBM-resident BVH4Q plan of path_megakernel (4-triangle leaves, LDS + scratch
 stack) at the tree depth the full scene has.
 
@@ -50,11 +51,14 @@ def ctx():
     c.close()
 
 
-def host_scene(obj, aspect, tree):
-    if tree == "sah":
+def host_scene(ctx, obj, aspect, tree):
+    if tree in ("sah", "gpu"):
         hs = frt.HostScene.from_spec({"objects": [{"obj": obj, "geo": True}], "camera": frt.CORNELL_CAMERA,
                                       "world": "list"}, aspect)
-        hs.build_bvh_sah()
+        if tree == "sah":
+            hs.build_bvh_sah()
+        else:
+            hs.build_bvh_gpu(ctx)                                    # binned SAH on the device
         return hs
     return frt.HostScene("cornell_box_obj", obj, aspect)
 
@@ -63,10 +67,10 @@ def rmse(a, b):
     return float(np.sqrt(np.mean((np.asarray(a, np.float64) - np.asarray(b, np.float64)) ** 2)))
 
 
-@pytest.mark.parametrize("tree", ["sah", "reference"])
+@pytest.mark.parametrize("tree", ["gpu", "sah", "reference"])
 def test_c4_1080p_pixel_sample(ctx, c1m, ora, tree):
     nx, ny, spp = 1920, 1080, 64
-    hs = host_scene(c1m, nx / ny, tree)
+    hs = host_scene(ctx, c1m, nx / ny, tree)
     assert hs.info.n_tris == N_TRIS
     ctx.upload(hs)
     film, st = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=7))
@@ -85,10 +89,10 @@ def test_c4_1080p_pixel_sample(ctx, c1m, ora, tree):
     assert abs(st.rays / st.samples - cnt.rays / cnt.samples) / (cnt.rays / cnt.samples) < 5e-3
 
 
-@pytest.mark.parametrize("tree", ["sah", "reference"])
+@pytest.mark.parametrize("tree", ["gpu", "sah", "reference"])
 def test_c4_small_frame_exact_counts(ctx, c1m, ora, tree):
     nx, ny, spp = 96, 54, 64
-    hs = host_scene(c1m, nx / ny, tree)
+    hs = host_scene(ctx, c1m, nx / ny, tree)
     ctx.upload(hs)
     film, st = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=3))
     ref, cnt = ora[nx / ny].render(nx, ny, spp, seed=3)

@@ -84,13 +84,13 @@ def test_gpu_bvh_large_scene_matches_host_tree(ctx, cornell_obj, tmp_path, flags
 
 
 def test_bench_default_tree_all_integrators(ctx, cornell_obj):
-    """The bench's default scene build (binned SAH tree) against the oracle
-    (reference topology) for every integrator: path, PSS-MLT short chains,
-    AO, normals."""
+    """The bench's default scene build (binned SAH tree built on the GPU)
+    against the oracle (reference topology) for every integrator: path,
+    PSS-MLT short chains, AO, normals."""
     nx, ny = 64, 48
     hs = frt.HostScene.from_spec({"objects": [{"obj": cornell_obj, "geo": True}], "camera": frt.CORNELL_CAMERA,
                                   "world": "list"}, nx / ny)
-    hs.build_bvh_sah()
+    hs.build_bvh_gpu(ctx)
     hs.set_env((1.0, 1.0, 1.0))
     ctx.upload(hs)
     osc = oracle.OracleScene("cornell_box_obj", cornell_obj, nx / ny)
