@@ -117,6 +117,23 @@ FRT_HD float fexp(float x)
     return expf(x);
 #endif
 }
+// ln x, x^y (x > 0) on the hardware log2 / exp2 (v_log_f32 / v_exp_f32)
+FRT_HD float flog(float x)
+{
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(FRT_EXP_IEEE_MATH)
+    return __builtin_amdgcn_logf(x) * 0.69314718055994530942f;
+#else
+    return logf(x);
+#endif
+}
+FRT_HD float fpow(float x, float y)
+{
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(FRT_EXP_IEEE_MATH)
+    return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
+#else
+    return powf(x, y);
+#endif
+}
 FRT_HD float rlen(f3 v) { return frsqrt(len2(v)); }
 FRT_HD f3 normalize(f3 v) { return rlen(v) * v; }
 
@@ -330,10 +347,13 @@ FRT_HD f3 dielectric_eval(f3 ks, float ior, f3 n, f3 wi, f3 wo)
 
 // ---- rough_conductor (material.h:246-315), roughconductor_pdf (pdf.h:231-486,
 //      pdf.cpp:5-12), microfacet.h; isotropic alpha.  fp32 restatement of the
-//      oracle's rough_* functions (oracle/frt_oracle.c), libm/OCML transcendentals
-//      (the lobe sampler is not on the lambertian hot path). ----
+//      oracle's rough_* functions (oracle/frt_oracle.c) on the hardware
+//      transcendentals (rcp, sqrt, rsq, exp2, log2, sin / cos in revolutions)
+//      like the rest of the shading code; only acos stays libm.  The OCML
+//      tan / pow / atan2 / sin / cos and IEEE divisions of round 1 made this the
+//      register-hungriest part of the material kernels. ----
 constexpr int kDistGgx = 0, kDistBeckmann = 1;
-FRT_HD float safe_sqrtf(float v) { const float r = sqrtf(v); return (0.0f < r) ? r : 0.0f; }   // util.h:43-46 (NaN -> 0)
+FRT_HD float safe_sqrtf(float v) { const float r = fsqrt(v); return (0.0f < r) ? r : 0.0f; }   // util.h:43-46 (NaN -> 0)
 FRT_HD f3 onb_to_local(const Onb &b, f3 a) { return f3{dot(a, b.u), dot(a, b.v), dot(a, b.w)}; }
 // microfacet::fresnelConductorExact (microfacet.h:8-31), one channel
 FRT_HD float fresnel_conductor1(float cos_i, float eta, float k)
@@ -343,9 +363,9 @@ FRT_HD float fresnel_conductor1(float cos_i, float eta, float k)
     const float a2pb2 = safe_sqrtf(temp1 * temp1 + 4.0f * (k * k * eta * eta));
     const float a = safe_sqrtf(0.5f * (a2pb2 + temp1));
     const float term1 = a2pb2 + c2, term2 = (2.0f * cos_i) * a;
-    const float rs2 = (term1 - term2) / (term1 + term2);
+    const float rs2 = fdiv(term1 - term2, term1 + term2);
     const float term3 = c2 * a2pb2 + s4, term4 = s2 * term2;
-    const float rp2 = rs2 * (term3 - term4) / (term3 + term4);
+    const float rp2 = rs2 * fdiv(term3 - term4, term3 + term4);
     return 0.5f * (rp2 + rs2);
 }
 // microfacet::smithG1 (microfacet.h:48-88)
@@ -355,15 +375,15 @@ FRT_HD float smith_g1(f3 v, f3 m, f3 n, float alpha, int dist)
     if (dot(v, m) * cos_t <= 0.0f) return 0.0f;
     const float temp = 1.0f - cos_t * cos_t;
     if (temp <= 0.0f) return 1.0f;
-    const float tan_t = sqrtf(temp) / cos_t;
+    const float tan_t = fdiv(fsqrt(temp), cos_t);
     if (dist == kDistBeckmann) {
-        const float a = 1.0f / (alpha * tan_t);
+        const float a = rcp(alpha * tan_t);
         if (a >= 1.6f) return 1.0f;
         const float a2 = a * a;
-        return (3.535f * a + 2.181f * a2) / (1.0f + 2.276f * a + 2.577f * a2);
+        return fdiv(3.535f * a + 2.181f * a2, 1.0f + 2.276f * a + 2.577f * a2);
     }
     const float root = alpha * tan_t;
-    return 2.0f / (1.0f + sqrtf(1.0f + root * root));              // hypot2(1, root) (util.h:239-254)
+    return fdiv(2.0f, 1.0f + fsqrt(1.0f + root * root));          // hypot2(1, root) (util.h:239-254)
 }
 // microfacet::eval (microfacet.h:90-135)
 FRT_HD float microfacet_d(f3 m, f3 n, float alpha, int dist)
@@ -372,20 +392,20 @@ FRT_HD float microfacet_d(f3 m, f3 n, float alpha, int dist)
     const float cos_t = ml.z;
     if (cos_t <= 0.0f) return 0.0f;
     const float c2 = cos_t * cos_t, a2 = alpha * alpha;
-    const float be = (ml.x * ml.x / a2 + ml.y * ml.y / a2) / c2;
+    const float be = fdiv(fdiv(ml.x * ml.x, a2) + fdiv(ml.y * ml.y, a2), c2);
     float r;
     if (dist == kDistBeckmann) {
-        r = expf(-be) / (kPi * a2 * c2 * c2);
+        r = fdiv(fexp(-be), kPi * a2 * c2 * c2);
     } else {
         const float root = (1.0f + be) * c2;
-        r = 1.0f / (kPi * a2 * root * root);
+        r = rcp(kPi * a2 * root * root);
     }
     return (r * cos_t < 1e-20f) ? 0.0f : r;
 }
 // util.h:185-236
 FRT_HD float erfinv_f(float x)
 {
-    float w = -logf((1.0f - x) * (1.0f + x)), p;
+    float w = -flog((1.0f - x) * (1.0f + x)), p;
     if (w < 5.0f) {
         w = w - 2.5f;
         p = 2.81022636e-08f;
@@ -398,7 +418,7 @@ FRT_HD float erfinv_f(float x)
         p = 0.246640727f + p * w;
         p = 1.50140941f + p * w;
     } else {
-        w = sqrtf(w) - 3.0f;
+        w = fsqrt(w) - 3.0f;
         p = -0.000200214257f;
         p = 0.000100950558f + p * w;
         p = 0.00134934322f + p * w;
@@ -415,9 +435,9 @@ FRT_HD float erf_f(float x)
 {
     const float sign = copysignf(1.0f, x);
     x = fabsf(x);
-    const float t = 1.0f / (1.0f + 0.3275911f * x);
+    const float t = rcp(1.0f + 0.3275911f * x);
     const float y = 1.0f - (((((1.061405429f * t - 1.453152027f) * t) + 1.421413741f) * t - 0.284496736f) * t +
-                            0.254829592f) * t * expf(-x * x);
+                            0.254829592f) * t * fexp(-x * x);
     return sign * y;
 }
 // roughconductor_pdf::sampleVisible11 (pdf.h:280-397)
@@ -425,49 +445,52 @@ FRT_HD void sample_visible11(float theta_i, float sx, float sy, int dist, float 
 {
     const float kSqrtPiInv = 0.564189583547756287f;
     if (theta_i < 1e-4f) {                                      // normal incidence
-        const float r = (dist == kDistBeckmann) ? sqrtf(-logf(1.0f - sx)) : safe_sqrtf(sx / (1.0f - sx));
-        const float phi = 2.0f * kPi * sy;
-        slx = r * cosf(phi); sly = r * sinf(phi);
+        const float r = (dist == kDistBeckmann) ? fsqrt(-flog(1.0f - sx)) : safe_sqrtf(fdiv(sx, 1.0f - sx));
+        float sp, cp;
+        sincos_2pi(sy, sp, cp);                                 // phi = 2 pi sy
+        slx = r * cp; sly = r * sp;
         return;
     }
-    const float tan_t = tanf(theta_i);
+    float st, ct;
+    sincos_2pi(theta_i * (0.5f * kInvPi), st, ct);
+    const float tan_t = fdiv(st, ct);
     if (dist == kDistBeckmann) {
-        const float cot_t = 1.0f / tan_t;
+        const float cot_t = rcp(tan_t);
         float a = -1.0f, c = erf_f(cot_t);
         const float sample_x = fmaxf(sx, 1e-6f);
         const float fit = 1.0f + theta_i * (-0.876f + theta_i * (0.4265f - 0.0594f * theta_i));
-        float b = c - (1.0f + c) * powf(1.0f - sample_x, fit);
-        const float norm = 1.0f / (1.0f + c + kSqrtPiInv * tan_t * expf(-cot_t * cot_t));
+        float b = c - (1.0f + c) * fpow(1.0f - sample_x, fit);
+        const float norm = rcp(1.0f + c + kSqrtPiInv * tan_t * fexp(-cot_t * cot_t));
         for (int it = 1; it < 10; ++it) {
             if (!(b >= a && b <= c)) b = 0.5f * (a + c);
             const float inv_erf = erfinv_f(b);
-            const float value = norm * (1.0f + b + kSqrtPiInv * tan_t * expf(-inv_erf * inv_erf)) - sample_x;
+            const float value = norm * (1.0f + b + kSqrtPiInv * tan_t * fexp(-inv_erf * inv_erf)) - sample_x;
             const float deriv = norm * (1.0f - inv_erf * tan_t);
             if (fabsf(value) < 1e-5f) break;
             if (value > 0.0f) c = b; else a = b;
-            b -= value / deriv;
+            b -= fdiv(value, deriv);
         }
         slx = erfinv_f(b);
         sly = erfinv_f(2.0f * fmaxf(sy, 1e-6f) - 1.0f);
         return;
     }
-    const float a = 1.0f / tan_t;
-    const float g1 = 2.0f / (1.0f + safe_sqrtf(1.0f + 1.0f / (a * a)));
-    float A = 2.0f * sx / g1 - 1.0f;
+    const float a = rcp(tan_t);
+    const float g1 = fdiv(2.0f, 1.0f + safe_sqrtf(1.0f + rcp(a * a)));
+    float A = fdiv(2.0f * sx, g1) - 1.0f;
     if (fabsf(A) == 1.0f) A -= copysignf(1.0f, A) * kEps;
-    const float tmp = 1.0f / (A * A - 1.0f);
+    const float tmp = rcp(A * A - 1.0f);
     const float B = tan_t;
     const float D = safe_sqrtf(B * B * tmp * tmp - (A * A - B * B) * tmp);
     const float s1 = B * tmp - D, s2 = B * tmp + D;
-    slx = (A < 0.0f || s2 > 1.0f / tan_t) ? s1 : s2;
+    slx = (A < 0.0f || s2 > a) ? s1 : s2;
     float S;
     if (sy > 0.5f) { S = 1.0f; sy = 2.0f * (sy - 0.5f); }
     else { S = -1.0f; sy = 2.0f * (0.5f - sy); }
-    const float z = (sy * (sy * (sy * -0.365728915865723f + 0.790235037209296f) - 0.424965825137544f) +
-                     0.000152998850436920f) /
-                    (sy * (sy * (sy * (sy * 0.169507819808272f - 0.397203533833404f) - 0.232500544458471f) + 1.0f) -
-                     0.539825872510702f);
-    sly = S * z * sqrtf(1.0f + slx * slx);
+    const float z = fdiv(sy * (sy * (sy * -0.365728915865723f + 0.790235037209296f) - 0.424965825137544f) +
+                             0.000152998850436920f,
+                         sy * (sy * (sy * (sy * 0.169507819808272f - 0.397203533833404f) - 0.232500544458471f) + 1.0f) -
+                             0.539825872510702f);
+    sly = S * z * fsqrt(1.0f + slx * slx);
 }
 // roughconductor_pdf::generate (pdf.h:409-482, pdf.cpp:5-12): wo, and the
 // sampled pdf (pdfVisible / (4 wo.m)) that path.cpp:82 prefers when > 0
@@ -476,23 +499,27 @@ FRT_HD f3 rough_generate(f3 n, f3 wi, float alpha, int dist, float s0, float s1,
     const Onb uvw = onb_from_w(n);
     const f3 wl = onb_to_local(uvw, wi);
     f3 ws = f3{alpha * wl.x, alpha * wl.y, wl.z};
-    ws = (1.0f / sqrtf(len2(ws))) * ws;
-    float theta = 0.0f, phi = 0.0f;
-    if (ws.z < 0.99999f) { theta = acosf(ws.z); phi = atan2f(ws.y, ws.x); }
-    const float sp = sinf(phi), cp = cosf(phi);
+    ws = frsqrt(len2(ws)) * ws;
+    // theta = acos(ws.z), phi = atan2(ws.y, ws.x): sin / cos phi as ws.y / r, ws.x / r
+    float theta = 0.0f, sp = 0.0f, cp = 1.0f;
+    if (ws.z < 0.99999f) {
+        theta = acosf(ws.z);
+        const float rr = ws.x * ws.x + ws.y * ws.y;
+        if (rr > 0.0f) { const float ir = frsqrt(rr); sp = ws.y * ir; cp = ws.x * ir; }
+    }
     float slx, sly;
     sample_visible11(theta, s0, s1, dist, slx, sly);
     if (!(fabsf(slx) <= 3.40282347e+38f)) slx = 0.0f;             // !std::isfinite
     const float rx = (cp * slx - sp * sly) * alpha, ry = (sp * slx + cp * sly) * alpha;
-    const float nrm = 1.0f / sqrtf(rx * rx + ry * ry + 1.0f);
+    const float nrm = frsqrt(rx * rx + ry * ry + 1.0f);
     const f3 ml = f3{-rx * nrm, -ry * nrm, nrm};
     const f3 mw = onb_local(uvw, ml);
     float pdf = 0.0f;
     if (wl.z != 0.0f)
-        pdf = smith_g1(onb_local(uvw, wl), mw, n, alpha, dist) * fabsf(dot(wl, ml)) * microfacet_d(mw, n, alpha, dist) /
-              fabsf(wl.z);
+        pdf = fdiv(smith_g1(onb_local(uvw, wl), mw, n, alpha, dist) * fabsf(dot(wl, ml)) * microfacet_d(mw, n, alpha, dist),
+                   fabsf(wl.z));
     const f3 wo = reflect(-wi, mw);
-    sampled_pdf = pdf / (4.0f * dot(wo, mw));
+    sampled_pdf = fdiv(pdf, 4.0f * dot(wo, mw));
     return wo;
 }
 // roughconductor_pdf::value (pdf.h:237-250)
@@ -500,7 +527,7 @@ FRT_HD float rough_value(f3 n, f3 wi, float alpha, int dist, f3 wo)
 {
     if (dot(n, wo) <= 0.0f || dot(n, wi) <= 0.0f) return 0.0f;
     const f3 H = normalize(wo + wi);
-    return microfacet_d(H, n, alpha, dist) * smith_g1(wi, H, n, alpha, dist) / (4.0f * dot(wi, n));
+    return fdiv(microfacet_d(H, n, alpha, dist) * smith_g1(wi, H, n, alpha, dist), 4.0f * dot(wi, n));
 }
 // rough_conductor::eval_bsdf (material.h:277-307); no cosine (is_specular)
 FRT_HD f3 rough_eval(f3 eta, f3 k, f3 spec, float alpha, int dist, f3 n, f3 wi, f3 wo)
@@ -514,7 +541,7 @@ FRT_HD f3 rough_eval(f3 eta, f3 k, f3 spec, float alpha, int dist, f3 n, f3 wi, 
     const f3 F = f3{fresnel_conductor1(c, eta.x, k.x), fresnel_conductor1(c, eta.y, k.y),
                     fresnel_conductor1(c, eta.z, k.z)} * spec;
     const float G = smith_g1(wi, H, n, alpha, dist) * smith_g1(wo, H, n, alpha, dist);
-    return (D * G / (4.0f * cos_wi)) * F;
+    return fdiv(D * G, 4.0f * cos_wi) * F;
 }
 
 // util.h:55-60

@@ -1455,7 +1455,16 @@ static Launcher make_launcher(size_t scene_bytes)
 template <int STACK, bool LDS, int WORLD = FRT_WORLD_BVH, bool SPEC = false, int MATS = kMatsNone>
 static Launcher bvh_launcher(int waves, size_t sb)
 {
-    if (waves == 6) return make_launcher<STACK, WORLD, LDS, FRT_EXP_W6, SPEC, MATS>(sb);
+    // The specular material kernels have no 6-wave build: at 80 VGPRs they
+    // spill 160-230 VGPRs, and one of them (rough conductors, HBM binary tree)
+    // compiled to a kernel with the oracle's ray counts and wrong radiance
+    // (RMSE 0.07, tests/test_gpu_conductors.py::test_register_caps_agree).
+    // A 6-wave request runs the 5-wave kernel.
+    if constexpr ((MATS & kMatsSpecAny) != 0) {
+        if (waves >= 6) waves = 5;
+    } else {
+        if (waves == 6) return make_launcher<STACK, WORLD, LDS, FRT_EXP_W6, SPEC, MATS>(sb);
+    }
     if (waves == 5) return make_launcher<STACK, WORLD, LDS, 5, SPEC, MATS>(sb);
     if constexpr (MATS != kMatsNone) {
         if (waves == 4) return make_launcher<STACK, WORLD, LDS, 4, SPEC, MATS>(sb);
