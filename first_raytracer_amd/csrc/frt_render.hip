@@ -357,7 +357,7 @@ struct MltWork {
     int trav_min;                        // see path_megakernel / trav_min()
     int min_desc;                        // leaf postponing: see bvh2_step
     float *U;                            // [kMltDims][n_local] current primary samples
-    float *film;                         // [nx*ny*3] splat accumulation
+    unsigned long long *film;            // [nx*ny*3] splat accumulation, fixed point (kSplatFix)
     unsigned *counter;
     unsigned long long *wave_rays;
 };
@@ -392,14 +392,29 @@ __global__ __launch_bounds__(kBlock) void mlt_bootstrap(const DevScene S0, int n
     sc[i] = fmaxf(fmaxf(M.P.L.x, M.P.L.y), M.P.L.z);
 }
 
+// Splats (AccumulatePathContribution, pssmlt.cpp) add into a fixed-point film:
+// a splat is rounded to a multiple of 2^-kSplatFix and added with a 64-bit
+// integer atomic.  Integer sums do not depend on the order the chains' atomics
+// land in, so the film is bit-reproducible run to run (float atomics were
+// not).  Splats are >= 0 (scale, weights and radiance are); the quantum
+// 2^-36 = 1.5e-11 is far below fp32's resolution of the pixel values, and
+// a pixel saturates only past 2^28.  mlt_film_to_float converts once at the end.
+constexpr int kSplatFix = 36;
 __device__ __forceinline__ void mlt_splat(const MltWork &W, float x, float y, f3 c, float w)
 {
     const int pix = mlt_pixel(x, y, W.nx, W.ny);
     if (pix < 0) return;
     const float k = W.scale * w;
-    atomicAdd(&W.film[3 * (size_t)pix + 0], k * c.x);
-    atomicAdd(&W.film[3 * (size_t)pix + 1], k * c.y);
-    atomicAdd(&W.film[3 * (size_t)pix + 2], k * c.z);
+    const double q = (double)(1ull << kSplatFix);
+    unsigned long long *f = W.film + 3 * (size_t)pix;
+    atomicAdd(f + 0, (unsigned long long)__double2ll_rn((double)(k * c.x) * q));
+    atomicAdd(f + 1, (unsigned long long)__double2ll_rn((double)(k * c.y) * q));
+    atomicAdd(f + 2, (unsigned long long)__double2ll_rn((double)(k * c.z) * q));
+}
+__global__ void mlt_film_to_float(const unsigned long long *__restrict__ acc, float *__restrict__ film, size_t n)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) film[i] = (float)((double)(long long)acc[i] * (1.0 / (double)(1ull << kSplatFix)));
 }
 
 // one lane = one chain tracing the rays of its current eye path (initial
@@ -625,6 +640,7 @@ struct frt_ctx {
     unsigned *counter = nullptr;
     unsigned long long *wave_rays = nullptr; size_t wave_rays_n = 0;
     float *slots_out = nullptr; size_t slots_out_bytes = 0;
+    unsigned long long *splat = nullptr; size_t splat_bytes = 0;   // PSS-MLT fixed-point splat film
     // frt_render_multi on this context as shard 0: RCCL communicators over the
     // member devices (one per member, cached while the device list is the
     // same), the gather buffer and the device film
@@ -700,6 +716,7 @@ extern "C" int frt_destroy(frt_ctx *c)
     if (c->counter) (void)hipFree(c->counter);
     if (c->wave_rays) (void)hipFree(c->wave_rays);
     if (c->slots_out) (void)hipFree(c->slots_out);
+    if (c->splat) (void)hipFree(c->splat);
     free_comms(c);
     if (c->gather) (void)hipFree(c->gather);
     if (c->film_dev) (void)hipFree(c->film_dev);
@@ -1675,10 +1692,17 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
     W.scale = (float)((double)p->nx * p->ny / ((double)steps * (double)n_chains));   // AccumulatePathContribution
     W.s2p = 0.1f;
     W.logp = (float)std::log((double)0.1f / (2.0 / (double)(p->nx + p->ny)));
-    W.U = c->partial; W.film = dev_film; W.counter = c->counter; W.wave_rays = c->wave_rays;
+    const size_t n_film = (size_t)p->nx * p->ny * 3;
+    if (n_film * sizeof(unsigned long long) > c->splat_bytes) {
+        if (c->splat) HIPCHK(c, hipFree(c->splat));
+        c->splat = nullptr;
+        HIPCHK(c, hipMalloc(&c->splat, n_film * sizeof(unsigned long long)));
+        c->splat_bytes = n_film * sizeof(unsigned long long);
+    }
+    W.U = c->partial; W.film = c->splat; W.counter = c->counter; W.wave_rays = c->wave_rays;
     W.trav_min = trav_min(lds_scene);
     W.min_desc = min_desc(lds_scene);
-    HIPCHK(c, hipMemsetAsync(dev_film, 0, (size_t)p->nx * p->ny * 3 * sizeof(float), st));
+    HIPCHK(c, hipMemsetAsync(c->splat, 0, n_film * sizeof(unsigned long long), st));
     HIPCHK(c, hipMemsetAsync(c->counter, 0, 64, st));
     HIPCHK(c, hipEventRecord(c->ev0, st));
     if (n_local > 0 && steps > 0) {
@@ -1687,6 +1711,8 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
         HIPCHK(c, hipLaunchKernel(kchain, dim3(grid), dim3(kBlock), args, lds, st));
     }
     HIPCHK(c, hipEventRecord(c->ev1, st));
+    mlt_film_to_float<<<dim3((unsigned)((n_film + kBlock - 1) / kBlock)), dim3(kBlock), 0, st>>>(c->splat, dev_film, n_film);
+    HIPCHK(c, hipGetLastError());
     std::vector<unsigned long long> wr(n_waves * 4, 0);
     if (n_local > 0 && steps > 0)
         HIPCHK(c, hipMemcpyAsync(wr.data(), c->wave_rays, wr.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));

@@ -88,6 +88,21 @@ def test_sharded_chains_sum_to_single(ctx, cornell_obj):
     assert np.allclose(one, two, rtol=1e-4, atol=1e-5)
 
 
+def test_splat_film_reproducible(ctx, cornell_obj):
+    """Splats land in a fixed-point film with 64-bit integer atomics, so the
+    film does not depend on the order the chains' atomics arrive in: two runs
+    give the same bytes (float atomics did not)."""
+    nx, ny = 96, 64
+    ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, nx / ny))
+    films = []
+    for _ in range(3):
+        f = np.zeros((ny, nx, 3), np.float32)
+        f, st = ctx.render(frt.RenderParams.pssmlt(nx, ny, 16, 4096, seed=9, bootstrap=1000), f)
+        films.append(f)
+    assert np.isfinite(films[0]).all() and films[0].max() > 0
+    assert np.array_equal(films[0], films[1]) and np.array_equal(films[0], films[2])
+
+
 def test_converges_to_path_tracer(ctx, cornell_obj):
     """Same image as the path tracer (depth <= 10) once the chains are long:
     the reference starts chains from uniform states with no burn-in, so short
