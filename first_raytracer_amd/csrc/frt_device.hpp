@@ -441,20 +441,24 @@ FRT_HD float erf_f(float x)
     return sign * y;
 }
 // roughconductor_pdf::sampleVisible11 (pdf.h:280-397)
-FRT_HD void sample_visible11(float theta_i, float sx, float sy, int dist, float &slx, float &sly)
+// theta_i enters as cos / sin (cos_t = ws.z, sin_t = sqrt((1 - z)(1 + z)));
+// normal: the reference's theta_i < 1e-4 test, which in fp32 holds exactly
+// when rough_generate left theta at 0 (ws.z >= 0.99999: acos of anything
+// below that is >= 4.5e-3).  tan(theta_i) = sin / cos, as tan(acos z) is;
+// theta_i itself only for the Beckmann fit, so GGX lanes run no acos.
+FRT_HD void sample_visible11(bool normal, float cos_t, float sin_t, float sx, float sy, int dist, float &slx, float &sly)
 {
     const float kSqrtPiInv = 0.564189583547756287f;
-    if (theta_i < 1e-4f) {                                      // normal incidence
+    if (normal) {                                               // normal incidence
         const float r = (dist == kDistBeckmann) ? fsqrt(-flog(1.0f - sx)) : safe_sqrtf(fdiv(sx, 1.0f - sx));
         float sp, cp;
         sincos_2pi(sy, sp, cp);                                 // phi = 2 pi sy
         slx = r * cp; sly = r * sp;
         return;
     }
-    float st, ct;
-    sincos_2pi(theta_i * (0.5f * kInvPi), st, ct);
-    const float tan_t = fdiv(st, ct);
+    const float tan_t = fdiv(sin_t, cos_t);
     if (dist == kDistBeckmann) {
+        const float theta_i = acosf(cos_t);
         const float cot_t = rcp(tan_t);
         float a = -1.0f, c = erf_f(cot_t);
         const float sample_x = fmaxf(sx, 1e-6f);
@@ -500,15 +504,16 @@ FRT_HD f3 rough_generate(f3 n, f3 wi, float alpha, int dist, float s0, float s1,
     const f3 wl = onb_to_local(uvw, wi);
     f3 ws = f3{alpha * wl.x, alpha * wl.y, wl.z};
     ws = frsqrt(len2(ws)) * ws;
-    // theta = acos(ws.z), phi = atan2(ws.y, ws.x): sin / cos phi as ws.y / r, ws.x / r
-    float theta = 0.0f, sp = 0.0f, cp = 1.0f;
-    if (ws.z < 0.99999f) {
-        theta = acosf(ws.z);
+    // theta = acos(ws.z) (0 at and above 0.99999), phi = atan2(ws.y, ws.x): sin / cos phi as
+    // ws.y / r, ws.x / r; sample_visible11 takes theta as cos / sin
+    const bool normal = !(ws.z < 0.99999f);
+    float sp = 0.0f, cp = 1.0f;
+    if (!normal) {
         const float rr = ws.x * ws.x + ws.y * ws.y;
         if (rr > 0.0f) { const float ir = frsqrt(rr); sp = ws.y * ir; cp = ws.x * ir; }
     }
     float slx, sly;
-    sample_visible11(theta, s0, s1, dist, slx, sly);
+    sample_visible11(normal, ws.z, fsqrt((1.0f - ws.z) * (1.0f + ws.z)), s0, s1, dist, slx, sly);
     if (!(fabsf(slx) <= 3.40282347e+38f)) slx = 0.0f;             // !std::isfinite
     const float rx = (cp * slx - sp * sly) * alpha, ry = (sp * slx + cp * sly) * alpha;
     const float nrm = frsqrt(rx * rx + ry * ry + 1.0f);
