@@ -18,11 +18,12 @@ LIB_PATH = os.environ.get("FRT_LIB_PATH") or os.path.join(HERE, "libfrt.so")
 FRT_WORLD_BVH, FRT_WORLD_LIST = 0, 1
 FRT_MAT_LAMBERTIAN, FRT_MAT_DIFFUSE_LIGHT = 0, 1
 FRT_PRIM_SPHERE = 1 << 30
-ABI_VERSION = 6                 # include/frt.h FRT_ABI_VERSION (frt_stats / frt_material layout)
+ABI_VERSION = 7                 # include/frt.h FRT_ABI_VERSION (frt_stats / frt_material layout)
 FRT_MAT_LAMBERTIAN, FRT_MAT_DIFFUSE_LIGHT, FRT_MAT_MODIFIED_PHONG, FRT_MAT_METAL, FRT_MAT_DIELECTRIC = 0, 1, 2, 3, 4
 FRT_MAT_ROUGH_CONDUCTOR = 5
 FRT_DIST_GGX, FRT_DIST_BECKMANN = 0, 1
-FRT_TEX_CONSTANT, FRT_TEX_CHECKER = 0, 1
+FRT_TEX_CONSTANT, FRT_TEX_CHECKER, FRT_TEX_IMAGE = 0, 1, 2
+FRT_IMAGE_SRGB8, FRT_IMAGE_F32 = 0, 1
 FRT_FLAG_NO_LDS_SCENE = 1
 FRT_FLAG_WAVES5 = 2
 FRT_FLAG_WAVES6 = 4
@@ -49,7 +50,7 @@ class Material(ctypes.Structure):
                 ("albedo", ctypes.c_double * 3), ("emit", ctypes.c_double * 3),
                 ("specular", ctypes.c_double * 3), ("exponent", ctypes.c_double), ("ior", ctypes.c_double),
                 ("alpha", ctypes.c_double), ("eta", ctypes.c_double * 3), ("k", ctypes.c_double * 3),
-                ("texture", ctypes.c_int32), ("reserved", ctypes.c_int32), ("tex_odd", ctypes.c_double * 3),
+                ("texture", ctypes.c_int32), ("image", ctypes.c_int32), ("tex_odd", ctypes.c_double * 3),
                 ("tex_scale", ctypes.c_double * 2)]
 
     @classmethod
@@ -68,7 +69,27 @@ class Material(ctypes.Structure):
             r.texture = FRT_TEX_CHECKER
             r.tex_odd[:] = [float(x) for x in tex["odd"]]
             r.tex_scale[:] = [float(x) for x in tex["scale"]]
+        if m.get("image") is not None:       # index into the spec's "images"
+            r.texture = FRT_TEX_IMAGE
+            r.image = int(m["image"])
         return r
+
+
+class Image(ctypes.Structure):
+    """frt_image: a decoded image for FRT_TEX_IMAGE (image_texture, texture.h:51-95)."""
+    _fields_ = [("nx", ctypes.c_int32), ("ny", ctypes.c_int32), ("format", ctypes.c_int32),
+                ("reserved", ctypes.c_int32), ("data", ctypes.c_void_p)]
+
+
+def image_array(img):
+    """(contiguous texel array, FRT_IMAGE_* format) of a spec image
+    {"data": (ny, nx, 3) uint8 (sRGB, stb's LDR bytes) or float32 (HDR)}."""
+    a = np.asarray(img["data"])
+    if a.ndim != 3 or a.shape[2] != 3:
+        raise ValueError("image data must be (ny, nx, 3)")
+    if a.dtype == np.uint8:
+        return np.ascontiguousarray(a), FRT_IMAGE_SRGB8
+    return np.ascontiguousarray(a, np.float32), FRT_IMAGE_F32
 
 
 # cornell_box_obj's camera (main.cpp:236-242): lookfrom (0, 1, 3.9f), vfov 40, focus 10
@@ -100,6 +121,7 @@ class SceneView(ctypes.Structure):
         ("cam_w", ctypes.c_double * 3),
         ("cam_half_height", ctypes.c_double),
         ("tri_uv", ctypes.c_void_p),
+        ("n_images", ctypes.c_int32), ("images", ctypes.c_void_p),
     ]
 
 
@@ -155,7 +177,7 @@ _lib = None
 EXPORTS = ("frt_get_abi_version", "frt_create", "frt_destroy", "frt_last_error", "frt_upload_scene",
            "frt_shard_slot_count", "frt_shard_slots", "frt_render", "frt_render_multi", "frt_render_device",
            "frt_scene_create", "frt_scene_new", "frt_scene_add_obj", "frt_scene_add_sphere", "frt_scene_set_camera",
-           "frt_scene_set_env", "frt_scene_finish", "frt_scene_build_bvh_gpu",
+           "frt_scene_set_env", "frt_scene_add_image", "frt_scene_finish", "frt_scene_build_bvh_gpu",
            "frt_scene_build_bvh_sah", "frt_scene_build_bvh_gpu_algo",
            "frt_scene_view_get", "frt_scene_info", "frt_scene_destroy", "frt_write_tessellated_obj",
            "frt_write_pfm", "frt_film_accumulate", "frt_tonemap_u8", "frt_write_image", "frt_selftest_path_host",
@@ -205,6 +227,7 @@ def lib():
     L.frt_scene_set_camera.argtypes = [vp, dp, dp, dp, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                        ctypes.c_double]
     L.frt_scene_set_env.argtypes = [vp, dp]
+    L.frt_scene_add_image.argtypes = [vp, ctypes.POINTER(Image), ctypes.POINTER(ctypes.c_int)]
     L.frt_scene_finish.argtypes = [vp, ctypes.c_int]
     L.frt_scene_build_bvh_gpu.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_double)]
     L.frt_scene_build_bvh_sah.argtypes = [vp]
@@ -255,11 +278,13 @@ class HostScene:
                        {"sphere": (x, y, z), "radius": r, "material": material,
                         "where": "world" | "lights" | "both"}, ...],
            "camera": {"lookfrom", "lookat", "vup", "vfov", "aperture", "focus"},
-           "world": "bvh" | "list", "env": (r, g, b) | None}
+           "world": "bvh" | "list", "env": (r, g, b) | None,
+           "images": [{"data": (ny, nx, 3) uint8 sRGB | float32}, ...]}
         material: {"type": "lambertian" | "diffuse_light" | "modified_phong" |
                    "metal" | "dielectric" | "rough_conductor", "albedo", "emit",
                    "specular", "exponent", "ior", "alpha", "distribution":
-                   "ggx" | "beckmann", "eta", "k"}.
+                   "ggx" | "beckmann", "eta", "k", "checker": {"odd", "scale"},
+                   "image": index into "images"}.
         oracle.OracleScene.from_spec builds the same scene in the oracle."""
         self = cls.__new__(cls)
         self.ptr = ctypes.c_void_p()
@@ -270,6 +295,11 @@ class HostScene:
         def dptr(x):
             a = np.ascontiguousarray(np.asarray(x, np.float64))
             return a, a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+        for img in spec.get("images", ()):   # materials refer to them by index ({"image": i})
+            a, fmt = image_array(img)
+            desc = Image(a.shape[1], a.shape[0], fmt, 0, a.ctypes.data)
+            idx = ctypes.c_int(-1)
+            _check(L.frt_scene_add_image(self.ptr, ctypes.byref(desc), ctypes.byref(idx)), "frt_scene_add_image")
         for o in spec["objects"]:
             if "obj" in o:
                 tw = dptr(o["to_world"]) if o.get("to_world") is not None else (None, None)

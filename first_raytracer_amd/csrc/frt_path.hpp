@@ -94,6 +94,7 @@ struct DevScene {
     const int *sphere_mat;
     const float4 *mats;      // kMatStride x float4 per material (see kMatStride)
     const float4 *tuv;       // 2 x float4 per triangle: (uv0, uv1) | (uv2, -): texture coordinates (textured scenes)
+    const float4 *texels;    // image_texture texels (rgb, -) of every image, in HBM
     const int *lights;       // device prim refs
     const int *list;         // device prim refs (list worlds)
     const uint4 *nodes4;     // 4 x uint4 per 4-wide node (HBM-resident scenes; DESIGN.md "BVH4Q")
@@ -590,18 +591,41 @@ FRT_HD void prim_uv(const DevScene &S, int ref, f3 p, float u, float v, float &t
 // checker_texture::value: the material's textured colour (m0 for lambertian /
 // modified_phong, m1 for dielectric / rough_conductor) becomes tex1 where
 // x * y == 1 (texture.h:37-41)
+FRT_HD int imodulo(int a, int b) { const int r = a % b; return r < 0 ? r + b : r; }   // util.h:125-128
+// image_texture::value (texture.h:59-88): the nearest texel at (u nx, v ny) in
+// stb's row order, indices outside [0, n] wrapped, n clamped to n - 1; the
+// texels hold the reference's linear value (FromSrgb(byte / 255) or the HDR
+// float) per texel, so only the index arithmetic runs here (fp32: a texel edge
+// can round to the neighbour, as the checker's cell edges do)
+FRT_HD f3 image_texel(const DevScene &S, float4 m4, float tu, float tv)
+{
+    const int nx = f2i(m4.x), ny = f2i(m4.y);
+    int i = x86_trunc(tu * (float)nx), j = x86_trunc(tv * (float)ny);
+    if (i < 0 || i > nx) i = imodulo(i, nx);
+    if (j < 0 || j > ny) j = imodulo(j, ny);
+    if (i == nx) i = nx - 1;
+    if (j == ny) j = ny - 1;
+    return xyz(S.texels[f2i(m4.z) + j * nx + i]);
+}
 FRT_HD void apply_texture(const DevScene &S, int mat, int mtype, int ref, f3 p, float u, float v, float4 &m0,
                           float4 &m1)
 {
     const float4 m3 = S.mats[kMatStride * mat + 3];
-    if (f2i(m3.w) != FRT_TEX_CHECKER) return;
+    const int tex = f2i(m3.w);
+    if (tex == FRT_TEX_CONSTANT) return;
     const float4 m4 = S.mats[kMatStride * mat + 4];
     float tu, tv;
     prim_uv(S, ref, p, u, v, tu, tv);
-    const int x = 2 * imodulo2(x86_trunc(tu * m4.x * 2.0f)) - 1, y = 2 * imodulo2(x86_trunc(tv * m4.y * 2.0f)) - 1;
-    if (x * y != 1) return;
-    if (mtype == FRT_MAT_LAMBERTIAN || mtype == FRT_MAT_MODIFIED_PHONG) { m0.x = m3.x; m0.y = m3.y; m0.z = m3.z; }
-    else { m1.x = m3.x; m1.y = m3.y; m1.z = m3.z; }
+    f3 c;
+    if (tex == FRT_TEX_IMAGE) {
+        c = image_texel(S, m4, tu, tv);
+    } else {
+        const int x = 2 * imodulo2(x86_trunc(tu * m4.x * 2.0f)) - 1, y = 2 * imodulo2(x86_trunc(tv * m4.y * 2.0f)) - 1;
+        if (x * y != 1) return;
+        c = xyz(m3);
+    }
+    if (mtype == FRT_MAT_LAMBERTIAN || mtype == FRT_MAT_MODIFIED_PHONG) { m0.x = c.x; m0.y = c.y; m0.z = c.z; }
+    else { m1.x = c.x; m1.y = c.y; m1.z = c.z; }
 }
 
 // ---------------------------------------------------------------------------

@@ -765,6 +765,7 @@ static inline float round_up(double x)
 // host image of the device scene (DESIGN.md "Data layout")
 struct FlatScene {
     std::vector<float4> nodes, tris, tshade, tnorm, spheres, mats, tuv;
+    std::vector<float4> texels;   // image_texture texels (rgb, -), all images back to back
     std::vector<uint4> nodes4;   // 4-wide quantized BVH
     std::vector<float4> nodes_oct;   // 8 octant copies of `nodes` (DevScene::nodes_oct)
     bool has4 = false;           // nodes4 / root4 usable
@@ -977,11 +978,19 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
             t != FRT_MAT_METAL && t != FRT_MAT_DIELECTRIC && t != FRT_MAT_ROUGH_CONDUCTOR)
             return fail(FRT_E_UNSUPPORTED, "material type " + std::to_string(t) + " is not supported");
         const int tex = sv->materials[i].texture;
-        if (tex != FRT_TEX_CONSTANT && tex != FRT_TEX_CHECKER)
-            return fail(FRT_E_INVALID, "material texture must be FRT_TEX_CONSTANT or FRT_TEX_CHECKER");
-        if (tex == FRT_TEX_CHECKER && (t == FRT_MAT_DIFFUSE_LIGHT || t == FRT_MAT_METAL))
-            return fail(FRT_E_UNSUPPORTED, "checker textures apply to lambertian / modified_phong / dielectric / "
+        if (tex != FRT_TEX_CONSTANT && tex != FRT_TEX_CHECKER && tex != FRT_TEX_IMAGE)
+            return fail(FRT_E_INVALID, "material texture must be FRT_TEX_CONSTANT, FRT_TEX_CHECKER or FRT_TEX_IMAGE");
+        if (tex != FRT_TEX_CONSTANT && (t == FRT_MAT_DIFFUSE_LIGHT || t == FRT_MAT_METAL))
+            return fail(FRT_E_UNSUPPORTED, "checker / image textures apply to lambertian / modified_phong / dielectric / "
                                            "rough_conductor colours");
+        if (tex == FRT_TEX_IMAGE) {
+            const int k = sv->materials[i].image;
+            if (k < 0 || k >= sv->n_images || !sv->images)
+                return fail(FRT_E_INVALID, "material image index out of range");
+            const frt_image &im = sv->images[k];
+            if (im.nx <= 0 || im.ny <= 0 || !im.data || (im.format != FRT_IMAGE_SRGB8 && im.format != FRT_IMAGE_F32))
+                return fail(FRT_E_INVALID, "scene view: bad image");
+        }
         if (t == FRT_MAT_ROUGH_CONDUCTOR &&
             (!(sv->materials[i].alpha > 0.0) || (sv->materials[i].distribution != FRT_DIST_GGX &&
                                                   sv->materials[i].distribution != FRT_DIST_BECKMANN)))
@@ -1137,7 +1146,7 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     }
     // texture coordinates, only when a material is textured (in HBM; read at textured hits)
     bool any_tex = false;
-    for (int i = 0; i < nm; ++i) any_tex |= sv->materials[i].texture == FRT_TEX_CHECKER;
+    for (int i = 0; i < nm; ++i) any_tex |= sv->materials[i].texture != FRT_TEX_CONSTANT;
     if (any_tex) {
         F.tuv.assign(2 * (size_t)std::max(nt, 1), make_float4(0.0f, 0.0f, 0.0f, 0.0f));
         if (sv->tri_uv)
@@ -1155,6 +1164,26 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
         F.smat[k] = sv->sphere_material[k];
         if (F.smat[k] < 0 || F.smat[k] >= nm) return fail(FRT_E_INVALID, "scene view: bad sphere material");
     }
+    // image_texture texels: the reference's value per texel (texture.h:76-87: the float of an
+    // HDR image, FromSrgb(byte / 255.0) in double otherwise, util.h:62-66) rounded to fp32
+    std::vector<int> image_off(std::max(sv->n_images, 0), -1);
+    for (int i = 0; i < nm; ++i) {
+        if (sv->materials[i].texture != FRT_TEX_IMAGE) continue;
+        const int k = sv->materials[i].image;
+        if (image_off[k] >= 0) continue;
+        const frt_image &im = sv->images[k];
+        const size_t n = (size_t)im.nx * im.ny;
+        if (F.texels.size() + n > (size_t)INT32_MAX) return fail(FRT_E_UNSUPPORTED, "images larger than 2^31 texels");
+        image_off[k] = (int)F.texels.size();
+        auto srgb = [](double v) { return v <= 0.04045 ? v * (1.0 / 12.92) : std::pow((v + 0.055) * (1.0 / 1.055), 2.4); };
+        for (size_t q = 0; q < n; ++q) {
+            double c[3];
+            for (int ch = 0; ch < 3; ++ch)
+                c[ch] = im.format == FRT_IMAGE_F32 ? (double)static_cast<const float *>(im.data)[3 * q + ch]
+                                                   : srgb(static_cast<const uint8_t *>(im.data)[3 * q + ch] / 255.0);
+            F.texels.push_back(make_float4((float)c[0], (float)c[1], (float)c[2], 0.0f));
+        }
+    }
     F.mats.assign(kMatStride * (size_t)nm, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     for (int i = 0; i < nm; ++i) {
         const frt_material &m = sv->materials[i];
@@ -1169,6 +1198,8 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
         d[2] = f4(m.k, i2f(m.distribution));
         d[3] = f4(m.tex_odd, i2f(m.texture));
         d[4] = make_float4((float)m.tex_scale[0], (float)m.tex_scale[1], 0.0f, 0.0f);
+        if (m.texture == FRT_TEX_IMAGE)   // (nx, ny, first texel)
+            d[4] = make_float4(i2f(sv->images[m.image].nx), i2f(sv->images[m.image].ny), i2f(image_off[m.image]), 0.0f);
     }
     if (sv->n_lights < 0 || (sv->n_lights > 0 && !sv->lights)) return fail(FRT_E_INVALID, "scene view: bad lights");
     F.lights.resize(sv->n_lights);
@@ -1254,7 +1285,7 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
         (rc = upload_vec(c, F.nodes_oct, &S.nodes_oct)) ||
         (rc = upload_vec(c, F.tris, &S.tris)) ||
         (rc = upload_vec(c, F.tshade, &S.tshade)) || (rc = upload_vec(c, F.tnorm, &S.tnorm)) ||
-        (rc = upload_vec(c, F.tuv, &S.tuv)) ||
+        (rc = upload_vec(c, F.tuv, &S.tuv)) || (rc = upload_vec(c, F.texels, &S.texels)) ||
         (rc = upload_vec(c, F.spheres, &S.spheres)) || (rc = upload_vec(c, F.smat, &S.sphere_mat)) ||
         (rc = upload_vec(c, F.mats, &S.mats)) || (rc = upload_vec(c, F.lights, &S.lights)) ||
         (rc = upload_vec(c, F.list, &S.list)))
@@ -1271,7 +1302,7 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
         const int t = sv->materials[i].type;
         if (t == FRT_MAT_MODIFIED_PHONG || t == FRT_MAT_METAL || t == FRT_MAT_DIELECTRIC) c->mats |= kMatsSpec;
         if (t == FRT_MAT_ROUGH_CONDUCTOR) c->mats |= kMatsRough;
-        if (sv->materials[i].texture == FRT_TEX_CHECKER) c->mats |= kMatsTex;
+        if (sv->materials[i].texture != FRT_TEX_CONSTANT) c->mats |= kMatsTex;
         if (t == FRT_MAT_METAL) c->has_metal = true;
     }
     c->has_spec_mats = c->mats != kMatsNone;
@@ -1304,7 +1335,7 @@ extern "C" int frt_selftest_path_host(const frt_scene_view *sv, const frt_render
     DevScene S = F.meta;
     S.nodes = F.nodes.data(); S.nodes4 = F.nodes4.data(); S.nodes_oct = F.nodes_oct.data();
     S.tris = F.tris.data(); S.tshade = F.tshade.data(); S.tnorm = F.tnorm.data();
-    S.tuv = F.tuv.data();
+    S.tuv = F.tuv.data(); S.texels = F.texels.data();
     S.spheres = F.spheres.data(); S.sphere_mat = F.smat.data(); S.mats = F.mats.data();
     S.lights = F.lights.data(); S.list = F.list.data();
     std::vector<int> stack(std::max(F.depth + 1, kSelftestStack));
@@ -1370,7 +1401,7 @@ extern "C" int frt_selftest_mlt_paths_host(const frt_scene_view *sv, int nx, int
     DevScene S = F.meta;
     S.nodes = F.nodes.data(); S.nodes4 = F.nodes4.data(); S.nodes_oct = F.nodes_oct.data();
     S.tris = F.tris.data(); S.tshade = F.tshade.data(); S.tnorm = F.tnorm.data();
-    S.tuv = F.tuv.data();
+    S.tuv = F.tuv.data(); S.texels = F.texels.data();
     S.spheres = F.spheres.data(); S.sphere_mat = F.smat.data(); S.mats = F.mats.data();
     S.lights = F.lights.data(); S.list = F.list.data();
     std::vector<int> stack(std::max(F.depth + 1, 1));

@@ -410,6 +410,8 @@ struct frt_host_scene {
     double cam[7][3] = {};   // origin, llc, horizontal, vertical, u, v, w
     double lens_radius = 0, half_height = 0;
     double env[3] = {0, 0, 0};
+    std::vector<frt_image> images;                    // data points into image_data
+    std::vector<std::vector<uint8_t>> image_data;
     int bvh_depth = 0;
     double load_ms = 0, build_ms = 0;
     bool finished = true;    // false between frt_scene_new and frt_scene_finish
@@ -907,10 +909,14 @@ extern "C" int frt_scene_new(frt_host_scene **out)
     return FRT_OK;
 }
 
-static bool material_ok(const frt_material *m)
+static bool material_ok(const frt_material *m, const frt_host_scene *s = nullptr)
 {
     if (!m) return false;
-    if (m->texture != FRT_TEX_CONSTANT && m->texture != FRT_TEX_CHECKER) return false;
+    if (m->texture == FRT_TEX_IMAGE) {
+        if (m->image < 0 || (s && m->image >= (int)s->images.size())) return false;
+    } else if (m->texture != FRT_TEX_CONSTANT && m->texture != FRT_TEX_CHECKER) {
+        return false;
+    }
     switch (m->type) {
     case FRT_MAT_LAMBERTIAN: case FRT_MAT_DIFFUSE_LIGHT: case FRT_MAT_MODIFIED_PHONG: case FRT_MAT_METAL:
     case FRT_MAT_DIELECTRIC: return true;
@@ -923,7 +929,7 @@ static bool material_ok(const frt_material *m)
 extern "C" int frt_scene_add_obj(frt_host_scene *s, const char *obj_path, const double *to_world16,
                                  const frt_material *bsdf, int use_geometry_normals)
 {
-    if (!s || !obj_path || s->finished || (bsdf && !material_ok(bsdf))) return FRT_E_INVALID;
+    if (!s || !obj_path || s->finished || (bsdf && !material_ok(bsdf, s))) return FRT_E_INVALID;
     const auto t0 = std::chrono::steady_clock::now();
     const int rc = add_obj(*s, obj_path, use_geometry_normals != 0, to_world16, bsdf);
     s->load_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -933,7 +939,7 @@ extern "C" int frt_scene_add_obj(frt_host_scene *s, const char *obj_path, const 
 extern "C" int frt_scene_add_sphere(frt_host_scene *s, const double *center, double radius, const frt_material *m,
                                     int where)
 {
-    if (!s || !center || s->finished || !material_ok(m) || !(where & FRT_SPHERE_BOTH)) return FRT_E_INVALID;
+    if (!s || !center || s->finished || !material_ok(m, s) || !(where & FRT_SPHERE_BOTH)) return FRT_E_INVALID;
     s->mats.push_back(*m);
     const int id = s->add_sphere({center[0], center[1], center[2]}, radius, (int)s->mats.size() - 1);
     if (where & FRT_SPHERE_WORLD) s->world.push_back(FRT_PRIM_SPHERE | id);
@@ -954,6 +960,22 @@ extern "C" int frt_scene_set_env(frt_host_scene *s, const double *rgb)
 {
     if (!s || !rgb) return FRT_E_INVALID;
     for (int k = 0; k < 3; ++k) s->env[k] = rgb[k];
+    return FRT_OK;
+}
+
+// image_texture's image (texture.h:51-95), copied: stb's decoded rows as given
+extern "C" int frt_scene_add_image(frt_host_scene *s, const frt_image *img, int *index)
+{
+    if (!s || !img || !index || s->finished || img->nx <= 0 || img->ny <= 0 || !img->data ||
+        (img->format != FRT_IMAGE_SRGB8 && img->format != FRT_IMAGE_F32))
+        return FRT_E_INVALID;
+    const size_t n = (size_t)img->nx * img->ny * 3 * (img->format == FRT_IMAGE_F32 ? sizeof(float) : 1);
+    const uint8_t *src = static_cast<const uint8_t *>(img->data);
+    s->image_data.emplace_back(src, src + n);
+    frt_image c = *img;
+    c.data = s->image_data.back().data();
+    s->images.push_back(c);
+    *index = (int)s->images.size() - 1;
     return FRT_OK;
 }
 
@@ -1139,6 +1161,8 @@ extern "C" int frt_scene_view_get(const frt_host_scene *s, frt_scene_view *v)
     }
     v->cam_lens_radius = s->lens_radius;
     v->cam_half_height = s->half_height;
+    v->n_images = (int32_t)s->images.size();
+    v->images = s->images.empty() ? nullptr : s->images.data();
     return FRT_OK;
 }
 

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FRT_ABI_VERSION 6
+#define FRT_ABI_VERSION 7
 
 enum {
     FRT_OK = 0,
@@ -81,13 +81,27 @@ typedef struct frt_material {
      * colour field above; FRT_TEX_CHECKER (checker_texture, texture.h:30-49) of two
      * constants -- that field as tex0 and tex_odd as tex1 -- at u_scale, v_scale,
      * looked up at the hit's uv (sphere: get_sphere_uv, hitable.h:15-21; triangle:
-     * interpolated OBJ vt, triangle.h:105-107). */
+     * interpolated OBJ vt, triangle.h:105-107).  FRT_TEX_IMAGE (image_texture,
+     * texture.h:51-95): the scene view's image `image`, nearest texel at (u nx, v ny)
+     * with the reference's wrap / clamp. */
     int32_t texture;
-    int32_t reserved;
+    int32_t image;           /* FRT_TEX_IMAGE: index into frt_scene_view.images      */
     double tex_odd[3];
     double tex_scale[2];
 } frt_material;
-enum { FRT_TEX_CONSTANT = 0, FRT_TEX_CHECKER = 1 };
+enum { FRT_TEX_CONSTANT = 0, FRT_TEX_CHECKER = 1, FRT_TEX_IMAGE = 2 };
+
+/* A decoded image for image_texture (texture.h:51-95; the reference's `image`,
+ * image.h, as stb_image returns it: rows top to bottom, 3 channels).
+ * FRT_IMAGE_SRGB8: nx*ny*3 bytes, the texel is FromSrgb(byte / 255) (util.h:62-66);
+ * FRT_IMAGE_F32: nx*ny*3 floats used as they are (the STBI_HDR branch). */
+enum { FRT_IMAGE_SRGB8 = 0, FRT_IMAGE_F32 = 1 };
+typedef struct frt_image {
+    int32_t nx, ny;
+    int32_t format;          /* FRT_IMAGE_*                                               */
+    int32_t reserved;
+    const void *data;
+} frt_image;
 
 typedef struct frt_scene_view {
     int32_t world_kind;                 /* FRT_WORLD_BVH or FRT_WORLD_LIST              */
@@ -128,6 +142,9 @@ typedef struct frt_scene_view {
     double cam_half_height;
     /* texture coordinates: 6 per tri (uv of v0, v1, v2, the OBJ's vt), or NULL = 0 */
     const double *tri_uv;
+    /* images of FRT_TEX_IMAGE materials (ABI 7) */
+    int32_t n_images;
+    const frt_image *images;
 } frt_scene_view;
 
 typedef struct frt_render_params {
@@ -246,6 +263,8 @@ int frt_scene_set_camera(frt_host_scene *s, const double *lookfrom, const double
                          double vfov, double aspect, double aperture, double focus_dist);
 /* environment_map with a constant texture (material.h:206-232) */
 int frt_scene_set_env(frt_host_scene *s, const double *rgb);
+/* a decoded image (copied) for FRT_TEX_IMAGE materials; *index = its frt_material.image */
+int frt_scene_add_image(frt_host_scene *s, const frt_image *img, int *index);
 /* world_kind FRT_WORLD_BVH (create_bvh) or FRT_WORLD_LIST */
 int frt_scene_finish(frt_host_scene *s, int world_kind);
 /* GPU BVH builders: replace the finished scene's world

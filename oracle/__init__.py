@@ -103,6 +103,8 @@ def lib():
         L.ora_scene_new.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
         L.ora_scene_add_obj.argtypes = [ctypes.c_void_p, ctypes.c_char_p, dp, dp, ctypes.c_int]
         L.ora_scene_add_sphere.argtypes = [ctypes.c_void_p, dp, ctypes.c_double, dp, ctypes.c_int]
+        L.ora_scene_add_image.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                          ctypes.POINTER(ctypes.c_int)]
         L.ora_scene_set_camera.argtypes = [ctypes.c_void_p, dp, dp, dp, ctypes.c_double, ctypes.c_double,
                                            ctypes.c_double, ctypes.c_double]
         L.ora_scene_set_camera.restype = None
@@ -125,7 +127,7 @@ SPHERE_WHERE = {"world": 1, "lights": 2, "both": 3}
 def material_desc(m):
     """The 26-double material description of frt_oracle.h from a scene-spec
     material dict (first_raytracer_amd.scene_spec documents the keys)."""
-    d = np.zeros(26)
+    d = np.zeros(27)
     d[0] = MAT_TYPES[m["type"]]
     d[1:4] = m.get("albedo", (0, 0, 0))
     d[4:7] = m.get("emit", (0, 0, 0))
@@ -140,6 +142,9 @@ def material_desc(m):
         d[20] = 1
         d[21:24] = m["checker"]["odd"]
         d[24:26] = m["checker"]["scale"]
+    if m.get("image") is not None:               # image_texture: index into the spec's "images"
+        d[20] = 2
+        d[26] = m["image"]
     return d
 
 
@@ -168,6 +173,15 @@ class OracleScene:
         L = lib()
         if L.ora_scene_new(ctypes.byref(self.ptr)) != 0:
             raise RuntimeError("ora_scene_new failed")
+        self._images = []
+        for img in spec.get("images", ()):
+            a = np.asarray(img["data"])
+            a = np.ascontiguousarray(a) if a.dtype == np.uint8 else np.ascontiguousarray(a, np.float32)
+            idx = ctypes.c_int(-1)
+            if L.ora_scene_add_image(self.ptr, a.shape[1], a.shape[0], 0 if a.dtype == np.uint8 else 1,
+                                     a.ctypes.data, ctypes.byref(idx)) != 0:
+                raise RuntimeError("ora_scene_add_image failed")
+            self._images.append(a)
         for o in spec["objects"]:
             if "obj" in o:
                 tw = darr(o["to_world"]) if o.get("to_world") is not None else (None, None)

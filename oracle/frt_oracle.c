@@ -212,8 +212,12 @@ enum { DIST_GGX = 0, DIST_BECKMANN = 1 };                                     /*
 typedef struct {
     int type; v3 albedo; v3 emit; double ks[3], ior, shininess; int dist; double alpha; v3 eta, k;
     int tex; v3 tex_odd; double tex_scale[2];   /* checker_texture (texture.h:30-49) of the textured colour */
+    int image;                                   /* image_texture (texture.h:51-95): scene image index */
 } material;
-enum { TEX_CONSTANT = 0, TEX_CHECKER = 1 };
+enum { TEX_CONSTANT = 0, TEX_CHECKER = 1, TEX_IMAGE = 2 };
+/* image_texture's decoded image: nx*ny*3 texel values, linear (FromSrgb(byte / 255)
+ * for 8-bit images, the floats of an HDR image) */
+typedef struct { int nx, ny; double *rgb; } ora_image;
 
 /* ---- specular materials (material.h:75-171, pdf.h:99-184, util.h:73-117) ---- */
 static const double DELTA_EPSILON = 1e-3f;                                   /* util.h:12 */
@@ -656,6 +660,7 @@ struct ora_scene {
     camera cam;
     v3 env;
     int bvh_depth;
+    ora_image *images; int nimages;
 };
 
 typedef struct {
@@ -683,9 +688,28 @@ static inline int checker_odd(double u, double v, double us, double vs)
 }
 /* the hit's material with its texture evaluated: lambertian albedo,
  * modified_phong diffuse_reflectance, dielectric / rough_conductor specular */
+/* image_texture::value (texture.h:59-88): nearest texel, out-of-range indices
+ * wrapped (util.h:125-128 modulo), the upper edge clamped */
+static v3 image_value(const ora_image *img, double u, double v)
+{
+    const int nx = img->nx, ny = img->ny;
+    int i = x86_trunc(u * nx), j = x86_trunc(v * ny);
+    if (i < 0 || i > nx) i = imodulo(i, nx);
+    if (j < 0 || j > ny) j = imodulo(j, ny);
+    if (i == nx) i = nx - 1;
+    if (j == ny) j = ny - 1;
+    return vload(img->rgb + 3 * ((size_t)j * nx + i));
+}
 static const material *mat_at(const ora_scene *s, const hit_record *h, material *tmp)
 {
     const material *m = &s->mats[h->mat];
+    if (m->tex == TEX_IMAGE) {
+        *tmp = *m;
+        const v3 c = image_value(&s->images[m->image], h->tu, h->tv);
+        if (m->type == MAT_LAMBERT || m->type == MAT_PHONG) tmp->albedo = c;
+        else vstore(tmp->ks, c);
+        return tmp;
+    }
     if (m->tex != TEX_CHECKER) return m;
     *tmp = *m;
     if (checker_odd(h->tu, h->tv, m->tex_scale[0], m->tex_scale[1])) {
@@ -1833,6 +1857,7 @@ static material material_from_desc(const double *d)
     m.shininess = d[10]; m.ior = d[11]; m.dist = (int)d[12]; m.alpha = d[13];
     m.eta = vload(d + 14); m.k = vload(d + 17);
     m.tex = (int)d[20]; m.tex_odd = vload(d + 21); m.tex_scale[0] = d[24]; m.tex_scale[1] = d[25];
+    if (m.tex == TEX_IMAGE) m.image = (int)d[26];   /* the description is 27 doubles then */
     return m;
 }
 
@@ -2060,7 +2085,32 @@ int ora_scene_finish(ora_scene *s, int world_kind)
 void ora_free_scene(ora_scene *s)
 {
     if (!s) return;
+    for (int i = 0; i < s->nimages; ++i) free(s->images[i].rgb);
+    free(s->images);
     free(s->tris); free(s->sph); free(s->mats); free(s->nodes); free(s->list); free(s->lights); free(s);
+}
+/* util.h:62-66 */
+static double from_srgb(double v)
+{
+    if (v <= 0.04045) return v * (1.0 / 12.92);
+    return pow((v + 0.055) * (1.0 / 1.055), 2.4);
+}
+/* image_texture's image as stb decodes it (rows as given, 3 channels): format 0 =
+ * 8-bit (texel FromSrgb(x / 255.0), texture.h:82-84), 1 = floats (the HDR branch) */
+int ora_scene_add_image(ora_scene *s, int nx, int ny, int format, const void *data, int *index)
+{
+    if (!s || nx <= 0 || ny <= 0 || !data || (format != 0 && format != 1)) return -1;
+    ora_image *im = (ora_image *)realloc(s->images, (size_t)(s->nimages + 1) * sizeof(ora_image));
+    if (!im) return -1;
+    s->images = im;
+    const size_t n = (size_t)nx * ny * 3;
+    double *rgb = (double *)malloc(n * sizeof(double));
+    if (!rgb) return -1;
+    for (size_t k = 0; k < n; ++k)
+        rgb[k] = format == 0 ? from_srgb(((const uint8_t *)data)[k] / 255.0) : (double)((const float *)data)[k];
+    s->images[s->nimages] = (ora_image){nx, ny, rgb};
+    *index = s->nimages++;
+    return 0;
 }
 /* Scene::env_map with another constant texture (material.h:206-232); the
  * reference scenes' environment is black, so AO / normals tests set one. */

@@ -98,6 +98,9 @@ int  ora_render_integrator(const ora_scene *s, int integrator, int nx, int ny, i
                            const int32_t *pixels, int npix, int nthreads, double *out_rgb, ora_counters *cnt);
 /* constant environment colour (the reference scenes use black) */
 void ora_scene_set_env(ora_scene *s, const double *rgb);
+/* image_texture's decoded image (format 0: nx*ny*3 bytes, sRGB; 1: floats); *index
+ * = its material description entry d[26] (d[20] = 2) */
+int ora_scene_add_image(ora_scene *s, int nx, int ny, int format, const void *data, int *index);
 /* ao.cpp:21 t_max = world bounding box height * 0.5 (NaN for list worlds) */
 double ora_scene_ao_tmax(const ora_scene *s);
 

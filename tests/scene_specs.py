@@ -67,3 +67,32 @@ def cornell_conductors(sphere_dist="ggx", cube_dist="beckmann", world="bvh", met
     objs.append({"obj": CUBE_OBJ, "to_world": to_world(0.15, 30.0, (-0.33, 1.35, -0.29)),     # on the tall box
                  "bsdf": rough(cube_dist, 0.25), "geo": False})
     return {"objects": objs, "camera": CORNELL_CAM, "world": world}
+
+
+def test_image(nx=48, ny=32, seed=5, hdr=False):
+    """A synthetic decoded image (no image assets ship with the reference's
+    configs): smooth gradients plus random texels, (ny, nx, 3) uint8 sRGB as
+    stb_image returns an LDR file, or float32 for the HDR branch."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:ny, 0:nx]
+    base = np.stack([x / max(nx - 1, 1), y / max(ny - 1, 1), 0.5 + 0.5 * np.sin(0.7 * x + 0.3 * y)], -1)
+    img = 0.6 * base + 0.4 * rng.random((ny, nx, 3))
+    if hdr:
+        return (img * 1.5).astype(np.float32)
+    return np.clip(np.round(img * 255.0), 0, 255).astype(np.uint8)
+
+
+def cornell_image_textured(world="bvh"):
+    """image_texture (texture.h:51-95) on the vt-mapped floor quad (lambertian albedo,
+    an 8-bit sRGB image), on a rough conductor sphere's specular reflectance (an
+    HDR float image; sphere uv from get_sphere_uv) and on a modified_phong's
+    diffuse reflectance (the same 8-bit image)."""
+    images = [{"data": test_image(48, 32, 5)}, {"data": test_image(16, 24, 9, hdr=True)}]
+    objs = [{"obj": CORNELL_OBJ, "geo": True},
+            {"obj": QUAD_UV_OBJ, "bsdf": {"type": "lambertian", "albedo": (0.5, 0.5, 0.5), "image": 0}, "geo": True},
+            {"sphere": (-0.6, 0.25, 0.6), "radius": 0.25, "material": dict(rough("ggx", 0.1), image=1)},
+            {"sphere": (0.33, 0.82, 0.37), "radius": 0.22,
+             "material": {"type": "modified_phong", "albedo": (0.5, 0.5, 0.5), "specular": (0.2, 0.2, 0.2),
+                          "exponent": 20.0, "image": 0}}]
+    return {"objects": objs, "camera": CORNELL_CAM, "world": world, "images": images}

@@ -84,3 +84,24 @@ def test_checker_light_rejected(ctx):
             "camera": SS.CORNELL_CAM}
     with pytest.raises(frt.FrtError, match="checker"):
         ctx.upload(frt.HostScene.from_spec(spec, 1.0))
+
+
+@pytest.mark.parametrize("world,flags", [
+    ("bvh", 0),                               # LDS-resident binary BVH (texels in HBM)
+    ("bvh", frt.FRT_FLAG_NO_LDS_SCENE),       # HBM 4-wide BVH
+    ("list", 0)])                             # hitable_list world
+def test_path_image_textures(ctx, world, flags):
+    """image_texture (texture.h:51-95): 8-bit sRGB and HDR images (tests/scene_specs.py
+    cornell_image_textured) against the oracle; a texel edge can round to the neighbour
+    in fp32, as the checker's cell edges can, so the gate is the image RMSE."""
+    spec = SS.cornell_image_textured(world)
+    nx, ny, spp = 96, 72, 32
+    ctx.upload(frt.HostScene.from_spec(spec, nx / ny))
+    film, st = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=11, flags=flags))
+    ref, cnt = oracle.OracleScene.from_spec(spec, nx / ny).render(nx, ny, spp, seed=11)
+    e = rmse(film, ref)
+    print(world, flags, "rmse", e, "rays", st.rays, cnt.rays)
+    assert st.samples == cnt.samples and st.camera_rays == cnt.camera_rays
+    assert abs(st.rays - cnt.rays) / cnt.rays < 2e-3
+    assert np.isfinite(film).all()
+    assert e <= 1e-3

@@ -178,3 +178,50 @@ def test_binned_sah_tree_host(cornell_obj):
     ref, cnt = oracle.OracleScene.from_spec(dict(spec, world="bvh"), 1.0).render(nx, ny, 4, seed=8)
     assert st.camera_rays == cnt.camera_rays
     assert float(np.sqrt(np.mean((g.reshape(-1, 3) - ref) ** 2))) < 1e-3
+
+
+@pytest.mark.parametrize("world", ["bvh", "list"])
+def test_image_textured_scene_host_vs_oracle(world):
+    """image_texture (texture.h:51-95): an 8-bit sRGB image on the vt-mapped floor quad and
+    on a modified_phong sphere, an HDR float image on a rough conductor sphere; the device
+    path code run on the host matches the oracle, and without the images the film differs."""
+    spec = SS.cornell_image_textured(world)
+    hs, osc = both(spec)
+    assert hs.view().n_images == 2
+    nx = ny = 48
+    g, st = frt.selftest_path_host(hs, frt.RenderParams.make(nx, ny, 8, seed=5), np.arange(nx * ny, dtype=np.int32))
+    ref, cnt = osc.render(nx, ny, 8, seed=5)
+    assert st.camera_rays == cnt.camera_rays
+    assert abs(st.rays - cnt.rays) / cnt.rays < 2e-3
+    assert float(np.sqrt(np.mean((g.reshape(-1, 3) - ref) ** 2))) < 1e-3
+    plain = dict(spec, objects=[{k: ({kk: vv for kk, vv in x.items() if kk != "image"} if isinstance(x, dict) else x)
+                                 for k, x in o.items()} for o in spec["objects"]])
+    ref0, _ = oracle.OracleScene.from_spec(plain, 1.0).render(nx, ny, 8, seed=5)
+    assert float(np.sqrt(np.mean((ref0 - ref) ** 2))) > 1e-2
+
+
+def test_image_texture_rejections():
+    """An image index with no image behind it fails in the builder; an image on a light's
+    emission is refused at upload; malformed images fail in frt_scene_add_image."""
+    L = frt.lib()
+    s = ctypes.c_void_p()
+    assert L.frt_scene_new(ctypes.byref(s)) == 0
+    m = frt.Material.from_spec({"type": "lambertian", "albedo": (0.5, 0.5, 0.5), "image": 0})
+    c = (ctypes.c_double * 3)(0, 0, 0)
+    assert L.frt_scene_add_sphere(s, c, ctypes.c_double(1.0), ctypes.byref(m), 1) != 0   # no image 0 yet
+    img = np.zeros((2, 3, 3), np.uint8)
+    idx = ctypes.c_int(-1)
+    assert L.frt_scene_add_image(s, ctypes.byref(frt.Image(3, 2, frt.FRT_IMAGE_SRGB8, 0, img.ctypes.data)),
+                                 ctypes.byref(idx)) == 0 and idx.value == 0
+    assert L.frt_scene_add_sphere(s, c, ctypes.c_double(1.0), ctypes.byref(m), 1) == 0
+    assert L.frt_scene_add_image(s, ctypes.byref(frt.Image(0, 2, frt.FRT_IMAGE_SRGB8, 0, img.ctypes.data)),
+                                 ctypes.byref(idx)) != 0
+    assert L.frt_scene_add_image(s, ctypes.byref(frt.Image(3, 2, 5, 0, img.ctypes.data)), ctypes.byref(idx)) != 0
+    L.frt_scene_destroy(s)
+    light = {"objects": [{"obj": SS.CORNELL_OBJ, "geo": True},
+                         {"sphere": (0, 1, 0), "radius": 0.1, "where": "both",
+                          "material": {"type": "diffuse_light", "emit": (4, 4, 4), "image": 0}}],
+             "camera": SS.CORNELL_CAM, "images": [{"data": SS.test_image(4, 4)}]}
+    hs = frt.HostScene.from_spec(light, 1.0)
+    with pytest.raises(frt.FrtError):
+        frt.selftest_path_host(hs, frt.RenderParams.make(4, 4, 1), np.arange(16, dtype=np.int32))
