@@ -64,8 +64,10 @@ def test_texture_edge_flips(ctx):
     assert rmse(film, ref) <= 1e-3
 
 
-def test_pssmlt_textures(ctx):
-    spec = SS.cornell_textured()
+@pytest.mark.parametrize("make", [SS.cornell_textured, SS.cornell_image_textured])
+def test_pssmlt_textures(ctx, make):
+    """pssmlt::Li with checker and image textures: short chains vs the oracle's."""
+    spec = make()
     nx, ny, mpp, chains = 48, 48, 4, 2304
     ctx.upload(frt.HostScene.from_spec(spec, 1.0))
     film = np.zeros((ny, nx, 3), np.float32)
