@@ -373,7 +373,7 @@ def main():
                          "order); ploc / lbvh: PLOC clustering / the Karras linear BVH on the GPU. List-world "
                          "scenes (veach) ignore it")
     ap.add_argument("--cpu-pixels", type=int, default=0, help="pixels in the CPU-baseline sample (0: calibrated)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline duration when calibrated")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-baseline duration when calibrated")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every CPU this process may use (host_cpus)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--north-star", default="auto", choices=["auto", "on", "off"],
