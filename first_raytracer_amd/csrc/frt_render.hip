@@ -776,14 +776,17 @@ struct FlatScene {
 };
 
 // Shading starts when at most this many lanes of a wave still traverse
-// (0 = every ray of the wave finishes first).  Per plan: measured best ~8-16
-// for LDS-resident scenes (short traversals), ~32 for HBM-resident ones
-// (profiles/r01_ab_perf6.jsonl).  FRT_TRAV_MIN overrides (tuning knob of this
-// library, not part of the C-ABI).
-static int trav_min(bool lds_scene)
+// (0 = every ray of the wave finishes first).  Per plan and integrator, at the
+// bench's 1080p / 512 spp (same call, profiles/r02/r02_ab_trav_min_512spp.txt):
+// path 28 from LDS (Cornell 308.0 -> 301.4 ms; 12 was round 1's 64-spp
+// optimum, profiles/r01_ab_perf6.jsonl) and 40 from HBM (cornell_1m 863.5 ->
+// 857.3 ms); PSS-MLT and AO keep 12 / 32 (28 costs them 4-5 %).
+// FRT_TRAV_MIN overrides (tuning knob of this library, not part of the C-ABI).
+static int trav_min(bool lds_scene, bool path = false)
 {
     const char *e = std::getenv("FRT_TRAV_MIN");
-    const int v = e ? std::atoi(e) : (lds_scene ? kTravMinLds : kTravMinHbm);
+    const int v = e ? std::atoi(e)
+                    : path ? (lds_scene ? kTravMinLdsPath : kTravMinHbmPath) : (lds_scene ? kTravMinLds : kTravMinHbm);
     return std::min(std::max(v, 0), 63);
 }
 
@@ -1831,7 +1834,7 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     W.tile = T; W.ntx = (p->nx + T - 1) / T; W.shard_index = p->shard_index; W.shard_count = p->shard_count;
     W.spi = spi; W.n_chunks = n_chunks; W.n_items = (uint32_t)n_items; W.n_slots = n_slots;
     W.partial = c->partial; W.counter = c->counter; W.wave_rays = c->wave_rays;
-    W.trav_min = trav_min(L.lds_scene);
+    W.trav_min = trav_min(L.lds_scene, p->integrator == FRT_INTEGRATOR_PATH);
     W.min_desc = min_desc(L.lds_scene);
 
     HIPCHK(c, hipMemsetAsync(c->counter, 0, 64, st));
