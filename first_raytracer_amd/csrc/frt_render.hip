@@ -1089,7 +1089,8 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
             F.nodes[4 * i + 3] = make_float4(i2f(cref[0]), i2f(cref[1]), 0.0f, 0.0f);
         }
         if (nt >= kLeafIndexLimit) return fail(FRT_E_INVALID, "scene view: too many triangles");
-        // leaf size by plan (profiles/r01_leaf_ab.txt): 2 triangles when the scene
+        // leaf size by plan (profiles/r01_leaf_ab.txt; re-checked at 512 spp in
+        // profiles/r02/r02z_ab_leaf_512spp.txt): 2 triangles when the scene
         // fits the LDS plan (Cornell +6 % over 4), else 4 (cornell_1m: +11 % over 2)
         const int forced = leaf_size_override();
         if (forced) {
