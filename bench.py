@@ -89,11 +89,12 @@ def load_profile(fname, key):
     return None
 
 
-def cpu_baseline(kind, obj, nx, ny, spp, seed, npix, threads, film, seconds, integrator=0, env=None):
+def cpu_baseline(kind, obj, nx, ny, spp, seed, npix, threads, film, seconds, integrator=0, env=None, min_frac=0.0):
     """The oracle (fp64 C restatement) on a bounded pixel sample of the same
     frame and RNG streams: CPU Mrays/s, reference traversal counters (for
     B_ray) and the RMSE of the GPU film on those pixels.  npix = 0: calibrate
-    on growing samples (from 512 pixels) until one takes about `seconds` of CPU work."""
+    on growing samples (from 512 pixels) until one takes about `seconds` of CPU
+    work and covers at least `min_frac` of the frame's pixels."""
     import oracle
     sc = oracle.OracleScene(kind, obj, nx / ny)
     if env is not None:
@@ -109,11 +110,13 @@ def cpu_baseline(kind, obj, nx, ny, spp, seed, npix, threads, film, seconds, int
         pix, out, cnt, dt = run(npix)
     else:                                   # grow the sample until it takes >= seconds/2
         npix = 512
+        min_pix = int(min_frac * nx * ny)
         while True:
             pix, out, cnt, dt = run(npix)
-            if dt >= 0.5 * seconds or npix >= nx * ny:
+            if (dt >= 0.5 * seconds and npix >= min_pix) or npix >= nx * ny:
                 break
-            npix = int(min(nx * ny, npix * min(16.0, max(2.0, seconds / max(dt, 1e-3)))))
+            npix = int(min(nx * ny, max(npix * min(16.0, max(2.0, seconds / max(dt, 1e-3))),
+                                        min_pix if dt >= 0.5 * seconds else 0)))
     rays = cnt.rays
     gpu = film.reshape(-1, 3)[pix].astype(np.float64)
     rmse = float(np.sqrt(np.mean((gpu - out) ** 2)))
@@ -277,6 +280,7 @@ class Runner:
         integ = {"path": frt.FRT_INTEGRATOR_PATH, "ao": frt.FRT_INTEGRATOR_AO,
                  "normals": frt.FRT_INTEGRATOR_NORMALS}.get(args.integrator, frt.FRT_INTEGRATOR_PSSMLT)
         ctx = self.ctx
+        ctx.set_precision(args.precision)           # read by the upload below (fp64 records) and the renders
         if bvh == "sah":
             hs.build_bvh_sah()                       # binned SAH on the host (in host_build_s)
         if bvh in ("gpu", "ploc", "lbvh"):
@@ -348,6 +352,7 @@ class Runner:
             "scene_bytes": last.scene_bytes,
             "launch": {"waves_cap": int(last.waves_cap), "stack": int(last.stack_entries),
                        "bvh_depth": int(last.bvh_depth)},
+            "fp64": bool(last.fp64),
             "film": film,
         }
 
@@ -379,7 +384,11 @@ def main():
     ap.add_argument("--north-star", default="auto", choices=["auto", "on", "off"],
                     help="auto: with the default config (cornell, path) also run cornell_1m 1080p/512spp")
     ap.add_argument("--ns-steps", type=int, default=3, help="timed frames of the north-star run")
-    ap.add_argument("--ns-pixels", type=int, default=4096, help="oracle pixel sample for the north-star RMSE")
+    ap.add_argument("--ns-pixels", type=int, default=32768, help="oracle pixel sample for the north-star RMSE")
+    ap.add_argument("--rmse-min-frac", type=float, default=0.25,
+                    help="the calibrated CPU sample covers at least this fraction of the frame's pixels")
+    ap.add_argument("--precision", default="auto", choices=["auto", "fp32", "fp64"],
+                    help="frt_set_precision: auto = fp64 for list worlds (veach), fp32 for BVH worlds")
     ap.add_argument("--pfm", default="", help="write the rank-0 film here")
     ap.add_argument("--integrator", default="path", choices=["path", "pssmlt", "ao", "normals"],
                     help="pssmlt: C5 config, --spp = mutations per pixel; ao (ao.cpp), normals (debug_renderer.h)")
@@ -407,7 +416,8 @@ def main():
                 cpu = cpu_baseline_mlt(res["kind"], res["obj"], nx, ny, args.seed, threads, args.cpu_seconds)
             else:
                 cpu = cpu_baseline(res["kind"], res["obj"], nx, ny, args.spp, args.seed, args.cpu_pixels, threads,
-                                    res["film"], args.cpu_seconds, integrator=res["integ"], env=res["env"])
+                                    res["film"], args.cpu_seconds, integrator=res["integ"], env=res["env"],
+                                    min_frac=args.rmse_min_frac)
         ts = load_profile("traversal_stats.json", key)
         V, T = (cpu["V"], cpu["T"]) if cpu is not None else (ts["V"], ts["T"]) if ts is not None else (None, None)
         li_name = {"path": "path::Li", "ao": "ao::Li", "normals": "normals_renderer::Li"}.get(args.integrator)
@@ -422,16 +432,18 @@ def main():
         line = {
             "metric": METRIC, "value": round(res["value"], 1), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(res["elapsed"] / args.steps * 1e3, 2),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "f64" if res["fp64"] else "f32", "data": "synthetic",
             "config": {"workload": workload,
                        "integrator": args.integrator, "scene": args.scene,
                        "nx": nx, "ny": ny, "spp": args.spp, "seed": args.seed, "tile": args.tile,
-                       "env": res["env"],
+                       "env": res["env"], "precision": args.precision,
                        "parallelism": (f"chains-interleaved x{world} + rccl all-reduce" if args.integrator == "pssmlt"
                                        else f"tiles-interleaved x{world} + rccl gather to rank 0")},
             "rmse": None if cpu is None else cpu["rmse"],
             "rmse_detail": None if cpu is None or "diverged_pixels" not in cpu else {
-                "pixels": cpu["npix"], "diverged_pixels": cpu["diverged_pixels"],
+                "pixels": cpu["npix"], "pixel_frac": round(cpu["npix"] / (nx * ny), 4),
+                "diverged_pixels": cpu["diverged_pixels"],
                 "rmse_converged": cpu["rmse_converged"], "diverged_threshold": 1e-3},
             "mutations_per_step": int(res["samples_per_launch"]) if args.integrator == "pssmlt" else None,
             "rays_per_step": int(res["rays"] // args.steps),

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("FRT_LIB_PATH") or os.path.join(HERE, "libfrt.so")
 FRT_WORLD_BVH, FRT_WORLD_LIST = 0, 1
 FRT_MAT_LAMBERTIAN, FRT_MAT_DIFFUSE_LIGHT = 0, 1
 FRT_PRIM_SPHERE = 1 << 30
-ABI_VERSION = 7                 # include/frt.h FRT_ABI_VERSION (frt_stats / frt_material layout)
+ABI_VERSION = 8                 # include/frt.h FRT_ABI_VERSION (frt_stats / frt_material layout)
 FRT_MAT_LAMBERTIAN, FRT_MAT_DIFFUSE_LIGHT, FRT_MAT_MODIFIED_PHONG, FRT_MAT_METAL, FRT_MAT_DIELECTRIC = 0, 1, 2, 3, 4
 FRT_MAT_ROUGH_CONDUCTOR = 5
 FRT_DIST_GGX, FRT_DIST_BECKMANN = 0, 1
@@ -33,6 +33,9 @@ FRT_FLAG_BVH4 = 32
 FRT_FLAG_BRUTE = 64
 FRT_FLAG_SPEC = 128
 FRT_FLAG_NO_OCT = 256
+FRT_FLAG_FP64 = 512
+FRT_FLAG_FP32 = 1024
+FRT_PRECISION_AUTO, FRT_PRECISION_FP32, FRT_PRECISION_FP64 = 0, 1, 2
 FRT_GPU_BVH_PLOC = 0
 FRT_GPU_BVH_LBVH = 1
 FRT_GPU_BVH_SAH = 2
@@ -153,7 +156,7 @@ class Stats(ctypes.Structure):
                                                "pixels", "work_items")] + [
         ("kernel_ms", ctypes.c_double), ("total_ms", ctypes.c_double)] + [
         (n, ctypes.c_uint32) for n in ("scene_in_lds", "waves_cap", "stack_entries", "bvh_depth")] + [
-        ("scene_bytes", ctypes.c_uint64)]
+        ("scene_bytes", ctypes.c_uint64), ("fp64", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
     @property
     def rays(self):
@@ -174,7 +177,7 @@ class HostSceneInfo(ctypes.Structure):
 _lib = None
 
 # every symbol include/frt.h declares
-EXPORTS = ("frt_get_abi_version", "frt_create", "frt_destroy", "frt_last_error", "frt_upload_scene",
+EXPORTS = ("frt_get_abi_version", "frt_create", "frt_destroy", "frt_last_error", "frt_set_precision", "frt_upload_scene",
            "frt_shard_slot_count", "frt_shard_slots", "frt_render", "frt_render_multi", "frt_render_device",
            "frt_scene_create", "frt_scene_new", "frt_scene_add_obj", "frt_scene_add_sphere", "frt_scene_set_camera",
            "frt_scene_set_env", "frt_scene_add_image", "frt_scene_finish", "frt_scene_build_bvh_gpu",
@@ -207,6 +210,7 @@ def lib():
     L.frt_destroy.argtypes = [vp]
     L.frt_last_error.argtypes = [vp]
     L.frt_last_error.restype = ctypes.c_char_p
+    L.frt_set_precision.argtypes = [vp, ctypes.c_int]
     L.frt_upload_scene.argtypes = [vp, ctypes.POINTER(SceneView)]
     L.frt_shard_slot_count.argtypes = [ctypes.POINTER(RenderParams)]
     L.frt_shard_slot_count.restype = ctypes.c_int64
@@ -380,9 +384,17 @@ class HostScene:
 class Context:
     """One GPU (frt_ctx).  Raises FrtError when no gfx950 device is present."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, precision=None):
         self.ptr = ctypes.c_void_p()
         _check(lib().frt_create(int(device), ctypes.byref(self.ptr)), f"frt_create(device={device})")
+        if precision is not None:
+            self.set_precision(precision)
+
+    def set_precision(self, precision):
+        """FRT_PRECISION_AUTO / _FP32 / _FP64 (or "auto" / "fp32" / "fp64"); before upload()."""
+        if isinstance(precision, str):
+            precision = {"auto": FRT_PRECISION_AUTO, "fp32": FRT_PRECISION_FP32, "fp64": FRT_PRECISION_FP64}[precision]
+        _check(lib().frt_set_precision(self.ptr, int(precision)), "frt_set_precision", self.ptr)
 
     def upload(self, scene):
         view = scene.view() if isinstance(scene, HostScene) else scene

@@ -1,8 +1,11 @@
-// frt_device.hpp -- fp32 device math shared by the path megakernel.
-// All functions are __host__ __device__ so the same code can be compiled for
-// the host-side self tests (frt_selftest_* in frt_render.hip).
+// frt_device.hpp -- device math shared by the path megakernel, templated on
+// the scalar type R: float for the product kernels, double for the fp64
+// kernels ("fp32 on the GPU, with an fp64 compile option for
+// debugging parity"; DESIGN.md "Precision").  All functions are
+// __host__ __device__ so the same code also runs in the host self tests
+// (frt_selftest_* in frt_render.hip).
 //
-// Reference semantics restated (fp64 there, fp32 here), first_ray/:
+// Reference semantics restated (fp64 there), first_ray/:
 //   aabb::hit           aabb.h:14-31       (slab test, NaN-tolerant)
 //   triangle::hit       triangle.h:69-118  (Moller-Trumbore)
 //   sphere::hit         sphere.h:26-56
@@ -12,6 +15,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
 
 #define FRT_HD __host__ __device__ __forceinline__
 
@@ -23,18 +28,61 @@ constexpr float kPi = 3.14159265358979323846f;
 constexpr float kInvPi = 0.318309886183790671538f;
 constexpr float kTMaxClosest = 3.40282347e+38f;   // FLT_MAX (path.cpp:10)
 
-struct f3 { float x, y, z; };
+// Per-precision constants.  The double set keeps the reference's values:
+// EPSILON is the double 1e-4 (util.h:10) while SHADOW_EPSILON and
+// DELTA_EPSILON are float literals widened to double (util.h:11-12).
+template <typename R> struct Cst;
+template <> struct Cst<float> {
+    static constexpr float eps = kEps, shadow_eps = kShadowEps, delta_eps = 1e-3f;
+    static constexpr float pi = kPi, inv_pi = kInvPi, tmax = kTMaxClosest;
+};
+template <> struct Cst<double> {
+    static constexpr double eps = 1e-4, shadow_eps = (double)1e-3f, delta_eps = (double)1e-3f;
+    static constexpr double pi = 3.14159265358979323846, inv_pi = 0.318309886183790671538;
+    static constexpr double tmax = (double)kTMaxClosest;
+};
+template <typename R> constexpr bool kIsF64 = std::is_same<R, double>::value;
+
+template <typename R> struct V3 { R x, y, z; };
+using f3 = V3<float>;
+using d3 = V3<double>;
 FRT_HD f3 mk3(float x, float y, float z) { return f3{x, y, z}; }
-FRT_HD f3 operator+(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
-FRT_HD f3 operator-(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
-FRT_HD f3 operator*(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
-FRT_HD f3 operator*(float t, f3 v) { return f3{t * v.x, t * v.y, t * v.z}; }
-FRT_HD f3 operator-(f3 v) { return f3{-v.x, -v.y, -v.z}; }
-FRT_HD float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-FRT_HD f3 cross(f3 a, f3 b) { return f3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
-FRT_HD float len2(f3 v) { return dot(v, v); }
-FRT_HD bool nonzero(f3 v) { return v.x != 0.0f || v.y != 0.0f || v.z != 0.0f; }
+template <typename R> FRT_HD V3<R> zero3() { return V3<R>{R(0), R(0), R(0)}; }
+template <typename R> FRT_HD V3<R> operator+(V3<R> a, V3<R> b) { return V3<R>{a.x + b.x, a.y + b.y, a.z + b.z}; }
+template <typename R> FRT_HD V3<R> operator-(V3<R> a, V3<R> b) { return V3<R>{a.x - b.x, a.y - b.y, a.z - b.z}; }
+template <typename R> FRT_HD V3<R> operator*(V3<R> a, V3<R> b) { return V3<R>{a.x * b.x, a.y * b.y, a.z * b.z}; }
+template <typename R> FRT_HD V3<R> operator*(R t, V3<R> v) { return V3<R>{t * v.x, t * v.y, t * v.z}; }
+template <typename R> FRT_HD V3<R> operator-(V3<R> v) { return V3<R>{-v.x, -v.y, -v.z}; }
+template <typename R> FRT_HD R dot(V3<R> a, V3<R> b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+template <typename R> FRT_HD V3<R> cross(V3<R> a, V3<R> b)
+{
+    return V3<R>{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+template <typename R> FRT_HD R len2(V3<R> v) { return dot(v, v); }
+template <typename R> FRT_HD bool nonzero(V3<R> v) { return v.x != R(0) || v.y != R(0) || v.z != R(0); }
 FRT_HD f3 xyz(float4 v) { return f3{v.x, v.y, v.z}; }
+FRT_HD d3 xyz(double4 v) { return d3{v.x, v.y, v.z}; }
+// an fp32 record (material colour, padded box) in the kernel's precision
+template <typename R> FRT_HD V3<R> rgb(float4 v) { return V3<R>{R(v.x), R(v.y), R(v.z)}; }
+
+// min / max / abs / fma / copysign of either precision (the float forms are
+// the fminf / fmaxf ... the fp32 kernels have always used)
+FRT_HD float vmin(float a, float b) { return fminf(a, b); }
+FRT_HD double vmin(double a, double b) { return fmin(a, b); }
+FRT_HD float vmax(float a, float b) { return fmaxf(a, b); }
+FRT_HD double vmax(double a, double b) { return fmax(a, b); }
+FRT_HD float vabs(float a) { return fabsf(a); }
+FRT_HD double vabs(double a) { return fabs(a); }
+FRT_HD float vfma(float a, float b, float c) { return fmaf(a, b, c); }
+FRT_HD double vfma(double a, double b, double c) { return fma(a, b, c); }
+FRT_HD float vcopysign(float a, float b) { return copysignf(a, b); }
+FRT_HD double vcopysign(double a, double b) { return copysign(a, b); }
+FRT_HD float vacos(float a) { return acosf(a); }
+FRT_HD double vacos(double a) { return acos(a); }
+FRT_HD float vcos(float a) { return cosf(a); }
+FRT_HD double vcos(double a) { return cos(a); }
+FRT_HD float vsin(float a) { return sinf(a); }
+FRT_HD double vsin(double a) { return sin(a); }
 
 // ---------------------------------------------------------------------------
 // RNG stream spec (identical to oracle/frt_oracle.c rng_make/rng_u)
@@ -59,6 +107,7 @@ FRT_HD float rng_u(RngKey k, uint32_t dim)
     const uint32_t h = mix32(mix32(k.k0 ^ (dim * 0x85EBCA77U + 0xC2B2AE3DU)) + k.k1);
     return (float)(h >> 8) * (1.0f / 16777216.0f);
 }
+template <typename R> FRT_HD R rng_r(RngKey k, uint32_t dim) { return R(rng_u(k, dim)); }
 // dimension layout: camera 0..3; bounce d: base 4 + 8d (+3 light pick,
 // +4..5 light sample, +6..7 bsdf direction; +0..2 reserved for get3d)
 FRT_HD uint32_t dim_bounce(int depth) { return 4u + 8u * (uint32_t)depth; }
@@ -66,13 +115,15 @@ FRT_HD uint32_t dim_bounce(int depth) { return 4u + 8u * (uint32_t)depth; }
 // ---------------------------------------------------------------------------
 // geometry
 // ---------------------------------------------------------------------------
-// Hardware transcendental units on the GPU (v_rcp / v_rsq / v_sqrt / v_sin /
-// v_cos / v_exp, ~1 ulp), libm on the host (self-test build).  The IEEE
-// sequences they replace (div_scale/fmas/fixup, denormal-scaled sqrt, sin/cos
-// range reduction) dominated the shading code; the parity gate is RMSE 1e-3
-// against the fp64 oracle, and the device results stay bit-identical across
-// kernel variants (same instructions everywhere).  -DFRT_EXP_IEEE_MATH builds
-// the IEEE versions (6 % slower on Cornell, 11 % on 1M: profiles/r01_exp2.txt).
+// fp32: hardware transcendental units on the GPU (v_rcp / v_rsq / v_sqrt /
+// v_sin / v_cos / v_exp, ~1 ulp), libm on the host (self-test build).  The
+// IEEE sequences they replace (div_scale/fmas/fixup, denormal-scaled sqrt,
+// sin/cos range reduction) dominated the shading code; the parity gate is RMSE
+// 1e-3 against the fp64 oracle, and the device results stay bit-identical
+// across kernel variants (same instructions everywhere).  -DFRT_EXP_IEEE_MATH
+// builds the IEEE versions (6 % slower on Cornell, 11 % on 1M:
+// profiles/r01_exp2.txt).  fp64: the IEEE double operations and OCML
+// (correctly rounded division and sqrt), as the reference's libm.
 FRT_HD float rcp(float x)
 {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(FRT_EXP_IEEE_MATH)
@@ -81,7 +132,9 @@ FRT_HD float rcp(float x)
     return 1.0f / x;
 #endif
 }
+FRT_HD double rcp(double x) { return 1.0 / x; }
 FRT_HD float fdiv(float a, float b) { return a * rcp(b); }
+FRT_HD double fdiv(double a, double b) { return a / b; }
 FRT_HD float fsqrt(float x)
 {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(FRT_EXP_IEEE_MATH)
@@ -90,6 +143,7 @@ FRT_HD float fsqrt(float x)
     return sqrtf(x);
 #endif
 }
+FRT_HD double fsqrt(double x) { return sqrt(x); }
 FRT_HD float frsqrt(float x)
 {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(FRT_EXP_IEEE_MATH)
@@ -98,6 +152,7 @@ FRT_HD float frsqrt(float x)
     return 1.0f / sqrtf(x);
 #endif
 }
+FRT_HD double frsqrt(double x) { return 1.0 / sqrt(x); }
 // sin / cos of 2*pi*r for r in [0, 1) (v_sin_f32 / v_cos_f32 take revolutions)
 FRT_HD void sincos_2pi(float r, float &s, float &c)
 {
@@ -108,6 +163,7 @@ FRT_HD void sincos_2pi(float r, float &s, float &c)
     sincosf(2.0f * 3.14159265358979323846f * r, &s, &c);
 #endif
 }
+FRT_HD void sincos_2pi(double r, double &s, double &c) { sincos(2.0 * Cst<double>::pi * r, &s, &c); }
 // e^x for moderate |x| (PSS-MLT perturbation: x in [-8, 0])
 FRT_HD float fexp(float x)
 {
@@ -117,6 +173,7 @@ FRT_HD float fexp(float x)
     return expf(x);
 #endif
 }
+FRT_HD double fexp(double x) { return exp(x); }
 // ln x, x^y (x > 0) on the hardware log2 / exp2 (v_log_f32 / v_exp_f32)
 FRT_HD float flog(float x)
 {
@@ -126,6 +183,7 @@ FRT_HD float flog(float x)
     return logf(x);
 #endif
 }
+FRT_HD double flog(double x) { return log(x); }
 FRT_HD float fpow(float x, float y)
 {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(FRT_EXP_IEEE_MATH)
@@ -134,8 +192,9 @@ FRT_HD float fpow(float x, float y)
     return powf(x, y);
 #endif
 }
-FRT_HD float rlen(f3 v) { return frsqrt(len2(v)); }
-FRT_HD f3 normalize(f3 v) { return rlen(v) * v; }
+FRT_HD double fpow(double x, double y) { return pow(x, y); }
+template <typename R> FRT_HD R rlen(V3<R> v) { return frsqrt(len2(v)); }
+template <typename R> FRT_HD V3<R> normalize(V3<R> v) { return rlen(v) * v; }
 
 // Ray prepared for slab tests: t = lo * invd + oinv with oinv = -o * invd
 // (one FMA per slab plane).  Zero direction components are nudged to
@@ -143,59 +202,61 @@ FRT_HD f3 normalize(f3 v) { return rlen(v) * v; }
 // (aabb.h:24-25) keeps the interval unchanged in that case, and so does this
 // (the near-parallel slab spans +-huge).  Device boxes are padded outward, so
 // neither the nudge nor the FMA rounding can cull a hit.
-struct SlabRay { f3 invd, oinv; };
-FRT_HD SlabRay slab_ray(f3 o, f3 d)
+template <typename R> struct SlabRay { V3<R> invd, oinv; };
+template <typename R> FRT_HD SlabRay<R> slab_ray(V3<R> o, V3<R> d)
 {
-    const float tiny = 1e-30f;
-    const float dx = fabsf(d.x) > tiny ? d.x : copysignf(tiny, d.x);
-    const float dy = fabsf(d.y) > tiny ? d.y : copysignf(tiny, d.y);
-    const float dz = fabsf(d.z) > tiny ? d.z : copysignf(tiny, d.z);
-    SlabRay r;
-    r.invd = f3{rcp(dx), rcp(dy), rcp(dz)};
-    r.oinv = f3{-o.x * r.invd.x, -o.y * r.invd.y, -o.z * r.invd.z};
+    const R tiny = R(1e-30f);
+    const R dx = vabs(d.x) > tiny ? d.x : vcopysign(tiny, d.x);
+    const R dy = vabs(d.y) > tiny ? d.y : vcopysign(tiny, d.y);
+    const R dz = vabs(d.z) > tiny ? d.z : vcopysign(tiny, d.z);
+    SlabRay<R> r;
+    r.invd = V3<R>{rcp(dx), rcp(dy), rcp(dz)};
+    r.oinv = V3<R>{-o.x * r.invd.x, -o.y * r.invd.y, -o.z * r.invd.z};
     return r;
 }
 // slab test of a box against [tmin, tmax]; returns entry distance or +inf on
 // miss (aabb.h:14-31: the reference's per-axis early exit decides the same).
-FRT_HD float slab_entry(float lox, float loy, float loz, float hix, float hiy, float hiz, const SlabRay &r,
-                        float tmin, float tmax)
+// The box planes are the padded fp32 boxes in either precision.
+template <typename R>
+FRT_HD R slab_entry(R lox, R loy, R loz, R hix, R hiy, R hiz, const SlabRay<R> &r, R tmin, R tmax)
 {
-    const float tx0 = fmaf(lox, r.invd.x, r.oinv.x), tx1 = fmaf(hix, r.invd.x, r.oinv.x);
-    const float ty0 = fmaf(loy, r.invd.y, r.oinv.y), ty1 = fmaf(hiy, r.invd.y, r.oinv.y);
-    const float tz0 = fmaf(loz, r.invd.z, r.oinv.z), tz1 = fmaf(hiz, r.invd.z, r.oinv.z);
-    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
-    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
-    return (tf < tn) ? __builtin_inff() : tn;
+    const R tx0 = vfma(lox, r.invd.x, r.oinv.x), tx1 = vfma(hix, r.invd.x, r.oinv.x);
+    const R ty0 = vfma(loy, r.invd.y, r.oinv.y), ty1 = vfma(hiy, r.invd.y, r.oinv.y);
+    const R tz0 = vfma(loz, r.invd.z, r.oinv.z), tz1 = vfma(hiz, r.invd.z, r.oinv.z);
+    const R tn = vmax(vmax(vmin(tx0, tx1), vmin(ty0, ty1)), vmax(vmin(tz0, tz1), tmin));
+    const R tf = vmin(vmin(vmax(tx0, tx1), vmax(ty0, ty1)), vmin(vmax(tz0, tz1), tmax));
+    return (tf < tn) ? R(__builtin_inff()) : tn;
 }
 
 // the same test on a box stored as (near, far) planes for the ray's octant
 // (bvh2_step OCT): bit-identical to slab_entry on the (lo, hi) box
-FRT_HD float slab_entry_nf(float nx, float ny, float nz, float fx, float fy, float fz, const SlabRay &r,
-                           float tmin, float tmax)
+template <typename R>
+FRT_HD R slab_entry_nf(R nx, R ny, R nz, R fx, R fy, R fz, const SlabRay<R> &r, R tmin, R tmax)
 {
-    const float tn = fmaxf(fmaxf(fmaf(nx, r.invd.x, r.oinv.x), fmaf(ny, r.invd.y, r.oinv.y)),
-                           fmaxf(fmaf(nz, r.invd.z, r.oinv.z), tmin));
-    const float tf = fminf(fminf(fmaf(fx, r.invd.x, r.oinv.x), fmaf(fy, r.invd.y, r.oinv.y)),
-                           fminf(fmaf(fz, r.invd.z, r.oinv.z), tmax));
-    return (tf < tn) ? __builtin_inff() : tn;
+    const R tn = vmax(vmax(vfma(nx, r.invd.x, r.oinv.x), vfma(ny, r.invd.y, r.oinv.y)),
+                      vmax(vfma(nz, r.invd.z, r.oinv.z), tmin));
+    const R tf = vmin(vmin(vfma(fx, r.invd.x, r.oinv.x), vfma(fy, r.invd.y, r.oinv.y)),
+                      vmin(vfma(fz, r.invd.z, r.oinv.z), tmax));
+    return (tf < tn) ? R(__builtin_inff()) : tn;
 }
 
 // Moller-Trumbore (triangle.h:69-118): returns t, or -1 on miss.  Accepts
 // t in (tmin, tmax] -- the caller resolves t == tmax with the DFS rank tie rule.
-FRT_HD float tri_intersect(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float tmin, float tmax, float &u, float &v)
+template <typename R>
+FRT_HD R tri_intersect(V3<R> o, V3<R> d, V3<R> v0, V3<R> e1, V3<R> e2, R tmin, R tmax, R &u, R &v)
 {
-    const f3 h = cross(d, e2);
-    const float a = dot(e1, h);
-    if (a == 0.0f) return -1.0f;
-    const float f = rcp(a);
-    const f3 s = o - v0;
+    const V3<R> h = cross(d, e2);
+    const R a = dot(e1, h);
+    if (a == R(0)) return R(-1);
+    const R f = rcp(a);
+    const V3<R> s = o - v0;
     u = f * dot(s, h);
-    if (u < 0.0f || u > 1.0f) return -1.0f;
-    const f3 q = cross(s, e1);
+    if (u < R(0) || u > R(1)) return R(-1);
+    const V3<R> q = cross(s, e1);
     v = f * dot(d, q);
-    if (!(v >= 0.0f && u + v <= 1.0f)) return -1.0f;
-    const float t = f * dot(e2, q);
-    return (t > tmin && t <= tmax) ? t : -1.0f;
+    if (!(v >= R(0) && u + v <= R(1))) return R(-1);
+    const R t = f * dot(e2, q);
+    return (t > tmin && t <= tmax) ? t : R(-1);
 }
 
 // sphere::hit (sphere.h:26-56): returns t or -1; accepts t in [tmin, tmax].
@@ -204,65 +265,65 @@ FRT_HD float tri_intersect(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float tmin, float tm
 // which blurs the silhouette the fp64 reference draws sharply).  It is formed
 // instead as a(r^2 - |oc - (b/a) d|^2) from the ray's perpendicular offset,
 // which keeps the error relative to r^2 (Hearn-Baker form); same roots.
-FRT_HD float sphere_intersect(f3 o, f3 d, f3 c, float r, float tmin, float tmax)
+template <typename R> FRT_HD R sphere_intersect(V3<R> o, V3<R> d, V3<R> c, R r, R tmin, R tmax)
 {
-    const f3 oc = o - c;
-    const float a = dot(d, d);
-    const float b = dot(oc, d);
-    const float ia = rcp(a);
-    const f3 l = oc - (b * ia) * d;
-    float disc = a * (r * r - dot(l, l));
-    if (!(disc >= 0.0f)) return -1.0f;
+    const V3<R> oc = o - c;
+    const R a = dot(d, d);
+    const R b = dot(oc, d);
+    const R ia = rcp(a);
+    const V3<R> l = oc - (b * ia) * d;
+    R disc = a * (r * r - dot(l, l));
+    if (!(disc >= R(0))) return R(-1);
     disc = fsqrt(disc);
-    float t = (-b - disc) * ia;
+    R t = (-b - disc) * ia;
     if (t < tmin) t = (-b + disc) * ia;
-    if (t < tmin || t > tmax) return -1.0f;
+    if (t < tmin || t > tmax) return R(-1);
     return t;
 }
 
 // onb::build_from_w (onb.h:18-30) + fromLocal
-struct Onb { f3 u, v, w; };
-FRT_HD Onb onb_from_w(f3 n)
+template <typename R> struct Onb { V3<R> u, v, w; };
+template <typename R> FRT_HD Onb<R> onb_from_w(V3<R> n)
 {
-    Onb b;
+    Onb<R> b;
     b.w = n;
-    if (fabsf(n.x) > fabsf(n.y)) {
-        const float inv = frsqrt(n.x * n.x + n.z * n.z);
-        b.v = f3{n.z * inv, 0.0f, -n.x * inv};
+    if (vabs(n.x) > vabs(n.y)) {
+        const R inv = frsqrt(n.x * n.x + n.z * n.z);
+        b.v = V3<R>{n.z * inv, R(0), -n.x * inv};
     } else {
-        const float inv = frsqrt(n.y * n.y + n.z * n.z);
-        b.v = f3{0.0f, n.z * inv, -n.y * inv};
+        const R inv = frsqrt(n.y * n.y + n.z * n.z);
+        b.v = V3<R>{R(0), n.z * inv, -n.y * inv};
     }
     b.u = cross(b.v, b.w);
     return b;
 }
-FRT_HD f3 onb_local(const Onb &b, f3 a) { return a.x * b.u + a.y * b.v + a.z * b.w; }
+template <typename R> FRT_HD V3<R> onb_local(const Onb<R> &b, V3<R> a) { return a.x * b.u + a.y * b.v + a.z * b.w; }
 
 // pdf.h:13-23
-FRT_HD f3 cosine_direction(float r0, float r1)
+template <typename R> FRT_HD V3<R> cosine_direction(R r0, R r1)
 {
-    const float r = fsqrt(r0);
-    float sp, cp;
+    const R r = fsqrt(r0);
+    R sp, cp;
     sincos_2pi(r1, sp, cp);                       // phi = 2 pi r1
-    return f3{r * cp, r * sp, fsqrt(1.0f - r0)};
+    return V3<R>{r * cp, r * sp, fsqrt(R(1) - r0)};
 }
 // pdf.h:38-44
-FRT_HD f3 uniform_sphere(float u0, float u1)
+template <typename R> FRT_HD V3<R> uniform_sphere(R u0, R u1)
 {
-    const float z = 1.0f - 2.0f * u0;
-    const float r = fsqrt(fmaxf(0.0f, 1.0f - z * z));
-    float sp, cp;
+    const R z = R(1) - R(2) * u0;
+    const R r = fsqrt(vmax(R(0), R(1) - z * z));
+    R sp, cp;
     sincos_2pi(u1, sp, cp);
-    return f3{r * cp, r * sp, z};
+    return V3<R>{r * cp, r * sp, z};
 }
 // pdf.h:46-56
-FRT_HD f3 random_to_sphere(float radius, float dist2, float r1, float r2)
+template <typename R> FRT_HD V3<R> random_to_sphere(R radius, R dist2, R r1, R r2)
 {
-    const float z = 1.0f + r2 * (fsqrt(1.0f - fdiv(radius * radius, dist2)) - 1.0f);
-    float sp, cp;
+    const R z = R(1) + r2 * (fsqrt(R(1) - fdiv(radius * radius, dist2)) - R(1));
+    R sp, cp;
     sincos_2pi(r1, sp, cp);
-    const float s = fsqrt(1.0f - z * z);
-    return f3{cp * s, sp * s, z};
+    const R s = fsqrt(R(1) - z * z);
+    return V3<R>{cp * s, sp * s, z};
 }
 // x^y for x in [0, 1], y > 0 (phong lobes): exp2(y log2 x) on the hardware units
 FRT_HD float fpow01(float x, float y)
@@ -273,171 +334,172 @@ FRT_HD float fpow01(float x, float y)
     return powf(x, y);
 #endif
 }
+FRT_HD double fpow01(double x, double y) { return pow(x, y); }
 
 // ---- specular materials (material.h:75-171, pdf.h:99-184, util.h:73-117) ----
-constexpr float kDeltaEps = 1e-3f;                               // util.h:12 DELTA_EPSILON
-FRT_HD f3 reflect(f3 v, f3 n) { return normalize(v - (2.0f * dot(v, n)) * n); }   // util.h:73-76
-FRT_HD f3 refract(f3 wi, f3 n, float eta, float cos_t)                            // util.h:79-84
+template <typename R> FRT_HD V3<R> reflect(V3<R> v, V3<R> n) { return normalize(v - (R(2) * dot(v, n)) * n); }   // util.h:73-76
+template <typename R> FRT_HD V3<R> refract(V3<R> wi, V3<R> n, R eta, R cos_t)                                    // util.h:79-84
 {
-    if (cos_t < 0.0f) eta = rcp(eta);
+    if (cos_t < R(0)) eta = rcp(eta);
     return normalize((dot(wi, n) * eta + cos_t) * n - eta * wi);
 }
-FRT_HD float fresnel_dielectric(float cos_i, float &cos_t_out, float eta)       // util.h:86-117
+template <typename R> FRT_HD R fresnel_dielectric(R cos_i, R &cos_t_out, R eta)                                  // util.h:86-117
 {
-    if (eta == 1.0f) { cos_t_out = -cos_i; return 0.0f; }
-    const float scale = (cos_i > 0.0f) ? rcp(eta) : eta;
-    const float cos_t2 = 1.0f - (1.0f - cos_i * cos_i) * (scale * scale);
-    if (cos_t2 <= 0.0f) { cos_t_out = 0.0f; return 1.0f; }      // total internal reflection
-    const float ci = fabsf(cos_i), ct = fsqrt(cos_t2);
-    const float rs = fdiv(ci - eta * ct, ci + eta * ct);
-    const float rp = fdiv(eta * ci - ct, eta * ci + ct);
-    cos_t_out = (cos_i > 0.0f) ? -ct : ct;
-    return 0.5f * (rs * rs + rp * rp);
+    if (eta == R(1)) { cos_t_out = -cos_i; return R(0); }
+    const R scale = (cos_i > R(0)) ? rcp(eta) : eta;
+    const R cos_t2 = R(1) - (R(1) - cos_i * cos_i) * (scale * scale);
+    if (cos_t2 <= R(0)) { cos_t_out = R(0); return R(1); }      // total internal reflection
+    const R ci = vabs(cos_i), ct = fsqrt(cos_t2);
+    const R rs = fdiv(ci - eta * ct, ci + eta * ct);
+    const R rp = fdiv(eta * ci - ct, eta * ci + ct);
+    cos_t_out = (cos_i > R(0)) ? -ct : ct;
+    return R(0.5f) * (rs * rs + rp * rp);
 }
 // cosine_power_pdf (pdf.h:99-136); the onb's w is the shading normal
-FRT_HD float cosine_power_value(f3 n, f3 wi, float e, f3 wo)
+template <typename R> FRT_HD R cosine_power_value(V3<R> n, V3<R> wi, R e, V3<R> wo)
 {
-    if (dot(n, wo) <= 0.0f || dot(n, wi) <= 0.0f) return 0.0f;
-    const float alpha = fmaxf(0.0f, dot(reflect(-wi, n), wo));
-    return fpow01(alpha, e) * (e + 1.0f) * (0.5f * kInvPi);
+    if (dot(n, wo) <= R(0) || dot(n, wi) <= R(0)) return R(0);
+    const R alpha = vmax(R(0), dot(reflect(-wi, n), wo));
+    return fpow01(alpha, e) * (e + R(1)) * (R(0.5f) * Cst<R>::inv_pi);
 }
-FRT_HD f3 cosine_power_generate(f3 n, f3 wi, float e, float s0, float s1)
+template <typename R> FRT_HD V3<R> cosine_power_generate(V3<R> n, V3<R> wi, R e, R s0, R s1)
 {
-    const f3 r = reflect(-wi, n);
-    const float sin_a = fsqrt(1.0f - fpow01(s1, fdiv(2.0f, e + 1.0f)));
-    const float cos_a = fpow01(s1, rcp(e + 1.0f));
-    float sp, cp;
+    const V3<R> r = reflect(-wi, n);
+    const R sin_a = fsqrt(R(1) - fpow01(s1, fdiv(R(2), e + R(1))));
+    const R cos_a = fpow01(s1, rcp(e + R(1)));
+    R sp, cp;
     sincos_2pi(s0, sp, cp);
-    return onb_local(onb_from_w(r), f3{sin_a * cp, sin_a * sp, cos_a});
+    return onb_local(onb_from_w(r), V3<R>{sin_a * cp, sin_a * sp, cos_a});
 }
 // modified_phong::eval_bsdf (material.h:92-100), cosine included
-FRT_HD f3 phong_eval(f3 kd, f3 ks, float e, f3 n, f3 wi, f3 wo)
+template <typename R> FRT_HD V3<R> phong_eval(V3<R> kd, V3<R> ks, R e, V3<R> n, V3<R> wi, V3<R> wo)
 {
-    const float alpha = fmaxf(0.0f, dot(normalize(reflect(-wi, n)), wo));
-    const f3 result = kInvPi * kd + ((e + 2.0f) * (0.5f * kInvPi) * fpow01(alpha, e)) * ks;
+    const R alpha = vmax(R(0), dot(normalize(reflect(-wi, n)), wo));
+    const V3<R> result = Cst<R>::inv_pi * kd + ((e + R(2)) * (R(0.5f) * Cst<R>::inv_pi) * fpow01(alpha, e)) * ks;
     return dot(n, wo) * result;
 }
 // dielectric_pdf (pdf.h:138-184) and dielectric::eval_bsdf (material.h:146-171)
-FRT_HD float dielectric_value(f3 n, f3 wi, float ior, f3 wo)
+template <typename R> FRT_HD R dielectric_value(V3<R> n, V3<R> wi, R ior, V3<R> wo)
 {
-    float cos_t;
-    const float F = fresnel_dielectric(dot(wi, n), cos_t, ior);
-    if (dot(wi, n) * dot(wo, n) >= 0.0f)
-        return (fabsf(dot(reflect(-wi, n), wo) - 1.0f) > kDeltaEps) ? 0.0f : F;
-    return (fabsf(dot(refract(wi, n, ior, cos_t), wo) - 1.0f) > kDeltaEps) ? 0.0f : 1.0f - F;
+    R cos_t;
+    const R F = fresnel_dielectric(dot(wi, n), cos_t, ior);
+    if (dot(wi, n) * dot(wo, n) >= R(0))
+        return (vabs(dot(reflect(-wi, n), wo) - R(1)) > Cst<R>::delta_eps) ? R(0) : F;
+    return (vabs(dot(refract(wi, n, ior, cos_t), wo) - R(1)) > Cst<R>::delta_eps) ? R(0) : R(1) - F;
 }
-FRT_HD f3 dielectric_generate(f3 n, f3 wi, float ior, float s0)
+template <typename R> FRT_HD V3<R> dielectric_generate(V3<R> n, V3<R> wi, R ior, R s0)
 {
-    float cos_t;
-    const float F = fresnel_dielectric(dot(wi, n), cos_t, ior);
+    R cos_t;
+    const R F = fresnel_dielectric(dot(wi, n), cos_t, ior);
     return (s0 <= F) ? reflect(-wi, n) : refract(wi, n, ior, cos_t);
 }
-FRT_HD f3 dielectric_eval(f3 ks, float ior, f3 n, f3 wi, f3 wo)
+template <typename R> FRT_HD V3<R> dielectric_eval(V3<R> ks, R ior, V3<R> n, V3<R> wi, V3<R> wo)
 {
-    float cos_t;
-    const float F = fresnel_dielectric(dot(wi, n), cos_t, ior);
-    if (dot(wi, n) * dot(wo, n) >= 0.0f) {
-        if (fabsf(dot(reflect(-wi, n), wo) - 1.0f) > kDeltaEps) return f3{0.0f, 0.0f, 0.0f};
+    R cos_t;
+    const R F = fresnel_dielectric(dot(wi, n), cos_t, ior);
+    if (dot(wi, n) * dot(wo, n) >= R(0)) {
+        if (vabs(dot(reflect(-wi, n), wo) - R(1)) > Cst<R>::delta_eps) return zero3<R>();
         return F * ks;
     }
-    if (fabsf(dot(refract(wi, n, ior, cos_t), wo) - 1.0f) > kDeltaEps) return f3{0.0f, 0.0f, 0.0f};
-    const float factor = cos_t < 0.0f ? rcp(ior) : ior;
-    return (factor * factor * (1.0f - F)) * ks;
+    if (vabs(dot(refract(wi, n, ior, cos_t), wo) - R(1)) > Cst<R>::delta_eps) return zero3<R>();
+    const R factor = cos_t < R(0) ? rcp(ior) : ior;
+    return (factor * factor * (R(1) - F)) * ks;
 }
 
 // ---- rough_conductor (material.h:246-315), roughconductor_pdf (pdf.h:231-486,
-//      pdf.cpp:5-12), microfacet.h; isotropic alpha.  fp32 restatement of the
-//      oracle's rough_* functions (oracle/frt_oracle.c) on the hardware
-//      transcendentals (rcp, sqrt, rsq, exp2, log2, sin / cos in revolutions)
-//      like the rest of the shading code; only acos stays libm.  The OCML
-//      tan / pow / atan2 / sin / cos and IEEE divisions of round 1 made this the
-//      register-hungriest part of the material kernels. ----
+//      pdf.cpp:5-12), microfacet.h; isotropic alpha.  Restatement of the
+//      oracle's rough_* functions (oracle/frt_oracle.c); in fp32 on the
+//      hardware transcendentals (rcp, sqrt, rsq, exp2, log2, sin / cos in
+//      revolutions) like the rest of the shading code, only acos stays libm.
+//      The OCML tan / pow / atan2 / sin / cos and IEEE divisions of round 1
+//      made this the register-hungriest part of the material kernels.  The
+//      fitted polynomials keep their fp32 coefficients in both precisions. ----
 constexpr int kDistGgx = 0, kDistBeckmann = 1;
-FRT_HD float safe_sqrtf(float v) { const float r = fsqrt(v); return (0.0f < r) ? r : 0.0f; }   // util.h:43-46 (NaN -> 0)
-FRT_HD f3 onb_to_local(const Onb &b, f3 a) { return f3{dot(a, b.u), dot(a, b.v), dot(a, b.w)}; }
+template <typename R> FRT_HD R safe_sqrtf(R v) { const R r = fsqrt(v); return (R(0) < r) ? r : R(0); }   // util.h:43-46 (NaN -> 0)
+template <typename R> FRT_HD V3<R> onb_to_local(const Onb<R> &b, V3<R> a) { return V3<R>{dot(a, b.u), dot(a, b.v), dot(a, b.w)}; }
 // microfacet::fresnelConductorExact (microfacet.h:8-31), one channel
-FRT_HD float fresnel_conductor1(float cos_i, float eta, float k)
+template <typename R> FRT_HD R fresnel_conductor1(R cos_i, R eta, R k)
 {
-    const float c2 = cos_i * cos_i, s2 = 1.0f - c2, s4 = s2 * s2;
-    const float temp1 = eta * eta - k * k - s2;
-    const float a2pb2 = safe_sqrtf(temp1 * temp1 + 4.0f * (k * k * eta * eta));
-    const float a = safe_sqrtf(0.5f * (a2pb2 + temp1));
-    const float term1 = a2pb2 + c2, term2 = (2.0f * cos_i) * a;
-    const float rs2 = fdiv(term1 - term2, term1 + term2);
-    const float term3 = c2 * a2pb2 + s4, term4 = s2 * term2;
-    const float rp2 = rs2 * fdiv(term3 - term4, term3 + term4);
-    return 0.5f * (rp2 + rs2);
+    const R c2 = cos_i * cos_i, s2 = R(1) - c2, s4 = s2 * s2;
+    const R temp1 = eta * eta - k * k - s2;
+    const R a2pb2 = safe_sqrtf(temp1 * temp1 + R(4) * (k * k * eta * eta));
+    const R a = safe_sqrtf(R(0.5f) * (a2pb2 + temp1));
+    const R term1 = a2pb2 + c2, term2 = (R(2) * cos_i) * a;
+    const R rs2 = fdiv(term1 - term2, term1 + term2);
+    const R term3 = c2 * a2pb2 + s4, term4 = s2 * term2;
+    const R rp2 = rs2 * fdiv(term3 - term4, term3 + term4);
+    return R(0.5f) * (rp2 + rs2);
 }
 // microfacet::smithG1 (microfacet.h:48-88)
-FRT_HD float smith_g1(f3 v, f3 m, f3 n, float alpha, int dist)
+template <typename R> FRT_HD R smith_g1(V3<R> v, V3<R> m, V3<R> n, R alpha, int dist)
 {
-    const float cos_t = dot(n, v);
-    if (dot(v, m) * cos_t <= 0.0f) return 0.0f;
-    const float temp = 1.0f - cos_t * cos_t;
-    if (temp <= 0.0f) return 1.0f;
-    const float tan_t = fdiv(fsqrt(temp), cos_t);
+    const R cos_t = dot(n, v);
+    if (dot(v, m) * cos_t <= R(0)) return R(0);
+    const R temp = R(1) - cos_t * cos_t;
+    if (temp <= R(0)) return R(1);
+    const R tan_t = fdiv(fsqrt(temp), cos_t);
     if (dist == kDistBeckmann) {
-        const float a = rcp(alpha * tan_t);
-        if (a >= 1.6f) return 1.0f;
-        const float a2 = a * a;
-        return fdiv(3.535f * a + 2.181f * a2, 1.0f + 2.276f * a + 2.577f * a2);
+        const R a = rcp(alpha * tan_t);
+        if (a >= R(1.6f)) return R(1);
+        const R a2 = a * a;
+        return fdiv(R(3.535f) * a + R(2.181f) * a2, R(1) + R(2.276f) * a + R(2.577f) * a2);
     }
-    const float root = alpha * tan_t;
-    return fdiv(2.0f, 1.0f + fsqrt(1.0f + root * root));          // hypot2(1, root) (util.h:239-254)
+    const R root = alpha * tan_t;
+    return fdiv(R(2), R(1) + fsqrt(R(1) + root * root));          // hypot2(1, root) (util.h:239-254)
 }
 // microfacet::eval (microfacet.h:90-135)
-FRT_HD float microfacet_d(f3 m, f3 n, float alpha, int dist)
+template <typename R> FRT_HD R microfacet_d(V3<R> m, V3<R> n, R alpha, int dist)
 {
-    const f3 ml = onb_to_local(onb_from_w(n), m);
-    const float cos_t = ml.z;
-    if (cos_t <= 0.0f) return 0.0f;
-    const float c2 = cos_t * cos_t, a2 = alpha * alpha;
-    const float be = fdiv(fdiv(ml.x * ml.x, a2) + fdiv(ml.y * ml.y, a2), c2);
-    float r;
+    const V3<R> ml = onb_to_local(onb_from_w(n), m);
+    const R cos_t = ml.z;
+    if (cos_t <= R(0)) return R(0);
+    const R c2 = cos_t * cos_t, a2 = alpha * alpha;
+    const R be = fdiv(fdiv(ml.x * ml.x, a2) + fdiv(ml.y * ml.y, a2), c2);
+    R r;
     if (dist == kDistBeckmann) {
-        r = fdiv(fexp(-be), kPi * a2 * c2 * c2);
+        r = fdiv(fexp(-be), Cst<R>::pi * a2 * c2 * c2);
     } else {
-        const float root = (1.0f + be) * c2;
-        r = rcp(kPi * a2 * root * root);
+        const R root = (R(1) + be) * c2;
+        r = rcp(Cst<R>::pi * a2 * root * root);
     }
-    return (r * cos_t < 1e-20f) ? 0.0f : r;
+    return (r * cos_t < R(1e-20f)) ? R(0) : r;
 }
 // util.h:185-236
-FRT_HD float erfinv_f(float x)
+template <typename R> FRT_HD R erfinv_f(R x)
 {
-    float w = -flog((1.0f - x) * (1.0f + x)), p;
-    if (w < 5.0f) {
-        w = w - 2.5f;
-        p = 2.81022636e-08f;
-        p = 3.43273939e-07f + p * w;
-        p = -3.5233877e-06f + p * w;
-        p = -4.39150654e-06f + p * w;
-        p = 0.00021858087f + p * w;
-        p = -0.00125372503f + p * w;
-        p = -0.00417768164f + p * w;
-        p = 0.246640727f + p * w;
-        p = 1.50140941f + p * w;
+    R w = -flog((R(1) - x) * (R(1) + x)), p;
+    if (w < R(5)) {
+        w = w - R(2.5f);
+        p = R(2.81022636e-08f);
+        p = R(3.43273939e-07f) + p * w;
+        p = R(-3.5233877e-06f) + p * w;
+        p = R(-4.39150654e-06f) + p * w;
+        p = R(0.00021858087f) + p * w;
+        p = R(-0.00125372503f) + p * w;
+        p = R(-0.00417768164f) + p * w;
+        p = R(0.246640727f) + p * w;
+        p = R(1.50140941f) + p * w;
     } else {
-        w = fsqrt(w) - 3.0f;
-        p = -0.000200214257f;
-        p = 0.000100950558f + p * w;
-        p = 0.00134934322f + p * w;
-        p = -0.00367342844f + p * w;
-        p = 0.00573950773f + p * w;
-        p = -0.0076224613f + p * w;
-        p = 0.00943887047f + p * w;
-        p = 1.00167406f + p * w;
-        p = 2.83297682f + p * w;
+        w = fsqrt(w) - R(3);
+        p = R(-0.000200214257f);
+        p = R(0.000100950558f) + p * w;
+        p = R(0.00134934322f) + p * w;
+        p = R(-0.00367342844f) + p * w;
+        p = R(0.00573950773f) + p * w;
+        p = R(-0.0076224613f) + p * w;
+        p = R(0.00943887047f) + p * w;
+        p = R(1.00167406f) + p * w;
+        p = R(2.83297682f) + p * w;
     }
     return p * x;
 }
-FRT_HD float erf_f(float x)
+template <typename R> FRT_HD R erf_f(R x)
 {
-    const float sign = copysignf(1.0f, x);
-    x = fabsf(x);
-    const float t = rcp(1.0f + 0.3275911f * x);
-    const float y = 1.0f - (((((1.061405429f * t - 1.453152027f) * t) + 1.421413741f) * t - 0.284496736f) * t +
-                            0.254829592f) * t * fexp(-x * x);
+    const R sign = vcopysign(R(1), x);
+    x = vabs(x);
+    const R t = rcp(R(1) + R(0.3275911f) * x);
+    const R y = R(1) - (((((R(1.061405429f) * t - R(1.453152027f)) * t) + R(1.421413741f)) * t - R(0.284496736f)) * t +
+                        R(0.254829592f)) * t * fexp(-x * x);
     return sign * y;
 }
 // roughconductor_pdf::sampleVisible11 (pdf.h:280-397)
@@ -446,111 +508,113 @@ FRT_HD float erf_f(float x)
 // when rough_generate left theta at 0 (ws.z >= 0.99999: acos of anything
 // below that is >= 4.5e-3).  tan(theta_i) = sin / cos, as tan(acos z) is;
 // theta_i itself only for the Beckmann fit, so GGX lanes run no acos.
-FRT_HD void sample_visible11(bool normal, float cos_t, float sin_t, float sx, float sy, int dist, float &slx, float &sly)
+template <typename R>
+FRT_HD void sample_visible11(bool normal, R cos_t, R sin_t, R sx, R sy, int dist, R &slx, R &sly)
 {
-    const float kSqrtPiInv = 0.564189583547756287f;
+    const R kSqrtPiInv = R(0.564189583547756287f);
     if (normal) {                                               // normal incidence
-        const float r = (dist == kDistBeckmann) ? fsqrt(-flog(1.0f - sx)) : safe_sqrtf(fdiv(sx, 1.0f - sx));
-        float sp, cp;
+        const R r = (dist == kDistBeckmann) ? fsqrt(-flog(R(1) - sx)) : safe_sqrtf(fdiv(sx, R(1) - sx));
+        R sp, cp;
         sincos_2pi(sy, sp, cp);                                 // phi = 2 pi sy
         slx = r * cp; sly = r * sp;
         return;
     }
-    const float tan_t = fdiv(sin_t, cos_t);
+    const R tan_t = fdiv(sin_t, cos_t);
     if (dist == kDistBeckmann) {
-        const float theta_i = acosf(cos_t);
-        const float cot_t = rcp(tan_t);
-        float a = -1.0f, c = erf_f(cot_t);
-        const float sample_x = fmaxf(sx, 1e-6f);
-        const float fit = 1.0f + theta_i * (-0.876f + theta_i * (0.4265f - 0.0594f * theta_i));
-        float b = c - (1.0f + c) * fpow(1.0f - sample_x, fit);
-        const float norm = rcp(1.0f + c + kSqrtPiInv * tan_t * fexp(-cot_t * cot_t));
+        const R theta_i = vacos(cos_t);
+        const R cot_t = rcp(tan_t);
+        R a = R(-1), c = erf_f(cot_t);
+        const R sample_x = vmax(sx, R(1e-6f));
+        const R fit = R(1) + theta_i * (R(-0.876f) + theta_i * (R(0.4265f) - R(0.0594f) * theta_i));
+        R b = c - (R(1) + c) * fpow(R(1) - sample_x, fit);
+        const R norm = rcp(R(1) + c + kSqrtPiInv * tan_t * fexp(-cot_t * cot_t));
         for (int it = 1; it < 10; ++it) {
-            if (!(b >= a && b <= c)) b = 0.5f * (a + c);
-            const float inv_erf = erfinv_f(b);
-            const float value = norm * (1.0f + b + kSqrtPiInv * tan_t * fexp(-inv_erf * inv_erf)) - sample_x;
-            const float deriv = norm * (1.0f - inv_erf * tan_t);
-            if (fabsf(value) < 1e-5f) break;
-            if (value > 0.0f) c = b; else a = b;
+            if (!(b >= a && b <= c)) b = R(0.5f) * (a + c);
+            const R inv_erf = erfinv_f(b);
+            const R value = norm * (R(1) + b + kSqrtPiInv * tan_t * fexp(-inv_erf * inv_erf)) - sample_x;
+            const R deriv = norm * (R(1) - inv_erf * tan_t);
+            if (vabs(value) < R(1e-5f)) break;
+            if (value > R(0)) c = b; else a = b;
             b -= fdiv(value, deriv);
         }
         slx = erfinv_f(b);
-        sly = erfinv_f(2.0f * fmaxf(sy, 1e-6f) - 1.0f);
+        sly = erfinv_f(R(2) * vmax(sy, R(1e-6f)) - R(1));
         return;
     }
-    const float a = rcp(tan_t);
-    const float g1 = fdiv(2.0f, 1.0f + safe_sqrtf(1.0f + rcp(a * a)));
-    float A = fdiv(2.0f * sx, g1) - 1.0f;
-    if (fabsf(A) == 1.0f) A -= copysignf(1.0f, A) * kEps;
-    const float tmp = rcp(A * A - 1.0f);
-    const float B = tan_t;
-    const float D = safe_sqrtf(B * B * tmp * tmp - (A * A - B * B) * tmp);
-    const float s1 = B * tmp - D, s2 = B * tmp + D;
-    slx = (A < 0.0f || s2 > a) ? s1 : s2;
-    float S;
-    if (sy > 0.5f) { S = 1.0f; sy = 2.0f * (sy - 0.5f); }
-    else { S = -1.0f; sy = 2.0f * (0.5f - sy); }
-    const float z = fdiv(sy * (sy * (sy * -0.365728915865723f + 0.790235037209296f) - 0.424965825137544f) +
-                             0.000152998850436920f,
-                         sy * (sy * (sy * (sy * 0.169507819808272f - 0.397203533833404f) - 0.232500544458471f) + 1.0f) -
-                             0.539825872510702f);
-    sly = S * z * fsqrt(1.0f + slx * slx);
+    const R a = rcp(tan_t);
+    const R g1 = fdiv(R(2), R(1) + safe_sqrtf(R(1) + rcp(a * a)));
+    R A = fdiv(R(2) * sx, g1) - R(1);
+    if (vabs(A) == R(1)) A -= vcopysign(R(1), A) * Cst<R>::eps;
+    const R tmp = rcp(A * A - R(1));
+    const R B = tan_t;
+    const R D = safe_sqrtf(B * B * tmp * tmp - (A * A - B * B) * tmp);
+    const R s1 = B * tmp - D, s2 = B * tmp + D;
+    slx = (A < R(0) || s2 > a) ? s1 : s2;
+    R S;
+    if (sy > R(0.5f)) { S = R(1); sy = R(2) * (sy - R(0.5f)); }
+    else { S = R(-1); sy = R(2) * (R(0.5f) - sy); }
+    const R z = fdiv(sy * (sy * (sy * R(-0.365728915865723f) + R(0.790235037209296f)) - R(0.424965825137544f)) +
+                         R(0.000152998850436920f),
+                     sy * (sy * (sy * (sy * R(0.169507819808272f) - R(0.397203533833404f)) - R(0.232500544458471f)) + R(1)) -
+                         R(0.539825872510702f));
+    sly = S * z * fsqrt(R(1) + slx * slx);
 }
 // roughconductor_pdf::generate (pdf.h:409-482, pdf.cpp:5-12): wo, and the
 // sampled pdf (pdfVisible / (4 wo.m)) that path.cpp:82 prefers when > 0
-FRT_HD f3 rough_generate(f3 n, f3 wi, float alpha, int dist, float s0, float s1, float &sampled_pdf)
+template <typename R> FRT_HD V3<R> rough_generate(V3<R> n, V3<R> wi, R alpha, int dist, R s0, R s1, R &sampled_pdf)
 {
-    const Onb uvw = onb_from_w(n);
-    const f3 wl = onb_to_local(uvw, wi);
-    f3 ws = f3{alpha * wl.x, alpha * wl.y, wl.z};
+    const Onb<R> uvw = onb_from_w(n);
+    const V3<R> wl = onb_to_local(uvw, wi);
+    V3<R> ws = V3<R>{alpha * wl.x, alpha * wl.y, wl.z};
     ws = frsqrt(len2(ws)) * ws;
     // theta = acos(ws.z) (0 at and above 0.99999), phi = atan2(ws.y, ws.x): sin / cos phi as
     // ws.y / r, ws.x / r; sample_visible11 takes theta as cos / sin
-    const bool normal = !(ws.z < 0.99999f);
-    float sp = 0.0f, cp = 1.0f;
+    const bool normal = !(ws.z < R(0.99999f));
+    R sp = R(0), cp = R(1);
     if (!normal) {
-        const float rr = ws.x * ws.x + ws.y * ws.y;
-        if (rr > 0.0f) { const float ir = frsqrt(rr); sp = ws.y * ir; cp = ws.x * ir; }
+        const R rr = ws.x * ws.x + ws.y * ws.y;
+        if (rr > R(0)) { const R ir = frsqrt(rr); sp = ws.y * ir; cp = ws.x * ir; }
     }
-    float slx, sly;
-    sample_visible11(normal, ws.z, fsqrt((1.0f - ws.z) * (1.0f + ws.z)), s0, s1, dist, slx, sly);
-    if (!(fabsf(slx) <= 3.40282347e+38f)) slx = 0.0f;             // !std::isfinite
-    const float rx = (cp * slx - sp * sly) * alpha, ry = (sp * slx + cp * sly) * alpha;
-    const float nrm = frsqrt(rx * rx + ry * ry + 1.0f);
-    const f3 ml = f3{-rx * nrm, -ry * nrm, nrm};
-    const f3 mw = onb_local(uvw, ml);
-    float pdf = 0.0f;
-    if (wl.z != 0.0f)
-        pdf = fdiv(smith_g1(onb_local(uvw, wl), mw, n, alpha, dist) * fabsf(dot(wl, ml)) * microfacet_d(mw, n, alpha, dist),
-                   fabsf(wl.z));
-    const f3 wo = reflect(-wi, mw);
-    sampled_pdf = fdiv(pdf, 4.0f * dot(wo, mw));
+    R slx, sly;
+    sample_visible11(normal, ws.z, fsqrt((R(1) - ws.z) * (R(1) + ws.z)), s0, s1, dist, slx, sly);
+    if (!(vabs(slx) <= R(3.40282347e+38f))) slx = R(0);          // !std::isfinite
+    const R rx = (cp * slx - sp * sly) * alpha, ry = (sp * slx + cp * sly) * alpha;
+    const R nrm = frsqrt(rx * rx + ry * ry + R(1));
+    const V3<R> ml = V3<R>{-rx * nrm, -ry * nrm, nrm};
+    const V3<R> mw = onb_local(uvw, ml);
+    R pdf = R(0);
+    if (wl.z != R(0))
+        pdf = fdiv(smith_g1(onb_local(uvw, wl), mw, n, alpha, dist) * vabs(dot(wl, ml)) * microfacet_d(mw, n, alpha, dist),
+                   vabs(wl.z));
+    const V3<R> wo = reflect(-wi, mw);
+    sampled_pdf = fdiv(pdf, R(4) * dot(wo, mw));
     return wo;
 }
 // roughconductor_pdf::value (pdf.h:237-250)
-FRT_HD float rough_value(f3 n, f3 wi, float alpha, int dist, f3 wo)
+template <typename R> FRT_HD R rough_value(V3<R> n, V3<R> wi, R alpha, int dist, V3<R> wo)
 {
-    if (dot(n, wo) <= 0.0f || dot(n, wi) <= 0.0f) return 0.0f;
-    const f3 H = normalize(wo + wi);
-    return fdiv(microfacet_d(H, n, alpha, dist) * smith_g1(wi, H, n, alpha, dist), 4.0f * dot(wi, n));
+    if (dot(n, wo) <= R(0) || dot(n, wi) <= R(0)) return R(0);
+    const V3<R> H = normalize(wo + wi);
+    return fdiv(microfacet_d(H, n, alpha, dist) * smith_g1(wi, H, n, alpha, dist), R(4) * dot(wi, n));
 }
 // rough_conductor::eval_bsdf (material.h:277-307); no cosine (is_specular)
-FRT_HD f3 rough_eval(f3 eta, f3 k, f3 spec, float alpha, int dist, f3 n, f3 wi, f3 wo)
+template <typename R>
+FRT_HD V3<R> rough_eval(V3<R> eta, V3<R> k, V3<R> spec, R alpha, int dist, V3<R> n, V3<R> wi, V3<R> wo)
 {
-    const float cos_wi = dot(wi, n);
-    if (cos_wi <= 0.0f || dot(wo, n) <= 0.0f) return f3{0.0f, 0.0f, 0.0f};
-    const f3 H = normalize(wo + wi);
-    const float D = microfacet_d(H, n, alpha, dist);
-    if (D == 0.0f) return f3{0.0f, 0.0f, 0.0f};
-    const float c = dot(wi, H);
-    const f3 F = f3{fresnel_conductor1(c, eta.x, k.x), fresnel_conductor1(c, eta.y, k.y),
-                    fresnel_conductor1(c, eta.z, k.z)} * spec;
-    const float G = smith_g1(wi, H, n, alpha, dist) * smith_g1(wo, H, n, alpha, dist);
-    return fdiv(D * G, 4.0f * cos_wi) * F;
+    const R cos_wi = dot(wi, n);
+    if (cos_wi <= R(0) || dot(wo, n) <= R(0)) return zero3<R>();
+    const V3<R> H = normalize(wo + wi);
+    const R D = microfacet_d(H, n, alpha, dist);
+    if (D == R(0)) return zero3<R>();
+    const R c = dot(wi, H);
+    const V3<R> F = V3<R>{fresnel_conductor1(c, eta.x, k.x), fresnel_conductor1(c, eta.y, k.y),
+                          fresnel_conductor1(c, eta.z, k.z)} * spec;
+    const R G = smith_g1(wi, H, n, alpha, dist) * smith_g1(wo, H, n, alpha, dist);
+    return fdiv(D * G, R(4) * cos_wi) * F;
 }
 
 // util.h:55-60
-FRT_HD float mi_weight(float p1, float p2)
+template <typename R> FRT_HD R mi_weight(R p1, R p2)
 {
     p1 *= p1;
     p2 *= p2;

@@ -63,7 +63,7 @@ struct PrndSource {
 };
 
 struct MltPath {
-    PathState P;           // ro, rd, rtmax, shadow, beta, L, nee, nxt_d, depth, prev_spec (prev_p unused)
+    PathState<float> P;    // ro, rd, rtmax, shadow, beta, L, nee, nxt_d, depth, prev_spec (prev_p unused)
     int off;               // PathRndsOffset
     float x, y;            // film position of the eye ray (GenerateEyePath)
 };
@@ -85,7 +85,7 @@ FRT_HD void mlt_begin(MltPath &M, const DevScene &S, const PrndSource &src, int 
         }
         off = (S.lens_r * rx) * S.cam_u + (S.lens_r * ry) * S.cam_vv;
     }
-    PathState &P = M.P;
+    PathState<float> &P = M.P;
     P.ro = S.cam_o + off;
     P.rd = ((S.cam_llc + s * S.cam_h + t * S.cam_v) - S.cam_o) - off;
     P.rtmax = kTMaxClosest;
@@ -111,10 +111,10 @@ FRT_HD bool mlt_beyond(const MltPath &M) { return !M.P.shadow && M.P.depth > kMl
 
 // pssmlt::Li, one hit at a time.  Returns true when the path is finished.
 template <bool MATS = true>   // false: lambertian / diffuse_light scenes (see path_shade)
-FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSource &src, uint32_t &n_ext,
+FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit<float> &h, const PrndSource &src, uint32_t &n_ext,
                       uint32_t &n_sh)
 {
-    PathState &P = M.P;
+    PathState<float> &P = M.P;
     if (P.shadow) {
         if (!path_after_shadow<(MATS ? kMatsAll : kMatsNone)>(P, h.prim < 0)) return true;
         if (P.depth <= kMltMaxPath) ++n_ext;
@@ -160,7 +160,7 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit &h, const PrndSou
     if (!MATS || lamb) {
         const float b0 = src.get(M.off), b1 = src.get(M.off + 1);
         M.off += 2;
-        const Onb uvw = onb_from_w(n);
+        const Onb<float> uvw = onb_from_w(n);
         wo = onb_local(uvw, cosine_direction(b0, b1));
         const float cw = dot(n, normalize(wo));
         pdf = fmaxf(cw, 0.0f) * kInvPi;                 // pdf 0: the vertex returns 0 (pssmlt.cpp:261-264)

@@ -1,6 +1,8 @@
 // frt_path.hpp -- per-path logic of the integrator, __host__ __device__ so the
 // HIP megakernel and the host self-test (frt_selftest_path_host) run the very
-// same code.  Restates, in fp32 (first_ray/ is fp64):
+// same code.  Templated on the scalar type R like frt_device.hpp: float for
+// the product kernels, double for the fp64 kernels (DESIGN.md "Precision").
+// Restates (first_ray/ is fp64):
 //   path::Li                  path.cpp:4-116 (iterative: one ray per step)
 //   parallel_bvh_node::hit    parallel_bvh.h:39-64 (ordered stack traversal)
 //   hitable_list::hit         hitable_list.cpp:4-21
@@ -100,6 +102,13 @@ struct DevScene {
     const uint4 *nodes4;     // 4 x uint4 per 4-wide node (HBM-resident scenes; DESIGN.md "BVH4Q")
     const float4 *nodes_oct; // 8 copies of `nodes`, copy o with each child box as (near xyz, far xyz) for
                              // rays of octant o (bit a set: 1/d_a < 0); LDS plans copy them (kWorldBvh2Oct)
+    // fp64 records of the fp64 kernels (null when the context uploaded none,
+    // frt_set_precision): the same device order as tris / tshade / tnorm /
+    // spheres, in the reference's doubles (edges taken in fp64, triangle.h:58-60)
+    const double4 *tris64;   // 3 per triangle: v0 | e1 | e2
+    const double4 *tshade64; // (n_geo, inv_area) per triangle
+    const double4 *tnorm64;  // 3 per triangle: vertex normals (smooth shading only)
+    const double4 *spheres64;// (centre, radius)
     int root;                // node index, or ~prim for a single-leaf world
     int root4;               // 4-wide root node, or the same leaf ref as root
     int n_lights, n_list, world_kind;
@@ -114,12 +123,14 @@ struct DevScene {
     int ao_spheres_only;     // list world: ao.cpp's t_max is NaN (see ao_shade)
     f3 cam_o, cam_llc, cam_h, cam_v, cam_u, cam_vv, cam_w;
     float lens_r, cam_half_height;
+    d3 cam64_o, cam64_llc, cam64_h, cam64_v, cam64_u, cam64_vv;   // the constructed camera in fp64
+    double lens_r64;
     f3 env;
 };
 
-struct Hit {
+template <typename R> struct Hit {
     int prim;     // device prim ref, -1 = miss
-    float t, u, v;
+    R t, u, v;
 };
 
 // BVH leaf ref ~x: x = FRT_PRIM_SPHERE | k, or first triangle | (count - 1) << kLeafCountShift
@@ -135,21 +146,61 @@ FRT_HD uint4 node4_part(const DevScene &S, int i, int k) { return S.nodes4[i * S
 FRT_HD float4 tri_part(const DevScene &S, int i, int k) { return S.tris[i * S.tri_es + k * S.tri_ps]; }
 FRT_HD float4 shade_part(const DevScene &S, int i, int k) { return S.tshade[i * S.sh_es + k * S.sh_ps]; }
 
-FRT_HD float prim_t(const DevScene &S, int ref, f3 o, f3 d, float tmin, float tmax, float &u, float &v)
+// geometry records in the kernel's precision: the fp32 arrays (LDS or HBM
+// strides) or the fp64 ones
+template <typename R> FRT_HD V3<R> tri_vec(const DevScene &S, int i, int k)   // v0 | e1 | e2
+{
+    if constexpr (kIsF64<R>) return xyz(S.tris64[3 * i + k]);
+    else return xyz(tri_part(S, i, k));
+}
+template <typename R> FRT_HD void sphere_get(const DevScene &S, int k, V3<R> &c, R &r)
+{
+    if constexpr (kIsF64<R>) { const double4 q = S.spheres64[k]; c = xyz(q); r = q.w; }
+    else { const float4 q = S.spheres[k]; c = xyz(q); r = q.w; }
+}
+template <typename R> FRT_HD V3<R> geo_normal(const DevScene &S, int i)
+{
+    if constexpr (kIsF64<R>) return xyz(S.tshade64[i]);
+    else return xyz(shade_part(S, i, 0));
+}
+template <typename R> FRT_HD R inv_area(const DevScene &S, int i)
+{
+    if constexpr (kIsF64<R>) return S.tshade64[i].w;
+    else return shade_part(S, i, 0).w;
+}
+template <typename R> FRT_HD V3<R> vert_normal(const DevScene &S, int i, int k)
+{
+    if constexpr (kIsF64<R>) return xyz(S.tnorm64[3 * i + k]);
+    else return xyz(S.tnorm[3 * i + k]);
+}
+// the constant environment colour (material.h:219-232) in the kernel's precision
+template <typename R> FRT_HD V3<R> env_of(const DevScene &S) { return V3<R>{R(S.env.x), R(S.env.y), R(S.env.z)}; }
+template <typename R> struct CamView { V3<R> o, llc, h, v, u, vv; R lens_r; };
+template <typename R> FRT_HD CamView<R> cam_view(const DevScene &S)
+{
+    if constexpr (kIsF64<R>) return CamView<R>{S.cam64_o, S.cam64_llc, S.cam64_h, S.cam64_v, S.cam64_u, S.cam64_vv, S.lens_r64};
+    else return CamView<R>{S.cam_o, S.cam_llc, S.cam_h, S.cam_v, S.cam_u, S.cam_vv, S.lens_r};
+}
+
+template <typename R>
+FRT_HD R prim_t(const DevScene &S, int ref, V3<R> o, V3<R> d, R tmin, R tmax, R &u, R &v)
 {
     if (ref & FRT_PRIM_SPHERE) {
-        const float4 sp = S.spheres[ref & ~FRT_PRIM_SPHERE];
-        u = v = 0.0f;
-        return sphere_intersect(o, d, xyz(sp), sp.w, tmin, tmax);
+        V3<R> c;
+        R r;
+        sphere_get(S, ref & ~FRT_PRIM_SPHERE, c, r);
+        u = v = R(0);
+        return sphere_intersect(o, d, c, r, tmin, tmax);
     }
-    const float4 a = tri_part(S, ref, 0), b = tri_part(S, ref, 1), c = tri_part(S, ref, 2);
-    return tri_intersect(o, d, xyz(a), xyz(b), xyz(c), tmin, tmax, u, v);
+    const V3<R> a = tri_vec<R>(S, ref, 0), b = tri_vec<R>(S, ref, 1), c = tri_vec<R>(S, ref, 2);
+    return tri_intersect(o, d, a, b, c, tmin, tmax, u, v);
 }
 
 // Leaf ~node: one sphere, or triangles [first, first + count) (collapse_leaves;
 // the reference's leaves hold one prim, parallel_bvh.h:129-149).  Updates the
 // closest hit with the DFS-rank tie rule; true = any-hit query satisfied.
-FRT_HD bool leaf_hit(const DevScene &S, int lref, f3 o, f3 d, float tmin, bool anyhit, Hit &h)
+template <typename R>
+FRT_HD bool leaf_hit(const DevScene &S, int lref, V3<R> o, V3<R> d, R tmin, bool anyhit, Hit<R> &h)
 {
     const bool is_sph = (lref & FRT_PRIM_SPHERE) != 0;
     const int first = is_sph ? lref : (lref & kLeafIndexMask);
@@ -157,9 +208,9 @@ FRT_HD bool leaf_hit(const DevScene &S, int lref, f3 o, f3 d, float tmin, bool a
     for (int k = 0; k < count; ++k) {
         FRT_DIAG_TICK(1);
         const int ref = first + k;
-        float u, v;
-        const float t = prim_t(S, ref, o, d, tmin, h.t, u, v);
-        if (t > 0.0f) {
+        R u, v;
+        const R t = prim_t(S, ref, o, d, tmin, h.t, u, v);
+        if (t > R(0)) {
             const bool better = (t < h.t) || (h.prim >= 0 && (is_sph || ref < h.prim));
             if (better) {
                 h.prim = ref; h.t = t; h.u = u; h.v = v;
@@ -182,25 +233,30 @@ FRT_HD bool leaf_hit(const DevScene &S, int lref, f3 o, f3 d, float tmin, bool a
 // stk[k * STRIDE] (LDS column per lane on the GPU, a plain array on the
 // host); the 4-wide traversal continues in `ovf` (private / scratch) after
 // LSTACK entries.
-struct Trav {
-    SlabRay sr;
-    float tmin;
+template <typename R> struct Trav {
+    SlabRay<R> sr;
+    R tmin;
     int node, sp;
-    Hit h;
+    Hit<R> h;
 };
 
-// Root box with the unscaled EPSILON (parallel_bvh.h:43), then
-// t_min = EPSILON * max(1, |o|_inf) (parallel_bvh.h:46-51).  False: the ray
-// misses the scene (T.h is the miss record).
-FRT_HD bool trav_begin(Trav &T, const DevScene &S, int root, f3 o, f3 d, float tmax)
+// t_min of a BVH query: EPSILON * max(1, |o|_inf) (parallel_bvh.h:46-51)
+template <typename R> FRT_HD R bvh_tmin(V3<R> o)
 {
-    T.h = Hit{-1, tmax, 0.0f, 0.0f};
+    return Cst<R>::eps * vmax(R(1), vmax(vabs(o.x), vmax(vabs(o.y), vabs(o.z))));
+}
+
+// Root box with the unscaled EPSILON (parallel_bvh.h:43), then bvh_tmin.
+// False: the ray misses the scene (T.h is the miss record).
+template <typename R> FRT_HD bool trav_begin(Trav<R> &T, const DevScene &S, int root, V3<R> o, V3<R> d, R tmax)
+{
+    T.h = Hit<R>{-1, tmax, R(0), R(0)};
     T.sp = 0;
     T.node = root;
     T.sr = slab_ray(o, d);
-    T.tmin = kEps * fmaxf(1.0f, fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z))));
-    return slab_entry(S.root_lo[0], S.root_lo[1], S.root_lo[2], S.root_hi[0], S.root_hi[1], S.root_hi[2], T.sr,
-                      kEps, tmax) != __builtin_inff();
+    T.tmin = bvh_tmin(o);
+    return slab_entry<R>(S.root_lo[0], S.root_lo[1], S.root_lo[2], S.root_hi[0], S.root_hi[1], S.root_hi[2], T.sr,
+                         Cst<R>::eps, tmax) != R(__builtin_inff());
 }
 
 // binary nodes: descend to a leaf, test it.  True when the query is finished.
@@ -214,13 +270,13 @@ FRT_HD bool trav_begin(Trav &T, const DevScene &S, int root, f3 o, f3 d, float t
 // box costs 6 FMAs and two 3-way max / min instead of also sorting each
 // slab's two distances (the same values: lo <= hi and 1/d has the octant's
 // sign, so the near plane's distance is the smaller one).
-template <int STRIDE, bool OCT = false>
-FRT_HD bool bvh2_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int min_desc = 0)
+template <int STRIDE, bool OCT = false, typename R>
+FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyhit, int *stk, int min_desc = 0)
 {
     int node = T.node, sp = T.sp;
     DevScene Sn = S;
     if constexpr (OCT) {
-        const int oct = (T.sr.invd.x < 0.0f ? 1 : 0) | (T.sr.invd.y < 0.0f ? 2 : 0) | (T.sr.invd.z < 0.0f ? 4 : 0);
+        const int oct = (T.sr.invd.x < R(0) ? 1 : 0) | (T.sr.invd.y < R(0) ? 2 : 0) | (T.sr.invd.z < R(0) ? 4 : 0);
         Sn.nodes = S.nodes + oct * 4 * S.node_ps;
     }
     // (a branch-free body -- speculative stack-top read, predicated push -- was
@@ -229,16 +285,16 @@ FRT_HD bool bvh2_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *
         FRT_DIAG_TICK(2);
         const float4 n0 = node_part(Sn, node, 0), n1 = node_part(Sn, node, 1);
         const float4 n2 = node_part(Sn, node, 2), n3 = node_part(Sn, node, 3);
-        float t0, t1;
+        R t0, t1;
         if constexpr (OCT) {
-            t0 = slab_entry_nf(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, T.tmin, T.h.t);
-            t1 = slab_entry_nf(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, T.sr, T.tmin, T.h.t);
+            t0 = slab_entry_nf<R>(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, T.tmin, T.h.t);
+            t1 = slab_entry_nf<R>(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, T.sr, T.tmin, T.h.t);
         } else {
-            t0 = slab_entry(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, T.tmin, T.h.t);
-            t1 = slab_entry(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, T.sr, T.tmin, T.h.t);
+            t0 = slab_entry<R>(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, T.tmin, T.h.t);
+            t1 = slab_entry<R>(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, T.sr, T.tmin, T.h.t);
         }
         const int c0 = f2i(n3.x), c1 = f2i(n3.y);
-        const bool h0 = t0 != __builtin_inff(), h1 = t1 != __builtin_inff();
+        const bool h0 = t0 != R(__builtin_inff()), h1 = t1 != R(__builtin_inff());
         if (h0 && h1) {
             const bool first0 = t0 <= t1;
             stk[sp * STRIDE] = first0 ? c1 : c0;
@@ -280,8 +336,9 @@ FRT_HD bool bvh2_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *
 // parks it and keeps descending while other lanes of its wave still search
 // for one; then every lane tests its parked leaf at once.  Visits more nodes
 // with a stale t_best (still conservative), keeps lanes busy.
+// fp32 only: the fp64 kernels traverse the binary tree.
 template <int STRIDE, int LSTACK, bool SPEC = false>
-FRT_HD bool bvh4_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int *ovf, int min_desc = 0)
+FRT_HD bool bvh4_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int *ovf, int min_desc = 0)
 {
     int node = T.node, sp = T.sp;
     int parked = 0;                                     // leaf refs are negative; 0 = none
@@ -309,7 +366,7 @@ FRT_HD bool bvh4_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *
         FRT_DIAG_TICK(0);
         const uint4 w0 = node4_part(S, node, 0), w1 = node4_part(S, node, 1);
         const uint4 w2 = node4_part(S, node, 2), w3 = node4_part(S, node, 3);
-        const SlabRay &sr = T.sr;
+        const SlabRay<float> &sr = T.sr;
         const float ax = u2f((w0.w & 0xffu) << 23) * sr.invd.x, bx = fmaf(u2f(w0.x), sr.invd.x, sr.oinv.x);
         const float ay = u2f(((w0.w >> 8) & 0xffu) << 23) * sr.invd.y, by = fmaf(u2f(w0.y), sr.invd.y, sr.oinv.y);
         const float az = u2f(((w0.w >> 16) & 0xffu) << 23) * sr.invd.z, bz = fmaf(u2f(w0.z), sr.invd.z, sr.oinv.z);
@@ -387,19 +444,19 @@ FRT_HD bool bvh4_step(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *
     return done;
 }
 
-template <int STRIDE>
-FRT_HD Hit trace_bvh(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int *stk)
+template <int STRIDE, typename R>
+FRT_HD Hit<R> trace_bvh(const DevScene &S, V3<R> o, V3<R> d, R tmax, bool anyhit, int *stk)
 {
-    Trav T;
+    Trav<R> T;
     if (trav_begin(T, S, S.root, o, d, tmax))
         while (!bvh2_step<STRIDE>(T, S, o, d, anyhit, stk)) {}
     return T.h;
 }
 
 template <int STRIDE, int LSTACK, int OVF>
-FRT_HD Hit trace_bvh4(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int *stk)
+FRT_HD Hit<float> trace_bvh4(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int *stk)
 {
-    Trav T;
+    Trav<float> T;
     int ovf[OVF];
     if (trav_begin(T, S, S.root4, o, d, tmax))
         while (!bvh4_step<STRIDE, LSTACK>(T, S, o, d, anyhit, stk, ovf)) {}
@@ -407,14 +464,14 @@ FRT_HD Hit trace_bvh4(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, in
 }
 
 // hitable_list::hit: in list order, triangles strict '<', spheres inclusive (sphere.h:34)
-FRT_HD Hit trace_list(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit)
+template <typename R> FRT_HD Hit<R> trace_list(const DevScene &S, V3<R> o, V3<R> d, R tmax, bool anyhit)
 {
-    Hit h{-1, tmax, 0.0f, 0.0f};
+    Hit<R> h{-1, tmax, R(0), R(0)};
     for (int i = 0; i < S.n_list; ++i) {
         const int ref = S.list[i];
-        float u, v;
-        const float t = prim_t(S, ref, o, d, kEps, h.t, u, v);
-        if (t > 0.0f && ((ref & FRT_PRIM_SPHERE) || t < h.t)) {
+        R u, v;
+        const R t = prim_t(S, ref, o, d, Cst<R>::eps, h.t, u, v);
+        if (t > R(0) && ((ref & FRT_PRIM_SPHERE) || t < h.t)) {
             h.prim = ref; h.t = t; h.u = u; h.v = v;
             if (anyhit) return h;
         }
@@ -422,8 +479,8 @@ FRT_HD Hit trace_list(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit)
     return h;
 }
 
-template <int WORLD, int STRIDE, int STACK = 0>
-FRT_HD Hit trace(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int *stk)
+template <int WORLD, int STRIDE, int STACK = 0, typename R>
+FRT_HD Hit<R> trace(const DevScene &S, V3<R> o, V3<R> d, R tmax, bool anyhit, int *stk)
 {
     if constexpr (WORLD == FRT_WORLD_LIST) return trace_list(S, o, d, tmax, anyhit);
     else if constexpr (WORLD == kWorldBvh4) return trace_bvh4<STRIDE, STACK, kBvh4Overflow>(S, o, d, tmax, anyhit, stk);
@@ -431,11 +488,11 @@ FRT_HD Hit trace(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int *st
 }
 
 // resumable form of trace<> (path_megakernel): begin, then steps until true
-template <int WORLD>
-FRT_HD bool trav_begin_world(Trav &T, const DevScene &S, f3 o, f3 d, float tmax)
+template <int WORLD, typename R>
+FRT_HD bool trav_begin_world(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, R tmax)
 {
     if constexpr (WORLD == FRT_WORLD_LIST) {
-        T.h = Hit{-1, tmax, 0.0f, 0.0f};
+        T.h = Hit<R>{-1, tmax, R(0), R(0)};
         return true;
     } else {
         return trav_begin(T, S, WORLD == kWorldBvh4 ? S.root4 : S.root, o, d, tmax);   // brute: root box + t_min
@@ -445,12 +502,12 @@ FRT_HD bool trav_begin_world(Trav &T, const DevScene &S, f3 o, f3 d, float tmax)
 // lanes of a wave read the same triangle (an LDS broadcast) and run the same
 // trip count, so no lane idles; the (t, DFS rank) minimum is the BVH's hit,
 // and the BVH's root box test and t_min stay (trav_begin).
-FRT_HD bool brute_all(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit)
+template <typename R> FRT_HD bool brute_all(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyhit)
 {
     for (int ref = 0; ref < S.n_tris; ++ref) {
-        float u, v;
-        const float t = prim_t(S, ref, o, d, T.tmin, T.h.t, u, v);
-        if (t > 0.0f && (t < T.h.t || (T.h.prim >= 0 && ref < T.h.prim))) {
+        R u, v;
+        const R t = prim_t(S, ref, o, d, T.tmin, T.h.t, u, v);
+        if (t > R(0) && (t < T.h.t || (T.h.prim >= 0 && ref < T.h.prim))) {
             T.h.prim = ref; T.h.t = t; T.h.u = u; T.h.v = v;
             if (anyhit) break;
         }
@@ -458,8 +515,8 @@ FRT_HD bool brute_all(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit)
     return true;
 }
 
-template <int WORLD, int STRIDE, int STACK, bool SPEC = false>
-FRT_HD bool trav_step_world(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int *ovf,
+template <int WORLD, int STRIDE, int STACK, bool SPEC = false, typename R>
+FRT_HD bool trav_step_world(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyhit, int *stk, int *ovf,
                             int min_desc = 0)
 {
     // 4-wide (HBM-resident scenes): the slab ray and t_min again from (o, d)
@@ -467,8 +524,9 @@ FRT_HD bool trav_step_world(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit,
     // megakernel's shading phases (spilled VGPRs 81 -> 36 at the 6-wave cap;
     // cornell_1m +2.8 %, same-call A/B).  The binary LDS plan keeps them.
     if constexpr (WORLD == kWorldBvh4) {
+        static_assert(!kIsF64<R>, "the fp64 kernels traverse the binary tree");
         T.sr = slab_ray(o, d);
-        T.tmin = kEps * fmaxf(1.0f, fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z))));
+        T.tmin = bvh_tmin(o);
     }
     if constexpr (WORLD == kWorldBrute) {
         return brute_all(T, S, o, d, anyhit);
@@ -483,73 +541,81 @@ FRT_HD bool trav_step_world(Trav &T, const DevScene &S, f3 o, f3 d, bool anyhit,
 }
 
 // hit record of a primitive: shading normal + material
-FRT_HD void prim_shade(const DevScene &S, int ref, f3 ro, f3 p, float u, float v, f3 &n, int &mat)
+template <typename R>
+FRT_HD void prim_shade(const DevScene &S, int ref, V3<R> ro, V3<R> p, R u, R v, V3<R> &n, int &mat)
 {
     if (ref & FRT_PRIM_SPHERE) {                               // sphere.h:47-50
         const int k = ref & ~FRT_PRIM_SPHERE;
-        const float4 sp = S.spheres[k];
-        n = rcp(sp.w) * (p - xyz(sp));
-        if (len2(ro - xyz(sp)) < sp.w * sp.w) n = -n;          // origin inside: flip
+        V3<R> c;
+        R r;
+        sphere_get(S, k, c, r);
+        n = rcp(r) * (p - c);
+        if (len2(ro - c) < r * r) n = -n;                      // origin inside: flip
         mat = S.sphere_mat[k];
         return;
     }
-    const float4 s0 = shade_part(S, ref, 0), s1 = shade_part(S, ref, 1);
+    const float4 s1 = shade_part(S, ref, 1);
     mat = f2i(s1.x);
     if (f2i(s1.y)) {                                           // use_geometry_normals (triangle.h:100-101)
-        n = xyz(s0);
+        n = geo_normal<R>(S, ref);
     } else {                                                   // triangle.h:103
-        const f3 n0 = xyz(S.tnorm[3 * ref]), n1 = xyz(S.tnorm[3 * ref + 1]), n2 = xyz(S.tnorm[3 * ref + 2]);
-        n = normalize((1.0f - u - v) * n0 + u * n1 + v * n2);
+        const V3<R> n0 = vert_normal<R>(S, ref, 0), n1 = vert_normal<R>(S, ref, 1), n2 = vert_normal<R>(S, ref, 2);
+        n = normalize((R(1) - u - v) * n0 + u * n1 + v * n2);
     }
 }
 
 // pdf_direct_sampling with the record's (p, t, normal) and direction
-FRT_HD float prim_pdf(const DevScene &S, int ref, f3 rec_p, float rec_t, f3 rec_n, f3 to_light)
+template <typename R>
+FRT_HD R prim_pdf(const DevScene &S, int ref, V3<R> rec_p, R rec_t, V3<R> rec_n, V3<R> to_light)
 {
-    if (!(ref & FRT_PRIM_SPHERE)) return shade_part(S, ref, 0).w;  // inv_area (triangle.h:139-144)
-    const float4 sp = S.spheres[ref & ~FRT_PRIM_SPHERE];           // sphere.h:64-78
-    const f3 o = rec_p - rec_t * to_light;
-    const f3 dir = xyz(sp) - o;
-    const float d2 = len2(dir);
-    const float r2 = sp.w * sp.w;
-    if (d2 <= r2) return rcp(4.0f * kPi * r2);
-    const float cos_max = fsqrt(1.0f - fdiv(r2, d2));
-    const float solid = 2.0f * kPi * (1.0f - cos_max);
-    return fdiv(rcp(solid) * fabsf(dot(to_light, rec_n)), d2);
+    if (!(ref & FRT_PRIM_SPHERE)) return inv_area<R>(S, ref);    // triangle.h:139-144
+    V3<R> c;                                                     // sphere.h:64-78
+    R r;
+    sphere_get(S, ref & ~FRT_PRIM_SPHERE, c, r);
+    const V3<R> o = rec_p - rec_t * to_light;
+    const V3<R> dir = c - o;
+    const R d2 = len2(dir);
+    const R r2 = r * r;
+    if (d2 <= r2) return rcp(R(4) * Cst<R>::pi * r2);
+    const R cos_max = fsqrt(R(1) - fdiv(r2, d2));
+    const R solid = R(2) * Cst<R>::pi * (R(1) - cos_max);
+    return fdiv(rcp(solid) * vabs(dot(to_light, rec_n)), d2);
 }
 
 // sample_direct: returns to_light (unnormalised, as the reference), light normal, material
-FRT_HD f3 prim_sample(const DevScene &S, int ref, f3 o, float u0, float u1, f3 &ln, int &lmat)
+template <typename R>
+FRT_HD V3<R> prim_sample(const DevScene &S, int ref, V3<R> o, R u0, R u1, V3<R> &ln, int &lmat)
 {
     if (ref & FRT_PRIM_SPHERE) {                                   // sphere.h:80-107
         const int k = ref & ~FRT_PRIM_SPHERE;
-        const float4 sp = S.spheres[k];
-        const f3 c = xyz(sp);
+        V3<R> c;
+        R r;
+        sphere_get(S, k, c, r);
         lmat = S.sphere_mat[k];
-        const f3 direction = c - o;
-        const float d2 = len2(direction);
-        if (d2 <= sp.w * sp.w) {
-            const f3 p = c + sp.w * uniform_sphere(u0, u1);
+        const V3<R> direction = c - o;
+        const R d2 = len2(direction);
+        if (d2 <= r * r) {
+            const V3<R> p = c + r * uniform_sphere(u0, u1);
             ln = normalize(c - p);
             return p - o;
         }
-        const Onb uvw = onb_from_w(direction);                     // unnormalised axis, as the reference
-        const f3 p = onb_local(uvw, random_to_sphere(sp.w, d2, u0, u1));
+        const Onb<R> uvw = onb_from_w(direction);                  // unnormalised axis, as the reference
+        const V3<R> p = onb_local(uvw, random_to_sphere(r, d2, u0, u1));
         ln = normalize(p);
         return p;
     }
-    const float4 a = tri_part(S, ref, 0), b = tri_part(S, ref, 1), c = tri_part(S, ref, 2);   // triangle.h:145-175
-    const float su0 = fsqrt(u0);
-    const float b0 = 1.0f - su0;
-    const float b1 = u1 * su0;
-    const f3 lp = xyz(a) + b0 * xyz(b) + b1 * xyz(c);            // (1-b0-b1) v0 + b0 v1 + b1 v2
-    const float4 s0 = shade_part(S, ref, 0), s1 = shade_part(S, ref, 1);
+    const V3<R> a = tri_vec<R>(S, ref, 0), b = tri_vec<R>(S, ref, 1), c = tri_vec<R>(S, ref, 2);   // triangle.h:145-175
+    const R su0 = fsqrt(u0);
+    const R b0 = R(1) - su0;
+    const R b1 = u1 * su0;
+    const V3<R> lp = a + b0 * b + b1 * c;                          // (1-b0-b1) v0 + b0 v1 + b1 v2
+    const float4 s1 = shade_part(S, ref, 1);
     lmat = f2i(s1.x);
     if (f2i(s1.y)) {
-        ln = xyz(s0);
+        ln = geo_normal<R>(S, ref);
     } else {
-        const f3 n0 = xyz(S.tnorm[3 * ref]), n1 = xyz(S.tnorm[3 * ref + 1]), n2 = xyz(S.tnorm[3 * ref + 2]);
-        ln = normalize((1.0f - b0 - b1) * n0 + b0 * n1 + b1 * n2);
+        const V3<R> n0 = vert_normal<R>(S, ref, 0), n1 = vert_normal<R>(S, ref, 1), n2 = vert_normal<R>(S, ref, 2);
+        ln = normalize((R(1) - b0 - b1) * n0 + b0 * n1 + b1 * n2);
     }
     return lp - o;
 }
@@ -566,28 +632,35 @@ constexpr int kMatsSpecAny = kMatsSpec | kMatsRough;
 // ---- textures (texture.h:30-49), MATS kernels only ----
 // (int)x as the reference's x86-64 build computes it (cvttsd2si): NaN and
 // out-of-range give INT_MIN
-FRT_HD int x86_trunc(float x)
+template <typename R> FRT_HD int x86_trunc(R x)
 {
-    if (!(x > -2147483649.0f && x < 2147483648.0f)) return (int)0x80000000;
+    if (!(x > R(-2147483649.0f) && x < R(2147483648.0f))) return (int)0x80000000;
     return (int)x;
 }
 FRT_HD int imodulo2(int a) { const int r = a % 2; return r < 0 ? r + 2 : r; }   // util.h:125-128
+FRT_HD float vatan2(float y, float x) { return atan2f(y, x); }
+FRT_HD double vatan2(double y, double x) { return atan2(y, x); }
+FRT_HD float vasin(float x) { return asinf(x); }
+FRT_HD double vasin(double x) { return asin(x); }
 // hit texture coordinates: get_sphere_uv(p - centre) (hitable.h:15-21; the
 // offset is not normalised, as in sphere.h:52) or the OBJ vt interpolated
 // with the barycentrics (triangle.h:105-107)
-FRT_HD void prim_uv(const DevScene &S, int ref, f3 p, float u, float v, float &tu, float &tv)
+template <typename R> FRT_HD void prim_uv(const DevScene &S, int ref, V3<R> p, R u, R v, R &tu, R &tv)
 {
     if (ref & FRT_PRIM_SPHERE) {
-        const f3 q = p - xyz(S.spheres[ref & ~FRT_PRIM_SPHERE]);
-        const float phi = atan2f(q.z, q.x), theta = asinf(q.y);
-        tu = 1.0f - (phi + kPi) / (2.0f * kPi);
-        tv = (theta + 0.5f * kPi) / kPi;
+        V3<R> c;
+        R r;
+        sphere_get(S, ref & ~FRT_PRIM_SPHERE, c, r);
+        const V3<R> q = p - c;
+        const R phi = vatan2(q.z, q.x), theta = vasin(q.y);
+        tu = R(1) - (phi + Cst<R>::pi) / (R(2) * Cst<R>::pi);
+        tv = (theta + R(0.5f) * Cst<R>::pi) / Cst<R>::pi;
         return;
     }
     const float4 a = S.tuv[2 * ref], b = S.tuv[2 * ref + 1];
-    const float w = 1.0f - u - v;
-    tu = (w * a.x + u * a.z) + v * b.x;
-    tv = (w * a.y + u * a.w) + v * b.y;
+    const R w = R(1) - u - v;
+    tu = (w * R(a.x) + u * R(a.z)) + v * R(b.x);
+    tv = (w * R(a.y) + u * R(a.w)) + v * R(b.y);
 }
 // checker_texture::value: the material's textured colour (m0 for lambertian /
 // modified_phong, m1 for dielectric / rough_conductor) becomes tex1 where
@@ -598,30 +671,30 @@ FRT_HD int imodulo(int a, int b) { const int r = a % b; return r < 0 ? r + b : r
 // texels hold the reference's linear value (FromSrgb(byte / 255) or the HDR
 // float) per texel, so only the index arithmetic runs here (fp32: a texel edge
 // can round to the neighbour, as the checker's cell edges do)
-FRT_HD f3 image_texel(const DevScene &S, float4 m4, float tu, float tv)
+template <typename R> FRT_HD f3 image_texel(const DevScene &S, float4 m4, R tu, R tv)
 {
     const int nx = f2i(m4.x), ny = f2i(m4.y);
-    int i = x86_trunc(tu * (float)nx), j = x86_trunc(tv * (float)ny);
+    int i = x86_trunc(tu * (R)nx), j = x86_trunc(tv * (R)ny);
     if (i < 0 || i > nx) i = imodulo(i, nx);
     if (j < 0 || j > ny) j = imodulo(j, ny);
     if (i == nx) i = nx - 1;
     if (j == ny) j = ny - 1;
     return xyz(S.texels[f2i(m4.z) + j * nx + i]);
 }
-FRT_HD void apply_texture(const DevScene &S, int mat, int mtype, int ref, f3 p, float u, float v, float4 &m0,
-                          float4 &m1)
+template <typename R>
+FRT_HD void apply_texture(const DevScene &S, int mat, int mtype, int ref, V3<R> p, R u, R v, float4 &m0, float4 &m1)
 {
     const float4 m3 = S.mats[kMatStride * mat + 3];
     const int tex = f2i(m3.w);
     if (tex == FRT_TEX_CONSTANT) return;
     const float4 m4 = S.mats[kMatStride * mat + 4];
-    float tu, tv;
+    R tu, tv;
     prim_uv(S, ref, p, u, v, tu, tv);
     f3 c;
     if (tex == FRT_TEX_IMAGE) {
         c = image_texel(S, m4, tu, tv);
     } else {
-        const int x = 2 * imodulo2(x86_trunc(tu * m4.x * 2.0f)) - 1, y = 2 * imodulo2(x86_trunc(tv * m4.y * 2.0f)) - 1;
+        const int x = 2 * imodulo2(x86_trunc(tu * R(m4.x) * R(2))) - 1, y = 2 * imodulo2(x86_trunc(tv * R(m4.y) * R(2))) - 1;
         if (x * y != 1) return;
         c = xyz(m3);
     }
@@ -634,51 +707,53 @@ FRT_HD void apply_texture(const DevScene &S, int mat, int mtype, int ref, f3 p, 
 // the hit of the ray just traced and sets up the next one (shadow first,
 // then the extension ray) or finishes the path.
 // ---------------------------------------------------------------------------
-struct PathState {
-    f3 ro, rd;            // ray to trace next
-    float rtmax;
+template <typename R> struct PathState {
+    V3<R> ro, rd;         // ray to trace next
+    R rtmax;
     bool shadow;          // any-hit query
     bool term;            // the path ends after this shadow ray (zero bsdf pdf)
-    f3 beta, L;           // throughput, radiance of this sample
-    f3 nee;               // NEE contribution if the shadow ray is unoccluded
-    f3 nxt_d;             // extension direction after the shadow ray
-    f3 nxt_o;             // its origin when it differs from the shadow ray's (specular kernels only)
-    f3 prev_p;            // previous hit point (MIS distance, path.cpp:25)
-    float prev_pdf;       // bsdf pdf of the previous bounce
+    V3<R> beta, L;        // throughput, radiance of this sample
+    V3<R> nee;            // NEE contribution if the shadow ray is unoccluded
+    V3<R> nxt_d;          // extension direction after the shadow ray
+    V3<R> nxt_o;          // its origin when it differs from the shadow ray's (specular kernels only)
+    V3<R> prev_p;         // previous hit point (MIS distance, path.cpp:25)
+    R prev_pdf;           // bsdf pdf of the previous bounce
     bool prev_spec;       // previous bounce was modified_phong / metal / dielectric: no MIS on light hits
     int depth;
     RngKey key;
 };
 
 // path.cpp:129-136 + camera.h:30-35 (+ util.h:21-41 thin lens)
-FRT_HD void path_begin(PathState &P, const DevScene &S, int px, int py, int nx, int ny, uint32_t seed,
+template <typename R>
+FRT_HD void path_begin(PathState<R> &P, const DevScene &S, int px, int py, int nx, int ny, uint32_t seed,
                        uint32_t pixel, uint32_t sample)
 {
     P.key = rng_key(seed, pixel, sample);
-    const float u = fdiv((float)px + rng_u(P.key, 0), (float)nx);
-    const float v = fdiv((float)py + rng_u(P.key, 1), (float)ny);
-    f3 off = mk3(0, 0, 0);
-    if (S.lens_r != 0.0f) {
-        const float a = rng_u(P.key, 2) * 2.0f - 1.0f, b = rng_u(P.key, 3) * 2.0f - 1.0f;
-        float rx = 0.0f, ry = 0.0f;
-        if (a != 0.0f || b != 0.0f) {
-            float r, phi;
-            if (a * a > b * b) { r = a; phi = (kPi / 4.0f) * (b / a); }
-            else { r = b; phi = (kPi / 2.0f) - (kPi / 4.0f) * (a / b); }
-            rx = r * cosf(phi); ry = r * sinf(phi);
+    const CamView<R> cam = cam_view<R>(S);
+    const R u = fdiv((R)px + rng_r<R>(P.key, 0), (R)nx);
+    const R v = fdiv((R)py + rng_r<R>(P.key, 1), (R)ny);
+    V3<R> off = zero3<R>();
+    if (cam.lens_r != R(0)) {
+        const R a = rng_r<R>(P.key, 2) * R(2) - R(1), b = rng_r<R>(P.key, 3) * R(2) - R(1);
+        R rx = R(0), ry = R(0);
+        if (a != R(0) || b != R(0)) {
+            R r, phi;
+            if (a * a > b * b) { r = a; phi = (Cst<R>::pi / R(4)) * (b / a); }
+            else { r = b; phi = (Cst<R>::pi / R(2)) - (Cst<R>::pi / R(4)) * (a / b); }
+            rx = r * vcos(phi); ry = r * vsin(phi);
         }
-        off = (S.lens_r * rx) * S.cam_u + (S.lens_r * ry) * S.cam_vv;
+        off = (cam.lens_r * rx) * cam.u + (cam.lens_r * ry) * cam.vv;
     }
-    P.ro = S.cam_o + off;
-    P.rd = ((S.cam_llc + u * S.cam_h + v * S.cam_v) - S.cam_o) - off;
-    P.rtmax = kTMaxClosest;
+    P.ro = cam.o + off;
+    P.rd = ((cam.llc + u * cam.h + v * cam.v) - cam.o) - off;
+    P.rtmax = Cst<R>::tmax;
     P.shadow = false;
     P.term = false;
     P.depth = 0;
-    P.beta = mk3(1, 1, 1);
-    P.L = mk3(0, 0, 0);
-    P.prev_pdf = 0.0f;
-    P.prev_p = mk3(0, 0, 0);
+    P.beta = V3<R>{R(1), R(1), R(1)};
+    P.L = zero3<R>();
+    P.prev_pdf = R(0);
+    P.prev_p = zero3<R>();
     P.prev_spec = false;
 }
 
@@ -691,14 +766,14 @@ FRT_HD void path_begin(PathState &P, const DevScene &S, int px, int py, int nx, 
 // so the reference returns 0 for the vertex after tracing the shadow ray
 // (path.cpp:45-77 run before :87-90 / :103-106) -- the ray is traced and
 // counted like the reference's, its NEE term dropped.
-template <int MATS = kMatsAll>
-FRT_HD bool path_after_shadow(PathState &P, bool unoccluded)
+template <int MATS = kMatsAll, typename R>
+FRT_HD bool path_after_shadow(PathState<R> &P, bool unoccluded)
 {
     P.shadow = false;
     if (P.term) return false;
     if (unoccluded) P.L = P.L + P.nee;
     if constexpr ((MATS & kMatsSpecAny) != 0) P.ro = P.nxt_o;
-    P.rd = P.nxt_d; P.rtmax = kTMaxClosest;
+    P.rd = P.nxt_d; P.rtmax = Cst<R>::tmax;
     ++P.depth;
     return true;
 }
@@ -720,43 +795,43 @@ FRT_HD SpecMat spec_mat(const DevScene &S, int mat, int type, float4 m0, float4 
 // 262-268) and srec.sampled_pdf (-1 unless the rough conductor sets it)
 // MATS without kMatsRough: the scene has no rough conductor, its lobes are
 // not compiled (the switch's default is then metal's).
-template <int MATS = kMatsAll>
-FRT_HD f3 spec_generate(const SpecMat &M, f3 n, f3 wi, float s0, float s1, float &sampled_pdf)
+template <int MATS = kMatsAll, typename R>
+FRT_HD V3<R> spec_generate(const SpecMat &M, V3<R> n, V3<R> wi, R s0, R s1, R &sampled_pdf)
 {
-    sampled_pdf = -1.0f;
+    sampled_pdf = R(-1);
     switch (M.type) {
-    case FRT_MAT_MODIFIED_PHONG: return cosine_power_generate(n, wi, M.m1.w, s0, s1);
-    case FRT_MAT_DIELECTRIC: return dielectric_generate(n, wi, M.m1.w, s0);
+    case FRT_MAT_MODIFIED_PHONG: return cosine_power_generate(n, wi, R(M.m1.w), s0, s1);
+    case FRT_MAT_DIELECTRIC: return dielectric_generate(n, wi, R(M.m1.w), s0);
     case FRT_MAT_METAL: return reflect(-wi, n);          // reflect(unit(r_in.d), n); -wi = unit(r_in.d)
     default:
         if constexpr ((MATS & kMatsRough) != 0)
-            return normalize(rough_generate(n, wi, M.m1.w, f2i(M.m2.w), s0, s1, sampled_pdf));
+            return normalize(rough_generate(n, wi, R(M.m1.w), f2i(M.m2.w), s0, s1, sampled_pdf));
         return reflect(-wi, n);
     }
 }
-template <int MATS = kMatsAll>
-FRT_HD float spec_value(const SpecMat &M, f3 n, f3 wi, f3 wo)     // srec.pdf_ptr->value
+template <int MATS = kMatsAll, typename R>
+FRT_HD R spec_value(const SpecMat &M, V3<R> n, V3<R> wi, V3<R> wo)     // srec.pdf_ptr->value
 {
     switch (M.type) {
-    case FRT_MAT_MODIFIED_PHONG: return cosine_power_value(n, wi, M.m1.w, wo);
-    case FRT_MAT_DIELECTRIC: return dielectric_value(n, wi, M.m1.w, wo);
-    case FRT_MAT_METAL: return 1.0f;                     // constant_pdf(1) (pdf.h:186-201)
+    case FRT_MAT_MODIFIED_PHONG: return cosine_power_value(n, wi, R(M.m1.w), wo);
+    case FRT_MAT_DIELECTRIC: return dielectric_value(n, wi, R(M.m1.w), wo);
+    case FRT_MAT_METAL: return R(1);                     // constant_pdf(1) (pdf.h:186-201)
     default:
-        if constexpr ((MATS & kMatsRough) != 0) return rough_value(n, wi, M.m1.w, f2i(M.m2.w), wo);
-        return 1.0f;
+        if constexpr ((MATS & kMatsRough) != 0) return rough_value(n, wi, R(M.m1.w), f2i(M.m2.w), wo);
+        return R(1);
     }
 }
-template <int MATS = kMatsAll>
-FRT_HD f3 spec_eval(const SpecMat &M, f3 n, f3 wi, f3 wo)          // eval_bsdf
+template <int MATS = kMatsAll, typename R>
+FRT_HD V3<R> spec_eval(const SpecMat &M, V3<R> n, V3<R> wi, V3<R> wo)          // eval_bsdf
 {
     switch (M.type) {
-    case FRT_MAT_MODIFIED_PHONG: return phong_eval(xyz(M.m0), xyz(M.m1), M.m1.w, n, wi, wo);
-    case FRT_MAT_DIELECTRIC: return dielectric_eval(xyz(M.m1), M.m1.w, n, wi, wo);
-    case FRT_MAT_METAL: return xyz(M.m0);
+    case FRT_MAT_MODIFIED_PHONG: return phong_eval(rgb<R>(M.m0), rgb<R>(M.m1), R(M.m1.w), n, wi, wo);
+    case FRT_MAT_DIELECTRIC: return dielectric_eval(rgb<R>(M.m1), R(M.m1.w), n, wi, wo);
+    case FRT_MAT_METAL: return rgb<R>(M.m0);
     default:
         if constexpr ((MATS & kMatsRough) != 0)
-            return rough_eval(xyz(M.m0), xyz(M.m2), xyz(M.m1), M.m1.w, f2i(M.m2.w), n, wi, wo);
-        return xyz(M.m0);
+            return rough_eval(rgb<R>(M.m0), rgb<R>(M.m2), rgb<R>(M.m1), R(M.m1.w), f2i(M.m2.w), n, wi, wo);
+        return rgb<R>(M.m0);
     }
 }
 FRT_HD bool mat_is_specular(int t)
@@ -769,8 +844,8 @@ FRT_HD bool mat_no_mis(int t) { return t == FRT_MAT_MODIFIED_PHONG || t == FRT_M
 // Returns true when the path is finished (P.L is the sample's radiance).
 // MATS = false compiles the lambertian / diffuse_light scenes' kernel: the
 // specular branch is dead code there (it would cost registers and code size).
-template <int MATS = kMatsAll>
-FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_depth, uint32_t &n_ext, uint32_t &n_sh)
+template <int MATS = kMatsAll, typename R>
+FRT_HD bool path_shade(PathState<R> &P, const DevScene &S, const Hit<R> &h, int max_depth, uint32_t &n_ext, uint32_t &n_sh)
 {
     if (P.shadow) {
         if (!path_after_shadow<MATS>(P, h.prim < 0)) return true;
@@ -779,26 +854,26 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
     }
     if (P.term) return true;                            // finished in the traversal loop
     if (h.prim < 0) {                                   // path.cpp:115 environment
-        P.L = P.L + P.beta * S.env;
+        P.L = P.L + P.beta * env_of<R>(S);
         return true;
     }
-    const f3 p = P.ro + h.t * P.rd;
-    f3 n;
+    const V3<R> p = P.ro + h.t * P.rd;
+    V3<R> n;
     int mat;
     prim_shade(S, h.prim, P.ro, p, h.u, h.v, n, mat);
     float4 m0 = S.mats[kMatStride * mat], m1 = S.mats[kMatStride * mat + 1];
     const int mtype = f2i(m0.w);
     if constexpr ((MATS & kMatsTex) != 0) apply_texture(S, mat, mtype, h.prim, p, h.u, h.v, m0, m1);
     // diffuse_light::emitted is one-sided (material.h:184-190)
-    if (mtype == FRT_MAT_DIFFUSE_LIGHT && dot(n, P.rd) < 0.0f) {
-        const f3 Le = xyz(m1);
+    if (mtype == FRT_MAT_DIFFUSE_LIGHT && dot(n, P.rd) < R(0)) {
+        const V3<R> Le = rgb<R>(m1);
         if (P.depth == 0 || P.prev_spec) {
             P.L = P.L + P.beta * Le;                    // path.cpp:16-22 (camera ray / after phong, metal, dielectric)
         } else {                                        // path.cpp:24-31: MIS against the bsdf sample
-            const float cos_wo = dot(n, -normalize(P.rd));
-            float d2 = len2(p - P.prev_p);
-            if (d2 <= kEps) d2 = kEps;
-            const float light_pdf = fdiv(prim_pdf(S, h.prim, p, h.t, n, P.rd) * d2, fabsf(cos_wo));
+            const R cos_wo = dot(n, -normalize(P.rd));
+            R d2 = len2(p - P.prev_p);
+            if (d2 <= Cst<R>::eps) d2 = Cst<R>::eps;
+            const R light_pdf = fdiv(prim_pdf(S, h.prim, p, h.t, n, P.rd) * d2, vabs(cos_wo));
             P.L = P.L + mi_weight(P.prev_pdf, light_pdf) * (P.beta * Le);
         }
         return true;
@@ -810,23 +885,23 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
     // The scattered direction first: a zero pdf returns 0 for this vertex,
     // dropping its NEE too (path.cpp:84-86, 103-106) -- after the reference has
     // traced the shadow ray, so that ray is still traced (P.term).
-    f3 wo, beta_next;
-    float pdf;
-    const f3 wi = -normalize(P.rd);                     // hrec.wi (triangle.h:108, sphere.h:47)
+    V3<R> wo, beta_next;
+    R pdf;
+    const V3<R> wi = -normalize(P.rd);                  // hrec.wi (triangle.h:108, sphere.h:47)
     SpecMat M{};
     if (!(MATS & kMatsSpecAny) || lamb) {               // cosine_pdf (path.cpp:96-110)
-        const Onb uvw = onb_from_w(n);
-        wo = onb_local(uvw, cosine_direction(rng_u(P.key, base + 6), rng_u(P.key, base + 7)));
-        const float cw = dot(n, normalize(wo));
-        pdf = fmaxf(cw, 0.0f) * kInvPi;
-        beta_next = fdiv(fabsf(cw), pdf) * (P.beta * (kInvPi * xyz(m0)));   // lambertian::eval_bsdf
+        const Onb<R> uvw = onb_from_w(n);
+        wo = onb_local(uvw, cosine_direction(rng_r<R>(P.key, base + 6), rng_r<R>(P.key, base + 7)));
+        const R cw = dot(n, normalize(wo));
+        pdf = vmax(cw, R(0)) * Cst<R>::inv_pi;
+        beta_next = fdiv(vabs(cw), pdf) * (P.beta * (Cst<R>::inv_pi * rgb<R>(m0)));   // lambertian::eval_bsdf
     } else {                                            // specular branch (path.cpp:78-95); the
         M = spec_mat(S, mat, mtype, m0, m1);            // scatter sample is get3d's (base + 0, 1)
-        float sampled;
-        wo = spec_generate<MATS>(M, n, wi, rng_u(P.key, base + 0), rng_u(P.key, base + 1), sampled);
+        R sampled;
+        wo = spec_generate<MATS>(M, n, wi, rng_r<R>(P.key, base + 0), rng_r<R>(P.key, base + 1), sampled);
         pdf = spec_value<MATS>(M, n, wi, wo);
-        if (sampled > 0.0f) pdf = sampled;              // path.cpp:82
-        const f3 bsdf = spec_eval<MATS>(M, n, wi, wo);
+        if (sampled > R(0)) pdf = sampled;              // path.cpp:82
+        const V3<R> bsdf = spec_eval<MATS>(M, n, wi, wo);
         beta_next = P.beta * (rcp(pdf) * bsdf);
     }
     // Lambertian-only kernels (MATS = false) never see pdf 0: the cosine lobe's
@@ -834,39 +909,39 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
     // dot(n, wo); the constant lets the compiler drop the state.
     // NEE's light pick (path.cpp:39-40)
     const int nl = S.n_lights;
-    int idx = (int)(rng_u(P.key, base + 3) * (float)nl);
+    int idx = (int)(rng_r<R>(P.key, base + 3) * (R)nl);
     if (idx == nl) idx -= 1;
     const bool nee = idx >= 0 && !diel;
-    P.term = (MATS & kMatsSpecAny) && pdf == 0.0f;
+    P.term = (MATS & kMatsSpecAny) && pdf == R(0);
     if (P.term && !nee) return true;
     // origin of the next ray: off the surface on the side it leaves (path.cpp:91-93, 99)
-    const f3 nee_o = p + kEps * n;
-    const f3 origin = (!(MATS & kMatsSpecAny) || lamb || dot(n, wo) > 0.0f) ? nee_o : p - kEps * n;
+    const V3<R> nee_o = p + Cst<R>::eps * n;
+    const V3<R> origin = (!(MATS & kMatsSpecAny) || lamb || dot(n, wo) > R(0)) ? nee_o : p - Cst<R>::eps * n;
     P.nxt_d = wo;
     if constexpr ((MATS & kMatsSpecAny) != 0) P.nxt_o = origin;
     // next-event estimation (path.cpp:38-77); not from dielectrics (path.cpp:40)
     if (nee) {
         const int lref = S.lights[idx];
-        f3 ln;
+        V3<R> ln;
         int lmat;
-        const f3 tl = prim_sample(S, lref, nee_o, rng_u(P.key, base + 4), rng_u(P.key, base + 5), ln, lmat);
-        const float dist2 = len2(tl);
-        const f3 tu = rlen(tl) * tl;
-        const float cos_wi = dot(n, tu);
-        const float cos_lo = dot(ln, -tu);
-        P.nee = mk3(0, 0, 0);
-        if (cos_lo != 0.0f) {
-            const float light_pdf = fdiv(prim_pdf(S, lref, p, h.t, n, tu) * dist2, fabsf(cos_lo));
+        const V3<R> tl = prim_sample(S, lref, nee_o, rng_r<R>(P.key, base + 4), rng_r<R>(P.key, base + 5), ln, lmat);
+        const R dist2 = len2(tl);
+        const V3<R> tu = rlen(tl) * tl;
+        const R cos_wi = dot(n, tu);
+        const R cos_lo = dot(ln, -tu);
+        P.nee = zero3<R>();
+        if (cos_lo != R(0)) {
+            const R light_pdf = fdiv(prim_pdf(S, lref, p, h.t, n, tu) * dist2, vabs(cos_lo));
             // eval_bsdf toward the light; only the non-specular bsdf gets the cosine (path.cpp:61-62)
             const bool l = !(MATS & kMatsSpecAny) || lamb;
-            const f3 f = l ? cos_wi * (kInvPi * xyz(m0)) : spec_eval<MATS>(M, n, wi, tu);
-            const float bsdf_pdf = l ? fmaxf(cos_wi, 0.0f) * kInvPi : spec_value<MATS>(M, n, wi, tu);
-            const float wgt = mi_weight(light_pdf, bsdf_pdf);
+            const V3<R> f = l ? cos_wi * (Cst<R>::inv_pi * rgb<R>(m0)) : spec_eval<MATS>(M, n, wi, tu);
+            const R bsdf_pdf = l ? vmax(cos_wi, R(0)) * Cst<R>::inv_pi : spec_value<MATS>(M, n, wi, tu);
+            const R wgt = mi_weight(light_pdf, bsdf_pdf);
             const float4 lm0 = S.mats[kMatStride * lmat], lm1 = S.mats[kMatStride * lmat + 1];
-            if (f2i(lm0.w) == FRT_MAT_DIFFUSE_LIGHT && dot(ln, tu) < 0.0f)
-                P.nee = fdiv(wgt, light_pdf) * (P.beta * (xyz(lm1) * f));
+            if (f2i(lm0.w) == FRT_MAT_DIFFUSE_LIGHT && dot(ln, tu) < R(0))
+                P.nee = fdiv(wgt, light_pdf) * (P.beta * (rgb<R>(lm1) * f));
         }
-        P.ro = nee_o; P.rd = tl; P.rtmax = 1.0f - kShadowEps;
+        P.ro = nee_o; P.rd = tl; P.rtmax = R(1) - Cst<R>::shadow_eps;
         P.shadow = true;
         ++n_sh;
     }
@@ -875,7 +950,7 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
     P.prev_p = p;
     P.prev_pdf = pdf;
     if (!P.shadow) {
-        P.ro = origin; P.rd = wo; P.rtmax = kTMaxClosest;
+        P.ro = origin; P.rd = wo; P.rtmax = Cst<R>::tmax;
         ++P.depth; ++n_ext;
     }
     return false;
@@ -893,34 +968,35 @@ FRT_HD bool path_shade(PathState &P, const DevScene &S, const Hit &h, int max_de
 // hitable_list.cpp:27-29: t_max is NaN): only spheres can occlude there
 // (sphere.h's `t > t_max` test passes NaN, triangle.h's `t < t_max` does
 // not), answered here with a loop over the list's spheres.
-template <int MATS = kMatsAll>
-FRT_HD bool ao_shade(PathState &P, const DevScene &S, const Hit &h, uint32_t &n_sh)
+template <int MATS = kMatsAll, typename R>
+FRT_HD bool ao_shade(PathState<R> &P, const DevScene &S, const Hit<R> &h, uint32_t &n_sh)
 {
+    const V3<R> env = env_of<R>(S);
     if (P.shadow) {                                     // visibility ray done
-        P.L = h.prim < 0 ? S.env : mk3(0, 0, 0);
+        P.L = h.prim < 0 ? env : zero3<R>();
         return true;
     }
-    P.L = S.env;
+    P.L = env;
     if (h.prim < 0) return true;
-    const f3 p = P.ro + h.t * P.rd;
-    f3 n;
+    const V3<R> p = P.ro + h.t * P.rd;
+    V3<R> n;
     int mat;
     prim_shade(S, h.prim, P.ro, p, h.u, h.v, n, mat);
     const float4 m0 = S.mats[kMatStride * mat], m1 = S.mats[kMatStride * mat + 1];
     const int mtype = f2i(m0.w);
     const uint32_t base = dim_bounce(0);
-    const float u0 = rng_u(P.key, base + 6), u1 = rng_u(P.key, base + 7);
-    f3 wo;
+    const R u0 = rng_r<R>(P.key, base + 6), u1 = rng_r<R>(P.key, base + 7);
+    V3<R> wo;
     if (mtype == FRT_MAT_LAMBERTIAN) {
         wo = onb_local(onb_from_w(n), cosine_direction(u0, u1));
     } else if ((MATS & kMatsSpec) && mtype == FRT_MAT_MODIFIED_PHONG) {
-        wo = cosine_power_generate(n, -normalize(P.rd), m1.w, u0, u1);
+        wo = cosine_power_generate(n, -normalize(P.rd), R(m1.w), u0, u1);
     } else if ((MATS & kMatsSpec) && mtype == FRT_MAT_DIELECTRIC) {
-        wo = dielectric_generate(n, -normalize(P.rd), m1.w, u0);
+        wo = dielectric_generate(n, -normalize(P.rd), R(m1.w), u0);
     } else if ((MATS & kMatsRough) && mtype == FRT_MAT_ROUGH_CONDUCTOR) {   // pdf.h:465-482 (metal: refused at launch)
         const float4 m2 = S.mats[kMatStride * mat + 2];
-        float unused;
-        if constexpr ((MATS & kMatsRough) != 0) wo = rough_generate(n, -normalize(P.rd), m1.w, f2i(m2.w), u0, u1, unused);
+        R unused;
+        if constexpr ((MATS & kMatsRough) != 0) wo = rough_generate(n, -normalize(P.rd), R(m1.w), f2i(m2.w), u0, u1, unused);
     } else {
         return true;                                    // no scatter (diffuse_light)
     }
@@ -929,29 +1005,31 @@ FRT_HD bool ao_shade(PathState &P, const DevScene &S, const Hit &h, uint32_t &n_
         for (int i = 0; i < S.n_list; ++i) {
             const int ref = S.list[i];
             if (!(ref & FRT_PRIM_SPHERE)) continue;
-            const float4 sp = S.spheres[ref & ~FRT_PRIM_SPHERE];
-            if (sphere_intersect(p, wo, xyz(sp), sp.w, kEps, kTMaxClosest) > 0.0f) {
-                P.L = mk3(0, 0, 0);
+            V3<R> c;
+            R r;
+            sphere_get(S, ref & ~FRT_PRIM_SPHERE, c, r);
+            if (sphere_intersect(p, wo, c, r, Cst<R>::eps, Cst<R>::tmax) > R(0)) {
+                P.L = zero3<R>();
                 break;
             }
         }
         return true;
     }
-    P.ro = p; P.rd = wo; P.rtmax = S.ao_tmax;
+    P.ro = p; P.rd = wo; P.rtmax = R(S.ao_tmax);
     P.shadow = true;
     return false;
 }
 
 // normals_renderer::Li (debug_renderer.h:8-17): the shading normal of the
 // camera hit, the environment on a miss.
-FRT_HD bool normals_shade(PathState &P, const DevScene &S, const Hit &h)
+template <typename R> FRT_HD bool normals_shade(PathState<R> &P, const DevScene &S, const Hit<R> &h)
 {
     if (h.prim < 0) {
-        P.L = S.env;
+        P.L = env_of<R>(S);
         return true;
     }
-    const f3 p = P.ro + h.t * P.rd;
-    f3 n;
+    const V3<R> p = P.ro + h.t * P.rd;
+    V3<R> n;
     int mat;
     prim_shade(S, h.prim, P.ro, p, h.u, h.v, n, mat);
     P.L = n;
@@ -959,8 +1037,8 @@ FRT_HD bool normals_shade(PathState &P, const DevScene &S, const Hit &h)
 }
 
 // integrator dispatch of the megakernel / self-test (KIND = FRT_INTEGRATOR_*)
-template <int KIND, int MATS>
-FRT_HD bool shade_kind(PathState &P, const DevScene &S, const Hit &h, int max_depth, uint32_t &n_ext, uint32_t &n_sh)
+template <int KIND, int MATS, typename R>
+FRT_HD bool shade_kind(PathState<R> &P, const DevScene &S, const Hit<R> &h, int max_depth, uint32_t &n_ext, uint32_t &n_sh)
 {
     if constexpr (KIND == FRT_INTEGRATOR_AO) return ao_shade<MATS>(P, S, h, n_sh);
     else if constexpr (KIND == FRT_INTEGRATOR_NORMALS) return normals_shade(P, S, h);

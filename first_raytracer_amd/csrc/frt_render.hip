@@ -140,8 +140,10 @@ struct ItemState {
     __device__ void set(int k, int x) const { b[k * kBlock] = x; }
 };
 
+// R: float (the product kernels) or double (the fp64 kernels, DESIGN.md
+// "Precision": list worlds under FRT_PRECISION_AUTO, every plan under _FP64)
 template <int STACK, int WORLD, bool LDS_SCENE, int WAVES = 1, bool SPEC = false, int MATS = kMatsNone,
-          int KIND = FRT_INTEGRATOR_PATH>
+          int KIND = FRT_INTEGRATOR_PATH, typename R = float>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void path_megakernel(
     const DevScene S0, const DevWork W)
 {
@@ -159,9 +161,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     // work-item state
     bool have_item = false, exhausted = false, active = false;
     const ItemState I{lds_mem + kStackInts + (int)threadIdx.x};
-    PathState P;
+    PathState<R> P;
     // ray in flight: tracing = traversal steps remain; pending = finished, not yet shaded
-    Trav T;
+    Trav<R> T;
     bool tracing = false, pending = false;
     int ovf[WORLD == kWorldBvh4 ? kBvh4Overflow : 1];
     // ray counters are wave-uniform (SGPRs): popcounts of per-iteration ballots
@@ -207,9 +209,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             FRT_DIAG_TICK(4);
             pending = false;
             if (shade_kind<KIND, MATS>(P, S, T.h, W.max_depth, ne, ns)) {
-                I.set(kIsAcc + 0, f2i(i2f(I.get(kIsAcc + 0)) + P.L.x));
-                I.set(kIsAcc + 1, f2i(i2f(I.get(kIsAcc + 1)) + P.L.y));
-                I.set(kIsAcc + 2, f2i(i2f(I.get(kIsAcc + 2)) + P.L.z));
+                I.set(kIsAcc + 0, f2i(i2f(I.get(kIsAcc + 0)) + (float)P.L.x));   // fp32 chunk sums in
+                I.set(kIsAcc + 1, f2i(i2f(I.get(kIsAcc + 1)) + (float)P.L.y));   // either precision
+                I.set(kIsAcc + 2, f2i(i2f(I.get(kIsAcc + 2)) + (float)P.L.z));
                 active = false;
             } else {
                 next_ray = true;
@@ -363,7 +365,7 @@ struct MltWork {
 };
 
 template <int WORLD, int STACK>
-__device__ __forceinline__ Hit trace_any(const DevScene &S, const PathState &P, int *stk)
+__device__ __forceinline__ Hit<float> trace_any(const DevScene &S, const PathState<float> &P, int *stk)
 {
     return trace<WORLD, kBlock, STACK>(S, P.ro, P.rd, P.rtmax, P.shadow, stk);
 }
@@ -386,7 +388,7 @@ __global__ __launch_bounds__(kBlock) void mlt_bootstrap(const DevScene S0, int n
     uint32_t ne = 0, ns = 0;
     for (;;) {
         if (mlt_beyond(M)) { M.P.L = M.P.L + M.P.beta * S.env; break; }
-        const Hit h = trace_any<WORLD, STACK>(S, M.P, stk);
+        const Hit<float> h = trace_any<WORLD, STACK>(S, M.P, stk);
         if (mlt_shade<MATS>(M, S, h, src, ne, ns)) break;
     }
     sc[i] = fmaxf(fmaxf(M.P.L.x, M.P.L.y), M.P.L.z);
@@ -450,7 +452,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
     };
     // ray in flight, as in path_megakernel: tracing = traversal steps remain;
     // pending = finished (or the path went beyond MaxPathLength), not yet shaded
-    Trav T;
+    Trav<float> T;
     bool tracing = false, pending = false, beyond = false;
     int ovf[WORLD == kWorldBvh4 ? kBvh4Overflow : 1];
     for (;;) {
@@ -633,6 +635,8 @@ struct frt_ctx {
     bool has_metal = false;       // ao::Li cannot sample metal (constant_pdf::generate throws, pdf.h:195-198)
     size_t scene_lds_bytes = 0, scene_lds_bytes4 = 0;   // LDS copy with binary / 4-wide nodes
     size_t scene_lds_bytes_oct = 0;                     // ... with the 8 octant copies of the binary nodes
+    int precision = FRT_PRECISION_AUTO;                 // frt_set_precision
+    bool has_f64 = false;                               // the scene's fp64 records are in HBM
     double last_mlt_b = 0.0;
     std::vector<void *> scene_bufs;
     // workspace
@@ -729,6 +733,18 @@ extern "C" int frt_destroy(frt_ctx *c)
 
 extern "C" const char *frt_last_error(const frt_ctx *c) { return c ? c->err.c_str() : "null context"; }
 
+// Precision of the context's kernels (DESIGN.md "Precision"): read by the
+// next frt_upload_scene (which then also uploads the fp64 records) and by
+// every render.
+extern "C" int frt_set_precision(frt_ctx *c, int precision)
+{
+    if (!c) return FRT_E_INVALID;
+    if (precision != FRT_PRECISION_AUTO && precision != FRT_PRECISION_FP32 && precision != FRT_PRECISION_FP64)
+        return set_err(c, FRT_E_INVALID, "precision must be FRT_PRECISION_AUTO, _FP32 or _FP64");
+    c->precision = precision;
+    return FRT_OK;
+}
+
 // GPU BVH build on this context's device and stream (frt_lbvh.hip); called
 // by frt_scene_build_bvh_gpu (csrc/host/scene.cpp).  Internal to libfrt.so.
 extern "C" int frt_internal_lbvh(frt_ctx *c, int n, const float *box6, int32_t *child2, float *node_box6,
@@ -767,7 +783,8 @@ struct FlatScene {
     std::vector<float4> nodes, tris, tshade, tnorm, spheres, mats, tuv;
     std::vector<float4> texels;   // image_texture texels (rgb, -), all images back to back
     std::vector<uint4> nodes4;   // 4-wide quantized BVH
-    std::vector<float4> nodes_oct;   // 8 octant copies of `nodes` (DevScene::nodes_oct)
+    std::vector<float4> nodes_oct;   // 8 octant copies of `nodes` (DevScene::nodes_oct), LDS plan scenes only
+    std::vector<double4> tris64, tshade64, tnorm64, spheres64;   // fp64 records (DevScene::tris64 ...)
     bool has4 = false;           // nodes4 / root4 usable
     int root4 = 0, depth4 = 0;
     std::vector<int> smat, lights, list;
@@ -968,7 +985,8 @@ static bool build_bvh4(FlatScene &F, int root_ref)
     return true;
 }
 
-static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &err)
+// f64: also build the fp64 records of the fp64 kernels (DESIGN.md "Precision")
+static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &err, bool f64)
 {
     auto fail = [&](int code, const std::string &m) { err = m; return code; };
     const int nt = sv->n_tris, ns = sv->n_spheres, nm = sv->n_materials;
@@ -1127,6 +1145,11 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     F.tris.resize(3 * (size_t)nt);
     F.tshade.resize(2 * (size_t)nt);
     if (any_smooth) F.tnorm.resize(3 * (size_t)nt);
+    if (f64) {
+        F.tris64.resize(3 * (size_t)nt);
+        F.tshade64.resize(nt);
+        if (any_smooth) F.tnorm64.resize(3 * (size_t)nt);
+    }
     for (int d = 0; d < nt; ++d) {
         const int i = tri_order[d];
         const double *v = &sv->tri_v[9 * i];
@@ -1147,6 +1170,16 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
             for (int k = 0; k < 3; ++k)
                 F.tnorm[3 * d + k] = make_float4((float)sv->tri_n[9 * i + 3 * k], (float)sv->tri_n[9 * i + 3 * k + 1],
                                                  (float)sv->tri_n[9 * i + 3 * k + 2], 0.0f);
+        if (f64) {
+            F.tris64[3 * d + 0] = make_double4(v[0], v[1], v[2], 0.0);
+            F.tris64[3 * d + 1] = make_double4(e1[0], e1[1], e1[2], 0.0);
+            F.tris64[3 * d + 2] = make_double4(e2[0], e2[1], e2[2], 0.0);
+            F.tshade64[d] = make_double4(ng[0], ng[1], ng[2], sv->tri_inv_area[i]);
+            if (any_smooth)
+                for (int k = 0; k < 3; ++k)
+                    F.tnorm64[3 * d + k] = make_double4(sv->tri_n[9 * i + 3 * k], sv->tri_n[9 * i + 3 * k + 1],
+                                                        sv->tri_n[9 * i + 3 * k + 2], 0.0);
+        }
     }
     // texture coordinates, only when a material is textured (in HBM; read at textured hits)
     bool any_tex = false;
@@ -1162,9 +1195,11 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     }
     F.spheres.resize(ns);
     F.smat.resize(ns);
+    if (f64) F.spheres64.resize(ns);
     for (int k = 0; k < ns; ++k) {
         const double *q = &sv->sphere[4 * k];
         F.spheres[k] = make_float4((float)q[0], (float)q[1], (float)q[2], (float)q[3]);
+        if (f64) F.spheres64[k] = make_double4(q[0], q[1], q[2], q[3]);
         F.smat[k] = sv->sphere_material[k];
         if (F.smat[k] < 0 || F.smat[k] >= nm) return fail(FRT_E_INVALID, "scene view: bad sphere material");
     }
@@ -1214,9 +1249,13 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     F.list.resize(sv->world_kind == FRT_WORLD_LIST ? sv->n_list : 0);
     for (size_t i = 0; i < F.list.size(); ++i) F.list[i] = dev_ref(sv->list[i]);
 
-    // octant copies of the binary nodes: child boxes as (near xyz, far xyz)
-    F.nodes_oct.resize(8 * F.nodes.size());
-    for (int o = 0; o < 8; ++o)
+    // octant copies of the binary nodes: child boxes as (near xyz, far xyz).
+    // Only the LDS binary plan reads them, and only when they fit its budget
+    // (pick_launcher_t): larger scenes get none (8x the node array otherwise).
+    const size_t oct_bytes = sizeof(float4) * (8 * F.nodes.size() + F.tris.size() + F.tshade.size() + F.mats.size());
+    if (sv->world_kind == FRT_WORLD_BVH && F.depth < kLdsMaxDepth && oct_bytes <= kLdsOctBytes)
+        F.nodes_oct.resize(8 * F.nodes.size());
+    for (int o = 0; o < 8 && !F.nodes_oct.empty(); ++o)
         for (size_t i = 0; i < F.nodes.size() / 4; ++i) {
             const float4 *n = &F.nodes[4 * i];
             const float b0[6] = {n[0].x, n[0].y, n[0].z, n[0].w, n[1].x, n[1].y};
@@ -1258,6 +1297,11 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     S.cam_w = f3d(sv->cam_w);
     S.cam_half_height = (float)sv->cam_half_height;
     S.env = f3d(sv->env_color);
+    auto d3d = [](const double *x) { return d3{x[0], x[1], x[2]}; };
+    S.cam64_o = d3d(sv->cam_origin); S.cam64_llc = d3d(sv->cam_lower_left);
+    S.cam64_h = d3d(sv->cam_horizontal); S.cam64_v = d3d(sv->cam_vertical);
+    S.cam64_u = d3d(sv->cam_u); S.cam64_vv = d3d(sv->cam_v);
+    S.lens_r64 = sv->cam_lens_radius;
     return FRT_OK;
 }
 
@@ -1279,7 +1323,10 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
     HIPCHK(c, hipSetDevice(c->device));
     FlatScene F;
     std::string err;
-    const int frc = flatten_scene(sv, F, err);
+    // fp64 records when this context's precision can pick the fp64 kernels for the scene
+    const bool want_f64 = c->precision == FRT_PRECISION_FP64 ||
+                          (c->precision == FRT_PRECISION_AUTO && sv->world_kind == FRT_WORLD_LIST);
+    const int frc = flatten_scene(sv, F, err, want_f64);
     if (frc != FRT_OK) return set_err(c, frc, err);
     free_scene(c);
     c->S = F.meta;
@@ -1293,6 +1340,10 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
         (rc = upload_vec(c, F.spheres, &S.spheres)) || (rc = upload_vec(c, F.smat, &S.sphere_mat)) ||
         (rc = upload_vec(c, F.mats, &S.mats)) || (rc = upload_vec(c, F.lights, &S.lights)) ||
         (rc = upload_vec(c, F.list, &S.list)))
+        return rc;
+    S.tris64 = nullptr; S.tshade64 = nullptr; S.tnorm64 = nullptr; S.spheres64 = nullptr;
+    if (want_f64 && ((rc = upload_vec(c, F.tris64, &S.tris64)) || (rc = upload_vec(c, F.tshade64, &S.tshade64)) ||
+                     (rc = upload_vec(c, F.tnorm64, &S.tnorm64)) || (rc = upload_vec(c, F.spheres64, &S.spheres64))))
         return rc;
     c->world_kind = S.world_kind;
     c->stack_needed = F.depth;
@@ -1313,7 +1364,9 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
     c->depth4 = F.depth4;
     c->scene_lds_bytes = sizeof(float4) * (F.nodes.size() + F.tris.size() + F.tshade.size() + F.mats.size());
     c->scene_lds_bytes4 = sizeof(float4) * (F.nodes4.size() + F.tris.size() + F.tshade.size() + F.mats.size());
-    c->scene_lds_bytes_oct = sizeof(float4) * (F.nodes_oct.size() + F.tris.size() + F.tshade.size() + F.mats.size());
+    c->scene_lds_bytes_oct = F.nodes_oct.empty() ? SIZE_MAX
+                             : sizeof(float4) * (F.nodes_oct.size() + F.tris.size() + F.tshade.size() + F.mats.size());
+    c->has_f64 = want_f64;
     c->have_scene = true;
     return FRT_OK;
 }
@@ -1322,71 +1375,95 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
 static bool bvh4_stack_fits(int depth4, int lds_entries) { return 3 * depth4 <= lds_entries + kBvh4Overflow; }
 constexpr int kSelftestStack = 8;   // small, so the host self-test exercises the overflow entries
 
-// Self-test hook (CPU-only unit tests): runs frt_path.hpp -- the code the
-// megakernel runs per lane -- on the host over the flattened scene.  Not a
-// render path: frt_render / frt_render_device never call it.
-extern "C" int frt_selftest_path_host(const frt_scene_view *sv, const frt_render_params *p, const int32_t *pixels,
-                                      int npix, float *out_rgb, frt_stats *st)
+// host image of the flattened scene as the kernels see it (HBM strides)
+static DevScene host_scene(const FlatScene &F)
 {
-    if (!sv || !p || !pixels || !out_rgb || npix < 0 || p->spp <= 0 || p->nx <= 0 || p->ny <= 0) return FRT_E_INVALID;
-    FlatScene F;
-    std::string err;
-    const int rc = flatten_scene(sv, F, err);
-    if (rc != FRT_OK) return rc;
-    if (p->integrator == FRT_INTEGRATOR_AO)
-        for (int i = 0; i < sv->n_materials; ++i)
-            if (sv->materials[i].type == FRT_MAT_METAL) return FRT_E_UNSUPPORTED;
     DevScene S = F.meta;
     S.nodes = F.nodes.data(); S.nodes4 = F.nodes4.data(); S.nodes_oct = F.nodes_oct.data();
     S.tris = F.tris.data(); S.tshade = F.tshade.data(); S.tnorm = F.tnorm.data();
     S.tuv = F.tuv.data(); S.texels = F.texels.data();
     S.spheres = F.spheres.data(); S.sphere_mat = F.smat.data(); S.mats = F.mats.data();
     S.lights = F.lights.data(); S.list = F.list.data();
-    std::vector<int> stack(std::max(F.depth + 1, kSelftestStack));
-    const bool brute = S.world_kind == FRT_WORLD_BVH && (p->flags & FRT_FLAG_BRUTE) && F.spheres.empty();
-    const bool wide = !brute && S.world_kind == FRT_WORLD_BVH && F.has4 && !(p->flags & FRT_FLAG_BVH2) &&
-                      bvh4_stack_fits(F.depth4, kSelftestStack);
+    S.tris64 = F.tris64.data(); S.tshade64 = F.tshade64.data(); S.tnorm64 = F.tnorm64.data();
+    S.spheres64 = F.spheres64.data();
+    return S;
+}
+
+// the self-test's per-pixel loop in precision R (fp64: the binary tree or the list)
+template <typename R>
+static void selftest_pixels(const DevScene &S, const FlatScene &F, const frt_render_params *p, const int32_t *pixels,
+                            int npix, bool brute, bool wide, std::vector<int> &stack, float *out_rgb, uint64_t cnt[3])
+{
     uint32_t n_ext = 0, n_sh = 0;
-    uint64_t n_cam = 0, ext = 0, sh = 0;
     for (int i = 0; i < npix; ++i) {
         const int pix = pixels[i];
-        if (pix < 0 || pix >= p->nx * p->ny) return FRT_E_INVALID;
         const int px = pix % p->nx, py = pix / p->nx;
-        f3 acc = mk3(0, 0, 0);
+        V3<R> acc = zero3<R>();
         for (int smp = 0; smp < p->spp; ++smp) {
-            PathState P;
+            PathState<R> P;
             path_begin(P, S, px, py, p->nx, p->ny, p->seed, (uint32_t)pix, (uint32_t)(smp + p->sample_offset));
-            ++n_cam;
+            ++cnt[0];
             for (;;) {
-                Hit h;
+                Hit<R> h;
                 if (brute) {
-                    Trav T;
+                    Trav<R> T;
                     if (trav_begin(T, S, S.root, P.ro, P.rd, P.rtmax)) brute_all(T, S, P.ro, P.rd, P.shadow);
                     h = T.h;
+                } else if (S.world_kind == FRT_WORLD_LIST) {
+                    h = trace<FRT_WORLD_LIST, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data());
+                } else if constexpr (!kIsF64<R>) {
+                    h = wide ? trace<kWorldBvh4, 1, kSelftestStack>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data())
+                             : trace<FRT_WORLD_BVH, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data());
                 } else {
-                    h = (S.world_kind == FRT_WORLD_LIST)
-                            ? trace<FRT_WORLD_LIST, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data())
-                        : wide ? trace<kWorldBvh4, 1, kSelftestStack>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data())
-                               : trace<FRT_WORLD_BVH, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data());
+                    h = trace<FRT_WORLD_BVH, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data());
                 }
                 n_ext = n_sh = 0;
                 const bool done = p->integrator == FRT_INTEGRATOR_AO ? ao_shade(P, S, h, n_sh)
                                   : p->integrator == FRT_INTEGRATOR_NORMALS ? normals_shade(P, S, h)
                                   : path_shade(P, S, h, p->max_depth, n_ext, n_sh);
-                ext += n_ext; sh += n_sh;
+                cnt[1] += n_ext; cnt[2] += n_sh;
                 if (done) break;
             }
             acc = acc + P.L;
         }
-        const float k = 1.0f / (float)p->spp;
-        out_rgb[3 * i] = acc.x * k; out_rgb[3 * i + 1] = acc.y * k; out_rgb[3 * i + 2] = acc.z * k;
+        const R k = R(1) / (R)p->spp;
+        out_rgb[3 * i] = (float)(acc.x * k); out_rgb[3 * i + 1] = (float)(acc.y * k); out_rgb[3 * i + 2] = (float)(acc.z * k);
     }
+}
+
+// Self-test hook (CPU-only unit tests): runs frt_path.hpp -- the code the
+// megakernel runs per lane -- on the host over the flattened scene, in fp32 or
+// (FRT_FLAG_FP64) in fp64.  Not a render path: frt_render / frt_render_device
+// never call it.
+extern "C" int frt_selftest_path_host(const frt_scene_view *sv, const frt_render_params *p, const int32_t *pixels,
+                                      int npix, float *out_rgb, frt_stats *st)
+{
+    if (!sv || !p || !pixels || !out_rgb || npix < 0 || p->spp <= 0 || p->nx <= 0 || p->ny <= 0) return FRT_E_INVALID;
+    for (int i = 0; i < npix; ++i)
+        if (pixels[i] < 0 || pixels[i] >= p->nx * p->ny) return FRT_E_INVALID;
+    const bool f64 = (p->flags & FRT_FLAG_FP64) != 0;
+    FlatScene F;
+    std::string err;
+    const int rc = flatten_scene(sv, F, err, f64);
+    if (rc != FRT_OK) return rc;
+    if (p->integrator == FRT_INTEGRATOR_AO)
+        for (int i = 0; i < sv->n_materials; ++i)
+            if (sv->materials[i].type == FRT_MAT_METAL) return FRT_E_UNSUPPORTED;
+    const DevScene S = host_scene(F);
+    std::vector<int> stack(std::max(F.depth + 1, kSelftestStack));
+    const bool brute = !f64 && S.world_kind == FRT_WORLD_BVH && (p->flags & FRT_FLAG_BRUTE) && F.spheres.empty();
+    const bool wide = !f64 && !brute && S.world_kind == FRT_WORLD_BVH && F.has4 && !(p->flags & FRT_FLAG_BVH2) &&
+                      bvh4_stack_fits(F.depth4, kSelftestStack);
+    uint64_t cnt[3] = {0, 0, 0};   // camera, extension, shadow
+    if (f64) selftest_pixels<double>(S, F, p, pixels, npix, brute, wide, stack, out_rgb, cnt);
+    else selftest_pixels<float>(S, F, p, pixels, npix, brute, wide, stack, out_rgb, cnt);
     if (st) {
         memset(st, 0, sizeof(*st));
-        st->camera_rays = n_cam; st->extension_rays = ext; st->shadow_rays = sh;
-        st->samples = n_cam; st->pixels = (uint64_t)npix;
+        st->camera_rays = cnt[0]; st->extension_rays = cnt[1]; st->shadow_rays = cnt[2];
+        st->samples = cnt[0]; st->pixels = (uint64_t)npix;
         st->stack_entries = wide ? (uint32_t)kSelftestStack : (uint32_t)stack.size();
         st->bvh_depth = (uint32_t)(wide ? F.depth4 : F.depth);   // which tree was traversed
+        st->fp64 = f64 ? 1u : 0u;
     }
     return FRT_OK;
 }
@@ -1400,14 +1477,9 @@ extern "C" int frt_selftest_mlt_paths_host(const frt_scene_view *sv, int nx, int
     if (!sv || !out6 || n < 0 || nx <= 0 || ny <= 0) return FRT_E_INVALID;
     FlatScene F;
     std::string err;
-    const int rc = flatten_scene(sv, F, err);
+    const int rc = flatten_scene(sv, F, err, false);
     if (rc != FRT_OK) return rc;
-    DevScene S = F.meta;
-    S.nodes = F.nodes.data(); S.nodes4 = F.nodes4.data(); S.nodes_oct = F.nodes_oct.data();
-    S.tris = F.tris.data(); S.tshade = F.tshade.data(); S.tnorm = F.tnorm.data();
-    S.tuv = F.tuv.data(); S.texels = F.texels.data();
-    S.spheres = F.spheres.data(); S.sphere_mat = F.smat.data(); S.mats = F.mats.data();
-    S.lights = F.lights.data(); S.list = F.list.data();
+    const DevScene S = host_scene(F);
     std::vector<int> stack(std::max(F.depth + 1, 1));
     for (int i = 0; i < n; ++i) {
         PrndSource src{nullptr, 0, 0, rng_key(seed ^ kMltBootSalt, (uint32_t)i, 0u), 0u, true, 0.0f, 0.0f};
@@ -1416,7 +1488,7 @@ extern "C" int frt_selftest_mlt_paths_host(const frt_scene_view *sv, int nx, int
         uint32_t ne = 0, ns = 0;
         for (;;) {
             if (mlt_beyond(M)) { M.P.L = M.P.L + M.P.beta * S.env; break; }
-            const Hit h = (S.world_kind == FRT_WORLD_LIST)
+            const Hit<float> h = (S.world_kind == FRT_WORLD_LIST)
                               ? trace<FRT_WORLD_LIST, 1>(S, M.P.ro, M.P.rd, M.P.rtmax, M.P.shadow, stack.data())
                               : trace<FRT_WORLD_BVH, 1>(S, M.P.ro, M.P.rd, M.P.rtmax, M.P.shadow, stack.data());
             if (mlt_shade(M, S, h, src, ne, ns)) break;
@@ -1486,13 +1558,15 @@ struct Launcher {
     int waves = 0;
     bool lds_scene = false;
     bool wide = false;      // 4-wide quantized BVH
+    bool f64 = false;       // the fp64 kernel
 };
 template <int STACK, int WORLD, bool LDS, int WAVES = 1, bool SPEC = false, int MATS = kMatsNone,
-          int KIND = FRT_INTEGRATOR_PATH>
+          int KIND = FRT_INTEGRATOR_PATH, typename R = float>
 static Launcher make_launcher(size_t scene_bytes)
 {
     Launcher L;
-    L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES, SPEC, MATS, KIND>);
+    L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES, SPEC, MATS, KIND, R>);
+    L.f64 = kIsF64<R>;
     L.lds = (WORLD != FRT_WORLD_LIST ? (size_t)STACK * kBlock * sizeof(int) : 0) +
             (size_t)kItemWords * kBlock * sizeof(int) + (LDS ? scene_bytes : 0);
     L.stack = STACK;
@@ -1632,8 +1706,42 @@ static int pick_launcher_kind(const frt_ctx *c, int flags, Launcher &L)
     }
     return FRT_OK;
 }
-static int pick_launcher(const frt_ctx *c, int integrator, int flags, Launcher &L)
+// fp64 kernels (path only; DESIGN.md "Precision"): the list world with the
+// scene's material set, or the binary tree from HBM with every material
+// compiled in (the debugging build; no register cap, stack 32 or 64)
+template <int MATS>
+static int pick_launcher_f64_t(const frt_ctx *c, Launcher &L)
 {
+    if (c->world_kind == FRT_WORLD_LIST) {
+        L = make_launcher<16, FRT_WORLD_LIST, false, 1, false, MATS, FRT_INTEGRATOR_PATH, double>(0);
+        return FRT_OK;
+    }
+    const int d = c->stack_needed;
+    if (d < 32) L = make_launcher<32, FRT_WORLD_BVH, false, 1, false, kMatsAll, FRT_INTEGRATOR_PATH, double>(0);
+    else if (d < 64) L = make_launcher<64, FRT_WORLD_BVH, false, 1, false, kMatsAll, FRT_INTEGRATOR_PATH, double>(0);
+    else return FRT_E_UNSUPPORTED;
+    return FRT_OK;
+}
+// does this render run the fp64 kernels?  FRT_FLAG_FP64 / _FP32 override the
+// context's precision for one call (A/B)
+static bool use_f64(const frt_ctx *c, const frt_render_params *p)
+{
+    if (p->integrator != FRT_INTEGRATOR_PATH || (p->flags & FRT_FLAG_FP32)) return false;
+    if (p->flags & FRT_FLAG_FP64) return true;
+    return c->precision == FRT_PRECISION_FP64 || (c->precision == FRT_PRECISION_AUTO && c->world_kind == FRT_WORLD_LIST);
+}
+static int pick_launcher(const frt_ctx *c, int integrator, int flags, Launcher &L, bool f64)
+{
+    if (f64) {
+        if (!c->has_f64) return FRT_E_INVALID;
+        switch (c->mats) {
+        case kMatsNone: return pick_launcher_f64_t<kMatsNone>(c, L);
+        case kMatsTex: return pick_launcher_f64_t<kMatsTex>(c, L);
+        case kMatsSpec:
+        case kMatsSpec | kMatsTex: return pick_launcher_f64_t<kMatsSpec | kMatsTex>(c, L);
+        default: return pick_launcher_f64_t<kMatsAll>(c, L);
+        }
+    }
     if (integrator == FRT_INTEGRATOR_AO) return pick_launcher_kind<FRT_INTEGRATOR_AO>(c, flags, L);
     if (integrator == FRT_INTEGRATOR_NORMALS) return pick_launcher_kind<FRT_INTEGRATOR_NORMALS>(c, flags, L);
     switch (c->mats) {   // the smallest kernel covering the scene's materials
@@ -1798,7 +1906,12 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     const uint32_t n_slots = (uint32_t)nmt * T * T;
     // kernel variant: stack depth, world kind, LDS-resident scene
     Launcher L;
-    if (pick_launcher(c, p->integrator, p->flags, L) != FRT_OK) return set_err(c, FRT_E_UNSUPPORTED, "BVH deeper than 63 levels");
+    const bool f64 = use_f64(c, p);
+    const int prc = pick_launcher(c, p->integrator, p->flags, L, f64);
+    if (prc == FRT_E_INVALID)
+        return set_err(c, prc, "fp64 render of a scene uploaded without fp64 records: frt_set_precision(FRT_PRECISION_FP64) "
+                               "before frt_upload_scene");
+    if (prc != FRT_OK) return set_err(c, FRT_E_UNSUPPORTED, "BVH deeper than 63 levels");
     int bpc = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, L.fn, kBlock, L.lds) != hipSuccess || bpc <= 0) bpc = 1;
     const int grid = c->n_cu * bpc;
@@ -1897,6 +2010,7 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
         stats->scene_bytes = c->scene_lds_bytes;
         stats->kernel_ms = ms;
         stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+        stats->fp64 = L.f64 ? 1u : 0u;
     }
     return FRT_OK;
 }

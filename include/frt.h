@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FRT_ABI_VERSION 7
+#define FRT_ABI_VERSION 8
 
 enum {
     FRT_OK = 0,
@@ -59,7 +59,18 @@ enum { FRT_FLAG_NO_LDS_SCENE = 1,      /* render_params.flags: keep small scenes
        FRT_FLAG_BVH4 = 32,             /* 4-wide nodes for LDS-resident scenes too (A/B timing)          */
        FRT_FLAG_BRUTE = 64,            /* tiny LDS scenes: every triangle in lockstep (A/B timing)       */
        FRT_FLAG_SPEC = 128,            /* 4-wide HBM plan: speculative traversal (A/B timing)            */
-       FRT_FLAG_NO_OCT = 256 };        /* LDS binary plan without the per-octant node copies (A/B timing) */
+       FRT_FLAG_NO_OCT = 256,          /* LDS binary plan without the per-octant node copies (A/B timing) */
+       FRT_FLAG_FP64 = 512,            /* path: the fp64 kernel for this call (self-test: fp64 host replay) */
+       FRT_FLAG_FP32 = 1024 };         /* path: the fp32 kernels even where the precision picks fp64      */
+
+/* Kernel precision (frt_set_precision).  The reference computes in fp64
+ * (geometry.h:351).  FRT_PRECISION_AUTO: fp64 for list worlds (hitable_list,
+ * e.g. veach_mis: a few primitives, and lights small enough -- r = 0.033 --
+ * that fp32 rounding moves samples onto or off them), fp32 for BVH worlds.
+ * FRT_PRECISION_FP64: every path render in fp64 (the binary tree from HBM:
+ * the debugging build SURVEY 8(a) names).  FRT_PRECISION_FP32: fp32 only.
+ * AO, normals and PSS-MLT always run in fp32. */
+enum { FRT_PRECISION_AUTO = 0, FRT_PRECISION_FP32 = 1, FRT_PRECISION_FP64 = 2 };
 
 /* primitive reference: triangle t -> t ; sphere k -> FRT_PRIM_SPHERE | k */
 #define FRT_PRIM_SPHERE (1 << 30)
@@ -185,6 +196,8 @@ typedef struct frt_stats {
     uint32_t stack_entries;  /* per-lane LDS traversal stack                    */
     uint32_t bvh_depth;      /* levels of the device BVH (after leaf collapse)  */
     uint64_t scene_bytes;    /* nodes + triangles + shading records + materials */
+    uint32_t fp64;           /* 1: the fp64 kernel ran (ABI 8)                  */
+    uint32_t reserved;
 } frt_stats;
 
 int frt_get_abi_version(void);
@@ -194,6 +207,10 @@ typedef struct frt_ctx frt_ctx;
 int frt_create(int hip_device, frt_ctx **out);
 int frt_destroy(frt_ctx *ctx);
 const char *frt_last_error(const frt_ctx *ctx);
+/* FRT_PRECISION_*; read by the next frt_upload_scene (fp64 records are
+ * uploaded only when the precision can select the fp64 kernels for that
+ * scene) and by every render.  Default FRT_PRECISION_AUTO. */
+int frt_set_precision(frt_ctx *ctx, int precision);
 
 /* Copy the scene to HBM (fp32 device layout, DESIGN.md "Data layout").  The
  * view's arrays are only read during the call. */
