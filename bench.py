@@ -465,6 +465,17 @@ def main():
                           (f"PSS-MLT {cpu['sample']} on the same {nx}x{ny} frame ({cpu['rays']} rays, "
                            f"{cpu['seconds']:.1f} s) on {threads} threads; fp64 C restatement of pssmlt.cpp")},
         }
+        ratio = load_profile(os.path.join("r03", "cpu_ratio.json"), "ratio_port_over_first_ray")
+        if line["cpu_baseline"] is not None and ratio:
+            # first_ray itself cannot be built here (cpp-taskflow, GLFW); the
+            # port's single-thread speed over first_ray's on C1 in the same container converts
+            line["cpu_baseline"]["first_ray_estimate"] = {
+                "value": round(cpu["mrays"] / ratio, 3), "unit": "Mrays/s", "ratio_port_over_first_ray": ratio,
+                "basis": ("cpu_baseline / ratio; ratio = the oracle's 1-thread Mrays/s on C1 (CornellBox "
+                          "256x256x16) over first_ray's 2.14 (SURVEY.md section 6), same container "
+                          "(profiles/r03/cpu_ratio.json, tools/cpu_ratio.py). Assumes first_ray scales like the "
+                          "port; as written its shared ray counters scale negatively (1.25 Mrays/s on 8 threads, "
+                          "SURVEY section 6)")}
         if ns is not None:
             nkey = f"cornell_1m:{ns['nx']}x{ns['ny']}"
             ncpu = None

@@ -788,6 +788,7 @@ struct FlatScene {
     bool has4 = false;           // nodes4 / root4 usable
     int root4 = 0, depth4 = 0;
     std::vector<int> smat, lights, list;
+    std::vector<float4> list_box;   // list worlds: 2 per entry (DevScene::list_box)
     DevScene meta{};     // scalars + camera; pointers filled by the consumer
     int depth = 0;
 };
@@ -1248,6 +1249,22 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     }
     F.list.resize(sv->world_kind == FRT_WORLD_LIST ? sv->n_list : 0);
     for (size_t i = 0; i < F.list.size(); ++i) F.list[i] = dev_ref(sv->list[i]);
+    // list worlds: each entry's box, padded outward as the BVH's (4e-6 of the scene scale)
+    if (!F.list.empty()) {
+        std::vector<double> lo(3 * F.list.size()), hi(3 * F.list.size());
+        double scale = 1.0;
+        for (size_t i = 0; i < F.list.size(); ++i) {
+            prim_box(sv->list[i], &lo[3 * i], &hi[3 * i]);
+            for (int k = 0; k < 3; ++k) scale = std::max(scale, std::max(std::fabs(lo[3 * i + k]), std::fabs(hi[3 * i + k])));
+        }
+        const double pad = 4e-6 * scale;
+        F.list_box.resize(2 * F.list.size());
+        for (size_t i = 0; i < F.list.size(); ++i) {
+            const double *l = &lo[3 * i], *h = &hi[3 * i];
+            F.list_box[2 * i] = make_float4(round_down(l[0] - pad), round_down(l[1] - pad), round_down(l[2] - pad), 0.0f);
+            F.list_box[2 * i + 1] = make_float4(round_up(h[0] + pad), round_up(h[1] + pad), round_up(h[2] + pad), 0.0f);
+        }
+    }
 
     // octant copies of the binary nodes: child boxes as (near xyz, far xyz).
     // Only the LDS binary plan reads them, and only when they fit its budget
@@ -1339,7 +1356,7 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
         (rc = upload_vec(c, F.tuv, &S.tuv)) || (rc = upload_vec(c, F.texels, &S.texels)) ||
         (rc = upload_vec(c, F.spheres, &S.spheres)) || (rc = upload_vec(c, F.smat, &S.sphere_mat)) ||
         (rc = upload_vec(c, F.mats, &S.mats)) || (rc = upload_vec(c, F.lights, &S.lights)) ||
-        (rc = upload_vec(c, F.list, &S.list)))
+        (rc = upload_vec(c, F.list, &S.list)) || (rc = upload_vec(c, F.list_box, &S.list_box)))
         return rc;
     S.tris64 = nullptr; S.tshade64 = nullptr; S.tnorm64 = nullptr; S.spheres64 = nullptr;
     if (want_f64 && ((rc = upload_vec(c, F.tris64, &S.tris64)) || (rc = upload_vec(c, F.tshade64, &S.tshade64)) ||
@@ -1383,7 +1400,7 @@ static DevScene host_scene(const FlatScene &F)
     S.tris = F.tris.data(); S.tshade = F.tshade.data(); S.tnorm = F.tnorm.data();
     S.tuv = F.tuv.data(); S.texels = F.texels.data();
     S.spheres = F.spheres.data(); S.sphere_mat = F.smat.data(); S.mats = F.mats.data();
-    S.lights = F.lights.data(); S.list = F.list.data();
+    S.lights = F.lights.data(); S.list = F.list.data(); S.list_box = F.list_box.data();
     S.tris64 = F.tris64.data(); S.tshade64 = F.tshade64.data(); S.tnorm64 = F.tnorm64.data();
     S.spheres64 = F.spheres64.data();
     return S;
@@ -1587,6 +1604,9 @@ static Launcher bvh_launcher(int waves, size_t sb)
     // (RMSE 0.07, tests/test_gpu_conductors.py::test_register_caps_agree).
     // A 6-wave request runs the 5-wave kernel.
     if constexpr ((MATS & kMatsSpecAny) != 0) {
+#if defined(FRT_EXP_SPEC_W6)   // experiment builds: the 6-wave specular kernels (register-cap investigation)
+        if (waves == 6) return make_launcher<STACK, WORLD, LDS, 6, SPEC, MATS>(sb);
+#endif
         if (waves >= 6) waves = 5;
     } else {
         if (waves == 6) return make_launcher<STACK, WORLD, LDS, FRT_EXP_W6, SPEC, MATS>(sb);
@@ -1737,7 +1757,7 @@ static int pick_launcher(const frt_ctx *c, int integrator, int flags, Launcher &
         switch (c->mats) {
         case kMatsNone: return pick_launcher_f64_t<kMatsNone>(c, L);
         case kMatsTex: return pick_launcher_f64_t<kMatsTex>(c, L);
-        case kMatsSpec:
+        case kMatsSpec: return pick_launcher_f64_t<kMatsSpec>(c, L);   // veach_mis (C3): phong plates
         case kMatsSpec | kMatsTex: return pick_launcher_f64_t<kMatsSpec | kMatsTex>(c, L);
         default: return pick_launcher_f64_t<kMatsAll>(c, L);
         }

@@ -105,6 +105,10 @@ def lib():
         L.ora_scene_add_sphere.argtypes = [ctypes.c_void_p, dp, ctypes.c_double, dp, ctypes.c_int]
         L.ora_scene_add_image.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                           ctypes.POINTER(ctypes.c_int)]
+        L.ora_image_lookup.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_double,
+                                       ctypes.c_double, dp]
+        L.ora_env_uv.argtypes = [dp, dp, dp]
+        L.ora_env_uv.restype = None
         L.ora_scene_set_camera.argtypes = [ctypes.c_void_p, dp, dp, dp, ctypes.c_double, ctypes.c_double,
                                            ctypes.c_double, ctypes.c_double]
         L.ora_scene_set_camera.restype = None

@@ -2112,6 +2112,33 @@ int ora_scene_add_image(ora_scene *s, int nx, int ny, int format, const void *da
     *index = s->nimages++;
     return 0;
 }
+/* Test hooks (pinned by the image KATs of oracle/ref_kat.cpp):
+ * image_texture::value on an image given as stb decodes it, and the direction
+ * -> (u, v) map of environment_map::eval (material.h:219-232). */
+int ora_image_lookup(int nx, int ny, int format, const void *data, double u, double v, double *out3)
+{
+    if (nx <= 0 || ny <= 0 || !data || !out3 || (format != 0 && format != 1)) return -1;
+    const size_t n = (size_t)nx * ny * 3;
+    double *rgb = (double *)malloc(n * sizeof(double));
+    if (!rgb) return -1;
+    for (size_t k = 0; k < n; ++k)
+        rgb[k] = format == 0 ? from_srgb(((const uint8_t *)data)[k] / 255.0) : (double)((const float *)data)[k];
+    const ora_image img = {nx, ny, rgb};
+    vstore(out3, image_value(&img, u, v));
+    free(rgb);
+    return 0;
+}
+void ora_env_uv(const double *d, double *u, double *v)
+{
+    const v3 direction = unit(vload(d));
+    double phi = atan2(direction.e[0], -direction.e[2]);
+    double theta = acos(direction.e[1]);
+    phi = (phi < 0) ? (phi + M_PI * 2) : phi;
+    theta = (theta < 0) ? (theta + M_PI) : theta;
+    *u = phi / (2.0 * M_PI);
+    *v = theta / (M_PI);
+}
+
 /* Scene::env_map with another constant texture (material.h:206-232); the
  * reference scenes' environment is black, so AO / normals tests set one. */
 void ora_scene_set_env(ora_scene *s, const double *rgb) { s->env = vload(rgb); }

@@ -101,6 +101,10 @@ void ora_scene_set_env(ora_scene *s, const double *rgb);
 /* image_texture's decoded image (format 0: nx*ny*3 bytes, sRGB; 1: floats); *index
  * = its material description entry d[26] (d[20] = 2) */
 int ora_scene_add_image(ora_scene *s, int nx, int ny, int format, const void *data, int *index);
+/* test hooks: image_texture::value (format 0 = 8-bit sRGB bytes, 1 = floats)
+ * and environment_map::eval's direction -> (u, v) */
+int ora_image_lookup(int nx, int ny, int format, const void *data, double u, double v, double *out3);
+void ora_env_uv(const double *d, double *u, double *v);
 /* ao.cpp:21 t_max = world bounding box height * 0.5 (NaN for list worlds) */
 double ora_scene_ao_tmax(const ora_scene *s);
 

@@ -410,6 +410,106 @@ static void kat_texture(int ncases)
     }
 }
 
+// image_texture::value (texture.h:59-95) on the reference's own `image`
+// (image.h / image.cpp, stb vendored): u, v -> the texel it returns.  The
+// queries cover the wrap (u < 0, u > 1) and the upper-edge clamp (u = 1).
+static void img_query(const char *kind, const image_texture &tex, double u, double v)
+{
+    hit_record h;
+    h.u = u;
+    h.v = v;
+    const Vector3f c = tex.value(h);
+    printf("%s", kind); p(u); p(v); bar(); pv(c); printf("\n");
+}
+static double edge_coord(int i, int n, int k)   // lands in texel i (k = 0) or wraps to it (k = +-1, +-2)
+{
+    return ((double)i + 0.25 + 0.5 * urand()) / n + k;
+}
+static void kat_image(const char *hdr_path)
+{
+    // 8-bit image through image(unsigned char *, nx, ny, nn) (image.h:25).  That
+    // constructor leaves `type` unset, so the harness sets it to an LDR format:
+    // the FromSrgb(byte / 255.0) branch (texture.h:82-84)
+    const int nx = 5, ny = 3;
+    static unsigned char bytes[nx * ny * 3];
+    for (int i = 0; i < nx * ny * 3; ++i) bytes[i] = (unsigned char)(next_u64() & 0xff);
+    bytes[0] = 0; bytes[1] = 10; bytes[2] = 255;                // the sRGB curve's linear segment and 1.0
+    printf("img_ldr_data"); p(nx); p(ny); for (unsigned char b : bytes) p(b); bar(); printf("\n");
+    {
+        auto img = std::make_unique<image>(bytes, nx, ny, 3);
+        img->type = formats::STBI_PNG;
+        image_texture tex(std::move(img));
+        for (int c = 0; c < 60; ++c)
+            img_query("img_ldr", tex, edge_coord((int)(next_u64() % nx), nx, (int)(next_u64() % 5) - 2),
+                      edge_coord((int)(next_u64() % ny), ny, (int)(next_u64() % 5) - 2));
+        img_query("img_ldr", tex, 1.0, 1.0);                    // i == nx, j == ny: clamped
+        img_query("img_ldr", tex, 0.0, 0.0);
+        img_query("img_ldr", tex, -1.0, 2.0);
+        img_query("img_ldr", tex, -0.1 / nx, -0.1 / ny);        // truncates to 0
+        tex.img.release();                                       // the harness owns `bytes`
+    }
+    // HDR branch (texture.h:74-79) on an in-memory float image, and
+    // environment_map::eval (material.h:219-232) over the same texture
+    const int hx = 7, hy = 5;
+    static float hdr[hx * hy * 3];
+    for (float &f : hdr) f = (float)(urand() * 4.0);
+    printf("img_hdr_data"); p(hx); p(hy); for (float f : hdr) p(f); bar(); printf("\n");
+    {
+        auto img = std::make_unique<image>(nullptr, hx, hy, 3);
+        img->type = formats::STBI_HDR;
+        img->dataf = hdr;
+        image_texture tex(std::move(img));
+        for (int c = 0; c < 60; ++c)
+            img_query("img_hdr", tex, edge_coord((int)(next_u64() % hx), hx, (int)(next_u64() % 5) - 2),
+                      edge_coord((int)(next_u64() % hy), hy, (int)(next_u64() % 5) - 2));
+        img_query("img_hdr", tex, 1.0, 1.0);
+        tex.img.release();
+        auto img2 = std::make_unique<image>(nullptr, hx, hy, 3);
+        img2->type = formats::STBI_HDR;
+        img2->dataf = hdr;
+        environment_map env(std::make_unique<image_texture>(std::move(img2)));
+        for (int c = 0; c < 120; ++c) {
+            Vector3f d(srand2(1), srand2(1), srand2(1));
+            if (c < 6) d = Vector3f(c == 0 ? 1 : c == 1 ? -1 : 0, c == 2 ? 1 : c == 3 ? -1 : 0, c == 4 ? 1 : c == 5 ? -1 : 0);
+            hit_record h;
+            const Vector3f e = env.eval(ray(Vector3f(0, 0, 0), d), h, 0);
+            printf("env_img"); pv(d); bar(); pv(e); printf("\n");
+        }
+        static_cast<image_texture *>(env.env_map_tex.get())->img.release();
+    }
+    // data/test.hdr through image(file, STBI_HDR) (image.cpp:11-17): the
+    // texels of a window -- 5 x 5 around the texel of highest local contrast plus the first
+    // and last columns / rows -- read with image_texture::value(x, y)
+    // (texture.h:90-95), and value(u, v) queries that land in the window
+    // directly or through the wrap (k = +1 maps back to texel i; k = -1 to
+    // i + 1, as (int) truncates toward zero) and the u = v = 1 clamp
+    auto img = std::make_unique<image>(hdr_path, formats::STBI_HDR);
+    const int fx = img->nx, fy = img->ny;
+    int bx = 2, by = 2;
+    float best = -1.0f;
+    for (int y = 2; y < fy - 3; ++y)
+        for (int x = 2; x < fx - 3; ++x) {
+            const float *t = &img->dataf[3 * ((size_t)y * fx + x)], *r = t + 3, *d = t + 3 * (size_t)fx;
+            float g = 0.0f;   // local contrast: distinct texels in the window
+            for (int ch = 0; ch < 3; ++ch) g += std::fabs(t[ch] - r[ch]) + std::fabs(t[ch] - d[ch]);
+            if (g > best) { best = g; bx = x; by = y; }
+        }
+    image_texture tex(std::move(img));
+    std::vector<int> cols = {0, 1, fx - 1}, rows = {0, 1, fy - 1};
+    for (int k = -2; k <= 3; ++k) { cols.push_back(bx + k); rows.push_back(by + k); }
+    for (int x : cols)
+        for (int y : rows) {
+            const Vector3f c = tex.value(x, y);
+            printf("hdr_file_texel"); p(fx); p(fy); p(x); p(y); bar(); pv(c); printf("\n");
+        }
+    for (int c = 0; c < 80; ++c) {
+        const int i = bx - 2 + (int)(next_u64() % 5), j = by - 2 + (int)(next_u64() % 5);
+        img_query("hdr_file", tex, edge_coord(i, fx, (int)(next_u64() % 3) - 1), edge_coord(j, fy, (int)(next_u64() % 3) - 1));
+    }
+    img_query("hdr_file", tex, 1.0, 1.0);
+    img_query("hdr_file", tex, 0.0, 0.0);
+}
+
 static void kat_pfm()
 {
     const int nx = 3, ny = 2, nn = 3;
@@ -435,5 +535,6 @@ int main(int argc, char **argv)
     kat_specular(n);
     kat_texture(n);
     kat_pfm();
+    kat_image(argc > 2 ? argv[2] : "/root/reference/first_ray/data/test.hdr");
     return 0;
 }

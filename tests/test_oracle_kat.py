@@ -1,6 +1,7 @@
 """The C restatement (oracle/) against known answers produced by the
 reference's OWN code (oracle/_ref/ref_kat built from /root/reference sources;
 fixtures in tests/golden/kat_ref.json).  Bit-exact (fp64) for every case."""
+import ctypes
 import json
 import os
 
@@ -222,6 +223,76 @@ def test_checker_texture(kat):
     assert 0 < odd < n and nan > 0, (n, odd, nan)
 
 
+def image_lookup(nx, ny, fmt, data, u, v):
+    out = np.zeros(3)
+    rc = oracle.lib().ora_image_lookup(nx, ny, fmt, data.ctypes.data, u, v, out.ctypes.data_as(darr([0])[1].__class__))
+    assert rc == 0
+    return out
+
+
+def test_image_texture_ldr(kat):
+    """image_texture::value (texture.h:59-88) on an 8-bit image built with the
+    reference's image(unsigned char *, nx, ny, nn) (image.h:25): FromSrgb(byte /
+    255), the wrap of indices outside [0, n] (util.h:125-128) and the u = 1 clamp."""
+    (ins, _), = kat["img_ldr_data"]
+    x = H(ins)
+    nx, ny = int(x[0]), int(x[1])
+    data = np.array(x[2:], np.uint8)
+    assert data.size == nx * ny * 3
+    for q, outs in kat["img_ldr"]:
+        u, v = H(q)
+        assert np.array_equal(image_lookup(nx, ny, 0, data, u, v), H(outs)), (u, v)
+    assert len(kat["img_ldr"]) >= 60
+
+
+def test_image_texture_hdr(kat):
+    """The HDR branch (texture.h:74-79: the float as is) on an in-memory float image."""
+    (ins, _), = kat["img_hdr_data"]
+    x = H(ins)
+    nx, ny = int(x[0]), int(x[1])
+    data = np.array(x[2:], np.float32)
+    for q, outs in kat["img_hdr"]:
+        u, v = H(q)
+        assert np.array_equal(image_lookup(nx, ny, 1, data, u, v), H(outs)), (u, v)
+
+
+def test_environment_map_image(kat):
+    """environment_map::eval (material.h:219-232) over that image texture: the
+    direction -> (phi = atan2(x, -z), theta = acos(y)) -> (u, v) map, then the lookup."""
+    (ins, _), = kat["img_hdr_data"]
+    x = H(ins)
+    nx, ny = int(x[0]), int(x[1])
+    data = np.array(x[2:], np.float32)
+    L = oracle.lib()
+    for d, outs in kat["env_img"]:
+        u, v = ctypes.c_double(), ctypes.c_double()
+        L.ora_env_uv(darr(H(d))[1], ctypes.byref(u), ctypes.byref(v))
+        assert np.array_equal(image_lookup(nx, ny, 1, data, u.value, v.value), H(outs)), d
+    assert len(kat["env_img"]) >= 100
+
+
+def test_image_texture_hdr_file(kat):
+    """data/test.hdr decoded by the reference's image(file, STBI_HDR) (image.cpp:11-17, stb):
+    the texels of a window (image_texture::value(x, y)) and value(u, v) queries landing in
+    it directly, through the wrap, and at the u = v = 1 clamp.  The window's texels go into
+    an otherwise-NaN image, so a wrong index shows up as NaN."""
+    tex = {}
+    fx = fy = None
+    for ins, outs in kat["hdr_file_texel"]:
+        fx, fy, xx, yy = (int(t) for t in H(ins))
+        tex[(xx, yy)] = H(outs)
+    data = np.full((fy, fx, 3), np.nan, np.float32)
+    for (xx, yy), c in tex.items():
+        data[yy, xx] = c
+    hit = 0
+    for q, outs in kat["hdr_file"]:
+        u, v = H(q)
+        got = image_lookup(fx, fy, 1, data, u, v)
+        assert np.array_equal(got, H(outs)), (u, v, got, H(outs))
+        hit += bool(got.sum() > 0)
+    assert hit > 20
+
+
 def test_pfm_bytes(kat, tmp_path):
     p = kat["pfm"]
     data = H(p["data"])
@@ -235,6 +306,7 @@ def test_kat_coverage(kat):
     assert {k for k in kat if not k.startswith("_")} == {
         "tri_hit", "sphere_hit", "aabb_hit", "camera", "cosine", "tri_sample", "sphere_sample",
         "miweight", "fromsrgb", "pick", "sort", "list_hit", "pfm", "fresnel", "phong", "dielectric",
-        "metal", "conductor", "tex_sphere", "tex_tri"}
+        "metal", "conductor", "tex_sphere", "tex_tri", "img_ldr_data", "img_ldr", "img_hdr_data", "img_hdr",
+        "env_img", "hdr_file_texel", "hdr_file"}
     hits = sum(int(float.fromhex(o[0])) for _, o in kat["tri_hit"])
     assert 20 < hits < len(kat["tri_hit"]) - 20, "KAT set should mix hits and misses"
