@@ -99,7 +99,6 @@ struct DevScene {
     const float4 *texels;    // image_texture texels (rgb, -) of every image, in HBM
     const int *lights;       // device prim refs
     const int *list;         // device prim refs (list worlds)
-    const float4 *list_box;  // 2 per list entry: the prim's box (lo | hi), padded outward like the BVH's
     const uint4 *nodes4;     // 4 x uint4 per 4-wide node (HBM-resident scenes; DESIGN.md "BVH4Q")
     const float4 *nodes_oct; // 8 copies of `nodes`, copy o with each child box as (near xyz, far xyz) for
                              // rays of octant o (bit a set: 1/d_a < 0); LDS plans copy them (kWorldBvh2Oct)
@@ -464,20 +463,14 @@ FRT_HD Hit<float> trace_bvh4(const DevScene &S, f3 o, f3 d, float tmax, bool any
     return T.h;
 }
 
-// hitable_list::hit: in list order, triangles strict '<', spheres inclusive
-// (sphere.h:34).  Each prim's padded box is tested first, in fp32 in either
-// precision: the boxes contain their prims with a margin (4e-6 of the scene
-// scale) far above the fp32 rounding of the ray and the slab test, so a
-// missed box is a missed prim, and the list order and tie rules are untouched.
-// In fp64 the box test replaces most of the fp64 primitive tests.
+// hitable_list::hit: in list order, triangles strict '<', spheres inclusive (sphere.h:34).
+// (A per-prim fp32 box test before the primitive test was 12-15 % slower on
+// veach_mis in both precisions -- its big plates and floor pass their boxes:
+// profiles/r03/r03c_ab_veach_listbox_f64waves.jsonl.)
 template <typename R> FRT_HD Hit<R> trace_list(const DevScene &S, V3<R> o, V3<R> d, R tmax, bool anyhit)
 {
     Hit<R> h{-1, tmax, R(0), R(0)};
-    const SlabRay<float> sr = slab_ray(f3{(float)o.x, (float)o.y, (float)o.z}, f3{(float)d.x, (float)d.y, (float)d.z});
     for (int i = 0; i < S.n_list; ++i) {
-        const float4 lo = S.list_box[2 * i], hi = S.list_box[2 * i + 1];
-        if (slab_entry<float>(lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, sr, 0.0f, (float)h.t * 1.0001f) == __builtin_inff())
-            continue;
         const int ref = S.list[i];
         R u, v;
         const R t = prim_t(S, ref, o, d, Cst<R>::eps, h.t, u, v);

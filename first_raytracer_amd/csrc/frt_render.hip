@@ -788,7 +788,6 @@ struct FlatScene {
     bool has4 = false;           // nodes4 / root4 usable
     int root4 = 0, depth4 = 0;
     std::vector<int> smat, lights, list;
-    std::vector<float4> list_box;   // list worlds: 2 per entry (DevScene::list_box)
     DevScene meta{};     // scalars + camera; pointers filled by the consumer
     int depth = 0;
 };
@@ -1249,22 +1248,6 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     }
     F.list.resize(sv->world_kind == FRT_WORLD_LIST ? sv->n_list : 0);
     for (size_t i = 0; i < F.list.size(); ++i) F.list[i] = dev_ref(sv->list[i]);
-    // list worlds: each entry's box, padded outward as the BVH's (4e-6 of the scene scale)
-    if (!F.list.empty()) {
-        std::vector<double> lo(3 * F.list.size()), hi(3 * F.list.size());
-        double scale = 1.0;
-        for (size_t i = 0; i < F.list.size(); ++i) {
-            prim_box(sv->list[i], &lo[3 * i], &hi[3 * i]);
-            for (int k = 0; k < 3; ++k) scale = std::max(scale, std::max(std::fabs(lo[3 * i + k]), std::fabs(hi[3 * i + k])));
-        }
-        const double pad = 4e-6 * scale;
-        F.list_box.resize(2 * F.list.size());
-        for (size_t i = 0; i < F.list.size(); ++i) {
-            const double *l = &lo[3 * i], *h = &hi[3 * i];
-            F.list_box[2 * i] = make_float4(round_down(l[0] - pad), round_down(l[1] - pad), round_down(l[2] - pad), 0.0f);
-            F.list_box[2 * i + 1] = make_float4(round_up(h[0] + pad), round_up(h[1] + pad), round_up(h[2] + pad), 0.0f);
-        }
-    }
 
     // octant copies of the binary nodes: child boxes as (near xyz, far xyz).
     // Only the LDS binary plan reads them, and only when they fit its budget
@@ -1356,7 +1339,7 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
         (rc = upload_vec(c, F.tuv, &S.tuv)) || (rc = upload_vec(c, F.texels, &S.texels)) ||
         (rc = upload_vec(c, F.spheres, &S.spheres)) || (rc = upload_vec(c, F.smat, &S.sphere_mat)) ||
         (rc = upload_vec(c, F.mats, &S.mats)) || (rc = upload_vec(c, F.lights, &S.lights)) ||
-        (rc = upload_vec(c, F.list, &S.list)) || (rc = upload_vec(c, F.list_box, &S.list_box)))
+        (rc = upload_vec(c, F.list, &S.list)))
         return rc;
     S.tris64 = nullptr; S.tshade64 = nullptr; S.tnorm64 = nullptr; S.spheres64 = nullptr;
     if (want_f64 && ((rc = upload_vec(c, F.tris64, &S.tris64)) || (rc = upload_vec(c, F.tshade64, &S.tshade64)) ||
@@ -1400,7 +1383,7 @@ static DevScene host_scene(const FlatScene &F)
     S.tris = F.tris.data(); S.tshade = F.tshade.data(); S.tnorm = F.tnorm.data();
     S.tuv = F.tuv.data(); S.texels = F.texels.data();
     S.spheres = F.spheres.data(); S.sphere_mat = F.smat.data(); S.mats = F.mats.data();
-    S.lights = F.lights.data(); S.list = F.list.data(); S.list_box = F.list_box.data();
+    S.lights = F.lights.data(); S.list = F.list.data();
     S.tris64 = F.tris64.data(); S.tshade64 = F.tshade64.data(); S.tnorm64 = F.tnorm64.data();
     S.spheres64 = F.spheres64.data();
     return S;
@@ -1733,6 +1716,7 @@ template <int MATS>
 static int pick_launcher_f64_t(const frt_ctx *c, Launcher &L)
 {
     if (c->world_kind == FRT_WORLD_LIST) {
+        // (a 2-wave register cap changed nothing: profiles/r03/r03c_ab_veach_listbox_f64waves.jsonl)
         L = make_launcher<16, FRT_WORLD_LIST, false, 1, false, MATS, FRT_INTEGRATOR_PATH, double>(0);
         return FRT_OK;
     }
