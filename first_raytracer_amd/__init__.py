@@ -178,7 +178,7 @@ _lib = None
 
 # every symbol include/frt.h declares
 EXPORTS = ("frt_get_abi_version", "frt_create", "frt_destroy", "frt_last_error", "frt_set_precision", "frt_upload_scene",
-           "frt_shard_slot_count", "frt_shard_slots", "frt_render", "frt_render_multi", "frt_render_device",
+           "frt_shard_slot_count", "frt_shard_slots", "frt_render", "frt_render_multi", "frt_render_device", "frt_trace_device",
            "frt_scene_create", "frt_scene_new", "frt_scene_add_obj", "frt_scene_add_sphere", "frt_scene_set_camera",
            "frt_scene_set_env", "frt_scene_add_image", "frt_scene_finish", "frt_scene_build_bvh_gpu",
            "frt_scene_build_bvh_sah", "frt_scene_build_bvh_gpu_algo",
@@ -217,6 +217,7 @@ def lib():
     L.frt_shard_slots.argtypes = [ctypes.POINTER(RenderParams), vp]
     L.frt_render.argtypes = [vp, ctypes.POINTER(RenderParams), vp, ctypes.POINTER(Stats)]
     L.frt_render_device.argtypes = [vp, ctypes.POINTER(RenderParams), vp, vp, ctypes.POINTER(Stats)]
+    L.frt_trace_device.argtypes = [vp, vp, ctypes.c_int64, vp, ctypes.c_int, vp, ctypes.POINTER(Stats)]
     L.frt_render_multi.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.POINTER(RenderParams), vp,
                                    ctypes.POINTER(Stats)]
     L.frt_scene_create.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_double, ctypes.POINTER(vp)]
@@ -416,6 +417,15 @@ class Context:
         _check(lib().frt_render_device(self.ptr, ctypes.byref(params), ctypes.c_void_p(dev_ptr),
                                        ctypes.c_void_p(stream_ptr) if stream_ptr else None, ctypes.byref(st)),
                "frt_render_device", self.ptr)
+        return st
+
+    def trace_device(self, rays_ptr, n, hits_ptr, flags=0, stream_ptr=None):
+        """Batched Scene::world->hit on device buffers: rays n x 8 floats (origin, t_max,
+        direction, flags bit 0 = any hit), hits n x 4 (t, u, v, prim bits).  Returns stats."""
+        st = Stats()
+        _check(lib().frt_trace_device(self.ptr, ctypes.c_void_p(rays_ptr), int(n), ctypes.c_void_p(hits_ptr), int(flags),
+                                      ctypes.c_void_p(stream_ptr) if stream_ptr else None, ctypes.byref(st)),
+               "frt_trace_device", self.ptr)
         return st
 
     def close(self):

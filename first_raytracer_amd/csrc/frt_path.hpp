@@ -99,6 +99,7 @@ struct DevScene {
     const float4 *texels;    // image_texture texels (rgb, -) of every image, in HBM
     const int *lights;       // device prim refs
     const int *list;         // device prim refs (list worlds)
+    const int *tri_view;     // device triangle id -> scene-view triangle index (ray queries, frt_trace_device)
     const uint4 *nodes4;     // 4 x uint4 per 4-wide node (HBM-resident scenes; DESIGN.md "BVH4Q")
     const float4 *nodes_oct; // 8 copies of `nodes`, copy o with each child box as (near xyz, far xyz) for
                              // rays of octant o (bit a set: 1/d_a < 0); LDS plans copy them (kWorldBvh2Oct)

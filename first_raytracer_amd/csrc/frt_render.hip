@@ -294,6 +294,103 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     }
 }
 
+// ------------------------------------------------------------------------
+// ray queries (frt_trace_device): a buffer of rays through the same
+// resumable traversal, Scene::world->hit (path.cpp:10, 50; parallel_bvh.h:39-64,
+// hitable_list.cpp:4-21) batched.  Persistent; a lane whose ray is done takes
+// the next ray at once, so the wave's lanes stay busy until the buffer runs
+// dry.  Rays come from a wave-local chunk (kTraceChunk rays taken with one
+// atomic); a global atomic per refill put its latency on every traversal
+// step (4 Grays/s on camera rays: profiles/r03/r03e_trace_atomic_per_step.jsonl).
+// ------------------------------------------------------------------------
+constexpr uint32_t kTraceChunk = 256;   // rays a wave takes from the buffer with one atomic
+struct DevRays {
+    const float4 *ray;       // 2 per ray: (origin, t_max) | (direction, flags: bit 0 = any-hit)
+    float4 *hit;             // 1 per ray: (t, u, v, prim ref of the scene view as int bits; -1 = miss)
+    uint32_t n;
+    int min_desc;            // leaf postponing (bvh2_step)
+    unsigned *counter;       // ray-queue head
+};
+template <int STACK, int WORLD, bool LDS_SCENE, int WAVES>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void trace_kernel(
+    const DevScene S0, const DevRays R)
+{
+    extern __shared__ __attribute__((aligned(16))) int lds_mem[];
+    int *stk = lds_mem + threadIdx.x;                                 // one LDS column per lane
+    constexpr int kStackInts = WORLD != FRT_WORLD_LIST ? STACK * kBlock : 0;
+    DevScene S = S0;
+    if constexpr (LDS_SCENE) scene_to_lds<WORLD>(S, lds_mem + kStackInts);
+    else scene_strides_hbm(S);
+    const int lane = threadIdx.x & 63;
+    Trav<float> T;
+    int ovf[WORLD == kWorldBvh4 ? kBvh4Overflow : 1];
+    f3 o = mk3(0, 0, 0), d = mk3(0, 0, 1);
+    bool anyhit = false, tracing = false, exhausted = false;
+    uint32_t id = 0;
+    auto finish = [&]() {
+        const int p = T.h.prim;
+        const int ref = (p < 0 || (p & FRT_PRIM_SPHERE)) ? p : S.tri_view[p];
+        R.hit[id] = make_float4(T.h.t, T.h.u, T.h.v, i2f(ref));
+    };
+    // Each lane holds the NEXT ray of its queue in registers (loaded while the
+    // current one traverses), so a lane that finishes starts its next ray
+    // without waiting on memory.
+    uint32_t chunk_next = 0, chunk_end = 0;                          // wave-uniform
+    float4 na = make_float4(0, 0, 0, 0), nb = make_float4(0, 0, 0, 0);
+    uint32_t nid = 0;
+    bool have_next = false;
+    for (;;) {
+        if (!tracing && have_next) {                                  // start the prefetched ray
+            id = nid;
+            o = xyz(na);
+            d = xyz(nb);
+            anyhit = (f2i(nb.w) & 1) != 0;
+            have_next = false;
+            tracing = trav_begin_world<WORLD>(T, S, o, d, na.w);
+            if (!tracing) finish();                                   // the ray misses the scene box
+        }
+        const bool need = !have_next && !exhausted;
+        const uint64_t m = __ballot(need);
+        if (m) {
+            // the wave's lanes without a queued ray take the rest of its chunk,
+            // then a new chunk (one atomic per kTraceChunk rays) once it runs short
+            const uint32_t want = (uint32_t)__popcll(m), left = chunk_end - chunk_next;
+            uint32_t fresh = 0xffffffffu;
+            if (left < want && chunk_end < R.n) {
+                uint32_t b0 = 0;
+                if (lane == 0) b0 = atomicAdd(R.counter, kTraceChunk);
+                fresh = __builtin_amdgcn_readfirstlane(__shfl(b0, 0));
+            }
+            const uint32_t rank = lane_rank(m);
+            const uint32_t w = rank < left ? chunk_next + rank : (fresh == 0xffffffffu ? 0xffffffffu : fresh + (rank - left));
+            if (left >= want) {
+                chunk_next += want;
+            } else if (fresh != 0xffffffffu) {
+                chunk_next = fresh + (want - left);
+                chunk_end = fresh + kTraceChunk;
+            } else {
+                chunk_next = chunk_end;
+            }
+            if (need) {
+                if (w >= R.n) {
+                    exhausted = true;
+                } else {
+                    nid = w;
+                    na = R.ray[2 * (size_t)w];
+                    nb = R.ray[2 * (size_t)w + 1];
+                    have_next = true;
+                }
+            }
+        }
+        if (__ballot(tracing || have_next) == 0) break;
+        if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, o, d, anyhit, stk, ovf,
+                                                             LDS_SCENE && WORLD == FRT_WORLD_BVH ? 0 : R.min_desc)) {
+            tracing = false;
+            finish();
+        }
+    }
+}
+
 // film: slot mean = sum over chunks (fixed order) * (1/spp)  (viewer.cpp:111)
 __global__ void film_reduce(const float *__restrict__ partial, float *__restrict__ out, uint32_t n_slots,
                             int n_chunks, int spp, int tile, int ntx, int shard_index, int shard_count, int nx, int ny)
@@ -788,6 +885,7 @@ struct FlatScene {
     bool has4 = false;           // nodes4 / root4 usable
     int root4 = 0, depth4 = 0;
     std::vector<int> smat, lights, list;
+    std::vector<int> tri_view;      // device triangle id -> scene-view triangle (DevScene::tri_view)
     DevScene meta{};     // scalars + camera; pointers filled by the consumer
     int depth = 0;
 };
@@ -1136,6 +1234,7 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
         return fail(FRT_E_INVALID, "scene view: unknown world kind");
     }
     auto dev_ref = [&](int ref) { return (ref & FRT_PRIM_SPHERE) ? ref : tri_dev[ref]; };
+    F.tri_view = tri_order;
 
     // triangles in device order: v0 | e1 | e2 with the edges taken in fp64 (triangle.h:58-60)
     bool any_smooth = false;
@@ -1339,7 +1438,7 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
         (rc = upload_vec(c, F.tuv, &S.tuv)) || (rc = upload_vec(c, F.texels, &S.texels)) ||
         (rc = upload_vec(c, F.spheres, &S.spheres)) || (rc = upload_vec(c, F.smat, &S.sphere_mat)) ||
         (rc = upload_vec(c, F.mats, &S.mats)) || (rc = upload_vec(c, F.lights, &S.lights)) ||
-        (rc = upload_vec(c, F.list, &S.list)))
+        (rc = upload_vec(c, F.list, &S.list)) || (rc = upload_vec(c, F.tri_view, &S.tri_view)))
         return rc;
     S.tris64 = nullptr; S.tshade64 = nullptr; S.tnorm64 = nullptr; S.spheres64 = nullptr;
     if (want_f64 && ((rc = upload_vec(c, F.tris64, &S.tris64)) || (rc = upload_vec(c, F.tshade64, &S.tshade64)) ||
@@ -1383,7 +1482,7 @@ static DevScene host_scene(const FlatScene &F)
     S.tris = F.tris.data(); S.tshade = F.tshade.data(); S.tnorm = F.tnorm.data();
     S.tuv = F.tuv.data(); S.texels = F.texels.data();
     S.spheres = F.spheres.data(); S.sphere_mat = F.smat.data(); S.mats = F.mats.data();
-    S.lights = F.lights.data(); S.list = F.list.data();
+    S.lights = F.lights.data(); S.list = F.list.data(); S.tri_view = F.tri_view.data();
     S.tris64 = F.tris64.data(); S.tshade64 = F.tshade64.data(); S.tnorm64 = F.tnorm64.data();
     S.spheres64 = F.spheres64.data();
     return S;
@@ -1581,19 +1680,18 @@ static Launcher make_launcher(size_t scene_bytes)
 template <int STACK, bool LDS, int WORLD = FRT_WORLD_BVH, bool SPEC = false, int MATS = kMatsNone>
 static Launcher bvh_launcher(int waves, size_t sb)
 {
-    // The specular material kernels have no 6-wave build: at 80 VGPRs they
-    // spill 160-230 VGPRs, and one of them (rough conductors, HBM binary tree)
-    // compiled to a kernel with the oracle's ray counts and wrong radiance
-    // (RMSE 0.07, tests/test_gpu_conductors.py::test_register_caps_agree).
-    // A 6-wave request runs the 5-wave kernel.
-    if constexpr ((MATS & kMatsSpecAny) != 0) {
-#if defined(FRT_EXP_SPEC_W6)   // experiment builds: the 6-wave specular kernels (register-cap investigation)
-        if (waves == 6) return make_launcher<STACK, WORLD, LDS, 6, SPEC, MATS>(sb);
-#endif
-        if (waves >= 6) waves = 5;
-    } else {
-        if (waves == 6) return make_launcher<STACK, WORLD, LDS, FRT_EXP_W6, SPEC, MATS>(sb);
-    }
+    // Every material set has a 6-wave build again (round 3).  In round 2 the
+    // rough-conductor kernel of the HBM binary plan compiled under that cap to
+    // a kernel with the oracle's ray counts and wrong radiance; that source
+    // state (5a5829a) reproduces it at -O3 and not at -O1, and moving the
+    // AMDGPU high-pressure rescheduling stage moves the failure to the 5-wave
+    // kernel: the result follows machine code generation.  The shading code's
+    // host replay is clean under ASan / UBSan / pattern init (the megakernel
+    // loop itself runs only on the device).  The current
+    // source agrees under every cap and plan (test_register_caps_agree;
+    // DESIGN.md "Register-cap hazard").  The defaults stay 4 / 5 waves for the
+    // specular sets (faster than 6: profiles/r02/r02_ab_sphere_hbm_mats.jsonl).
+    if (waves == 6) return make_launcher<STACK, WORLD, LDS, FRT_EXP_W6, SPEC, MATS>(sb);
     if (waves == 5) return make_launcher<STACK, WORLD, LDS, 5, SPEC, MATS>(sb);
     if constexpr (MATS != kMatsNone) {
         if (waves == 4) return make_launcher<STACK, WORLD, LDS, 4, SPEC, MATS>(sb);
@@ -1757,6 +1855,104 @@ static int pick_launcher(const frt_ctx *c, int integrator, int flags, Launcher &
     }
 }
 
+
+// ---- ray queries: trace_kernel plans (the path plans' residency rules) ----
+struct TraceLauncher {
+    const void *fn = nullptr;
+    size_t lds = 0;
+    int waves = 0;
+    bool lds_scene = false;
+};
+template <int STACK, int WORLD, bool LDS, int WAVES>
+static TraceLauncher make_trace(size_t scene_bytes)
+{
+    TraceLauncher L;
+    L.fn = reinterpret_cast<const void *>(&trace_kernel<STACK, WORLD, LDS, WAVES>);
+    L.lds = (WORLD != FRT_WORLD_LIST ? (size_t)STACK * kBlock * sizeof(int) : 0) + (LDS ? scene_bytes : 0);
+    L.waves = WAVES;
+    L.lds_scene = LDS;
+    return L;
+}
+// register cap of the ray-query kernel: FRT_TRACE_WAVES (6 / 8 / 10; A/B knob, not part of the C-ABI)
+template <int STACK, int WORLD, bool LDS>
+static TraceLauncher trace_waves(size_t sb)
+{
+    const char *e = std::getenv("FRT_TRACE_WAVES");
+    const int w = e ? std::atoi(e) : 8;
+    if (w == 6) return make_trace<STACK, WORLD, LDS, 6>(sb);
+    if (w == 10) return make_trace<STACK, WORLD, LDS, 10>(sb);
+    return make_trace<STACK, WORLD, LDS, 8>(sb);
+}
+static int pick_trace(const frt_ctx *c, int flags, TraceLauncher &L)
+{
+    if (c->world_kind == FRT_WORLD_LIST) { L = make_trace<16, FRT_WORLD_LIST, false, 8>(0); return FRT_OK; }
+    const int d = c->stack_needed;
+    const bool lds = d < kLdsMaxDepth && c->scene_lds_bytes <= kLdsSceneBytes && !(flags & FRT_FLAG_NO_LDS_SCENE);
+    if (lds && !(flags & FRT_FLAG_NO_OCT) && c->scene_lds_bytes_oct <= kLdsOctBytes) {
+        L = d < 8 ? trace_waves<8, kWorldBvh2Oct, true>(c->scene_lds_bytes_oct)
+                  : trace_waves<16, kWorldBvh2Oct, true>(c->scene_lds_bytes_oct);
+    } else if (lds) {
+        L = d < 8 ? make_trace<8, FRT_WORLD_BVH, true, 8>(c->scene_lds_bytes)
+                  : make_trace<16, FRT_WORLD_BVH, true, 8>(c->scene_lds_bytes);
+    } else if (c->has_bvh4 && !(flags & FRT_FLAG_BVH2) && bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
+        L = trace_waves<kBvh4LdsStack, kWorldBvh4, false>(0);
+    } else if (d < 16) {
+        L = make_trace<16, FRT_WORLD_BVH, false, 8>(0);
+    } else if (d < 32) {
+        L = make_trace<32, FRT_WORLD_BVH, false, 8>(0);
+    } else if (d < 64) {
+        L = make_trace<64, FRT_WORLD_BVH, false, 1>(0);
+    } else {
+        return FRT_E_UNSUPPORTED;
+    }
+    return FRT_OK;
+}
+
+// Batched Scene::world->hit (include/frt.h frt_trace_device)
+extern "C" int frt_trace_device(frt_ctx *c, const float *rays, int64_t n, float *hits, int flags, void *hip_stream,
+                                frt_stats *st)
+{
+    const auto t_start = std::chrono::steady_clock::now();
+    if (!c || n < 0 || (n > 0 && (!rays || !hits))) return FRT_E_INVALID;
+    if (n >= (int64_t)0xffffffffLL) return set_err(c, FRT_E_UNSUPPORTED, "frt_trace_device: more than 2^32 - 1 rays");
+    if (!c->have_scene) return set_err(c, FRT_E_NO_SCENE, "no scene uploaded");
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t stream = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    TraceLauncher L;
+    if (pick_trace(c, flags, L) != FRT_OK) return set_err(c, FRT_E_UNSUPPORTED, "BVH deeper than 63 levels");
+    int bpc = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, L.fn, kBlock, L.lds) != hipSuccess || bpc <= 0) bpc = 1;
+    const int64_t want = std::max<int64_t>(1, (n + kBlock - 1) / kBlock);
+    const int grid = (int)std::min<int64_t>((int64_t)c->n_cu * bpc, want);
+    DevRays R{};
+    R.ray = reinterpret_cast<const float4 *>(rays);
+    R.hit = reinterpret_cast<float4 *>(hits);
+    R.n = (uint32_t)n;
+    R.min_desc = min_desc(L.lds_scene);
+    R.counter = c->counter;
+    HIPCHK(c, hipMemsetAsync(c->counter, 0, 64, stream));
+    HIPCHK(c, hipEventRecord(c->ev0, stream));
+    if (n > 0) {
+        DevScene Sarg = c->S;
+        void *args[] = {&Sarg, &R};
+        const hipError_t le = hipLaunchKernel(L.fn, dim3(grid), dim3(kBlock), args, L.lds, stream);
+        if (le != hipSuccess) return set_err(c, FRT_E_HIP, std::string("trace_kernel launch: ") + hipGetErrorString(le));
+    }
+    HIPCHK(c, hipEventRecord(c->ev1, stream));
+    HIPCHK(c, hipStreamSynchronize(stream));
+    float ms = 0.0f;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    if (st) {
+        memset(st, 0, sizeof(*st));
+        st->camera_rays = (uint64_t)n;
+        st->kernel_ms = ms;
+        st->scene_in_lds = L.lds_scene ? 1u : 0u;
+        st->waves_cap = (uint32_t)L.waves;
+        st->scene_bytes = c->scene_lds_bytes;
+        st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    }
+    return FRT_OK;
+}
 
 // ---- PSS-MLT render: bootstrap b, then the chain megakernel splatting into dev_film ----
 template <int STACK, int WORLD, bool LDS = false>

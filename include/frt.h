@@ -244,6 +244,19 @@ int frt_render_multi(frt_ctx **ctxs, int n, const frt_render_params *p, float *f
 int frt_render_device(frt_ctx *ctx, const frt_render_params *p, float *slots_rgb, void *hip_stream,
                       frt_stats *st);
 
+/* Ray queries on the uploaded scene: Scene::world->hit (path.cpp:10, 50;
+ * parallel_bvh_node::hit parallel_bvh.h:39-64, hitable_list::hit
+ * hitable_list.cpp:4-21) for a batch of rays, with the world's own t_min
+ * (EPSILON * max(1, |o|) for a BVH, EPSILON for a list).  Device memory:
+ * rays = n x 8 floats (origin xyz, t_max, direction xyz, flags: bit 0 = any
+ * hit, the shadow query of path.cpp:50), hits = n x 4 floats (t, u, v, prim
+ * as int32 bits: the scene view's triangle index or FRT_PRIM_SPHERE | k, -1 =
+ * miss; a miss leaves t = t_max).  flags: FRT_FLAG_NO_LDS_SCENE / _BVH2 /
+ * _NO_OCT choose the plan as for frt_render.  Returns after the work has
+ * completed on `hip_stream` (NULL = the context's stream); st->kernel_ms. */
+int frt_trace_device(frt_ctx *ctx, const float *rays, int64_t n, float *hits, int flags, void *hip_stream,
+                     frt_stats *st);
+
 /* ---- host-side scene pipeline (native C++; what main.cpp + mesh_loader +
  *      parallel_bvh_node::create_bvh do in the reference) ---- */
 typedef struct frt_host_scene frt_host_scene;

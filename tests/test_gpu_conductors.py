@@ -43,8 +43,7 @@ def test_path_conductors(ctx, sphere_dist, cube_dist, world, flags):
 
 def test_register_caps_agree(ctx, monkeypatch):
     """The material kernels give the same film under every register cap and
-    plan (FRT_MATS_WAVES 0 / 3 / 4 / 5, and 6, which runs the 5-wave kernel; LDS
-    binary, HBM 4-wide, HBM binary).
+    plan (FRT_MATS_WAVES 0 / 3 / 4 / 5 / 6; LDS binary, HBM 4-wide, HBM binary).
     A source restructuring of the specular dispatch once compiled to kernels
     that were right uncapped and wrong (RMSE 0.04-0.18) under some caps, with
     unchanged ray counts; this pins every cap against the oracle."""
@@ -57,8 +56,7 @@ def test_register_caps_agree(ctx, monkeypatch):
         for w in ("0", "3", "4", "5", "6"):
             monkeypatch.setenv("FRT_MATS_WAVES", w)
             film, st = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=12, flags=flags))
-            # specular kernels have no 6-wave build: the 5-wave kernel runs (frt_render.hip bvh_launcher)
-            assert st.waves_cap == min(int(w), 5)
+            assert st.waves_cap == int(w)
             e = rmse(film, ref)
             assert e <= 1e-3, (flags, w, e)
             films.append(film)
