@@ -519,19 +519,24 @@ __global__ __launch_bounds__(kBlock) void mlt_bootstrap(const DevScene S0, int n
 // integer atomic.  Integer sums do not depend on the order the chains' atomics
 // land in, so the film is bit-reproducible run to run (float atomics were
 // not).  Splats are >= 0 (scale, weights and radiance are); the quantum
-// 2^-36 = 1.5e-11 is far below fp32's resolution of the pixel values, and
-// a pixel saturates only past 2^28.  mlt_film_to_float converts once at the end.
+// 2^-36 = 1.5e-11 is far below fp32's resolution of the pixel values, and a
+// signed 64-bit pixel holds up to 2^27 before it wraps.  A splat that is not a
+// finite value in [0, 2^27) is dropped (the reference's pixel would turn NaN /
+// Inf there; none occurs in the test scenes).  mlt_film_to_float converts once
+// at the end.
 constexpr int kSplatFix = 36;
 __device__ __forceinline__ void mlt_splat(const MltWork &W, float x, float y, f3 c, float w)
 {
     const int pix = mlt_pixel(x, y, W.nx, W.ny);
     if (pix < 0) return;
     const float k = W.scale * w;
-    const double q = (double)(1ull << kSplatFix);
+    const double q = (double)(1ull << kSplatFix), lim = 9.2233720368547758e18;   // 2^63
+    const double v[3] = {(double)(k * c.x) * q, (double)(k * c.y) * q, (double)(k * c.z) * q};
+    if (!(v[0] >= 0.0 && v[0] < lim && v[1] >= 0.0 && v[1] < lim && v[2] >= 0.0 && v[2] < lim)) return;
     unsigned long long *f = W.film + 3 * (size_t)pix;
-    atomicAdd(f + 0, (unsigned long long)__double2ll_rn((double)(k * c.x) * q));
-    atomicAdd(f + 1, (unsigned long long)__double2ll_rn((double)(k * c.y) * q));
-    atomicAdd(f + 2, (unsigned long long)__double2ll_rn((double)(k * c.z) * q));
+    atomicAdd(f + 0, (unsigned long long)__double2ll_rn(v[0]));
+    atomicAdd(f + 1, (unsigned long long)__double2ll_rn(v[1]));
+    atomicAdd(f + 2, (unsigned long long)__double2ll_rn(v[2]));
 }
 __global__ void mlt_film_to_float(const unsigned long long *__restrict__ acc, float *__restrict__ film, size_t n)
 {

@@ -127,3 +127,47 @@ def test_specular_scenes(objfix, request):
     assert float(np.sqrt(np.mean((out.astype(np.float64).reshape(-1, 3) - ref.reshape(-1, 3)) ** 2))) < 1e-4
     assert st.rays == pytest.approx(cnt.rays, rel=1e-3)
     assert float(ref.mean()) > 0.01
+
+
+def test_bvh4_tiny_far_nodes(tmp_path):
+    """4-wide nodes tiny against their distance from the ray origin, where an
+    axis' quantized planes round to one value (255 * a vanishes in the slab
+    FMA): a real child's hit is then tn == tf and must stay a hit, while empty
+    slots (inverted boxes) are rejected by their ref.  A 20 x 20 grid of
+    1e-6-sized triangles around the origin (nodes of ~1e-5, the padding of a
+    unit-scale scene) seen from 1e3 away (farther, the reference's own
+    t_min = EPSILON * |o| would cull the hits, parallel_bvh.h:46-51).  Shading
+    normals (normals_renderer::Li) of the 4-wide traversal vs the binary one
+    and the oracle."""
+    lines, k = [], 1
+    for i in range(20):
+        for j in range(20):
+            x, y = (i - 10) * 2e-6, (j - 10) * 2e-6
+            z = 1e-7 * ((i * 7 + j * 3) % 5)
+            lines += [f"v {x!r} {y!r} {z!r}", f"v {x + 1e-6!r} {y!r} {z!r}", f"v {x!r} {y + 1e-6!r} {z + 5e-7!r}"]
+            lines.append(f"f {k} {k + 1} {k + 2}")
+            k += 3
+    obj = tmp_path / "tiny.obj"
+    obj.write_text("\n".join(lines) + "\n")
+    nx, ny = 40, 40
+    cam = {"lookfrom": (0.0, 0.0, 1e3), "lookat": (0.0, 0.0, 0.0), "vup": (0.0, 1.0, 0.0),
+           "vfov": 2.4e-6, "aperture": 0.0, "focus": 1e3}
+    spec = {"objects": [{"obj": str(obj), "geo": True,
+                         "bsdf": {"type": "lambertian", "albedo": (0.5, 0.5, 0.5)}}],
+            "camera": cam, "world": "bvh"}
+    env = (0.25, 0.5, 0.75)
+    hs = frt.HostScene.from_spec(spec, 1.0)
+    hs.set_env(env)
+    pix = np.arange(nx * ny, dtype=np.int32)
+    p = dict(integrator=frt.FRT_INTEGRATOR_NORMALS)
+    wide, st4 = frt.selftest_path_host(hs, frt.RenderParams.make(nx, ny, 1, seed=1, **p), pix)
+    bin2, st2 = frt.selftest_path_host(hs, frt.RenderParams.make(nx, ny, 1, seed=1, flags=frt.FRT_FLAG_BVH2, **p), pix)
+    osc = oracle.OracleScene.from_spec(spec, 1.0)
+    osc.set_env(env)
+    ref, _ = osc.render(nx, ny, 1, seed=1, pixels=pix, integrator=3)
+    assert st4.bvh_depth < st2.bvh_depth                       # the 4-wide tree was traversed
+    hit = np.abs(ref - env).max(axis=1) > 1e-6
+    assert hit.mean() > 0.05
+    assert np.array_equal(wide, bin2)
+    # fp32 vs fp64: a few edge pixels may round to the other side
+    assert (np.abs(wide.astype(np.float64) - ref).max(axis=1) > 1e-3).mean() < 0.01

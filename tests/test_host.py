@@ -167,3 +167,16 @@ def test_specular_scene_materials_and_topology(objfix, request):
     want = frt.FRT_MAT_DIELECTRIC if objfix == "glass_obj" else frt.FRT_MAT_MODIFIED_PHONG
     assert want in types
     assert hs.info.n_nodes == osc.info.n_nodes and hs.info.bvh_depth == osc.info.bvh_depth
+
+
+def test_one_hip_and_rccl_runtime_per_process():
+    """libfrt.so links librccl.so.1 / libamdhip64.so.7 by soname; with torch imported
+    first (as the binding does) those sonames resolve to torch's bundled copies, so the
+    process holds one HIP runtime and one RCCL (frt_render_multi's RCCL and
+    torch.distributed's are the same library)."""
+    import torch  # noqa: F401
+    frt.lib()
+    maps = open("/proc/self/maps").read().splitlines()
+    libs = {l.split()[-1] for l in maps if "librccl" in l or "libamdhip64" in l}
+    assert len([x for x in libs if "librccl" in x]) <= 1, libs
+    assert len([x for x in libs if "libamdhip64" in x]) == 1, libs
