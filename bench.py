@@ -39,6 +39,7 @@ SCENES = os.path.join(ROOT, "tests", "golden", "scenes")
 HBM_PEAK_GBS = 8000.0
 VALU_PEAK_GINST = 256 * 4 * 2.4 / 2.0
 LDS_PEAK_GBS = 150000.0
+L2_XCD_BYTES = 4 << 20          # one XCD's L2 (MI355X_MICROARCH.md)
 NODE_BYTES, TRI_BYTES, RAY_BYTES = 32, 48, 32   # B_ray = 32 V + 48 T + 32
 NS_TARGET_MRAYS = 1000.0                        # north_star: >= 1 Gray/s on one MI355X
 
@@ -162,10 +163,13 @@ def roofline(integrator, key, world, res, V, T):
     """Roofline of the dominant kernel (the megakernel) for this config.
 
     The bound follows where the scene lives (DESIGN.md §7 "Roofline"):
-    * scene in LDS (Cornell, 5 KiB): the kernel issues divergent VALU work and
-      reads its scene from LDS; HBM carries only the per-(chunk, slot) partial
-      sums.  bound "valu": achieved = VALU wave-instructions per launch (PMC
-      SQ_INSTS_VALU per ray x rays per launch) / launch time, peak = 1228.8 G/s.
+    * scene in LDS (Cornell, 5 KiB) or a cache-resident list world (veach,
+      ~20 KiB, read through L1/L2): the kernel issues divergent VALU work;
+      HBM carries only the per-(chunk, slot) partial sums.  bound "valu":
+      achieved = VALU issue slots per launch (PMC SQ_INSTS_VALU per ray, fp64
+      FMA/ADD/MUL counted twice and fp64 transcendentals four times when the
+      kernel computes in fp64 -- tools/roofline_pmc.py valu_issue_per_ray --
+      x rays per launch) / launch time, peak = 1228.8 G fp32 wave-slots/s.
     * scene in HBM (cornell_1m, ~150 MB): bound "hbm": achieved = HBM bytes per
       launch from the PMC passes (2 x FETCH_SIZE + WRITE_SIZE per ray, the
       gfx950 correction of MI355X_MICROARCH.md) x rays per launch / launch time.
@@ -175,10 +179,11 @@ def roofline(integrator, key, world, res, V, T):
     (B_ray = 32 V + 48 T + 32 on the reference's tree) are reported beside it."""
     launch_s = res["avg_kernel_ms"] * 1e-3
     rays = res["rays_per_launch"]
-    pmc = load_profile("roofline_pmc.json", f"{integrator}:{key}")
+    pmc = load_profile("roofline_pmc.json", f"{integrator}:{key}" + (":fp64" if res.get("fp64") else ""))
+    valu_bound = res["scene_in_lds"] or res["scene_bytes"] <= L2_XCD_BYTES   # LDS or L2-resident scene
     out = {"kernel": "mlt_megakernel" if integrator == "pssmlt" else "path_megakernel",
            "rays_per_launch": int(rays), "avg_launch_ms": round(res["avg_kernel_ms"], 3),
-           "scene_residency": "lds" if res["scene_in_lds"] else "hbm",
+           "scene_residency": "lds" if res["scene_in_lds"] else ("l2" if valu_bound else "hbm"),
            "scene_bytes": int(res["scene_bytes"]), "launch": res["launch"]}
     algo = None
     if V is not None:
@@ -192,8 +197,11 @@ def roofline(integrator, key, world, res, V, T):
             out["valu_lane_util"] = round(pmc["valu_lane_util"], 4)
         hbm = pmc.get("hbm_bytes_per_ray")
         hbm_gbs = rays * hbm / launch_s / 1e9 if hbm is not None else None
-        if res["scene_in_lds"] and pmc.get("valu_insts_per_ray") is not None:
-            ach = rays * pmc["valu_insts_per_ray"] / launch_s / 1e9
+        issue = pmc.get("valu_issue_per_ray", pmc.get("valu_insts_per_ray"))
+        if pmc.get("l2_hit_rate") is not None:
+            out["l2_hit_rate"] = round(pmc["l2_hit_rate"], 4)
+        if valu_bound and issue is not None:
+            ach = rays * issue / launch_s / 1e9
             out.update({"bound": "valu", "achieved": round(ach, 1), "peak": VALU_PEAK_GINST, "unit": "Ginst/s",
                         "frac": round(ach / VALU_PEAK_GINST, 4),
                         "traffic": None if hbm is None else int(rays * hbm),
@@ -203,8 +211,8 @@ def roofline(integrator, key, world, res, V, T):
             out.update({"bound": "hbm", "achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(hbm_gbs / HBM_PEAK_GBS, 4), "traffic": int(rays * hbm),
                         "algorithmic_over_traffic": None if algo is None else round(algo / hbm_gbs, 3)})
-            if pmc.get("valu_insts_per_ray") is not None:
-                out["valu_issue_frac"] = round(rays * pmc["valu_insts_per_ray"] / launch_s / 1e9 / VALU_PEAK_GINST, 4)
+            if issue is not None:
+                out["valu_issue_frac"] = round(rays * issue / launch_s / 1e9 / VALU_PEAK_GINST, 4)
     if "bound" not in out:
         # no counter profile for this config: the algorithmic model alone (it can
         # exceed 1 when L2 / the Infinity Cache / LDS serve the node reads)

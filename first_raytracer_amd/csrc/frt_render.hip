@@ -133,7 +133,6 @@ __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
 // VGPRs at the register cap: cornell_1m 51 -> 24, Cornell 31 -> 6; same-call
 // A/B +4.5 % / +1 %).
 constexpr int kItemWords = 10;
-constexpr int kCountInts = (kBlock / 64) * 4 * 2;   // per wave: 4 x 64-bit ray counters
 enum { kIsCur, kIsEnd, kIsSlot, kIsChunk, kIsPix, kIsPx, kIsPy, kIsAcc };   // kIsAcc..+2: r, g, b
 struct ItemState {
     int *b;      // the lane's column
@@ -148,52 +147,28 @@ template <int STACK, int WORLD, bool LDS_SCENE, int WAVES = 1, bool SPEC = false
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void path_megakernel(
     const DevScene S0, const DevWork W)
 {
-    // [STACK][kBlock] stack, [kItemWords][kBlock] item state, the waves' ray
-    // counters, then the scene
+    // [STACK][kBlock] stack, [kItemWords][kBlock] item state, then the scene
     extern __shared__ __attribute__((aligned(16))) int lds_mem[];
     int *stk = lds_mem + threadIdx.x;                                 // one LDS column per lane
     constexpr int kStackInts = WORLD != FRT_WORLD_LIST ? STACK * kBlock : 0;
     constexpr int kItemInts = kItemWords * kBlock;
     DevScene S = S0;
-    if constexpr (LDS_SCENE) scene_to_lds<WORLD>(S, lds_mem + kStackInts + kItemInts + kCountInts);
+    if constexpr (LDS_SCENE) scene_to_lds<WORLD>(S, lds_mem + kStackInts + kItemInts);
     else scene_strides_hbm(S);
     const int lane = threadIdx.x & 63;
     const int T2 = W.tile * W.tile;
+
     // work-item state
     bool have_item = false, exhausted = false, active = false;
-    PathState<R> P;
     const ItemState I{lds_mem + kStackInts + (int)threadIdx.x};
-    // ray counters of this wave (camera, extension, shadow, samples), 64-bit in
-    // LDS, added by lane 0 at wave-uniform points: as SGPR pairs they pushed the
-    // kernel's scalar registers into VGPR lanes (v_writelane / v_readlane)
-    unsigned long long *cnt = reinterpret_cast<unsigned long long *>(lds_mem + kStackInts + kItemInts) +
-                              4 * (threadIdx.x >> 6);
-    if (lane == 0)
-        for (int k = 0; k < 4; ++k) cnt[k] = 0;
-    auto count = [&](int k, bool x) {
-        const unsigned v = (unsigned)__popcll(__ballot(x));
-        if (lane == 0 && v) cnt[k] += v;
-    };
-    // path: the sample's radiance goes into the item's LDS sum as it is found
-    // (NEE after a shadow ray, emission, environment), so P.L is not live across
-    // the traversal steps (fp32 sum per item in either precision)
-    auto flush_L = [&]() {
-        I.set(kIsAcc + 0, f2i(i2f(I.get(kIsAcc + 0)) + (float)P.L.x));
-        I.set(kIsAcc + 1, f2i(i2f(I.get(kIsAcc + 1)) + (float)P.L.y));
-        I.set(kIsAcc + 2, f2i(i2f(I.get(kIsAcc + 2)) + (float)P.L.z));
-        P.L = zero3<R>();
-    };
-    // the next ray's t_max: path rays are either shadow (1 - SHADOW_EPSILON,
-    // path.cpp:50) or closest-hit (FLT_MAX, path.cpp:10) -- not kept per lane
-    auto ray_tmax = [&]() -> R {
-        if constexpr (KIND == FRT_INTEGRATOR_PATH) return P.shadow ? R(1) - Cst<R>::shadow_eps : Cst<R>::tmax;
-        else return P.rtmax;
-    };
-
+    PathState<R> P;
     // ray in flight: tracing = traversal steps remain; pending = finished, not yet shaded
     Trav<R> T;
     bool tracing = false, pending = false;
     int ovf[WORLD == kWorldBvh4 ? kBvh4Overflow : 1];
+    // ray counters are wave-uniform (SGPRs): popcounts of per-iteration ballots
+    unsigned long long n_cam = 0, n_ext = 0, n_sh = 0, n_smp = 0;
+
     unsigned long long diag_t0 = FRT_DIAG_CLOCK();
     for (;;) {
         FRT_DIAG_TICK(6);
@@ -210,9 +185,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
                                                                            ? 0 : W.min_desc)) {
                 if (KIND == FRT_INTEGRATOR_PATH && P.shadow) {   // finish the shadow ray here, keep traversing
                     if (path_after_shadow<MATS>(P, T.h.prim < 0)) {
-                        flush_L();
                         shadow_done = true;
-                        tracing = trav_begin_world<WORLD>(T, S, P.ro, P.rd, ray_tmax());
+                        tracing = trav_begin_world<WORLD>(T, S, P.ro, P.rd, P.rtmax);
                         pending = !tracing;
                     } else {                                      // path ended (P.term): shade finishes it
                         tracing = false;
@@ -223,7 +197,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
                     pending = true;
                 }
             }
-            count(1, shadow_done);
+            n_ext += __popcll(__ballot(shadow_done));
             if (__popcll(__ballot(tracing)) <= W.trav_min) break;
         }
         // ---- shade the finished rays ----
@@ -234,16 +208,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         if (pending) {
             FRT_DIAG_TICK(4);
             pending = false;
-            // the sample's RNG key again from its item (pixel, sample index): not
-            // live across the traversal steps either
-            P.key = rng_key(W.seed, (uint32_t)I.get(kIsPix), (uint32_t)(I.get(kIsCur) - 1) + W.s_off);
-            const bool done = shade_kind<KIND, MATS>(P, S, T.h, W.max_depth, ne, ns);
-            if (done || KIND == FRT_INTEGRATOR_PATH) flush_L();
-            active = !done;
-            next_ray = !done;
+            if (shade_kind<KIND, MATS>(P, S, T.h, W.max_depth, ne, ns)) {
+                I.set(kIsAcc + 0, f2i(i2f(I.get(kIsAcc + 0)) + (float)P.L.x));   // fp32 chunk sums in
+                I.set(kIsAcc + 1, f2i(i2f(I.get(kIsAcc + 1)) + (float)P.L.y));   // either precision
+                I.set(kIsAcc + 2, f2i(i2f(I.get(kIsAcc + 2)) + (float)P.L.z));
+                active = false;
+            } else {
+                next_ray = true;
+            }
         }
-        count(1, ne != 0);
-        count(2, ns != 0);
+        n_ext += __popcll(__ballot(ne != 0));
+        n_sh += __popcll(__ballot(ns != 0));
         const unsigned long long diag_t2 = FRT_DIAG_CLOCK();
         FRT_DIAG_CYC(17, diag_t2 - diag_t1);
         // ---- retire a finished item: its chunk sum goes to its own slot ----
@@ -299,11 +274,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             active = true;
             next_ray = true;
         }
-        count(0, start);
-        count(3, start);
+        const unsigned long long started = __popcll(__ballot(start));
+        n_cam += started;
+        n_smp += started;
         // ---- set up the next ray's traversal (a scene miss is finished at once) ----
         if (next_ray) {
-            tracing = trav_begin_world<WORLD>(T, S, P.ro, P.rd, ray_tmax());
+            tracing = trav_begin_world<WORLD>(T, S, P.ro, P.rd, P.rtmax);
             pending = !tracing;
         }
         diag_t0 = FRT_DIAG_CLOCK();
@@ -311,9 +287,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         if (__ballot(active || !exhausted) == 0) break;
     }
     // per-wave ray counters, no atomics: lane 0 writes the wave's sums
+    const unsigned long long c[4] = {n_cam, n_ext, n_sh, n_smp};
     if (lane == 0) {
         const size_t wv = ((size_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-        for (int k = 0; k < 4; ++k) W.wave_rays[4 * wv + k] = cnt[k];
+        for (int k = 0; k < 4; ++k) W.wave_rays[4 * wv + k] = c[k];
     }
 }
 
@@ -1695,7 +1672,7 @@ static Launcher make_launcher(size_t scene_bytes)
     L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES, SPEC, MATS, KIND, R>);
     L.f64 = kIsF64<R>;
     L.lds = (WORLD != FRT_WORLD_LIST ? (size_t)STACK * kBlock * sizeof(int) : 0) +
-            (size_t)(kItemWords * kBlock + kCountInts) * sizeof(int) + (LDS ? scene_bytes : 0);
+            (size_t)kItemWords * kBlock * sizeof(int) + (LDS ? scene_bytes : 0);
     L.stack = STACK;
     L.waves = WAVES > 1 ? WAVES : 0;
     L.lds_scene = LDS;

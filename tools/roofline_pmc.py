@@ -2,13 +2,21 @@
 """Per-ray PMC figures of the megakernel for bench.py's roofline, from
 rocprofv3 --pmc passes of ONE bench command (each pass its own run):
 
-  python tools/roofline_pmc.py KEY --sq DIR --fetch DIR --write DIR --bench BENCH.json [--copy-to profiles/r02]
+  python tools/roofline_pmc.py KEY --sq DIR --fetch DIR --write DIR --bench BENCH.json
+         [--f64 DIR] [--tcc DIR] [--copy-to profiles/r03]
 
 KEY is "<integrator>:<scene>:<nx>x<ny>" (bench.py's key).  From the LAST
 *_megakernel dispatch of each pass (counters summed over dimensions):
   valu_insts_per_ray  = SQ_INSTS_VALU / rays per launch
   valu_lane_util      = SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU)
   hbm_bytes_per_ray   = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 / rays per launch
+  valu_issue_per_ray  = (SQ_INSTS_VALU + F64 FMA/ADD/MUL + 3 x F64 TRANS) / rays
+                        (--f64 pass: an fp64 FMA/ADD/MUL wave-instruction issues at
+                        half the fp32 rate on MI355X, 78.6 vs 157.3 TFLOP/s vector,
+                        so it takes two fp32 issue slots; an fp64 transcendental
+                        (rcp/sqrt/rsq_f64) is weighted four; without the pass
+                        valu_issue_per_ray = valu_insts_per_ray)
+  l2_hit_rate         = TCC_HIT / (TCC_HIT + TCC_MISS)   (--tcc pass)
 FETCH_SIZE / WRITE_SIZE are KiB; FETCH_SIZE is doubled as MI355X_MICROARCH.md
 "HBM [CDNA4]" prescribes for gfx950 (it tallies 128-B requests at 64 B).
 The rays per launch come from the bench JSON the passes printed (every pass
@@ -49,6 +57,8 @@ def main():
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     ap.add_argument("--bench", required=True)
+    ap.add_argument("--f64", default="")
+    ap.add_argument("--tcc", default="")
     ap.add_argument("--copy-to", default="")
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "roofline_pmc.json"))
     a = ap.parse_args()
@@ -70,8 +80,22 @@ def main():
         "read_bytes_per_ray": fetch_b / rays, "write_bytes_per_ray": write_b / rays,
         "correction": "hbm = 2 x FETCH_SIZE + WRITE_SIZE (KiB x 1024), MI355X_MICROARCH.md HBM [CDNA4]",
     }
+    passes = [("sq", p_sq), ("fetch", p_fe), ("write", p_wr)]
+    issue = sq["SQ_INSTS_VALU"]
+    if a.f64:
+        _, f6, p_f6 = last_megakernel(a.f64)
+        passes.append(("f64", p_f6))
+        arith = sum(f6.get(f"SQ_INSTS_VALU_{k}_F64", 0.0) for k in ("FMA", "ADD", "MUL"))
+        trans = f6.get("SQ_INSTS_VALU_TRANS_F64", 0.0)
+        rec.update({"F64": f6, "f64_insts_per_ray": (arith + trans) / rays})
+        issue += arith + 3.0 * trans
+    rec["valu_issue_per_ray"] = issue / rays
+    if a.tcc:
+        _, tc, p_tc = last_megakernel(a.tcc)
+        passes.append(("tcc", p_tc))
+        rec.update({"TCC": tc, "l2_hit_rate": tc["TCC_HIT"] / max(1.0, tc["TCC_HIT"] + tc["TCC_MISS"])})
     srcs = []
-    for tag, p in (("sq", p_sq), ("fetch", p_fe), ("write", p_wr)):
+    for tag, p in passes:
         if a.copy_to:
             os.makedirs(a.copy_to, exist_ok=True)
             dst = os.path.join(a.copy_to, f"pmc_{a.key.replace(':', '_')}_{tag}.csv")
