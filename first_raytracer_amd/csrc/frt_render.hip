@@ -712,7 +712,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
 
 }  // namespace
 
-#if defined(FRT_DIAG)
+#if defined(FRT_DIAG) && !defined(FRT_TU_MATS)
 __device__ unsigned long long *frt::frt_diag;
 #endif
 
@@ -755,6 +755,241 @@ struct frt_ctx {
     float *gather = nullptr; size_t gather_bytes = 0;
     float *film_dev = nullptr; size_t film_dev_bytes = 0;
 };
+
+// ---- launch plans ----
+// Shared by the two translation units of the library: this file, and
+// frt_render_mats.hip, which includes it with FRT_TU_MATS defined and holds
+// every kernel compiled with a material set (MATS != kMatsNone: the path
+// kernels of specular / textured scenes, AO, the fp64 kernels of such scenes,
+// PSS-MLT on them).  That unit is compiled with the basic SGPR register
+// allocator (Makefile): under the default greedy allocator these kernels
+// have given the oracle's ray counts with wrong radiance at some register
+// caps, in every failing source state on record, and the basic SGPR (or
+// VGPR) allocator removed every such failure at an equal or larger spill
+// count (DESIGN.md "Register-cap hazard").  The lambertian kernels (the
+// bench configurations) stay on the greedy allocator.
+static bool bvh4_stack_fits(int depth4, int lds_entries) { return 3 * depth4 <= lds_entries + kBvh4Overflow; }
+struct Launcher {
+    const void *fn = nullptr;
+    size_t lds = 0;
+    int stack = 0;
+    int waves = 0;
+    bool lds_scene = false;
+    bool wide = false;      // 4-wide quantized BVH
+    bool f64 = false;       // the fp64 kernel
+};
+template <int STACK, int WORLD, bool LDS, int WAVES = 1, bool SPEC = false, int MATS = kMatsNone,
+          int KIND = FRT_INTEGRATOR_PATH, typename R = float>
+static Launcher make_launcher(size_t scene_bytes)
+{
+    Launcher L;
+    L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES, SPEC, MATS, KIND, R>);
+    L.f64 = kIsF64<R>;
+    L.lds = (WORLD != FRT_WORLD_LIST ? (size_t)STACK * kBlock * sizeof(int) : 0) +
+            (size_t)kItemWords * kBlock * sizeof(int) + (LDS ? scene_bytes : 0);
+    L.stack = STACK;
+    L.waves = WAVES > 1 ? WAVES : 0;
+    L.lds_scene = LDS;
+    L.wide = WORLD == kWorldBvh4;
+    return L;
+}
+#ifndef FRT_EXP_W6
+#define FRT_EXP_W6 6   // experiment builds: the register cap behind the "6 waves" plans
+#endif
+template <int STACK, bool LDS, int WORLD = FRT_WORLD_BVH, bool SPEC = false, int MATS = kMatsNone>
+static Launcher bvh_launcher(int waves, size_t sb)
+{
+    // Every material set has a 6-wave build again (round 3).  Under the greedy
+    // register allocator the material kernels have compiled, at some caps, to
+    // kernels with the oracle's ray counts and wrong radiance; they now come
+    // from frt_render_mats.hip, built with the basic SGPR allocator, which
+    // removed every such failure on record (DESIGN.md "Register-cap hazard";
+    // test_register_caps_agree checks every cap and plan).  The defaults stay
+    // 4 / 5 waves for the specular sets (faster than 6:
+    // profiles/r02/r02_ab_sphere_hbm_mats.jsonl).
+    if (waves == 6) return make_launcher<STACK, WORLD, LDS, FRT_EXP_W6, SPEC, MATS>(sb);
+    if (waves == 5) return make_launcher<STACK, WORLD, LDS, 5, SPEC, MATS>(sb);
+    if constexpr (MATS != kMatsNone) {
+        if (waves == 4) return make_launcher<STACK, WORLD, LDS, 4, SPEC, MATS>(sb);
+        if (waves == 3) return make_launcher<STACK, WORLD, LDS, 3, SPEC, MATS>(sb);
+    }
+    return make_launcher<STACK, WORLD, LDS, 1, SPEC, MATS>(sb);
+}
+#ifndef FRT_EXP_BVH4_LSTACK
+#define FRT_EXP_BVH4_LSTACK 16
+#endif
+constexpr int kBvh4LdsStack = FRT_EXP_BVH4_LSTACK;   // 16 KiB of LDS per block; deeper entries go to scratch
+constexpr int kBvh4LdsStackSmall = 8;   // LDS-resident scenes (shallow trees)
+constexpr int kBruteMaxTris = 128;
+// MATS: the material set the kernel is compiled for (kMats* mask, frt_path.hpp)
+template <int MATS>
+static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
+{
+    if (c->world_kind == FRT_WORLD_LIST) { L = make_launcher<16, FRT_WORLD_LIST, false, 1, false, MATS>(0); return FRT_OK; }
+    const int d = c->stack_needed;
+    const size_t sb = c->scene_lds_bytes;
+    const bool lds = d < kLdsMaxDepth && sb <= kLdsSceneBytes && !(flags & FRT_FLAG_NO_LDS_SCENE);
+    // register cap: waves/SIMD the compiler must fit (its spills land in the
+    // shading code, not the traversal loops).  Measured (profiles/r01_ab_perf3.jsonl):
+    // 5 waves best for LDS-resident scenes, 6 for HBM-resident ones.  The
+    // material kernels (MATS) in LDS run 15-21 % faster on the compiler's own
+    // allocation than under the 5-wave cap (profiles/r01d_perf_mats.jsonl).
+    // Material kernels: textures alone cost about the lambertian kernel's
+    // registers (117 vs 111 VGPRs uncapped; the compiler's 4 waves are best),
+    // the specular branch 152, the rough conductor lobes 170 -- capped at 4
+    // waves/SIMD (128 VGPRs; a few spills in the specular shading) they run
+    // +40 % over the compiler's 2-wave allocation (same-call A/B,
+    // profiles/r02/r02_mats*.jsonl).
+    // (The lambertian LDS kernel fits 111 VGPRs without spills since its work-
+    // item state moved to LDS; the compiler's 4 waves win 2 % at 64 spp but lose
+    // 10 % at the bench's 512 spp -- 337 vs 307 ms, same call --, so the cap stays:
+    // profiles/r02/r02_ab_cornell_knobs.jsonl, r02_ab_cornell_512spp.jsonl.)
+    int waves = (MATS & kMatsSpecAny) ? (lds ? 4 : 5) : MATS == kMatsTex && lds ? 0 : lds ? 5 : 6;
+    if constexpr (MATS != kMatsNone) {   // FRT_MATS_WAVES: register cap of the material kernels (tuning knob, not part of the C-ABI)
+        const char *e = std::getenv("FRT_MATS_WAVES");
+        if (e) waves = std::atoi(e);
+    }
+    if (flags & FRT_FLAG_WAVES4) waves = 0;   // the compiler's own allocation (~120 VGPRs, 4 waves)
+    if (flags & FRT_FLAG_WAVES5) waves = 5;
+    if (flags & FRT_FLAG_WAVES6) waves = 6;
+    if constexpr (MATS == kMatsNone) {   // A/B plans, lambertian scenes only
+        // tiny triangle-only scenes from LDS, every triangle in lockstep (FRT_FLAG_BRUTE)
+        if (lds && (flags & FRT_FLAG_BRUTE) && c->n_spheres == 0 && c->n_tris <= kBruteMaxTris) {
+            L = bvh_launcher<8, true, kWorldBrute>(waves, sb);
+            return FRT_OK;
+        }
+        // LDS-resident scenes, 4-wide (FRT_FLAG_BVH4)
+        if (lds && (flags & FRT_FLAG_BVH4) && c->has_bvh4 && c->scene_lds_bytes4 <= kLdsSceneBytes &&
+            bvh4_stack_fits(c->depth4, kBvh4LdsStackSmall)) {
+            L = bvh_launcher<kBvh4LdsStackSmall, true, kWorldBvh4>(waves, c->scene_lds_bytes4);
+            return FRT_OK;
+        }
+        // speculative 4-wide traversal (FRT_FLAG_SPEC)
+        if (!lds && (flags & FRT_FLAG_SPEC) && c->has_bvh4 && !(flags & FRT_FLAG_BVH2) &&
+            bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
+            L = bvh_launcher<kBvh4LdsStack, false, kWorldBvh4, true>(waves, 0);
+            return FRT_OK;
+        }
+    }
+    // HBM-resident scenes: the 4-wide quantized BVH (half the bytes per box test)
+    if (!lds && c->has_bvh4 && !(flags & FRT_FLAG_BVH2) && bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
+        L = bvh_launcher<kBvh4LdsStack, false, kWorldBvh4, false, MATS>(waves, 0);
+        return FRT_OK;
+    }
+    // LDS-resident binary tree: the per-octant node copies when they fit
+    const bool oct = lds && !(flags & FRT_FLAG_NO_OCT) && c->scene_lds_bytes_oct <= kLdsOctBytes;
+    if (oct) {
+        L = d < 8 ? bvh_launcher<8, true, kWorldBvh2Oct, false, MATS>(waves, c->scene_lds_bytes_oct)
+                  : bvh_launcher<16, true, kWorldBvh2Oct, false, MATS>(waves, c->scene_lds_bytes_oct);
+        return FRT_OK;
+    }
+    if (d < 8) L = lds ? bvh_launcher<8, true, FRT_WORLD_BVH, false, MATS>(waves, sb)
+                       : bvh_launcher<8, false, FRT_WORLD_BVH, false, MATS>(waves, 0);
+    else if (d < 16) L = lds ? bvh_launcher<16, true, FRT_WORLD_BVH, false, MATS>(waves, sb)
+                             : bvh_launcher<16, false, FRT_WORLD_BVH, false, MATS>(waves, 0);
+    else if (d < 24) L = bvh_launcher<24, false, FRT_WORLD_BVH, false, MATS>(waves, 0);
+    else if (d < 32) L = bvh_launcher<32, false, FRT_WORLD_BVH, false, MATS>(waves, 0);
+    else if (d < 64) L = make_launcher<64, FRT_WORLD_BVH, false, 1, false, MATS>(0);
+    else return FRT_E_UNSUPPORTED;
+    return FRT_OK;
+}
+// AO / normals: the default plans only (LDS-resident binary BVH, HBM 4-wide or
+// binary), register caps as for path; ao keeps the specular generate() code.
+template <int KIND>
+static int pick_launcher_kind(const frt_ctx *c, int flags, Launcher &L)
+{
+    constexpr int M = KIND == FRT_INTEGRATOR_AO ? kMatsAll : kMatsNone;
+    if (c->world_kind == FRT_WORLD_LIST) { L = make_launcher<16, FRT_WORLD_LIST, false, 1, false, M, KIND>(0); return FRT_OK; }
+    const int d = c->stack_needed;
+    const size_t sb = c->scene_lds_bytes;
+    const bool lds = d < kLdsMaxDepth && sb <= kLdsSceneBytes && !(flags & FRT_FLAG_NO_LDS_SCENE);
+    const bool oct = lds && !(flags & FRT_FLAG_NO_OCT) && c->scene_lds_bytes_oct <= kLdsOctBytes;
+    if (oct) {
+        L = d < 8 ? make_launcher<8, kWorldBvh2Oct, true, 5, false, M, KIND>(c->scene_lds_bytes_oct)
+                  : make_launcher<16, kWorldBvh2Oct, true, 5, false, M, KIND>(c->scene_lds_bytes_oct);
+    } else if (lds) {
+        L = d < 8 ? make_launcher<8, FRT_WORLD_BVH, true, 5, false, M, KIND>(sb)
+                  : make_launcher<16, FRT_WORLD_BVH, true, 5, false, M, KIND>(sb);
+    } else if (c->has_bvh4 && !(flags & FRT_FLAG_BVH2) && bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
+        L = make_launcher<kBvh4LdsStack, kWorldBvh4, false, 6, false, M, KIND>(0);
+    } else if (d < 16) {
+        L = make_launcher<16, FRT_WORLD_BVH, false, 6, false, M, KIND>(0);
+    } else if (d < 32) {
+        L = make_launcher<32, FRT_WORLD_BVH, false, 6, false, M, KIND>(0);
+    } else if (d < 64) {
+        L = make_launcher<64, FRT_WORLD_BVH, false, 1, false, M, KIND>(0);
+    } else {
+        return FRT_E_UNSUPPORTED;
+    }
+    return FRT_OK;
+}
+// fp64 kernels (path only; DESIGN.md "Precision"): the list world with the
+// scene's material set, or the binary tree from HBM with every material
+// compiled in (the debugging build; no register cap, stack 32 or 64)
+template <int MATS>
+static int pick_launcher_f64_t(const frt_ctx *c, Launcher &L)
+{
+    if (c->world_kind == FRT_WORLD_LIST) {
+        // (a 2-wave register cap changed nothing: profiles/r03/r03c_ab_veach_listbox_f64waves.jsonl)
+        L = make_launcher<16, FRT_WORLD_LIST, false, 1, false, MATS, FRT_INTEGRATOR_PATH, double>(0);
+        return FRT_OK;
+    }
+    const int d = c->stack_needed;
+    if (d < 32) L = make_launcher<32, FRT_WORLD_BVH, false, 1, false, kMatsAll, FRT_INTEGRATOR_PATH, double>(0);
+    else if (d < 64) L = make_launcher<64, FRT_WORLD_BVH, false, 1, false, kMatsAll, FRT_INTEGRATOR_PATH, double>(0);
+    else return FRT_E_UNSUPPORTED;
+    return FRT_OK;
+}
+template <int STACK, int WORLD, bool LDS, bool MATS>
+static void mlt_kernels_t(const void **boot, const void **chains)
+{
+    *boot = reinterpret_cast<const void *>(&mlt_bootstrap<STACK, WORLD, MATS>);
+    *chains = reinterpret_cast<const void *>(&mlt_megakernel<STACK, WORLD, LDS, MATS>);
+}
+
+// the material unit's entry points (frt_render_mats.hip)
+namespace frt_mats {
+// path (KIND = FRT_INTEGRATOR_PATH, fp32), fp64 path (f64) or AO: the plan for
+// the scene's material set c->mats (!= kMatsNone)
+int pick(const frt_ctx *c, int integrator, int flags, bool f64, Launcher &L);
+// PSS-MLT with the material branch, for the (stack, world, lds) plans of render_mlt
+int mlt(int stack, int world, bool lds, const void **boot, const void **chains);
+}  // namespace frt_mats
+
+#ifdef FRT_TU_MATS
+int frt_mats::pick(const frt_ctx *c, int integrator, int flags, bool f64, Launcher &L)
+{
+    if (integrator == FRT_INTEGRATOR_AO) return pick_launcher_kind<FRT_INTEGRATOR_AO>(c, flags, L);
+    if (f64) {
+        switch (c->mats) {
+        case kMatsNone: return pick_launcher_f64_t<kMatsNone>(c, L);   // BVH worlds: kMatsAll kernels
+        case kMatsTex: return pick_launcher_f64_t<kMatsTex>(c, L);
+        case kMatsSpec: return pick_launcher_f64_t<kMatsSpec>(c, L);   // veach_mis (C3): phong plates
+        case kMatsSpec | kMatsTex: return pick_launcher_f64_t<kMatsSpec | kMatsTex>(c, L);
+        default: return pick_launcher_f64_t<kMatsAll>(c, L);
+        }
+    }
+    switch (c->mats) {   // the smallest kernel covering the scene's materials
+    case kMatsTex: return pick_launcher_t<kMatsTex>(c, flags, L);
+    case kMatsSpec:
+    case kMatsSpec | kMatsTex: return pick_launcher_t<kMatsSpec | kMatsTex>(c, flags, L);
+    default: return pick_launcher_t<kMatsAll>(c, flags, L);
+    }
+}
+int frt_mats::mlt(int stack, int world, bool lds, const void **boot, const void **chains)
+{
+    if (world == FRT_WORLD_LIST) mlt_kernels_t<16, FRT_WORLD_LIST, false, true>(boot, chains);
+    else if (world == kWorldBvh4) mlt_kernels_t<kBvh4LdsStack, kWorldBvh4, false, true>(boot, chains);
+    else if (lds && stack == 8) mlt_kernels_t<8, FRT_WORLD_BVH, true, true>(boot, chains);
+    else if (lds && stack == 16) mlt_kernels_t<16, FRT_WORLD_BVH, true, true>(boot, chains);
+    else if (!lds && stack == 16) mlt_kernels_t<16, FRT_WORLD_BVH, false, true>(boot, chains);
+    else if (!lds && stack == 32) mlt_kernels_t<32, FRT_WORLD_BVH, false, true>(boot, chains);
+    else if (!lds && stack == 64) mlt_kernels_t<64, FRT_WORLD_BVH, false, true>(boot, chains);
+    else return FRT_E_UNSUPPORTED;
+    return FRT_OK;
+}
+#else   // the main unit: everything else
+
 
 static void free_comms(frt_ctx *c)
 {
@@ -1476,7 +1711,6 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
 }
 
 // 4-wide traversal holds at most 3 pending siblings per level of the path
-static bool bvh4_stack_fits(int depth4, int lds_entries) { return 3 * depth4 <= lds_entries + kBvh4Overflow; }
 constexpr int kSelftestStack = 8;   // small, so the host self-test exercises the overflow entries
 
 // host image of the flattened scene as the kernels see it (HBM strides)
@@ -1655,180 +1889,6 @@ extern "C" int frt_shard_slots(const frt_render_params *p, int32_t *slot_pixel)
 }
 
 
-struct Launcher {
-    const void *fn = nullptr;
-    size_t lds = 0;
-    int stack = 0;
-    int waves = 0;
-    bool lds_scene = false;
-    bool wide = false;      // 4-wide quantized BVH
-    bool f64 = false;       // the fp64 kernel
-};
-template <int STACK, int WORLD, bool LDS, int WAVES = 1, bool SPEC = false, int MATS = kMatsNone,
-          int KIND = FRT_INTEGRATOR_PATH, typename R = float>
-static Launcher make_launcher(size_t scene_bytes)
-{
-    Launcher L;
-    L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES, SPEC, MATS, KIND, R>);
-    L.f64 = kIsF64<R>;
-    L.lds = (WORLD != FRT_WORLD_LIST ? (size_t)STACK * kBlock * sizeof(int) : 0) +
-            (size_t)kItemWords * kBlock * sizeof(int) + (LDS ? scene_bytes : 0);
-    L.stack = STACK;
-    L.waves = WAVES > 1 ? WAVES : 0;
-    L.lds_scene = LDS;
-    L.wide = WORLD == kWorldBvh4;
-    return L;
-}
-#ifndef FRT_EXP_W6
-#define FRT_EXP_W6 6   // experiment builds: the register cap behind the "6 waves" plans
-#endif
-template <int STACK, bool LDS, int WORLD = FRT_WORLD_BVH, bool SPEC = false, int MATS = kMatsNone>
-static Launcher bvh_launcher(int waves, size_t sb)
-{
-    // Every material set has a 6-wave build again (round 3).  In round 2 the
-    // rough-conductor kernel of the HBM binary plan compiled under that cap to
-    // a kernel with the oracle's ray counts and wrong radiance; that source
-    // state (5a5829a) reproduces it at -O3 and not at -O1, and moving the
-    // AMDGPU high-pressure rescheduling stage moves the failure to the 5-wave
-    // kernel: the result follows machine code generation.  The shading code's
-    // host replay is clean under ASan / UBSan / pattern init (the megakernel
-    // loop itself runs only on the device).  The current
-    // source agrees under every cap and plan (test_register_caps_agree;
-    // DESIGN.md "Register-cap hazard").  The defaults stay 4 / 5 waves for the
-    // specular sets (faster than 6: profiles/r02/r02_ab_sphere_hbm_mats.jsonl).
-    if (waves == 6) return make_launcher<STACK, WORLD, LDS, FRT_EXP_W6, SPEC, MATS>(sb);
-    if (waves == 5) return make_launcher<STACK, WORLD, LDS, 5, SPEC, MATS>(sb);
-    if constexpr (MATS != kMatsNone) {
-        if (waves == 4) return make_launcher<STACK, WORLD, LDS, 4, SPEC, MATS>(sb);
-        if (waves == 3) return make_launcher<STACK, WORLD, LDS, 3, SPEC, MATS>(sb);
-    }
-    return make_launcher<STACK, WORLD, LDS, 1, SPEC, MATS>(sb);
-}
-#ifndef FRT_EXP_BVH4_LSTACK
-#define FRT_EXP_BVH4_LSTACK 16
-#endif
-constexpr int kBvh4LdsStack = FRT_EXP_BVH4_LSTACK;   // 16 KiB of LDS per block; deeper entries go to scratch
-constexpr int kBvh4LdsStackSmall = 8;   // LDS-resident scenes (shallow trees)
-constexpr int kBruteMaxTris = 128;
-// MATS: the material set the kernel is compiled for (kMats* mask, frt_path.hpp)
-template <int MATS>
-static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
-{
-    if (c->world_kind == FRT_WORLD_LIST) { L = make_launcher<16, FRT_WORLD_LIST, false, 1, false, MATS>(0); return FRT_OK; }
-    const int d = c->stack_needed;
-    const size_t sb = c->scene_lds_bytes;
-    const bool lds = d < kLdsMaxDepth && sb <= kLdsSceneBytes && !(flags & FRT_FLAG_NO_LDS_SCENE);
-    // register cap: waves/SIMD the compiler must fit (its spills land in the
-    // shading code, not the traversal loops).  Measured (profiles/r01_ab_perf3.jsonl):
-    // 5 waves best for LDS-resident scenes, 6 for HBM-resident ones.  The
-    // material kernels (MATS) in LDS run 15-21 % faster on the compiler's own
-    // allocation than under the 5-wave cap (profiles/r01d_perf_mats.jsonl).
-    // Material kernels: textures alone cost about the lambertian kernel's
-    // registers (117 vs 111 VGPRs uncapped; the compiler's 4 waves are best),
-    // the specular branch 152, the rough conductor lobes 170 -- capped at 4
-    // waves/SIMD (128 VGPRs; a few spills in the specular shading) they run
-    // +40 % over the compiler's 2-wave allocation (same-call A/B,
-    // profiles/r02/r02_mats*.jsonl).
-    // (The lambertian LDS kernel fits 111 VGPRs without spills since its work-
-    // item state moved to LDS; the compiler's 4 waves win 2 % at 64 spp but lose
-    // 10 % at the bench's 512 spp -- 337 vs 307 ms, same call --, so the cap stays:
-    // profiles/r02/r02_ab_cornell_knobs.jsonl, r02_ab_cornell_512spp.jsonl.)
-    int waves = (MATS & kMatsSpecAny) ? (lds ? 4 : 5) : MATS == kMatsTex && lds ? 0 : lds ? 5 : 6;
-    if constexpr (MATS != kMatsNone) {   // FRT_MATS_WAVES: register cap of the material kernels (tuning knob, not part of the C-ABI)
-        const char *e = std::getenv("FRT_MATS_WAVES");
-        if (e) waves = std::atoi(e);
-    }
-    if (flags & FRT_FLAG_WAVES4) waves = 0;   // the compiler's own allocation (~120 VGPRs, 4 waves)
-    if (flags & FRT_FLAG_WAVES5) waves = 5;
-    if (flags & FRT_FLAG_WAVES6) waves = 6;
-    if constexpr (MATS == kMatsNone) {   // A/B plans, lambertian scenes only
-        // tiny triangle-only scenes from LDS, every triangle in lockstep (FRT_FLAG_BRUTE)
-        if (lds && (flags & FRT_FLAG_BRUTE) && c->n_spheres == 0 && c->n_tris <= kBruteMaxTris) {
-            L = bvh_launcher<8, true, kWorldBrute>(waves, sb);
-            return FRT_OK;
-        }
-        // LDS-resident scenes, 4-wide (FRT_FLAG_BVH4)
-        if (lds && (flags & FRT_FLAG_BVH4) && c->has_bvh4 && c->scene_lds_bytes4 <= kLdsSceneBytes &&
-            bvh4_stack_fits(c->depth4, kBvh4LdsStackSmall)) {
-            L = bvh_launcher<kBvh4LdsStackSmall, true, kWorldBvh4>(waves, c->scene_lds_bytes4);
-            return FRT_OK;
-        }
-        // speculative 4-wide traversal (FRT_FLAG_SPEC)
-        if (!lds && (flags & FRT_FLAG_SPEC) && c->has_bvh4 && !(flags & FRT_FLAG_BVH2) &&
-            bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
-            L = bvh_launcher<kBvh4LdsStack, false, kWorldBvh4, true>(waves, 0);
-            return FRT_OK;
-        }
-    }
-    // HBM-resident scenes: the 4-wide quantized BVH (half the bytes per box test)
-    if (!lds && c->has_bvh4 && !(flags & FRT_FLAG_BVH2) && bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
-        L = bvh_launcher<kBvh4LdsStack, false, kWorldBvh4, false, MATS>(waves, 0);
-        return FRT_OK;
-    }
-    // LDS-resident binary tree: the per-octant node copies when they fit
-    const bool oct = lds && !(flags & FRT_FLAG_NO_OCT) && c->scene_lds_bytes_oct <= kLdsOctBytes;
-    if (oct) {
-        L = d < 8 ? bvh_launcher<8, true, kWorldBvh2Oct, false, MATS>(waves, c->scene_lds_bytes_oct)
-                  : bvh_launcher<16, true, kWorldBvh2Oct, false, MATS>(waves, c->scene_lds_bytes_oct);
-        return FRT_OK;
-    }
-    if (d < 8) L = lds ? bvh_launcher<8, true, FRT_WORLD_BVH, false, MATS>(waves, sb)
-                       : bvh_launcher<8, false, FRT_WORLD_BVH, false, MATS>(waves, 0);
-    else if (d < 16) L = lds ? bvh_launcher<16, true, FRT_WORLD_BVH, false, MATS>(waves, sb)
-                             : bvh_launcher<16, false, FRT_WORLD_BVH, false, MATS>(waves, 0);
-    else if (d < 24) L = bvh_launcher<24, false, FRT_WORLD_BVH, false, MATS>(waves, 0);
-    else if (d < 32) L = bvh_launcher<32, false, FRT_WORLD_BVH, false, MATS>(waves, 0);
-    else if (d < 64) L = make_launcher<64, FRT_WORLD_BVH, false, 1, false, MATS>(0);
-    else return FRT_E_UNSUPPORTED;
-    return FRT_OK;
-}
-// AO / normals: the default plans only (LDS-resident binary BVH, HBM 4-wide or
-// binary), register caps as for path; ao keeps the specular generate() code.
-template <int KIND>
-static int pick_launcher_kind(const frt_ctx *c, int flags, Launcher &L)
-{
-    constexpr int M = KIND == FRT_INTEGRATOR_AO ? kMatsAll : kMatsNone;
-    if (c->world_kind == FRT_WORLD_LIST) { L = make_launcher<16, FRT_WORLD_LIST, false, 1, false, M, KIND>(0); return FRT_OK; }
-    const int d = c->stack_needed;
-    const size_t sb = c->scene_lds_bytes;
-    const bool lds = d < kLdsMaxDepth && sb <= kLdsSceneBytes && !(flags & FRT_FLAG_NO_LDS_SCENE);
-    const bool oct = lds && !(flags & FRT_FLAG_NO_OCT) && c->scene_lds_bytes_oct <= kLdsOctBytes;
-    if (oct) {
-        L = d < 8 ? make_launcher<8, kWorldBvh2Oct, true, 5, false, M, KIND>(c->scene_lds_bytes_oct)
-                  : make_launcher<16, kWorldBvh2Oct, true, 5, false, M, KIND>(c->scene_lds_bytes_oct);
-    } else if (lds) {
-        L = d < 8 ? make_launcher<8, FRT_WORLD_BVH, true, 5, false, M, KIND>(sb)
-                  : make_launcher<16, FRT_WORLD_BVH, true, 5, false, M, KIND>(sb);
-    } else if (c->has_bvh4 && !(flags & FRT_FLAG_BVH2) && bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
-        L = make_launcher<kBvh4LdsStack, kWorldBvh4, false, 6, false, M, KIND>(0);
-    } else if (d < 16) {
-        L = make_launcher<16, FRT_WORLD_BVH, false, 6, false, M, KIND>(0);
-    } else if (d < 32) {
-        L = make_launcher<32, FRT_WORLD_BVH, false, 6, false, M, KIND>(0);
-    } else if (d < 64) {
-        L = make_launcher<64, FRT_WORLD_BVH, false, 1, false, M, KIND>(0);
-    } else {
-        return FRT_E_UNSUPPORTED;
-    }
-    return FRT_OK;
-}
-// fp64 kernels (path only; DESIGN.md "Precision"): the list world with the
-// scene's material set, or the binary tree from HBM with every material
-// compiled in (the debugging build; no register cap, stack 32 or 64)
-template <int MATS>
-static int pick_launcher_f64_t(const frt_ctx *c, Launcher &L)
-{
-    if (c->world_kind == FRT_WORLD_LIST) {
-        // (a 2-wave register cap changed nothing: profiles/r03/r03c_ab_veach_listbox_f64waves.jsonl)
-        L = make_launcher<16, FRT_WORLD_LIST, false, 1, false, MATS, FRT_INTEGRATOR_PATH, double>(0);
-        return FRT_OK;
-    }
-    const int d = c->stack_needed;
-    if (d < 32) L = make_launcher<32, FRT_WORLD_BVH, false, 1, false, kMatsAll, FRT_INTEGRATOR_PATH, double>(0);
-    else if (d < 64) L = make_launcher<64, FRT_WORLD_BVH, false, 1, false, kMatsAll, FRT_INTEGRATOR_PATH, double>(0);
-    else return FRT_E_UNSUPPORTED;
-    return FRT_OK;
-}
 // does this render run the fp64 kernels?  FRT_FLAG_FP64 / _FP32 override the
 // context's precision for one call (A/B)
 static bool use_f64(const frt_ctx *c, const frt_render_params *p)
@@ -1839,25 +1899,15 @@ static bool use_f64(const frt_ctx *c, const frt_render_params *p)
 }
 static int pick_launcher(const frt_ctx *c, int integrator, int flags, Launcher &L, bool f64)
 {
-    if (f64) {
-        if (!c->has_f64) return FRT_E_INVALID;
-        switch (c->mats) {
-        case kMatsNone: return pick_launcher_f64_t<kMatsNone>(c, L);
-        case kMatsTex: return pick_launcher_f64_t<kMatsTex>(c, L);
-        case kMatsSpec: return pick_launcher_f64_t<kMatsSpec>(c, L);   // veach_mis (C3): phong plates
-        case kMatsSpec | kMatsTex: return pick_launcher_f64_t<kMatsSpec | kMatsTex>(c, L);
-        default: return pick_launcher_f64_t<kMatsAll>(c, L);
-        }
-    }
-    if (integrator == FRT_INTEGRATOR_AO) return pick_launcher_kind<FRT_INTEGRATOR_AO>(c, flags, L);
+    if (f64 && !c->has_f64) return FRT_E_INVALID;
     if (integrator == FRT_INTEGRATOR_NORMALS) return pick_launcher_kind<FRT_INTEGRATOR_NORMALS>(c, flags, L);
-    switch (c->mats) {   // the smallest kernel covering the scene's materials
-    case kMatsNone: return pick_launcher_t<kMatsNone>(c, flags, L);
-    case kMatsTex: return pick_launcher_t<kMatsTex>(c, flags, L);
-    case kMatsSpec:
-    case kMatsSpec | kMatsTex: return pick_launcher_t<kMatsSpec | kMatsTex>(c, flags, L);
-    default: return pick_launcher_t<kMatsAll>(c, flags, L);
+    if (integrator == FRT_INTEGRATOR_AO || c->mats != kMatsNone || (f64 && c->world_kind != FRT_WORLD_LIST))
+        return frt_mats::pick(c, integrator, flags, f64, L);   // every kernel with a material set
+    if (f64) {   // a lambertian list world (BVH worlds' fp64 kernels carry every material: the other unit)
+        L = make_launcher<16, FRT_WORLD_LIST, false, 1, false, kMatsNone, FRT_INTEGRATOR_PATH, double>(0);
+        return FRT_OK;
     }
+    return pick_launcher_t<kMatsNone>(c, flags, L);
 }
 
 
@@ -1960,16 +2010,12 @@ extern "C" int frt_trace_device(frt_ctx *c, const float *rays, int64_t n, float 
 }
 
 // ---- PSS-MLT render: bootstrap b, then the chain megakernel splatting into dev_film ----
+// PSS-MLT kernels of a plan: the material branch from the material unit
 template <int STACK, int WORLD, bool LDS = false>
 static void mlt_kernels(bool mats, const void **boot, const void **chains)
 {
-    if (mats) {
-        *boot = reinterpret_cast<const void *>(&mlt_bootstrap<STACK, WORLD, true>);
-        *chains = reinterpret_cast<const void *>(&mlt_megakernel<STACK, WORLD, LDS, true>);
-    } else {
-        *boot = reinterpret_cast<const void *>(&mlt_bootstrap<STACK, WORLD, false>);
-        *chains = reinterpret_cast<const void *>(&mlt_megakernel<STACK, WORLD, LDS, false>);
-    }
+    if (mats) frt_mats::mlt(STACK, WORLD, LDS, boot, chains);
+    else mlt_kernels_t<STACK, WORLD, LDS, false>(boot, chains);
 }
 
 static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, hipStream_t st, frt_stats *stats)
@@ -2420,3 +2466,5 @@ extern "C" int frt_render_multi(frt_ctx **ctxs, int n, const frt_render_params *
     }
     return FRT_OK;
 }
+
+#endif  // FRT_TU_MATS

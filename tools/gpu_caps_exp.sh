@@ -13,4 +13,11 @@ for n in cur ${LIBS:-base wz sgv nohirp o1}; do
   timeout -k 10 240 python -u tools/caps_table.py --tag $n >> $O/caps.jsonl 2>> $O/log.txt || { rc=$?; break; }
 done
 echo "rc=$rc" > $O/rc.txt
+# DBG=<lib name>: then the per-vertex capture of that build (tools/caps_dbg.py)
+if [ $rc = 0 ] && [ -n "$DBG" ]; then
+  FRT_LIB_PATH=first_raytracer_amd/build/exp/libfrt_$DBG.so timeout -k 10 240 python -u tools/caps_dbg.py \
+      --flags ${DBG_FLAGS:-17} --good 0 --bad ${DBG_BAD:-4} > $O/dbg.txt 2>> $O/log.txt
+  rc=$?
+  echo "rc=$rc" > $O/rc.txt
+fi
 exit $rc
