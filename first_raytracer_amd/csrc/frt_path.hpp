@@ -80,7 +80,6 @@ __device__ __forceinline__ unsigned long long *diag_slot()
 #endif
 
 constexpr int kSentinel = 0x7fffffff;   // "stack empty"; never a node index
-constexpr int kEmptyChild = kSentinel;  // unused slot of a 4-wide node (never pushed)
 constexpr int kWorldBvh4 = 2;           // internal world kind: 4-wide quantized BVH
 constexpr int kWorldBrute = 3;          // internal world kind: every triangle, in lockstep (tiny scenes)
 constexpr int kWorldBvh2Oct = 4;        // internal world kind: binary nodes from LDS, one copy per ray octant
@@ -374,14 +373,9 @@ FRT_HD bool bvh4_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit
         // near / far plane words per axis by the ray's direction sign: a
         // negative 1/d turns the hi plane into the entry plane.  Per child this
         // replaces the per-axis min / max of the two plane distances (the same
-        // values: q_lo <= q_hi and the scale a has the sign of 1/d), and empty
-        // slots are stored as the inverted box q_lo = 255 > q_hi = 0 (build_bvh4)
-        // and are also rejected by their ref: on a node thin against its
-        // distance from the ray origin an axis' planes can round to one value
-        // (255 * a vanishes against b in the FMA), and a real child's hit is
-        // then tn == tf -- it must stay a hit (tests/test_device_logic_host.py
-        // test_bvh4_tiny_far_nodes), so the slab test alone cannot tell an
-        // empty slot whose three axes all collapsed.
+        // values: q_lo <= q_hi and the scale a has the sign of 1/d).  Empty
+        // slots are the inverted box q_lo = 255 > q_hi = 0 with a harmless ref
+        // (build_bvh4), so they need no test here.
         const bool sx = sr.invd.x < 0.0f, sy = sr.invd.y < 0.0f, sz = sr.invd.z < 0.0f;
         const uint32_t xn = sx ? w2.y : w2.x, xf = sx ? w2.x : w2.y;
         const uint32_t yn = sy ? w2.w : w2.z, yf = sy ? w2.z : w2.w;
@@ -396,7 +390,7 @@ FRT_HD bool bvh4_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit
             const float tzn = fmaf((float)((zn >> sh) & 0xffu), az, bz), tzf = fmaf((float)((zf >> sh) & 0xffu), az, bz);
             const float tn = fmaxf(fmaxf(txn, tyn), fmaxf(tzn, T.tmin));
             const float tf = fminf(fminf(txf, tyf), fminf(tzf, T.h.t));
-            t[i] = (tf < tn || c[i] == kEmptyChild) ? __builtin_inff() : tn;
+            t[i] = (tf < tn) ? __builtin_inff() : tn;
         }
         // nearest first: sorting network on (t, child), as selects (no branches)
         auto cx = [&](int i, int j) {

@@ -1304,14 +1304,23 @@ static bool build_bvh4(FlatScene &F, int root_ref)
             }
         }
         // empty slots: the inverted box q_lo = 255 > q_hi = 0 on every axis,
-        // which the near / far slab test of bvh4_step rejects by itself
+        // which the near / far slab test of bvh4_step rejects -- except on a
+        // node so small against its distance from the ray origin that each
+        // axis' planes round to one value (then a real child's hit has tn ==
+        // tf and must stay a hit, so the test cannot reject it either; ADVICE
+        // r2, test_bvh4_tiny_far_nodes).  Their ref is a one-primitive leaf of
+        // the scene's first primitive: a spurious visit re-tests a real
+        // primitive, which cannot change a closest hit (same t, same DFS rank)
+        // or an any-hit answer, and needs no per-child ref compare in the node
+        // loop (that compare cost 2 % on cornell_1m).
         for (int k = n; k < 4; ++k)
             for (int a = 0; a < 3; ++a) qlo[a] |= 0xffu << (8 * k);
+        const uint32_t empty_ref = (uint32_t)~(F.tris.empty() ? FRT_PRIM_SPHERE : 0);
         uint4 w0, w1, w2, w3;
         w0.x = (uint32_t)f2i(org[0]); w0.y = (uint32_t)f2i(org[1]); w0.z = (uint32_t)f2i(org[2]);
         w0.w = (uint32_t)(ex[0] + 127) | ((uint32_t)(ex[1] + 127) << 8) | ((uint32_t)(ex[2] + 127) << 16);
         uint32_t refs[4];
-        for (int k = 0; k < 4; ++k) refs[k] = (uint32_t)(k < n ? ch[k].ref : kEmptyChild);
+        for (int k = 0; k < 4; ++k) refs[k] = k < n ? (uint32_t)ch[k].ref : empty_ref;
         w1.x = refs[0]; w1.y = refs[1]; w1.z = refs[2]; w1.w = refs[3];
         w2.x = qlo[0]; w2.y = qhi[0]; w2.z = qlo[1]; w2.w = qhi[1];
         w3.x = qlo[2]; w3.y = qhi[2]; w3.z = 0; w3.w = 0;

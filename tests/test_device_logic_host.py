@@ -132,8 +132,11 @@ def test_specular_scenes(objfix, request):
 def test_bvh4_tiny_far_nodes(tmp_path):
     """4-wide nodes tiny against their distance from the ray origin, where an
     axis' quantized planes round to one value (255 * a vanishes in the slab
-    FMA): a real child's hit is then tn == tf and must stay a hit, while empty
-    slots (inverted boxes) are rejected by their ref.  A 20 x 20 grid of
+    FMA): a real child's hit is then tn == tf and must stay a hit.  (An empty
+    slot, an inverted box, passes the same test only when all three axes
+    collapse and their entry distances are equal in fp32; its ref is then a
+    one-primitive leaf of the scene's first primitive, which cannot change the
+    answer: build_bvh4, ADVICE r2.  This scene collapses the z axis only.)  A 20 x 20 grid of
     1e-6-sized triangles around the origin (nodes of ~1e-5, the padding of a
     unit-scale scene) seen from 1e3 away (farther, the reference's own
     t_min = EPSILON * |o| would cull the hits, parallel_bvh.h:46-51).  Shading

@@ -18,6 +18,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+if os.environ.get("FRT_PKG_ROOT"):   # another revision's package (its binding + libfrt.so), same-call A/B
+    sys.path.insert(0, os.environ["FRT_PKG_ROOT"])
 
 
 def main():
