@@ -165,7 +165,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     // ray in flight: tracing = traversal steps remain; pending = finished, not yet shaded
     Trav<R> T;
     bool tracing = false, pending = false;
-    int ovf[WORLD == kWorldBvh4 ? kBvh4Overflow : 1];
+    int ovf[kOverflow<WORLD>];
     // ray counters are wave-uniform (SGPRs): popcounts of per-iteration ballots
     unsigned long long n_cam = 0, n_ext = 0, n_sh = 0, n_smp = 0;
 
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     else scene_strides_hbm(S);
     const int lane = threadIdx.x & 63;
     Trav<float> T;
-    int ovf[WORLD == kWorldBvh4 ? kBvh4Overflow : 1];
+    int ovf[kOverflow<WORLD>];
     f3 o = mk3(0, 0, 0), d = mk3(0, 0, 1);
     bool anyhit = false, tracing = false, exhausted = false;
     uint32_t id = 0;
@@ -556,7 +556,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
     // pending = finished (or the path went beyond MaxPathLength), not yet shaded
     Trav<float> T;
     bool tracing = false, pending = false, beyond = false;
-    int ovf[WORLD == kWorldBvh4 ? kBvh4Overflow : 1];
+    int ovf[kOverflow<WORLD>];
     for (;;) {
         // ---- traversal steps until at most trav_min lanes still traverse ----
         for (;;) {
@@ -729,8 +729,9 @@ struct frt_ctx {
     bool have_scene = false;
     DevScene S{};
     int world_kind = 0, stack_needed = 0;
-    bool has_bvh4 = false;
-    int depth4 = 0;
+    bool has_bvh4 = false;        // nodes4 holds the 4-wide BVH4Q
+    bool has_bvh8 = false;        // ... or the 8-wide nodes (FRT_WIDE=8 at upload)
+    int depth4 = 0;               // levels of that wide tree
     int n_tris = 0, n_spheres = 0;
     bool has_spec_mats = false;   // a non-lambertian scattering material or a texture: MATS kernels
     int mats = kMatsNone;         // kMats* mask of the scene's material set (pick_launcher)
@@ -769,6 +770,7 @@ struct frt_ctx {
 // count (DESIGN.md "Register-cap hazard").  The lambertian kernels (the
 // bench configurations) stay on the greedy allocator.
 static bool bvh4_stack_fits(int depth4, int lds_entries) { return 3 * depth4 <= lds_entries + kBvh4Overflow; }
+static bool bvh8_stack_fits(int depth8, int lds_entries) { return 7 * depth8 <= lds_entries + kBvh8Overflow; }
 struct Launcher {
     const void *fn = nullptr;
     size_t lds = 0;
@@ -790,7 +792,7 @@ static Launcher make_launcher(size_t scene_bytes)
     L.stack = STACK;
     L.waves = WAVES > 1 ? WAVES : 0;
     L.lds_scene = LDS;
-    L.wide = WORLD == kWorldBvh4;
+    L.wide = WORLD == kWorldBvh4 || WORLD == kWorldBvh8;
     return L;
 }
 #ifndef FRT_EXP_W6
@@ -868,6 +870,14 @@ static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
         if (!lds && (flags & FRT_FLAG_SPEC) && c->has_bvh4 && !(flags & FRT_FLAG_BVH2) &&
             bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
             L = bvh_launcher<kBvh4LdsStack, false, kWorldBvh4, true>(waves, 0);
+            return FRT_OK;
+        }
+    }
+    // HBM-resident scenes: the 8-wide nodes when uploaded (lambertian kernels; the
+    // material kernels take the binary tree then)
+    if constexpr (MATS == kMatsNone) {
+        if (!lds && c->has_bvh8 && !(flags & FRT_FLAG_BVH2) && bvh8_stack_fits(c->depth4, kBvh4LdsStack)) {
+            L = bvh_launcher<kBvh4LdsStack, false, kWorldBvh8>(waves, 0);
             return FRT_OK;
         }
     }
@@ -1123,6 +1133,7 @@ struct FlatScene {
     std::vector<float4> nodes_oct;   // 8 octant copies of `nodes` (DevScene::nodes_oct), LDS plan scenes only
     std::vector<double4> tris64, tshade64, tnorm64, spheres64;   // fp64 records (DevScene::tris64 ...)
     bool has4 = false;           // nodes4 / root4 usable
+    int width = 4;               // nodes4 holds 4-wide (4 uint4 / node) or 8-wide (8 uint4 / node) nodes
     int root4 = 0, depth4 = 0;
     std::vector<int> smat, lights, list;
     std::vector<int> tri_view;      // device triangle id -> scene-view triangle (DevScene::tri_view)
@@ -1158,6 +1169,13 @@ static int min_desc(bool lds_scene)
 // Triangles per leaf: FRT_LEAF_SIZE overrides (1 = the reference's one-prim
 // leaves), else 0 = by plan (see flatten_scene).  A tuning knob of this
 // library, not part of the C-ABI.
+// Width of the HBM plans' wide tree: FRT_WIDE=8 builds the 8-wide nodes of
+// bvh8_step instead of BVH4Q (read at upload; an A/B knob, not part of the C-ABI).
+static int wide_override()
+{
+    const char *e = std::getenv("FRT_WIDE");
+    return e && std::atoi(e) == 8 ? 8 : 4;
+}
 static int leaf_size_override()
 {
     const char *e = std::getenv("FRT_LEAF_SIZE");
@@ -1228,9 +1246,14 @@ static void collapse_leaves(FlatScene &F, int leaf_max)
 // bits per plane on a per-node power-of-two grid, rounded outward.  Nodes in
 // pre-order.  Returns false (no BVH4; the binary tree is used) when a node's
 // grid would overflow the slab arithmetic.
-static bool build_bvh4(FlatScene &F, int root_ref)
+// W = 4: BVH4Q (bvh4_step), 4 uint4 per node.  W = 8: the 8-wide nodes of
+// bvh8_step, 8 uint4 per node (6 used), children in octant slots.
+template <int W>
+static bool build_wide(FlatScene &F, int root_ref)
 {
+    constexpr int NU = W == 4 ? 4 : 8;                // uint4 per node
     F.nodes4.clear();
+    F.width = W;
     F.depth4 = 0;
     F.root4 = root_ref;
     const int nn = (int)(F.nodes.size() / 4);
@@ -1245,21 +1268,33 @@ static bool build_bvh4(FlatScene &F, int root_ref)
         const double dx = (double)c.hi[0] - c.lo[0], dy = (double)c.hi[1] - c.lo[1], dz = (double)c.hi[2] - c.lo[2];
         return dx * dy + dy * dz + dz * dx;
     };
-    struct Item { int bin, parent, slot, lvl; };   // binary node, 4-wide parent (-1 root), child slot, level
+    // empty slots: the inverted box q_lo = 255 > q_hi = 0 on every axis,
+    // which the near / far slab test rejects -- except on a node so small
+    // against its distance from the ray origin that each axis' planes round
+    // to one value (then a real child's hit has tn == tf and must stay a hit,
+    // so the test cannot reject it either; ADVICE r2,
+    // test_bvh4_tiny_far_nodes).  Their ref is a one-primitive leaf of the
+    // scene's first primitive: a spurious visit re-tests a real primitive,
+    // which cannot change a closest hit (same t, same DFS rank) or an any-hit
+    // answer, and needs no per-child ref compare in the node loop (that
+    // compare cost 2 % on cornell_1m).
+    const uint32_t empty_ref = (uint32_t)~(F.tris.empty() ? FRT_PRIM_SPHERE : 0);
+    struct Item { int bin, parent, slot, lvl; };   // binary node, wide parent (-1 root), child slot, level
     std::vector<Item> st{{root_ref, -1, 0, 1}};
     while (!st.empty()) {
         const Item it = st.back();
         st.pop_back();
-        const int me = (int)(F.nodes4.size() / 4);
+        const int me = (int)(F.nodes4.size() / NU);
         if (it.parent >= 0) {
-            uint4 &r = F.nodes4[4 * it.parent + 1];
-            (it.slot == 0 ? r.x : it.slot == 1 ? r.y : it.slot == 2 ? r.z : r.w) = (uint32_t)me;
+            uint4 &r = F.nodes4[NU * it.parent + 1 + it.slot / 4];
+            const int q = it.slot & 3;
+            (q == 0 ? r.x : q == 1 ? r.y : q == 2 ? r.z : r.w) = (uint32_t)me;
         }
         F.depth4 = std::max(F.depth4, it.lvl);
-        Child ch[4];
+        Child ch[W];
         int n = 2;
         kids(it.bin, ch);
-        while (n < 4) {
+        while (n < W) {                                // open the largest interior child
             int best = -1;
             double best_a = -1.0;
             for (int k = 0; k < n; ++k)
@@ -1272,10 +1307,37 @@ static bool build_bvh4(FlatScene &F, int root_ref)
             ch[best + 1] = two[1];
             ++n;
         }
+        // slot k of the node: child ch[kid[k]], or empty (-1)
+        int kid[W];
+        for (int k = 0; k < W; ++k) kid[k] = k < n ? k : -1;
+        if constexpr (W == 8) {
+            // octant slots (bvh8_step): child k goes to the slot whose octant of the
+            // node's centre best matches its box centre; greedy over (cost, k, s)
+            double cc[W][3];
+            for (int a = 0; a < 3; ++a) {
+                float lo = ch[0].lo[a], hi = ch[0].hi[a];
+                for (int k = 1; k < n; ++k) { lo = std::min(lo, ch[k].lo[a]); hi = std::max(hi, ch[k].hi[a]); }
+                const double cen = 0.5 * ((double)lo + (double)hi);
+                for (int k = 0; k < n; ++k) cc[k][a] = 0.5 * ((double)ch[k].lo[a] + (double)ch[k].hi[a]) - cen;
+            }
+            struct Cand { double cost; int k, s; };
+            std::vector<Cand> cand;
+            for (int k = 0; k < n; ++k)
+                for (int sl = 0; sl < W; ++sl) {
+                    double c = 0.0;
+                    for (int a = 0; a < 3; ++a) c -= ((sl >> a) & 1) ? cc[k][a] : -cc[k][a];
+                    cand.push_back({c, k, sl});
+                }
+            std::stable_sort(cand.begin(), cand.end(), [](const Cand &x, const Cand &y) { return x.cost < y.cost; });
+            bool placed[W];
+            for (int k = 0; k < W; ++k) { placed[k] = false; kid[k] = -1; }
+            for (const Cand &q : cand)
+                if (!placed[q.k] && kid[q.s] < 0) { placed[q.k] = true; kid[q.s] = q.k; }
+        }
         // per-axis grid: origin = min child lo, step 2^e with every plane within 255 steps
         float org[3];
         int ex[3];
-        uint32_t qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
+        uint64_t qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
         for (int a = 0; a < 3; ++a) {
             float lo = ch[0].lo[a], hi = ch[0].hi[a];
             for (int k = 1; k < n; ++k) { lo = std::min(lo, ch[k].lo[a]); hi = std::max(hi, ch[k].hi[a]); }
@@ -1291,42 +1353,43 @@ static bool build_bvh4(FlatScene &F, int root_ref)
             if (e < -100) return false;                // 2^e / |d| must stay a normal float for the empty-slot
                                                        // test (padded boxes are never this thin)
             ex[a] = e;
-            for (int k = 0; k < n; ++k) {
-                double ql = std::floor(((double)ch[k].lo[a] - lo) / std::ldexp(1.0, e));
-                double qh = std::ceil(((double)ch[k].hi[a] - lo) / std::ldexp(1.0, e));
-                ql = std::min(std::max(ql, 0.0), 255.0);
-                qh = std::min(std::max(qh, 0.0), 255.0);
-                // outward: the decoded plane must enclose the fp32 box (exact in double)
-                while (ql > 0.0 && (double)lo + ql * std::ldexp(1.0, e) > (double)ch[k].lo[a]) ql -= 1.0;
-                while (qh < 255.0 && (double)lo + qh * std::ldexp(1.0, e) < (double)ch[k].hi[a]) qh += 1.0;
-                qlo[a] |= (uint32_t)ql << (8 * k);
-                qhi[a] |= (uint32_t)qh << (8 * k);
+            for (int s = 0; s < W; ++s) {
+                double ql = 255.0, qh = 0.0;           // empty slot: the inverted box
+                if (kid[s] >= 0) {
+                    const Child &c = ch[kid[s]];
+                    ql = std::floor(((double)c.lo[a] - lo) / std::ldexp(1.0, e));
+                    qh = std::ceil(((double)c.hi[a] - lo) / std::ldexp(1.0, e));
+                    ql = std::min(std::max(ql, 0.0), 255.0);
+                    qh = std::min(std::max(qh, 0.0), 255.0);
+                    // outward: the decoded plane must enclose the fp32 box (exact in double)
+                    while (ql > 0.0 && (double)lo + ql * std::ldexp(1.0, e) > (double)c.lo[a]) ql -= 1.0;
+                    while (qh < 255.0 && (double)lo + qh * std::ldexp(1.0, e) < (double)c.hi[a]) qh += 1.0;
+                }
+                qlo[a] |= (uint64_t)ql << (8 * s);
+                qhi[a] |= (uint64_t)qh << (8 * s);
             }
         }
-        // empty slots: the inverted box q_lo = 255 > q_hi = 0 on every axis,
-        // which the near / far slab test of bvh4_step rejects -- except on a
-        // node so small against its distance from the ray origin that each
-        // axis' planes round to one value (then a real child's hit has tn ==
-        // tf and must stay a hit, so the test cannot reject it either; ADVICE
-        // r2, test_bvh4_tiny_far_nodes).  Their ref is a one-primitive leaf of
-        // the scene's first primitive: a spurious visit re-tests a real
-        // primitive, which cannot change a closest hit (same t, same DFS rank)
-        // or an any-hit answer, and needs no per-child ref compare in the node
-        // loop (that compare cost 2 % on cornell_1m).
-        for (int k = n; k < 4; ++k)
-            for (int a = 0; a < 3; ++a) qlo[a] |= 0xffu << (8 * k);
-        const uint32_t empty_ref = (uint32_t)~(F.tris.empty() ? FRT_PRIM_SPHERE : 0);
-        uint4 w0, w1, w2, w3;
+        uint32_t refs[W];
+        for (int s = 0; s < W; ++s) refs[s] = kid[s] >= 0 ? (uint32_t)ch[kid[s]].ref : empty_ref;
+        uint4 w0;
         w0.x = (uint32_t)f2i(org[0]); w0.y = (uint32_t)f2i(org[1]); w0.z = (uint32_t)f2i(org[2]);
         w0.w = (uint32_t)(ex[0] + 127) | ((uint32_t)(ex[1] + 127) << 8) | ((uint32_t)(ex[2] + 127) << 16);
-        uint32_t refs[4];
-        for (int k = 0; k < 4; ++k) refs[k] = k < n ? (uint32_t)ch[k].ref : empty_ref;
-        w1.x = refs[0]; w1.y = refs[1]; w1.z = refs[2]; w1.w = refs[3];
-        w2.x = qlo[0]; w2.y = qhi[0]; w2.z = qlo[1]; w2.w = qhi[1];
-        w3.x = qlo[2]; w3.y = qhi[2]; w3.z = 0; w3.w = 0;
-        F.nodes4.push_back(w0); F.nodes4.push_back(w1); F.nodes4.push_back(w2); F.nodes4.push_back(w3);
-        for (int k = n - 1; k >= 0; --k)                // interior children, pre-order (first child next)
-            if (ch[k].ref >= 0) st.push_back({ch[k].ref, me, k, it.lvl + 1});
+        F.nodes4.push_back(w0);
+        if constexpr (W == 4) {
+            F.nodes4.push_back(make_uint4(refs[0], refs[1], refs[2], refs[3]));
+            F.nodes4.push_back(make_uint4((uint32_t)qlo[0], (uint32_t)qhi[0], (uint32_t)qlo[1], (uint32_t)qhi[1]));
+            F.nodes4.push_back(make_uint4((uint32_t)qlo[2], (uint32_t)qhi[2], 0u, 0u));
+        } else {   // refs 0-3 | 4-7, then per axis (lo 0-3, lo 4-7, hi 0-3, hi 4-7), padding to 128 B
+            F.nodes4.push_back(make_uint4(refs[0], refs[1], refs[2], refs[3]));
+            F.nodes4.push_back(make_uint4(refs[4], refs[5], refs[6], refs[7]));
+            for (int a = 0; a < 3; ++a)
+                F.nodes4.push_back(make_uint4((uint32_t)qlo[a], (uint32_t)(qlo[a] >> 32), (uint32_t)qhi[a],
+                                              (uint32_t)(qhi[a] >> 32)));
+            F.nodes4.push_back(make_uint4(0u, 0u, 0u, 0u));
+            F.nodes4.push_back(make_uint4(0u, 0u, 0u, 0u));
+        }
+        for (int s = W - 1; s >= 0; --s)                // interior children, pre-order (first slot next)
+            if (kid[s] >= 0 && ch[kid[s]].ref >= 0) st.push_back({ch[kid[s]].ref, me, s, it.lvl + 1});
     }
     F.root4 = 0;
     return true;
@@ -1623,7 +1686,8 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
             d[3] = n[3];
         }
     S.root = (sv->world_kind == FRT_WORLD_BVH) ? ((sv->root >= 0) ? 0 : ~dev_ref(~sv->root)) : 0;
-    F.has4 = sv->world_kind == FRT_WORLD_BVH && build_bvh4(F, S.root);
+    F.has4 = sv->world_kind == FRT_WORLD_BVH &&
+             (wide_override() == 8 ? build_wide<8>(F, S.root) : build_wide<4>(F, S.root));
     if (!F.has4) F.nodes4.clear();
     S.root4 = F.has4 ? F.root4 : S.root;
     S.n_lights = sv->n_lights;
@@ -1631,7 +1695,7 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     S.n_nodes = (int)(F.nodes.size() / 4);
     S.n_tris = nt;
     S.n_mats = nm;
-    S.n_nodes4 = (int)(F.nodes4.size() / 4);
+    S.n_nodes4 = (int)(F.nodes4.size() / (F.width == 8 ? 8 : 4));
     S.node_es = 4; S.node_ps = 1;
     S.node4_es = 4; S.node4_ps = 1;
     S.tri_es = 3; S.tri_ps = 1;
@@ -1695,7 +1759,8 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
         return rc;
     c->world_kind = S.world_kind;
     c->stack_needed = F.depth;
-    c->has_bvh4 = F.has4;
+    c->has_bvh4 = F.has4 && F.width == 4;
+    c->has_bvh8 = F.has4 && F.width == 8;
     c->n_tris = S.n_tris;
     c->n_spheres = (int)F.spheres.size();
     c->has_spec_mats = false;
@@ -1759,8 +1824,9 @@ static void selftest_pixels(const DevScene &S, const FlatScene &F, const frt_ren
                 } else if (S.world_kind == FRT_WORLD_LIST) {
                     h = trace<FRT_WORLD_LIST, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data());
                 } else if constexpr (!kIsF64<R>) {
-                    h = wide ? trace<kWorldBvh4, 1, kSelftestStack>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data())
-                             : trace<FRT_WORLD_BVH, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data());
+                    h = wide && F.width == 8 ? trace<kWorldBvh8, 1, kSelftestStack>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data())
+                        : wide ? trace<kWorldBvh4, 1, kSelftestStack>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data())
+                               : trace<FRT_WORLD_BVH, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data());
                 } else {
                     h = trace<FRT_WORLD_BVH, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data());
                 }
@@ -1800,7 +1866,7 @@ extern "C" int frt_selftest_path_host(const frt_scene_view *sv, const frt_render
     std::vector<int> stack(std::max(F.depth + 1, kSelftestStack));
     const bool brute = !f64 && S.world_kind == FRT_WORLD_BVH && (p->flags & FRT_FLAG_BRUTE) && F.spheres.empty();
     const bool wide = !f64 && !brute && S.world_kind == FRT_WORLD_BVH && F.has4 && !(p->flags & FRT_FLAG_BVH2) &&
-                      bvh4_stack_fits(F.depth4, kSelftestStack);
+                      (F.width == 8 ? bvh8_stack_fits(F.depth4, kSelftestStack) : bvh4_stack_fits(F.depth4, kSelftestStack));
     uint64_t cnt[3] = {0, 0, 0};   // camera, extension, shadow
     if (f64) selftest_pixels<double>(S, F, p, pixels, npix, brute, wide, stack, out_rgb, cnt);
     else selftest_pixels<float>(S, F, p, pixels, npix, brute, wide, stack, out_rgb, cnt);

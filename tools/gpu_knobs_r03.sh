@@ -7,9 +7,9 @@ export TMPDIR=/tmp
 O=gpurun_out/${TAG:-knobs}
 mkdir -p $O
 timeout -k 10 400 python tools/perf_ab.py --scene cornell --spp 512 --rounds 3 --bvh gsah \
-    --variants default/trav=20,default/trav=24,default/trav=28,default/trav=32,default/trav=36 > $O/cornell.jsonl 2>> $O/log.txt \
+    --variants default/trav20,default/trav24,default/trav28,default/trav32,default/trav36 > $O/cornell.jsonl 2>> $O/log.txt \
  && timeout -k 10 500 python tools/perf_ab.py --scene cornell_1m --spp 256 --rounds 3 --bvh gsah \
-    --variants default/trav=32/desc=8,default/trav=40/desc=8,default/trav=48/desc=8,default/trav=40/desc=4,default/trav=40/desc=12,default/trav=48/desc=12 > $O/cornell_1m.jsonl 2>> $O/log.txt
+    --variants default/trav32/desc8,default/trav40/desc8,default/trav48/desc8,default/trav40/desc4,default/trav40/desc12,default/trav48/desc12 > $O/cornell_1m.jsonl 2>> $O/log.txt
 rc=$?
 echo "rc=$rc" > $O/rc.txt
 exit $rc

@@ -65,22 +65,24 @@ def main():
     else:
         hs = frt.HostScene(kind, obj, nx / ny)
     ctxs = {}
-    for v in chosen:
-        leaf = opt(v, "leaf")
+    for v in chosen:   # one context per upload-time option (leaf size, wide-tree width)
+        leaf = (opt(v, "leaf"), opt(v, "wide"))
         if leaf not in ctxs:
-            if leaf:
-                os.environ["FRT_LEAF_SIZE"] = leaf
-            else:
-                os.environ.pop("FRT_LEAF_SIZE", None)
+            for val, env in ((leaf[0], "FRT_LEAF_SIZE"), (leaf[1], "FRT_WIDE")):
+                if val:
+                    os.environ[env] = val
+                else:
+                    os.environ.pop(env, None)
             ctxs[leaf] = frt.Context(0)
             ctxs[leaf].upload(hs)
     os.environ.pop("FRT_LEAF_SIZE", None)
+    os.environ.pop("FRT_WIDE", None)
     res = {v: [] for v in chosen}
     rays = {}
     films = {}
     for r in range(args.rounds + 1):
         for v in chosen:
-            leaf = opt(v, "leaf")
+            leaf = (opt(v, "leaf"), opt(v, "wide"))
             for key, env in (("trav", "FRT_TRAV_MIN"), ("desc", "FRT_MIN_DESC")):
                 if opt(v, key):
                     os.environ[env] = opt(v, key)
