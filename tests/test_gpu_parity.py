@@ -158,6 +158,15 @@ def test_bvh4_matches_binary(ctx, cornell_obj, tmp_path):
     spec, sts = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21,
                                                  flags=frt.FRT_FLAG_NO_LDS_SCENE | frt.FRT_FLAG_SPEC))
     assert np.array_equal(spec, bin2) and sts.rays == st2.rays        # speculative traversal
+    # the 8-wide nodes with octant-ordered children (FRT_WIDE=8 at upload, an A/B plan)
+    import os
+    os.environ["FRT_WIDE"] = "8"
+    try:
+        ctx.upload(frt.HostScene("cornell_box_obj", dst, nx / ny))
+    finally:
+        del os.environ["FRT_WIDE"]
+    w8, st8 = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21, flags=frt.FRT_FLAG_NO_LDS_SCENE))
+    assert 0 < st8.bvh_depth < st4.bvh_depth and np.array_equal(w8, bin2) and st8.rays == st2.rays
     # small scene: 4-wide nodes from LDS (FRT_FLAG_BVH4) vs the default binary LDS plan
     ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, nx / ny))
     w_lds, stw = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21, flags=frt.FRT_FLAG_BVH4))
