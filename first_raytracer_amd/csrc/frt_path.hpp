@@ -273,10 +273,15 @@ template <typename R> FRT_HD bool trav_begin(Trav<R> &T, const DevScene &S, int 
 // box costs 6 FMAs and two 3-way max / min instead of also sorting each
 // slab's two distances (the same values: lo <= hi and 1/d has the octant's
 // sign, so the near plane's distance is the smaller one).
-template <int STRIDE, bool OCT = false, typename R>
+// SPEC (FRT_FLAG_SPEC on the LDS plans): a lane that reaches a leaf parks it
+// and keeps descending while other lanes of its wave have none yet; then every
+// lane tests its parked leaf (Aila & Laine 2009), as bvh4_step's SPEC.
+template <int STRIDE, bool OCT = false, bool SPEC = false, typename R>
 FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyhit, int *stk, int min_desc = 0)
 {
     int node = T.node, sp = T.sp;
+    int parked = 0;                                     // leaf refs are negative; 0 = none
+    if (SPEC && node < 0) { parked = node; node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel; }
     DevScene Sn = S;
     if constexpr (OCT) {
         const int oct = (T.sr.invd.x < R(0) ? 1 : 0) | (T.sr.invd.y < R(0) ? 2 : 0) | (T.sr.invd.z < R(0) ? 4 : 0);
@@ -310,7 +315,22 @@ FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyh
         } else {
             node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel;
         }
-        if (min_desc > 0 && wave_count((unsigned)node < (unsigned)kSentinel) < min_desc) break;
+        if constexpr (SPEC) {
+            if (parked == 0 && node < 0) { parked = node; node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel; }
+            // keep going while some lane of the wave still has no leaf to test
+            if (!wave_any(parked == 0 && (unsigned)node < (unsigned)kSentinel)) break;
+        } else {
+            if (min_desc > 0 && wave_count((unsigned)node < (unsigned)kSentinel) < min_desc) break;
+        }
+    }
+    if constexpr (SPEC) {
+        if (parked != 0 && leaf_hit(S, ~parked, o, d, T.tmin, anyhit, T.h)) {
+            T.node = node; T.sp = sp;
+            return true;
+        }
+        T.node = node;
+        T.sp = sp;
+        return node == kSentinel;
     }
     if ((unsigned)node < (unsigned)kSentinel) {          // postponed: still descending
         T.node = node;
@@ -659,7 +679,7 @@ FRT_HD bool trav_step_world(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, boo
     } else if constexpr (WORLD == kWorldBvh8) {
         return bvh8_step<STRIDE, STACK>(T, S, o, d, anyhit, stk, ovf, min_desc);
     } else {
-        return bvh2_step<STRIDE, WORLD == kWorldBvh2Oct>(T, S, o, d, anyhit, stk, min_desc);
+        return bvh2_step<STRIDE, WORLD == kWorldBvh2Oct, SPEC>(T, S, o, d, anyhit, stk, min_desc);
     }
 }
 

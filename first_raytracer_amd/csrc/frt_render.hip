@@ -866,6 +866,12 @@ static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
             L = bvh_launcher<kBvh4LdsStackSmall, true, kWorldBvh4>(waves, c->scene_lds_bytes4);
             return FRT_OK;
         }
+        // speculative binary traversal from LDS (FRT_FLAG_SPEC on an LDS-resident scene)
+        if (lds && (flags & FRT_FLAG_SPEC) && !(flags & FRT_FLAG_NO_OCT) && c->scene_lds_bytes_oct <= kLdsOctBytes) {
+            L = d < 8 ? bvh_launcher<8, true, kWorldBvh2Oct, true>(waves, c->scene_lds_bytes_oct)
+                      : bvh_launcher<16, true, kWorldBvh2Oct, true>(waves, c->scene_lds_bytes_oct);
+            return FRT_OK;
+        }
         // speculative 4-wide traversal (FRT_FLAG_SPEC)
         if (!lds && (flags & FRT_FLAG_SPEC) && c->has_bvh4 && !(flags & FRT_FLAG_BVH2) &&
             bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {

@@ -58,7 +58,7 @@ enum { FRT_FLAG_NO_LDS_SCENE = 1,      /* render_params.flags: keep small scenes
        FRT_FLAG_BVH2 = 16,             /* binary nodes for HBM-resident scenes (A/B timing, self-test)   */
        FRT_FLAG_BVH4 = 32,             /* 4-wide nodes for LDS-resident scenes too (A/B timing)          */
        FRT_FLAG_BRUTE = 64,            /* tiny LDS scenes: every triangle in lockstep (A/B timing)       */
-       FRT_FLAG_SPEC = 128,            /* 4-wide HBM plan: speculative traversal (A/B timing)            */
+       FRT_FLAG_SPEC = 128,            /* speculative traversal: 4-wide HBM plan, binary LDS plan (A/B)  */
        FRT_FLAG_NO_OCT = 256,          /* LDS binary plan without the per-octant node copies (A/B timing) */
        FRT_FLAG_FP64 = 512,            /* path: the fp64 kernel for this call (self-test: fp64 host replay) */
        FRT_FLAG_FP32 = 1024 };         /* path: the fp32 kernels even where the precision picks fp64      */

@@ -176,6 +176,9 @@ def test_bvh4_matches_binary(ctx, cornell_obj, tmp_path):
     # LDS binary plan: the per-octant node copies (default) vs the (lo, hi) boxes
     noct, stn = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21, flags=frt.FRT_FLAG_NO_OCT))
     assert stn.scene_in_lds == 1 and np.array_equal(noct, b_lds) and stn.rays == stb.rays
+    # LDS binary plan with speculative (parked-leaf) traversal (FRT_FLAG_SPEC)
+    sp_lds, sts2 = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21, flags=frt.FRT_FLAG_SPEC))
+    assert sts2.scene_in_lds == 1 and np.array_equal(sp_lds, b_lds) and sts2.rays == stb.rays
     # tiny scene: every triangle in lockstep (FRT_FLAG_BRUTE)
     br, stbr = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21, flags=frt.FRT_FLAG_BRUTE))
     assert stbr.scene_in_lds == 1 and np.array_equal(br, b_lds) and stbr.rays == stb.rays
