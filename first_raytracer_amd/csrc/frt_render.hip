@@ -168,6 +168,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     int ovf[kOverflow<WORLD>];
     // ray counters are wave-uniform (SGPRs): popcounts of per-iteration ballots
     unsigned long long n_cam = 0, n_ext = 0, n_sh = 0, n_smp = 0;
+    // HBM plans of the lambertian path kernels keep less per-lane state across
+    // the traversal steps: the sample's radiance goes into the item's LDS sum
+    // as it is found (NEE after a shadow ray, emission, environment), the RNG
+    // key is re-derived from the item at shading, t_max from the ray kind.
+    // cornell_1m +1.2 % (spilled VGPRs 26 -> 14); on the LDS plan it costs
+    // 0.3 % (same-call A/B, profiles/r03/samecall/lean_*.jsonl).  The material
+    // kernels keep the full state (DESIGN.md "Register-cap hazard").
+    constexpr bool kLean = !LDS_SCENE && MATS == kMatsNone && KIND == FRT_INTEGRATOR_PATH;
+    auto flush_L = [&]() {
+        I.set(kIsAcc + 0, f2i(i2f(I.get(kIsAcc + 0)) + (float)P.L.x));
+        I.set(kIsAcc + 1, f2i(i2f(I.get(kIsAcc + 1)) + (float)P.L.y));
+        I.set(kIsAcc + 2, f2i(i2f(I.get(kIsAcc + 2)) + (float)P.L.z));
+        P.L = zero3<R>();
+    };
+    auto ray_tmax = [&]() -> R {
+        if constexpr (kLean) return P.shadow ? R(1) - Cst<R>::shadow_eps : Cst<R>::tmax;
+        else return P.rtmax;
+    };
 
     unsigned long long diag_t0 = FRT_DIAG_CLOCK();
     for (;;) {
@@ -185,8 +203,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
                                                                            ? 0 : W.min_desc)) {
                 if (KIND == FRT_INTEGRATOR_PATH && P.shadow) {   // finish the shadow ray here, keep traversing
                     if (path_after_shadow<MATS>(P, T.h.prim < 0)) {
+                        if constexpr (kLean) flush_L();
                         shadow_done = true;
-                        tracing = trav_begin_world<WORLD>(T, S, P.ro, P.rd, P.rtmax);
+                        tracing = trav_begin_world<WORLD>(T, S, P.ro, P.rd, ray_tmax());
                         pending = !tracing;
                     } else {                                      // path ended (P.term): shade finishes it
                         tracing = false;
@@ -208,14 +227,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         if (pending) {
             FRT_DIAG_TICK(4);
             pending = false;
-            if (shade_kind<KIND, MATS>(P, S, T.h, W.max_depth, ne, ns)) {
-                I.set(kIsAcc + 0, f2i(i2f(I.get(kIsAcc + 0)) + (float)P.L.x));   // fp32 chunk sums in
-                I.set(kIsAcc + 1, f2i(i2f(I.get(kIsAcc + 1)) + (float)P.L.y));   // either precision
-                I.set(kIsAcc + 2, f2i(i2f(I.get(kIsAcc + 2)) + (float)P.L.z));
-                active = false;
-            } else {
-                next_ray = true;
-            }
+            if constexpr (kLean)
+                P.key = rng_key(W.seed, (uint32_t)I.get(kIsPix), (uint32_t)(I.get(kIsCur) - 1) + W.s_off);
+            const bool done = shade_kind<KIND, MATS>(P, S, T.h, W.max_depth, ne, ns);
+            if (done || kLean) flush_L();   // fp32 chunk sums in either precision
+            active = !done;
+            next_ray = !done;
         }
         n_ext += __popcll(__ballot(ne != 0));
         n_sh += __popcll(__ballot(ns != 0));
@@ -279,7 +296,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         n_smp += started;
         // ---- set up the next ray's traversal (a scene miss is finished at once) ----
         if (next_ray) {
-            tracing = trav_begin_world<WORLD>(T, S, P.ro, P.rd, P.rtmax);
+            tracing = trav_begin_world<WORLD>(T, S, P.ro, P.rd, ray_tmax());
             pending = !tracing;
         }
         diag_t0 = FRT_DIAG_CLOCK();

@@ -203,6 +203,30 @@ def test_trav_min_invariance(ctx, cornell_obj, tmp_path, monkeypatch, flags):
         assert np.array_equal(f, res[0][0]) and r == res[0][1]
 
 
+def test_lambertian_caps_agree(ctx, cornell_obj, tmp_path):
+    """The lambertian kernels of the HBM plans (4-wide and binary; the lean
+    per-lane state) under every register cap they are built for -- the
+    compiler's own, 5 and 6 waves/SIMD -- render the same film bit for bit,
+    within the parity tolerance of the oracle (DESIGN.md "Register-cap
+    hazard": the material kernels' fault never showed here; this pins it)."""
+    dst = str(tmp_path / "tess.obj")
+    frt.write_tessellated_obj(cornell_obj, 16, dst)
+    nx, ny, spp = 64, 48, 16
+    ctx.upload(frt.HostScene("cornell_box_obj", dst, nx / ny))
+    ref, cnt = oracle.OracleScene("cornell_box_obj", dst, nx / ny).render(nx, ny, spp, seed=12)
+    ref = np.asarray(ref, np.float64).reshape(-1, 3)
+    films = []
+    for plan in (frt.FRT_FLAG_NO_LDS_SCENE, frt.FRT_FLAG_NO_LDS_SCENE | frt.FRT_FLAG_BVH2):
+        for cap, w in ((frt.FRT_FLAG_WAVES4, 0), (frt.FRT_FLAG_WAVES5, 5), (frt.FRT_FLAG_WAVES6, 6)):
+            film, st = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=12, flags=plan | cap))
+            assert st.scene_in_lds == 0 and st.waves_cap == w
+            e = float(np.sqrt(np.mean((np.asarray(film, np.float64).reshape(-1, 3) - ref) ** 2)))
+            assert e <= 1e-3, (plan, w, e)
+            films.append(film)
+    for f in films[1:]:
+        assert np.array_equal(f, films[0])
+
+
 def test_launch_plan(ctx, cornell_obj, mirror_obj, sphere_obj, tmp_path):
     """The launcher picks the planned kernel: small scenes from LDS with the
     binary BVH at 5 waves/SIMD, HBM-resident scenes on the 4-wide BVH at 6;

@@ -29,22 +29,33 @@ def main():
     ap.add_argument("--res", default="64x48")
     ap.add_argument("--spp", type=int, default=16)
     ap.add_argument("--seed", type=int, default=12)
+    ap.add_argument("--scene", default="conductors", choices=["conductors", "lambert"],
+                    help="lambert: tessellated Cornell (lambertian kernels; caps by FRT_FLAG_WAVES*)")
     a = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime: torch's)
     import first_raytracer_amd as frt
     import oracle
     import scene_specs as SS
     nx, ny = (int(v) for v in a.res.split("x"))
-    spec = SS.cornell_conductors("beckmann", "ggx", "bvh")
-    ref, cnt = oracle.OracleScene.from_spec(spec, nx / ny).render(nx, ny, a.spp, seed=a.seed)
-    ref = np.asarray(ref, np.float64).reshape(-1, 3)
     ctx = frt.Context(0)
-    ctx.upload(frt.HostScene.from_spec(spec, nx / ny))
+    if a.scene == "conductors":
+        spec = SS.cornell_conductors("beckmann", "ggx", "bvh")
+        ref, cnt = oracle.OracleScene.from_spec(spec, nx / ny).render(nx, ny, a.spp, seed=a.seed)
+        ctx.upload(frt.HostScene.from_spec(spec, nx / ny))
+        cap_flags = {w: 0 for w in a.caps.split(",")}
+    else:                       # the lambertian kernels' caps come from flags: compiler's own, 5, 6
+        obj = os.path.join(ROOT, "tests", "golden", "scenes", "CornellBox-Original.obj")
+        tess = os.path.join("/tmp", "caps_tess.obj")
+        frt.write_tessellated_obj(obj, 16, tess)
+        ref, cnt = oracle.OracleScene("cornell_box_obj", tess, nx / ny).render(nx, ny, a.spp, seed=a.seed)
+        ctx.upload(frt.HostScene("cornell_box_obj", tess, nx / ny))
+        cap_flags = {"4": frt.FRT_FLAG_WAVES4, "5": frt.FRT_FLAG_WAVES5, "6": frt.FRT_FLAG_WAVES6}
+    ref = np.asarray(ref, np.float64).reshape(-1, 3)
     for flags in (int(f) for f in a.flags.split(",")):
         base = None
-        for w in a.caps.split(","):
+        for w, cf in cap_flags.items():
             os.environ["FRT_MATS_WAVES"] = w
-            film, st = ctx.render(frt.RenderParams.make(nx, ny, a.spp, seed=a.seed, flags=flags))
+            film, st = ctx.render(frt.RenderParams.make(nx, ny, a.spp, seed=a.seed, flags=flags | cf))
             f = np.asarray(film, np.float64).reshape(-1, 3)
             if base is None:
                 base = f
