@@ -2265,11 +2265,15 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, L.fn, kBlock, L.lds) != hipSuccess || bpc <= 0) bpc = 1;
     const int grid = c->n_cu * bpc;
     const long long lanes = (long long)grid * kBlock;
-    // work granule: aim for >= 16 items per resident lane
+    // work granule: the frame's samples cut into k chunks of equal length, k
+    // chosen for about 40 items per resident lane.  Same-call A/B at the bench
+    // configs (profiles/r03/samecall/spi_*.jsonl): Cornell 512 spp is best at
+    // 5-6 chunks (294 ms against 303 with the round-2 rule's 206 / 206 / 100),
+    // cornell_1m 512 spp at 8-12 (837-839 ms against 868 with 170 x 3 + 2).
     int spi = p->samples_per_item;
     if (spi <= 0) {
-        const double want_items = 16.0 * (double)lanes;
-        spi = (int)std::floor((double)p->spp * (double)n_slots / std::max(want_items, 1.0));
+        const double k = std::max(1.0, std::round(40.0 * (double)lanes / std::max((double)n_slots, 1.0)));
+        spi = (int)std::ceil((double)p->spp / k);
         spi = std::max(1, std::min(spi, p->spp));
     }
     spi = std::min(spi, p->spp);

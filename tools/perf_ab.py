@@ -88,7 +88,8 @@ def main():
                     os.environ[env] = opt(v, key)
                 else:
                     os.environ.pop(env, None)
-            p = frt.RenderParams.make(nx, ny, args.spp, seed=0, flags=flags[v.split("/")[0]])
+            spi = int(opt(v, "spi") or 0)       # samples per work item (0: automatic)
+            p = frt.RenderParams.make(nx, ny, args.spp, seed=0, flags=flags[v.split("/")[0]], samples_per_item=spi)
             films[leaf], st = ctxs[leaf].render(p, films.get(leaf))
             if r > 0:
                 res[v].append(st.kernel_ms)
