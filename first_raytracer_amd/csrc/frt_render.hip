@@ -54,7 +54,14 @@ struct DevWork {
     float *partial;                      // [n_chunks][n_slots][3]
     unsigned *counter;                   // work-queue head
     unsigned long long *wave_rays;       // [n_waves][4]: camera, extension, shadow, samples
+    int guided, n_tiles;                 // guided: chunk-major items, chunk i of weight n_chunks - i
 };
+// guided granule: chunk i of n starts at spp * (i n - i (i - 1) / 2) / (n (n + 1) / 2)
+__host__ __device__ __forceinline__ int guided_start(int i, int n, int spp)
+{
+    const unsigned long long num = (unsigned long long)i * n - (unsigned long long)i * (i - 1) / 2;
+    return (int)((unsigned long long)spp * num / ((unsigned long long)n * (n + 1) / 2));
+}
 
 // slot -> pixel inside a tile: 8x8 blocks, row-major inside a block
 __device__ __host__ __forceinline__ void slot_to_local(int s, int tile, int &lx, int &ly)
@@ -259,8 +266,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
                 } else {
                     const uint32_t s = w % (uint32_t)T2;
                     const uint32_t q = w / (uint32_t)T2;
-                    const uint32_t chunk = q % (uint32_t)W.n_chunks;
-                    const uint32_t t_ord = q / (uint32_t)W.n_chunks;
+                    const uint32_t chunk = W.guided ? q / (uint32_t)W.n_tiles : q % (uint32_t)W.n_chunks;
+                    const uint32_t t_ord = W.guided ? q % (uint32_t)W.n_tiles : q / (uint32_t)W.n_chunks;
                     const int tile_id = W.shard_index + (int)t_ord * W.shard_count;
                     int lx, ly;
                     slot_to_local((int)s, W.tile, lx, ly);
@@ -268,9 +275,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
                     const int py = (tile_id / W.ntx) * W.tile + ly;
                     if (px < W.nx && py < W.ny) {   // padding slots of edge tiles carry no work
                         have_item = true;
-                        const int s_cur = (int)chunk * W.spi;
+                        const int s_cur = W.guided ? guided_start((int)chunk, W.n_chunks, W.spp) : (int)chunk * W.spi;
                         I.set(kIsCur, s_cur);
-                        I.set(kIsEnd, min(W.spp, s_cur + W.spi));
+                        I.set(kIsEnd, W.guided ? guided_start((int)chunk + 1, W.n_chunks, W.spp) : min(W.spp, s_cur + W.spi));
                         I.set(kIsSlot, (int)(t_ord * (uint32_t)T2 + s));
                         I.set(kIsChunk, (int)chunk);
                         I.set(kIsPix, py * W.nx + px);
@@ -2277,7 +2284,13 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
         spi = std::max(1, std::min(spi, p->spp));
     }
     spi = std::min(spi, p->spp);
-    const int n_chunks = (p->spp + spi - 1) / spi;
+    // FRT_GRANULE=guided (A/B knob): chunk-major items whose lengths fall
+    // linearly, so the last items handed out are the shortest
+    const char *ge = std::getenv("FRT_GRANULE");
+    const bool guided = ge && std::strcmp(ge, "guided") == 0 && p->samples_per_item <= 0;
+    const char *gk = guided ? std::getenv("FRT_GUIDED_CHUNKS") : nullptr;
+    const int n_chunks = guided ? std::min(p->spp, std::max(1, gk ? std::atoi(gk) : (p->spp + spi - 1) / spi))
+                                : (p->spp + spi - 1) / spi;
     const unsigned long long n_items = (unsigned long long)n_slots * n_chunks;
     if (n_items >= 0xffffffffULL) return set_err(c, FRT_E_UNSUPPORTED, "frame too large for one call: shard it");
     // workspace
@@ -2300,6 +2313,7 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     W.s_off = (uint32_t)p->sample_offset;
     W.tile = T; W.ntx = (p->nx + T - 1) / T; W.shard_index = p->shard_index; W.shard_count = p->shard_count;
     W.spi = spi; W.n_chunks = n_chunks; W.n_items = (uint32_t)n_items; W.n_slots = n_slots;
+    W.guided = guided ? 1 : 0; W.n_tiles = nmt;
     W.partial = c->partial; W.counter = c->counter; W.wave_rays = c->wave_rays;
     W.trav_min = trav_min(L.lds_scene, p->integrator == FRT_INTEGRATOR_PATH);
     W.min_desc = min_desc(L.lds_scene);

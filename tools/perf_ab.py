@@ -6,7 +6,7 @@ kernel ms and Grays/s as JSON lines.
   python tools/perf_ab.py [--scene cornell|cornell_1m|veach] [--spp 64] [--rounds 5]
                           [--variants default,waves5,default/leaf1]
 
-A variant is FLAG[+FLAG...][/leafN][/travN][/descN]: render flags (travN sets
+A variant is FLAG[+FLAG...][/leafN][/travN][/descN][/granguided][/gkN]: render flags (travN sets
 FRT_TRAV_MIN=N, descN FRT_MIN_DESC=N for its renders), on a scene uploaded with
 FRT_LEAF_SIZE=N (one context per leaf size; default = the library default).
 """
@@ -83,7 +83,8 @@ def main():
     for r in range(args.rounds + 1):
         for v in chosen:
             leaf = (opt(v, "leaf"), opt(v, "wide"))
-            for key, env in (("trav", "FRT_TRAV_MIN"), ("desc", "FRT_MIN_DESC")):
+            for key, env in (("trav", "FRT_TRAV_MIN"), ("desc", "FRT_MIN_DESC"), ("gran", "FRT_GRANULE"),
+                             ("gk", "FRT_GUIDED_CHUNKS")):
                 if opt(v, key):
                     os.environ[env] = opt(v, key)
                 else:
