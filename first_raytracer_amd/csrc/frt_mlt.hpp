@@ -48,7 +48,7 @@ FRT_HD float mlt_mutate(float cur, float r, int d, float s2p, float logp)
 
 // Source of primary samples for one eye path.
 struct PrndSource {
-    const float *U;        // chain states [dim][n_chains] (null: bootstrap / fresh)
+    const float *U;        // chain states [n_chains][dim] (null: bootstrap / fresh)
     uint32_t n_chains, chain;
     RngKey key;            // step key (chain, step) or bootstrap key
     uint32_t dim0;         // first RNG dimension holding prnd 0

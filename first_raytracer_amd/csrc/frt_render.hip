@@ -479,7 +479,7 @@ struct MltWork {
     float b, scale, s2p, logp;           // normaliser, nx*ny/ns, pixel-dim perturb constants
     int trav_min;                        // see path_megakernel / trav_min()
     int min_desc;                        // leaf postponing: see bvh2_step
-    float *U;                            // [kMltDims][n_local] current primary samples
+    float *U;                            // [n_local][kMltDims] current primary samples (one row per chain)
     unsigned long long *film;            // [nx*ny*3] splat accumulation, fixed point (kSplatFix)
     unsigned *counter;
     unsigned long long *wave_rays;
