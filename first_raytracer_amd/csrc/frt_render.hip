@@ -1206,6 +1206,16 @@ static int wide_override()
     const char *e = std::getenv("FRT_WIDE");
     return e && std::atoi(e) == 8 ? 8 : 4;
 }
+// Order of the wide nodes in memory (FRT_NODE_ORDER, read at upload; an A/B
+// knob, not part of the C-ABI): 0 = depth-first pre-order (a node's first
+// interior child follows it), 1 = sibling blocks (a node's interior children
+// take consecutive indices, the blocks laid out depth-first), 2 = breadth-first.
+// Only addresses change: hits are the same (t, DFS rank) minimum in every order.
+static int node_order_override()
+{
+    const char *e = std::getenv("FRT_NODE_ORDER");
+    return e ? std::min(std::max(std::atoi(e), 0), 2) : 0;
+}
 static int leaf_size_override()
 {
     const char *e = std::getenv("FRT_LEAF_SIZE");
@@ -1309,13 +1319,17 @@ static bool build_wide(FlatScene &F, int root_ref)
     // answer, and needs no per-child ref compare in the node loop (that
     // compare cost 2 % on cornell_1m).
     const uint32_t empty_ref = (uint32_t)~(F.tris.empty() ? FRT_PRIM_SPHERE : 0);
-    struct Item { int bin, parent, slot, lvl; };   // binary node, wide parent (-1 root), child slot, level
-    std::vector<Item> st{{root_ref, -1, 0, 1}};
-    while (!st.empty()) {
-        const Item it = st.back();
-        st.pop_back();
-        const int me = (int)(F.nodes4.size() / NU);
-        if (it.parent >= 0) {
+    // binary node, wide parent (-1 root), child slot, level, own index (orders 1 and 2)
+    struct Item { int bin, parent, slot, lvl, me; };
+    const int order = node_order_override();
+    std::vector<Item> st{{root_ref, -1, 0, 1, 0}};
+    size_t head = 0;                                   // breadth-first: st is the queue
+    int next_free = 1;
+    while (order == 2 ? head < st.size() : !st.empty()) {
+        const Item it = order == 2 ? st[head++] : st.back();
+        if (order != 2) st.pop_back();
+        const int me = order == 0 ? (int)(F.nodes4.size() / NU) : it.me;
+        if (order == 0 && it.parent >= 0) {
             uint4 &r = F.nodes4[NU * it.parent + 1 + it.slot / 4];
             const int q = it.slot & 3;
             (q == 0 ? r.x : q == 1 ? r.y : q == 2 ? r.z : r.w) = (uint32_t)me;
@@ -1400,26 +1414,38 @@ static bool build_wide(FlatScene &F, int root_ref)
             }
         }
         uint32_t refs[W];
-        for (int s = 0; s < W; ++s) refs[s] = kid[s] >= 0 ? (uint32_t)ch[kid[s]].ref : empty_ref;
+        int own[W];                                    // orders 1 and 2: the interior children's indices
+        for (int s = 0; s < W; ++s) {
+            refs[s] = kid[s] >= 0 ? (uint32_t)ch[kid[s]].ref : empty_ref;
+            own[s] = -1;
+            if (order != 0 && kid[s] >= 0 && ch[kid[s]].ref >= 0) { own[s] = next_free++; refs[s] = (uint32_t)own[s]; }
+        }
+        if (F.nodes4.size() < (size_t)(me + 1) * NU) F.nodes4.resize((size_t)(me + 1) * NU);
+        uint4 *out = F.nodes4.data() + (size_t)me * NU;
         uint4 w0;
         w0.x = (uint32_t)f2i(org[0]); w0.y = (uint32_t)f2i(org[1]); w0.z = (uint32_t)f2i(org[2]);
         w0.w = (uint32_t)(ex[0] + 127) | ((uint32_t)(ex[1] + 127) << 8) | ((uint32_t)(ex[2] + 127) << 16);
-        F.nodes4.push_back(w0);
+        out[0] = w0;
         if constexpr (W == 4) {
-            F.nodes4.push_back(make_uint4(refs[0], refs[1], refs[2], refs[3]));
-            F.nodes4.push_back(make_uint4((uint32_t)qlo[0], (uint32_t)qhi[0], (uint32_t)qlo[1], (uint32_t)qhi[1]));
-            F.nodes4.push_back(make_uint4((uint32_t)qlo[2], (uint32_t)qhi[2], 0u, 0u));
+            out[1] = make_uint4(refs[0], refs[1], refs[2], refs[3]);
+            out[2] = make_uint4((uint32_t)qlo[0], (uint32_t)qhi[0], (uint32_t)qlo[1], (uint32_t)qhi[1]);
+            out[3] = make_uint4((uint32_t)qlo[2], (uint32_t)qhi[2], 0u, 0u);
         } else {   // refs 0-3 | 4-7, then per axis (lo 0-3, lo 4-7, hi 0-3, hi 4-7), padding to 128 B
-            F.nodes4.push_back(make_uint4(refs[0], refs[1], refs[2], refs[3]));
-            F.nodes4.push_back(make_uint4(refs[4], refs[5], refs[6], refs[7]));
+            out[1] = make_uint4(refs[0], refs[1], refs[2], refs[3]);
+            out[2] = make_uint4(refs[4], refs[5], refs[6], refs[7]);
             for (int a = 0; a < 3; ++a)
-                F.nodes4.push_back(make_uint4((uint32_t)qlo[a], (uint32_t)(qlo[a] >> 32), (uint32_t)qhi[a],
-                                              (uint32_t)(qhi[a] >> 32)));
-            F.nodes4.push_back(make_uint4(0u, 0u, 0u, 0u));
-            F.nodes4.push_back(make_uint4(0u, 0u, 0u, 0u));
+                out[3 + a] = make_uint4((uint32_t)qlo[a], (uint32_t)(qlo[a] >> 32), (uint32_t)qhi[a],
+                                        (uint32_t)(qhi[a] >> 32));
+            out[6] = make_uint4(0u, 0u, 0u, 0u);
+            out[7] = make_uint4(0u, 0u, 0u, 0u);
         }
-        for (int s = W - 1; s >= 0; --s)                // interior children, pre-order (first slot next)
-            if (kid[s] >= 0 && ch[kid[s]].ref >= 0) st.push_back({ch[kid[s]].ref, me, s, it.lvl + 1});
+        if (order == 2) {                               // interior children, slot order (queue)
+            for (int s = 0; s < W; ++s)
+                if (own[s] >= 0) st.push_back({ch[kid[s]].ref, me, s, it.lvl + 1, own[s]});
+        } else {                                        // pre-order (first slot next)
+            for (int s = W - 1; s >= 0; --s)
+                if (kid[s] >= 0 && ch[kid[s]].ref >= 0) st.push_back({ch[kid[s]].ref, me, s, it.lvl + 1, own[s]});
+        }
     }
     F.root4 = 0;
     return true;

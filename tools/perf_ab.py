@@ -6,7 +6,7 @@ kernel ms and Grays/s as JSON lines.
   python tools/perf_ab.py [--scene cornell|cornell_1m|veach] [--spp 64] [--rounds 5]
                           [--variants default,waves5,default/leaf1]
 
-A variant is FLAG[+FLAG...][/leafN][/travN][/descN][/granguided][/gkN]: render flags (travN sets
+A variant is FLAG[+FLAG...][/leafN][/wideN][/orderN][/travN][/descN][/granguided][/gkN]: render flags (travN sets
 FRT_TRAV_MIN=N, descN FRT_MIN_DESC=N for its renders), on a scene uploaded with
 FRT_LEAF_SIZE=N (one context per leaf size; default = the library default).
 """
@@ -66,9 +66,9 @@ def main():
         hs = frt.HostScene(kind, obj, nx / ny)
     ctxs = {}
     for v in chosen:   # one context per upload-time option (leaf size, wide-tree width)
-        leaf = (opt(v, "leaf"), opt(v, "wide"))
+        leaf = (opt(v, "leaf"), opt(v, "wide"), opt(v, "order"))
         if leaf not in ctxs:
-            for val, env in ((leaf[0], "FRT_LEAF_SIZE"), (leaf[1], "FRT_WIDE")):
+            for val, env in ((leaf[0], "FRT_LEAF_SIZE"), (leaf[1], "FRT_WIDE"), (leaf[2], "FRT_NODE_ORDER")):
                 if val:
                     os.environ[env] = val
                 else:
@@ -77,12 +77,13 @@ def main():
             ctxs[leaf].upload(hs)
     os.environ.pop("FRT_LEAF_SIZE", None)
     os.environ.pop("FRT_WIDE", None)
+    os.environ.pop("FRT_NODE_ORDER", None)
     res = {v: [] for v in chosen}
     rays = {}
     films = {}
     for r in range(args.rounds + 1):
         for v in chosen:
-            leaf = (opt(v, "leaf"), opt(v, "wide"))
+            leaf = (opt(v, "leaf"), opt(v, "wide"), opt(v, "order"))
             for key, env in (("trav", "FRT_TRAV_MIN"), ("desc", "FRT_MIN_DESC"), ("gran", "FRT_GRANULE"),
                              ("gk", "FRT_GUIDED_CHUNKS")):
                 if opt(v, key):
@@ -100,6 +101,12 @@ def main():
         print(json.dumps({"scene": args.scene, "variant": v, "spp": args.spp, "median_ms": statistics.median(ms),
                           "min_ms": min(ms), "grays_per_s": rays[v] / (statistics.median(ms) * 1e-3) / 1e9,
                           "rays": rays[v]}), flush=True)
+    if len(films) > 1:   # upload-time options change addresses only: the films must be identical
+        import numpy as np
+        keys = list(films)
+        print(json.dumps({"films_identical": {"/".join(k): bool(np.array_equal(np.asarray(films[k]),
+                                                                               np.asarray(films[keys[0]])))
+                                              for k in keys[1:]}}), flush=True)
     for c in ctxs.values():
         c.close()
 
