@@ -665,17 +665,31 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
                 }
             }
         }
-        // ---- materialise accepted proposals: the whole wave writes one chain's
-        // 92-dimension row at a time (lane = dimension; coalesced, no idle lanes) ----
-        for (uint64_t mm = __ballot(mat); mm; mm &= mm - 1) {
-            const int l = __ffsll((unsigned long long)mm) - 1;
-            const uint32_t jl = __shfl(j, l);
-            const RngKey kl{(uint32_t)__shfl((int)mat_key.k0, l), (uint32_t)__shfl((int)mat_key.k1, l)};
-            const bool fresh_l = __shfl((int)mat_fresh, l) != 0;
-            float *row = W.U + (size_t)jl * kMltDims;
-            for (int d = lane; d < kMltDims; d += 64) {
-                const float r = rng_u(kl, 2u + (uint32_t)d);
-                row[d] = fresh_l ? r : mlt_mutate(row[d], r, d, W.s2p, W.logp);
+        // ---- materialise accepted proposals: the rows of the wave's n accepted
+        // chains as one flat range of n * 92 elements over the 64 lanes
+        // (element e: chain rank e / 92, dimension e % 92).  A ds_permute first
+        // moves the r-th accepted chain's (row, key, fresh) to lane r (the other
+        // lanes fill lanes n..63, so it is a permutation).  Coalesced along each
+        // row; only the last trip has idle lanes (one chain at a time left 28 of
+        // 64 lanes idle on every second trip).  The whole wave is active here. ----
+        if (const uint64_t mm = __ballot(mat)) {
+            const uint32_t n = (uint32_t)__popcll(mm);
+            const int dst = 4 * (int)(mat ? lane_rank(mm) : n + lane_rank(~mm));   // byte address of the target lane
+            const uint32_t rj = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(j | (mat_fresh ? 0x80000000u : 0u)));
+            const uint32_t rk0 = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)mat_key.k0);
+            const uint32_t rk1 = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)mat_key.k1);
+            const uint32_t total = n * (uint32_t)kMltDims;
+            for (uint32_t e0 = 0; e0 < total; e0 += 64) {
+                const uint32_t e = e0 + (uint32_t)lane;
+                const uint32_t r = min(e / (uint32_t)kMltDims, n - 1u);
+                const uint32_t jl = (uint32_t)__shfl((int)rj, (int)r);   // every lane active: sources are lanes < n
+                const RngKey kl{(uint32_t)__shfl((int)rk0, (int)r), (uint32_t)__shfl((int)rk1, (int)r)};
+                if (e < total) {
+                    const int d = (int)(e - r * (uint32_t)kMltDims);
+                    float *row = W.U + (size_t)(jl & 0x7fffffffu) * kMltDims;   // j < 2^31: bit 31 = fresh
+                    const float u = rng_u(kl, 2u + (uint32_t)d);
+                    row[d] = (jl >> 31) ? u : mlt_mutate(row[d], u, d, W.s2p, W.logp);
+                }
             }
         }
         if (setup_next) {                               // next proposal reads the new state
