@@ -6,7 +6,7 @@ kernel ms and Grays/s as JSON lines.
   python tools/perf_ab.py [--scene cornell|cornell_1m|veach] [--spp 64] [--rounds 5]
                           [--variants default,waves5,default/leaf1]
 
-A variant is FLAG[+FLAG...][/leafN][/wideN][/orderN][/travN][/descN][/granguided][/gkN]: render flags (travN sets
+A variant is FLAG[+FLAG...][/leafN][/wideN][/orderN][/travN][/descN][/granguided][/gkN][/grabN]: render flags (travN sets
 FRT_TRAV_MIN=N, descN FRT_MIN_DESC=N for its renders), on a scene uploaded with
 FRT_LEAF_SIZE=N (one context per leaf size; default = the library default).
 """
@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--bvh", default="sah", choices=["host", "sah", "ploc", "lbvh", "gsah"],
                     help="sah: binned SAH tree (bench default); host: the reference topology; "
                          "ploc / lbvh: the GPU builders")
+    ap.add_argument("--integrator", default="path", choices=["path", "ao", "normals"])
+    ap.add_argument("--env", default="", help="constant environment r,g,b (AO: 1,1,1 unless given)")
     args = ap.parse_args()
     import torch  # noqa: F401  (single HIP runtime)
     import first_raytracer_amd as frt
@@ -64,6 +66,10 @@ def main():
                               "depth": hs.info.bvh_depth}), file=sys.stderr, flush=True)
     else:
         hs = frt.HostScene(kind, obj, nx / ny)
+    integ = {"path": 0, "ao": frt.FRT_INTEGRATOR_AO, "normals": frt.FRT_INTEGRATOR_NORMALS}[args.integrator]
+    env = args.env or ("1,1,1" if args.integrator == "ao" else "")
+    if env:
+        hs.set_env([float(x) for x in env.split(",")])
     ctxs = {}
     for v in chosen:   # one context per upload-time option (leaf size, wide-tree width)
         leaf = (opt(v, "leaf"), opt(v, "wide"), opt(v, "order"))
@@ -85,13 +91,14 @@ def main():
         for v in chosen:
             leaf = (opt(v, "leaf"), opt(v, "wide"), opt(v, "order"))
             for key, env in (("trav", "FRT_TRAV_MIN"), ("desc", "FRT_MIN_DESC"), ("gran", "FRT_GRANULE"),
-                             ("gk", "FRT_GUIDED_CHUNKS")):
+                             ("gk", "FRT_GUIDED_CHUNKS"), ("grab", "FRT_GRAB")):
                 if opt(v, key):
                     os.environ[env] = opt(v, key)
                 else:
                     os.environ.pop(env, None)
             spi = int(opt(v, "spi") or 0)       # samples per work item (0: automatic)
-            p = frt.RenderParams.make(nx, ny, args.spp, seed=0, flags=flags[v.split("/")[0]], samples_per_item=spi)
+            p = frt.RenderParams.make(nx, ny, args.spp, seed=0, flags=flags[v.split("/")[0]], samples_per_item=spi,
+                                       integrator=integ)
             films[leaf], st = ctxs[leaf].render(p, films.get(leaf))
             if r > 0:
                 res[v].append(st.kernel_ms)
