@@ -2338,13 +2338,21 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     const int grid = c->n_cu * bpc;
     const long long lanes = (long long)grid * kBlock;
     // work granule: the frame's samples cut into k chunks of equal length, k
-    // chosen for about 40 items per resident lane.  Same-call A/B at the bench
-    // configs (profiles/r03/samecall/spi_*.jsonl): Cornell 512 spp is best at
-    // 5-6 chunks (294 ms against 303 with the round-2 rule's 206 / 206 / 100),
-    // cornell_1m 512 spp at 8-12 (837-839 ms against 868 with 170 x 3 + 2).
+    // chosen for at least about 40 items per resident lane and at most
+    // `target` samples an item (about 150 rays: path 24, AO 96, normals 128).
+    // With one queue atomic per refill the first rule alone was best (Cornell
+    // 512 spp at 5-6 chunks, profiles/r03/samecall/spi_*.jsonl); with 64-item
+    // grabs smaller items pay: Cornell 512 spp 289.7 ms at 6 chunks, 281.9 at
+    // 23 (flat from 16 to 64 chunks), cornell_1m 824.1 -> 810.0 ms, while AO
+    // stays best at 6 chunks (1.5 rays a sample; profiles/r03/samecall/grab64_spi_*.jsonl).
+    // FRT_SPI_TARGET overrides the target (0: the first rule alone; A/B knob).
     int spi = p->samples_per_item;
     if (spi <= 0) {
-        const double k = std::max(1.0, std::round(40.0 * (double)lanes / std::max((double)n_slots, 1.0)));
+        const char *st = std::getenv("FRT_SPI_TARGET");
+        const int target = st ? std::atoi(st)
+                              : p->integrator == FRT_INTEGRATOR_PATH ? 24 : p->integrator == FRT_INTEGRATOR_AO ? 96 : 128;
+        double k = std::max(1.0, std::round(40.0 * (double)lanes / std::max((double)n_slots, 1.0)));
+        if (target > 0) k = std::max(k, std::ceil((double)p->spp / (double)target));
         spi = (int)std::ceil((double)p->spp / k);
         spi = std::max(1, std::min(spi, p->spp));
     }
