@@ -214,11 +214,11 @@ def roofline(integrator, key, world, res, V, T):
             if issue is not None:
                 out["valu_issue_frac"] = round(rays * issue / launch_s / 1e9 / VALU_PEAK_GINST, 4)
     if "bound" not in out:
-        # no counter profile for this config: the algorithmic model alone (it can
-        # exceed 1 when L2 / the Infinity Cache / LDS serve the node reads)
-        out.update({"bound": "hbm", "achieved": None if algo is None else round(algo, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": None if algo is None else round(algo / HBM_PEAK_GBS, 4),
-                    "traffic": None, "basis": "algorithmic bytes, no PMC profile for this config"})
+        # no counter profile for this config: no roofline.  The algorithmic bytes
+        # (algorithmic_GBps above) are not one: L1 / L2 / the Infinity Cache / LDS
+        # serve most node reads, so priced against HBM they exceed the peak.
+        out.update({"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None,
+                    "traffic": None, "basis": "no PMC profile for this config (tools/roofline_pmc.py)"})
     return out
 
 
