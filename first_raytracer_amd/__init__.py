@@ -29,9 +29,6 @@ FRT_FLAG_WAVES5 = 2
 FRT_FLAG_WAVES6 = 4
 FRT_FLAG_WAVES4 = 8
 FRT_FLAG_BVH2 = 16
-FRT_FLAG_BVH4 = 32
-FRT_FLAG_BRUTE = 64
-FRT_FLAG_SPEC = 128
 FRT_FLAG_NO_OCT = 256
 FRT_FLAG_FP64 = 512
 FRT_FLAG_FP32 = 1024
@@ -516,6 +513,18 @@ def write_image(path, rgb_u8, fmt="png"):
     rgb_u8 = np.ascontiguousarray(rgb_u8, dtype=np.uint8)
     ny, nx = rgb_u8.shape[0], rgb_u8.shape[1]
     _check(lib().frt_write_image(path.encode(), nx, ny, rgb_u8.ctypes.data, IMAGE_FORMATS[fmt]), "frt_write_image")
+
+
+def work_granule(integrator, spp, n_slots, lanes, spi_req=0):
+    """The render's work granule rule (frt_render.hip work_granule; an internal
+    symbol of libfrt.so, for host tests): (samples per item, chunks)."""
+    L = lib()
+    f = L.frt_internal_work_granule
+    f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                  ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+    spi, k = ctypes.c_int(0), ctypes.c_int(0)
+    _check(f(integrator, spp, n_slots, lanes, spi_req, ctypes.byref(spi), ctypes.byref(k)), "work_granule")
+    return spi.value, k.value
 
 
 def write_tessellated_obj(src_obj, k, dst_obj):

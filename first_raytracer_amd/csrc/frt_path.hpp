@@ -81,12 +81,9 @@ __device__ __forceinline__ unsigned long long *diag_slot()
 
 constexpr int kSentinel = 0x7fffffff;   // "stack empty"; never a node index
 constexpr int kWorldBvh4 = 2;           // internal world kind: 4-wide quantized BVH
-constexpr int kWorldBrute = 3;          // internal world kind: every triangle, in lockstep (tiny scenes)
 constexpr int kWorldBvh2Oct = 4;        // internal world kind: binary nodes from LDS, one copy per ray octant
 constexpr int kBvh4Overflow = 40;       // private stack entries after the LDS ones
-constexpr int kWorldBvh8 = 5;           // internal world kind: 8-wide quantized BVH (HBM plans)
-constexpr int kBvh8Overflow = 72;       // its private stack entries (7 pending siblings per level)
-template <int WORLD> constexpr int kOverflow = WORLD == kWorldBvh4 ? kBvh4Overflow : WORLD == kWorldBvh8 ? kBvh8Overflow : 1;
+template <int WORLD> constexpr int kOverflow = WORLD == kWorldBvh4 ? kBvh4Overflow : 1;
 
 // device scene (fp32, HBM-resident; DESIGN.md "Data layout")
 struct DevScene {
@@ -273,15 +270,14 @@ template <typename R> FRT_HD bool trav_begin(Trav<R> &T, const DevScene &S, int 
 // box costs 6 FMAs and two 3-way max / min instead of also sorting each
 // slab's two distances (the same values: lo <= hi and 1/d has the octant's
 // sign, so the near plane's distance is the smaller one).
-// SPEC (FRT_FLAG_SPEC on the LDS plans): a lane that reaches a leaf parks it
-// and keeps descending while other lanes of its wave have none yet; then every
-// lane tests its parked leaf (Aila & Laine 2009), as bvh4_step's SPEC.
-template <int STRIDE, bool OCT = false, bool SPEC = false, typename R>
+// (Speculative traversal -- a lane that reaches a leaf parks it and keeps
+// descending while other lanes of its wave have none yet, Aila & Laine 2009 --
+// was measured on both plans and removed: +1 % on cornell_1m in round 1,
+// -0.4 % on Cornell and -14 % on cornell_1m at 512 spp in round 3, DESIGN.md.)
+template <int STRIDE, bool OCT = false, typename R>
 FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyhit, int *stk, int min_desc = 0)
 {
     int node = T.node, sp = T.sp;
-    int parked = 0;                                     // leaf refs are negative; 0 = none
-    if (SPEC && node < 0) { parked = node; node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel; }
     DevScene Sn = S;
     if constexpr (OCT) {
         const int oct = (T.sr.invd.x < R(0) ? 1 : 0) | (T.sr.invd.y < R(0) ? 2 : 0) | (T.sr.invd.z < R(0) ? 4 : 0);
@@ -315,22 +311,7 @@ FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyh
         } else {
             node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel;
         }
-        if constexpr (SPEC) {
-            if (parked == 0 && node < 0) { parked = node; node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel; }
-            // keep going while some lane of the wave still has no leaf to test
-            if (!wave_any(parked == 0 && (unsigned)node < (unsigned)kSentinel)) break;
-        } else {
-            if (min_desc > 0 && wave_count((unsigned)node < (unsigned)kSentinel) < min_desc) break;
-        }
-    }
-    if constexpr (SPEC) {
-        if (parked != 0 && leaf_hit(S, ~parked, o, d, T.tmin, anyhit, T.h)) {
-            T.node = node; T.sp = sp;
-            return true;
-        }
-        T.node = node;
-        T.sp = sp;
-        return node == kSentinel;
+        if (min_desc > 0 && wave_count((unsigned)node < (unsigned)kSentinel) < min_desc) break;
     }
     if ((unsigned)node < (unsigned)kSentinel) {          // postponed: still descending
         T.node = node;
@@ -355,16 +336,11 @@ FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyh
 // one FMA.  Quantised planes round outward and the boxes keep their padding,
 // so culling stays conservative and the hit equals the binary traversal's
 // bit for bit (the (t, DFS rank) minimum does not depend on visit order).
-// SPEC (speculative traversal, Aila & Laine 2009): a lane that reaches a leaf
-// parks it and keeps descending while other lanes of its wave still search
-// for one; then every lane tests its parked leaf at once.  Visits more nodes
-// with a stale t_best (still conservative), keeps lanes busy.
 // fp32 only: the fp64 kernels traverse the binary tree.
-template <int STRIDE, int LSTACK, bool SPEC = false>
+template <int STRIDE, int LSTACK>
 FRT_HD bool bvh4_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int *ovf, int min_desc = 0)
 {
     int node = T.node, sp = T.sp;
-    int parked = 0;                                     // leaf refs are negative; 0 = none
     // Entries below LSTACK live in the lane's LDS column, deeper ones in `ovf`
     // (scratch).  A wave-uniform test keeps the common case on plain LDS
     // accesses: a per-lane select between the two would make the compiler
@@ -384,7 +360,6 @@ FRT_HD bool bvh4_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit
         if (!wave_any(sp >= LSTACK)) return stk[sp * STRIDE];
         return sp < LSTACK ? stk[sp * STRIDE] : ovf[sp - LSTACK];
     };
-    if (SPEC && node < 0) { parked = node; node = pop(); }
     while ((unsigned)node < (unsigned)kSentinel) {
         FRT_DIAG_TICK(0);
         const uint4 w0 = node4_part(S, node, 0), w1 = node4_part(S, node, 1);
@@ -435,22 +410,7 @@ FRT_HD bool bvh4_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit
             if (t[1] != __builtin_inff()) push(c[1]);
         }
         node = (t[0] != __builtin_inff()) ? c[0] : pop();
-        if constexpr (SPEC) {
-            if (parked == 0 && node < 0) { parked = node; node = pop(); }
-            // keep going while some lane of the wave still has no leaf to test
-            if (!wave_any(parked == 0 && (unsigned)node < (unsigned)kSentinel)) break;
-        } else {
-            if (min_desc > 0 && wave_count((unsigned)node < (unsigned)kSentinel) < min_desc) break;
-        }
-    }
-    if constexpr (SPEC) {
-        if (parked != 0 && leaf_hit(S, ~parked, o, d, T.tmin, anyhit, T.h)) {
-            T.node = node; T.sp = sp;
-            return true;
-        }
-        T.node = node;
-        T.sp = sp;
-        return node == kSentinel;
+        if (min_desc > 0 && wave_count((unsigned)node < (unsigned)kSentinel) < min_desc) break;
     }
     if ((unsigned)node < (unsigned)kSentinel) {          // postponed (min_desc): still descending
         T.node = node;
@@ -473,120 +433,6 @@ FRT_HD Hit<R> trace_bvh(const DevScene &S, V3<R> o, V3<R> d, R tmax, bool anyhit
     Trav<R> T;
     if (trav_begin(T, S, S.root, o, d, tmax))
         while (!bvh2_step<STRIDE>(T, S, o, d, anyhit, stk)) {}
-    return T.h;
-}
-
-// The same query over the 8-wide quantized BVH (build_wide<8>): node = 128 B,
-// 8 uint4 (6 used): frame origin xyz + exponent bytes | 8 child refs | per
-// axis the 8 lo planes and the 8 hi planes (two words each).  Children sit in
-// octant slots: slot s holds the child whose box centre lies in octant s of
-// the node's centre (bit a set: the upper half on axis a).  A ray whose
-// direction is negative on axis a meets the upper half first, so position
-// p = s ^ neg (neg: the ray's direction-sign bits) orders the children
-// roughly front to back without a sort: three conditional swap stages, then
-// the hit children are pushed farthest first (Ylitie et al. 2017's octant
-// order).  The hit is the same (t, DFS rank) minimum as every other layout.
-template <int STRIDE, int LSTACK>
-FRT_HD bool bvh8_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int *ovf, int min_desc = 0)
-{
-    int node = T.node, sp = T.sp;
-    auto push = [&](int v) {
-        if (!wave_any(sp >= LSTACK)) {
-            stk[sp * STRIDE] = v;
-        } else {
-            if (sp < LSTACK) stk[sp * STRIDE] = v;
-            else ovf[sp - LSTACK] = v;
-        }
-        ++sp;
-    };
-    auto pop = [&]() -> int {
-        if (sp == 0) return kSentinel;
-        --sp;
-        if (!wave_any(sp >= LSTACK)) return stk[sp * STRIDE];
-        return sp < LSTACK ? stk[sp * STRIDE] : ovf[sp - LSTACK];
-    };
-    const SlabRay<float> &sr = T.sr;
-    const bool sx = sr.invd.x < 0.0f, sy = sr.invd.y < 0.0f, sz = sr.invd.z < 0.0f;
-    while ((unsigned)node < (unsigned)kSentinel) {
-        FRT_DIAG_TICK(0);
-        const uint4 *nd = S.nodes4 + (size_t)node * 8;
-        const uint4 w0 = nd[0], w1 = nd[1], w2 = nd[2], w3 = nd[3], w4 = nd[4], w5 = nd[5];
-        const float ax = u2f((w0.w & 0xffu) << 23) * sr.invd.x, bx = fmaf(u2f(w0.x), sr.invd.x, sr.oinv.x);
-        const float ay = u2f(((w0.w >> 8) & 0xffu) << 23) * sr.invd.y, by = fmaf(u2f(w0.y), sr.invd.y, sr.oinv.y);
-        const float az = u2f(((w0.w >> 16) & 0xffu) << 23) * sr.invd.z, bz = fmaf(u2f(w0.z), sr.invd.z, sr.oinv.z);
-        // near / far plane words by direction sign (children 0-3 | 4-7)
-        const uint32_t xn[2] = {sx ? w3.z : w3.x, sx ? w3.w : w3.y}, xf[2] = {sx ? w3.x : w3.z, sx ? w3.y : w3.w};
-        const uint32_t yn[2] = {sy ? w4.z : w4.x, sy ? w4.w : w4.y}, yf[2] = {sy ? w4.x : w4.z, sy ? w4.y : w4.w};
-        const uint32_t zn[2] = {sz ? w5.z : w5.x, sz ? w5.w : w5.y}, zf[2] = {sz ? w5.x : w5.z, sz ? w5.y : w5.w};
-        int c[8] = {(int)w1.x, (int)w1.y, (int)w1.z, (int)w1.w, (int)w2.x, (int)w2.y, (int)w2.z, (int)w2.w};
-        uint32_t hm = 0;                                // bit i: slot i is hit
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int wd = i >> 2, sh = 8 * (i & 3);
-            const float txn = fmaf((float)((xn[wd] >> sh) & 0xffu), ax, bx), txf = fmaf((float)((xf[wd] >> sh) & 0xffu), ax, bx);
-            const float tyn = fmaf((float)((yn[wd] >> sh) & 0xffu), ay, by), tyf = fmaf((float)((yf[wd] >> sh) & 0xffu), ay, by);
-            const float tzn = fmaf((float)((zn[wd] >> sh) & 0xffu), az, bz), tzf = fmaf((float)((zf[wd] >> sh) & 0xffu), az, bz);
-            const float tn = fmaxf(fmaxf(txn, tyn), fmaxf(tzn, T.tmin));
-            const float tf = fminf(fminf(txf, tyf), fminf(tzf, T.h.t));
-            hm |= (tf < tn ? 0u : 1u) << i;
-        }
-        // octant order: position p = slot ^ neg -- per axis, swap the halves of
-        // the refs and of the hit bits where the ray runs in -a
-        {
-            const uint32_t m0 = ((hm & 0x55u) << 1) | ((hm >> 1) & 0x55u);
-            hm = sx ? m0 : hm;
-            const uint32_t m1 = ((hm & 0x33u) << 2) | ((hm >> 2) & 0x33u);
-            hm = sy ? m1 : hm;
-            const uint32_t m2 = ((hm & 0x0fu) << 4) | ((hm >> 4) & 0x0fu);
-            hm = sz ? m2 : hm;
-        }
-#pragma unroll
-        for (int b = 0; b < 3; ++b) {
-            const bool fl = b == 0 ? sx : b == 1 ? sy : sz;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                if (i & (1 << b)) continue;
-                const int j = i | (1 << b);
-                const int ci = c[i], cj = c[j];
-                c[i] = fl ? cj : ci;
-                c[j] = fl ? ci : cj;
-            }
-        }
-        // the hit children after the first go on the stack, farthest first
-        if (!wave_any(sp > LSTACK - 7)) {               // wave-uniform: every push stays in LDS
-#pragma unroll
-            for (int i = 7; i >= 1; --i)
-                if ((hm >> i) & 1u) stk[sp++ * STRIDE] = c[i];
-        } else {
-#pragma unroll
-            for (int i = 7; i >= 1; --i)
-                if ((hm >> i) & 1u) push(c[i]);
-        }
-        node = (hm & 1u) ? c[0] : pop();
-        if (min_desc > 0 && wave_count((unsigned)node < (unsigned)kSentinel) < min_desc) break;
-    }
-    if ((unsigned)node < (unsigned)kSentinel) {          // postponed (min_desc): still descending
-        T.node = node;
-        T.sp = sp;
-        return false;
-    }
-    bool done = node == kSentinel || leaf_hit(S, ~node, o, d, T.tmin, anyhit, T.h);
-    if (!done) {
-        node = pop();
-        done = node == kSentinel;
-    }
-    T.node = node;
-    T.sp = sp;
-    return done;
-}
-
-template <int STRIDE, int LSTACK, int OVF>
-FRT_HD Hit<float> trace_bvh8(const DevScene &S, f3 o, f3 d, float tmax, bool anyhit, int *stk)
-{
-    Trav<float> T;
-    int ovf[OVF];
-    if (trav_begin(T, S, S.root4, o, d, tmax))
-        while (!bvh8_step<STRIDE, LSTACK>(T, S, o, d, anyhit, stk, ovf)) {}
     return T.h;
 }
 
@@ -624,7 +470,6 @@ FRT_HD Hit<R> trace(const DevScene &S, V3<R> o, V3<R> d, R tmax, bool anyhit, in
 {
     if constexpr (WORLD == FRT_WORLD_LIST) return trace_list(S, o, d, tmax, anyhit);
     else if constexpr (WORLD == kWorldBvh4) return trace_bvh4<STRIDE, STACK, kBvh4Overflow>(S, o, d, tmax, anyhit, stk);
-    else if constexpr (WORLD == kWorldBvh8) return trace_bvh8<STRIDE, STACK, kBvh8Overflow>(S, o, d, tmax, anyhit, stk);
     else return trace_bvh<STRIDE>(S, o, d, tmax, anyhit, stk);
 }
 
@@ -636,27 +481,10 @@ FRT_HD bool trav_begin_world(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, R 
         T.h = Hit<R>{-1, tmax, R(0), R(0)};
         return true;
     } else {
-        return trav_begin(T, S, WORLD == kWorldBvh4 || WORLD == kWorldBvh8 ? S.root4 : S.root, o, d, tmax);   // brute: root box + t_min
+        return trav_begin(T, S, WORLD == kWorldBvh4 ? S.root4 : S.root, o, d, tmax);
     }
 }
-// Tiny triangle-only BVH scenes: test every triangle in index order.  All
-// lanes of a wave read the same triangle (an LDS broadcast) and run the same
-// trip count, so no lane idles; the (t, DFS rank) minimum is the BVH's hit,
-// and the BVH's root box test and t_min stay (trav_begin).
-template <typename R> FRT_HD bool brute_all(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyhit)
-{
-    for (int ref = 0; ref < S.n_tris; ++ref) {
-        R u, v;
-        const R t = prim_t(S, ref, o, d, T.tmin, T.h.t, u, v);
-        if (t > R(0) && (t < T.h.t || (T.h.prim >= 0 && ref < T.h.prim))) {
-            T.h.prim = ref; T.h.t = t; T.h.u = u; T.h.v = v;
-            if (anyhit) break;
-        }
-    }
-    return true;
-}
-
-template <int WORLD, int STRIDE, int STACK, bool SPEC = false, typename R>
+template <int WORLD, int STRIDE, int STACK, typename R>
 FRT_HD bool trav_step_world(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyhit, int *stk, int *ovf,
                             int min_desc = 0)
 {
@@ -664,22 +492,18 @@ FRT_HD bool trav_step_world(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, boo
     // (the values trav_begin set), so that they are not live across the
     // megakernel's shading phases (spilled VGPRs 81 -> 36 at the 6-wave cap;
     // cornell_1m +2.8 %, same-call A/B).  The binary LDS plan keeps them.
-    if constexpr (WORLD == kWorldBvh4 || WORLD == kWorldBvh8) {
+    if constexpr (WORLD == kWorldBvh4) {
         static_assert(!kIsF64<R>, "the fp64 kernels traverse the binary tree");
         T.sr = slab_ray(o, d);
         T.tmin = bvh_tmin(o);
     }
-    if constexpr (WORLD == kWorldBrute) {
-        return brute_all(T, S, o, d, anyhit);
-    } else if constexpr (WORLD == FRT_WORLD_LIST) {
+    if constexpr (WORLD == FRT_WORLD_LIST) {
         T.h = trace_list(S, o, d, T.h.t, anyhit);
         return true;
     } else if constexpr (WORLD == kWorldBvh4) {
-        return bvh4_step<STRIDE, STACK, SPEC>(T, S, o, d, anyhit, stk, ovf, min_desc);
-    } else if constexpr (WORLD == kWorldBvh8) {
-        return bvh8_step<STRIDE, STACK>(T, S, o, d, anyhit, stk, ovf, min_desc);
+        return bvh4_step<STRIDE, STACK>(T, S, o, d, anyhit, stk, ovf, min_desc);
     } else {
-        return bvh2_step<STRIDE, WORLD == kWorldBvh2Oct, SPEC>(T, S, o, d, anyhit, stk, min_desc);
+        return bvh2_step<STRIDE, WORLD == kWorldBvh2Oct>(T, S, o, d, anyhit, stk, min_desc);
     }
 }
 

@@ -58,15 +58,8 @@ struct DevWork {
     float *partial;                      // [n_chunks][n_slots][3]
     unsigned *counter;                   // work-queue head
     unsigned long long *wave_rays;       // [n_waves][4]: camera, extension, shadow, samples
-    int guided, n_tiles;                 // guided: chunk-major items, chunk i of weight n_chunks - i
     uint32_t grab;                       // items a wave takes per queue atomic (at least those it needs)
 };
-// guided granule: chunk i of n starts at spp * (i n - i (i - 1) / 2) / (n (n + 1) / 2)
-__host__ __device__ __forceinline__ int guided_start(int i, int n, int spp)
-{
-    const unsigned long long num = (unsigned long long)i * n - (unsigned long long)i * (i - 1) / 2;
-    return (int)((unsigned long long)spp * num / ((unsigned long long)n * (n + 1) / 2));
-}
 
 // slot -> pixel inside a tile: 8x8 blocks, row-major inside a block
 __device__ __host__ __forceinline__ void slot_to_local(int s, int tile, int &lx, int &ly)
@@ -154,7 +147,7 @@ struct ItemState {
 
 // R: float (the product kernels) or double (the fp64 kernels, DESIGN.md
 // "Precision": list worlds under FRT_PRECISION_AUTO, every plan under _FP64)
-template <int STACK, int WORLD, bool LDS_SCENE, int WAVES = 1, bool SPEC = false, int MATS = kMatsNone,
+template <int STACK, int WORLD, bool LDS_SCENE, int WAVES = 1, int MATS = kMatsNone,
           int KIND = FRT_INTEGRATOR_PATH, typename R = float>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void path_megakernel(
     const DevScene S0, const DevWork W)
@@ -188,8 +181,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     // key is re-derived from the item at shading, t_max from the ray kind.
     // cornell_1m +1.2 % (spilled VGPRs 26 -> 14); on the LDS plan it costs
     // 0.3 % (same-call A/B, profiles/r03/samecall/lean_*.jsonl).  The material
-    // kernels keep the full state (DESIGN.md "Register-cap hazard").
-    constexpr bool kLean = !LDS_SCENE && MATS == kMatsNone && KIND == FRT_INTEGRATOR_PATH;
+    // kernels keep the full state (DESIGN.md "Register-cap hazard"), and so do
+    // the fp64 kernels (their per-sample sum stays fp64 until the sample ends).
+    // The flushes round each contribution into the fp32 item sum, so a lean
+    // plan's film equals the per-sample plans' to fp32 rounding, not bit for
+    // bit (tests/test_gpu_parity.py::test_lean_plan_rounding).
+    constexpr bool kLean = !LDS_SCENE && MATS == kMatsNone && KIND == FRT_INTEGRATOR_PATH && !kIsF64<R>;
     auto flush_L = [&]() {
         I.set(kIsAcc + 0, f2i(i2f(I.get(kIsAcc + 0)) + (float)P.L.x));
         I.set(kIsAcc + 1, f2i(i2f(I.get(kIsAcc + 1)) + (float)P.L.y));
@@ -212,7 +209,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             bool shadow_done = false;
             if (tracing) FRT_DIAG_TICK(3);
             // (LDS-resident binary plans: no leaf postponing, compiled out)
-            if (tracing && trav_step_world<WORLD, kBlock, STACK, SPEC>(T, S, P.ro, P.rd, P.shadow, stk, ovf,
+            if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, P.ro, P.rd, P.shadow, stk, ovf,
                                                                        LDS_SCENE && WORLD == FRT_WORLD_BVH
                                                                            ? 0 : W.min_desc)) {
                 if (KIND == FRT_INTEGRATOR_PATH && P.shadow) {   // finish the shadow ray here, keep traversing
@@ -291,8 +288,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
                 } else {
                     const uint32_t s = w % (uint32_t)T2;
                     const uint32_t q = w / (uint32_t)T2;
-                    const uint32_t chunk = W.guided ? q / (uint32_t)W.n_tiles : q % (uint32_t)W.n_chunks;
-                    const uint32_t t_ord = W.guided ? q % (uint32_t)W.n_tiles : q / (uint32_t)W.n_chunks;
+                    const uint32_t chunk = q % (uint32_t)W.n_chunks;
+                    const uint32_t t_ord = q / (uint32_t)W.n_chunks;
                     const int tile_id = W.shard_index + (int)t_ord * W.shard_count;
                     int lx, ly;
                     slot_to_local((int)s, W.tile, lx, ly);
@@ -300,9 +297,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
                     const int py = (tile_id / W.ntx) * W.tile + ly;
                     if (px < W.nx && py < W.ny) {   // padding slots of edge tiles carry no work
                         have_item = true;
-                        const int s_cur = W.guided ? guided_start((int)chunk, W.n_chunks, W.spp) : (int)chunk * W.spi;
+                        const int s_cur = (int)chunk * W.spi;
                         I.set(kIsCur, s_cur);
-                        I.set(kIsEnd, W.guided ? guided_start((int)chunk + 1, W.n_chunks, W.spp) : min(W.spp, s_cur + W.spi));
+                        I.set(kIsEnd, min(W.spp, s_cur + W.spi));
                         I.set(kIsSlot, (int)(t_ord * (uint32_t)T2 + s));
                         I.set(kIsChunk, (int)chunk);
                         I.set(kIsPix, py * W.nx + px);
@@ -353,6 +350,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
 // step (4 Grays/s on camera rays: profiles/r03/r03e_trace_atomic_per_step.jsonl).
 // ------------------------------------------------------------------------
 constexpr uint32_t kTraceChunk = 256;   // rays a wave takes from the buffer with one atomic
+// the context's queue words: [0] the render / PSS-MLT work queue, [kTraceCounterWord] the ray-query queue
+constexpr size_t kCounterBytes = 256;
+constexpr int kTraceCounterWord = 32;   // 128 B after the render queue's word
 struct DevRays {
     const float4 *ray;       // 2 per ray: (origin, t_max) | (direction, flags: bit 0 = any-hit)
     float4 *hit;             // 1 per ray: (t, u, v, prim ref of the scene view as int bits; -1 = miss)
@@ -793,13 +793,12 @@ struct frt_ctx {
     DevScene S{};
     int world_kind = 0, stack_needed = 0;
     bool has_bvh4 = false;        // nodes4 holds the 4-wide BVH4Q
-    bool has_bvh8 = false;        // ... or the 8-wide nodes (FRT_WIDE=8 at upload)
     int depth4 = 0;               // levels of that wide tree
     int n_tris = 0, n_spheres = 0;
     bool has_spec_mats = false;   // a non-lambertian scattering material or a texture: MATS kernels
     int mats = kMatsNone;         // kMats* mask of the scene's material set (pick_launcher)
     bool has_metal = false;       // ao::Li cannot sample metal (constant_pdf::generate throws, pdf.h:195-198)
-    size_t scene_lds_bytes = 0, scene_lds_bytes4 = 0;   // LDS copy with binary / 4-wide nodes
+    size_t scene_lds_bytes = 0;                         // LDS copy with the binary nodes
     size_t scene_lds_bytes_oct = 0;                     // ... with the 8 octant copies of the binary nodes
     int precision = FRT_PRECISION_AUTO;                 // frt_set_precision
     bool has_f64 = false;                               // the scene's fp64 records are in HBM
@@ -833,7 +832,6 @@ struct frt_ctx {
 // count (DESIGN.md "Register-cap hazard").  The lambertian kernels (the
 // bench configurations) stay on the greedy allocator.
 static bool bvh4_stack_fits(int depth4, int lds_entries) { return 3 * depth4 <= lds_entries + kBvh4Overflow; }
-static bool bvh8_stack_fits(int depth8, int lds_entries) { return 7 * depth8 <= lds_entries + kBvh8Overflow; }
 struct Launcher {
     const void *fn = nullptr;
     size_t lds = 0;
@@ -843,25 +841,25 @@ struct Launcher {
     bool wide = false;      // 4-wide quantized BVH
     bool f64 = false;       // the fp64 kernel
 };
-template <int STACK, int WORLD, bool LDS, int WAVES = 1, bool SPEC = false, int MATS = kMatsNone,
+template <int STACK, int WORLD, bool LDS, int WAVES = 1, int MATS = kMatsNone,
           int KIND = FRT_INTEGRATOR_PATH, typename R = float>
 static Launcher make_launcher(size_t scene_bytes)
 {
     Launcher L;
-    L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES, SPEC, MATS, KIND, R>);
+    L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES, MATS, KIND, R>);
     L.f64 = kIsF64<R>;
     L.lds = (WORLD != FRT_WORLD_LIST ? (size_t)STACK * kBlock * sizeof(int) : 0) +
             (size_t)kItemWords * kBlock * sizeof(int) + (LDS ? scene_bytes : 0);
     L.stack = STACK;
     L.waves = WAVES > 1 ? WAVES : 0;
     L.lds_scene = LDS;
-    L.wide = WORLD == kWorldBvh4 || WORLD == kWorldBvh8;
+    L.wide = WORLD == kWorldBvh4;
     return L;
 }
 #ifndef FRT_EXP_W6
 #define FRT_EXP_W6 6   // experiment builds: the register cap behind the "6 waves" plans
 #endif
-template <int STACK, bool LDS, int WORLD = FRT_WORLD_BVH, bool SPEC = false, int MATS = kMatsNone>
+template <int STACK, bool LDS, int WORLD = FRT_WORLD_BVH, int MATS = kMatsNone>
 static Launcher bvh_launcher(int waves, size_t sb)
 {
     // Every material set has a 6-wave build again (round 3).  Under the greedy
@@ -872,25 +870,23 @@ static Launcher bvh_launcher(int waves, size_t sb)
     // test_register_caps_agree checks every cap and plan).  The defaults stay
     // 4 / 5 waves for the specular sets (faster than 6:
     // profiles/r02/r02_ab_sphere_hbm_mats.jsonl).
-    if (waves == 6) return make_launcher<STACK, WORLD, LDS, FRT_EXP_W6, SPEC, MATS>(sb);
-    if (waves == 5) return make_launcher<STACK, WORLD, LDS, 5, SPEC, MATS>(sb);
+    if (waves == 6) return make_launcher<STACK, WORLD, LDS, FRT_EXP_W6, MATS>(sb);
+    if (waves == 5) return make_launcher<STACK, WORLD, LDS, 5, MATS>(sb);
     if constexpr (MATS != kMatsNone) {
-        if (waves == 4) return make_launcher<STACK, WORLD, LDS, 4, SPEC, MATS>(sb);
-        if (waves == 3) return make_launcher<STACK, WORLD, LDS, 3, SPEC, MATS>(sb);
+        if (waves == 4) return make_launcher<STACK, WORLD, LDS, 4, MATS>(sb);
+        if (waves == 3) return make_launcher<STACK, WORLD, LDS, 3, MATS>(sb);
     }
-    return make_launcher<STACK, WORLD, LDS, 1, SPEC, MATS>(sb);
+    return make_launcher<STACK, WORLD, LDS, 1, MATS>(sb);
 }
 #ifndef FRT_EXP_BVH4_LSTACK
 #define FRT_EXP_BVH4_LSTACK 16
 #endif
 constexpr int kBvh4LdsStack = FRT_EXP_BVH4_LSTACK;   // 16 KiB of LDS per block; deeper entries go to scratch
-constexpr int kBvh4LdsStackSmall = 8;   // LDS-resident scenes (shallow trees)
-constexpr int kBruteMaxTris = 128;
 // MATS: the material set the kernel is compiled for (kMats* mask, frt_path.hpp)
 template <int MATS>
 static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
 {
-    if (c->world_kind == FRT_WORLD_LIST) { L = make_launcher<16, FRT_WORLD_LIST, false, 1, false, MATS>(0); return FRT_OK; }
+    if (c->world_kind == FRT_WORLD_LIST) { L = make_launcher<16, FRT_WORLD_LIST, false, 1, MATS>(0); return FRT_OK; }
     const int d = c->stack_needed;
     const size_t sb = c->scene_lds_bytes;
     const bool lds = d < kLdsMaxDepth && sb <= kLdsSceneBytes && !(flags & FRT_FLAG_NO_LDS_SCENE);
@@ -917,58 +913,27 @@ static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
     if (flags & FRT_FLAG_WAVES4) waves = 0;   // the compiler's own allocation (~120 VGPRs, 4 waves)
     if (flags & FRT_FLAG_WAVES5) waves = 5;
     if (flags & FRT_FLAG_WAVES6) waves = 6;
-    if constexpr (MATS == kMatsNone) {   // A/B plans, lambertian scenes only
-        // tiny triangle-only scenes from LDS, every triangle in lockstep (FRT_FLAG_BRUTE)
-        if (lds && (flags & FRT_FLAG_BRUTE) && c->n_spheres == 0 && c->n_tris <= kBruteMaxTris) {
-            L = bvh_launcher<8, true, kWorldBrute>(waves, sb);
-            return FRT_OK;
-        }
-        // LDS-resident scenes, 4-wide (FRT_FLAG_BVH4)
-        if (lds && (flags & FRT_FLAG_BVH4) && c->has_bvh4 && c->scene_lds_bytes4 <= kLdsSceneBytes &&
-            bvh4_stack_fits(c->depth4, kBvh4LdsStackSmall)) {
-            L = bvh_launcher<kBvh4LdsStackSmall, true, kWorldBvh4>(waves, c->scene_lds_bytes4);
-            return FRT_OK;
-        }
-        // speculative binary traversal from LDS (FRT_FLAG_SPEC on an LDS-resident scene)
-        if (lds && (flags & FRT_FLAG_SPEC) && !(flags & FRT_FLAG_NO_OCT) && c->scene_lds_bytes_oct <= kLdsOctBytes) {
-            L = d < 8 ? bvh_launcher<8, true, kWorldBvh2Oct, true>(waves, c->scene_lds_bytes_oct)
-                      : bvh_launcher<16, true, kWorldBvh2Oct, true>(waves, c->scene_lds_bytes_oct);
-            return FRT_OK;
-        }
-        // speculative 4-wide traversal (FRT_FLAG_SPEC)
-        if (!lds && (flags & FRT_FLAG_SPEC) && c->has_bvh4 && !(flags & FRT_FLAG_BVH2) &&
-            bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
-            L = bvh_launcher<kBvh4LdsStack, false, kWorldBvh4, true>(waves, 0);
-            return FRT_OK;
-        }
-    }
-    // HBM-resident scenes: the 8-wide nodes when uploaded (lambertian kernels; the
-    // material kernels take the binary tree then)
-    if constexpr (MATS == kMatsNone) {
-        if (!lds && c->has_bvh8 && !(flags & FRT_FLAG_BVH2) && bvh8_stack_fits(c->depth4, kBvh4LdsStack)) {
-            L = bvh_launcher<kBvh4LdsStack, false, kWorldBvh8>(waves, 0);
-            return FRT_OK;
-        }
-    }
+    // (Measured and removed A/B plans, DESIGN.md section 5: lockstep brute force over tiny
+    // scenes, 4-wide nodes from LDS, speculative traversal, an 8-wide HBM tree.)
     // HBM-resident scenes: the 4-wide quantized BVH (half the bytes per box test)
     if (!lds && c->has_bvh4 && !(flags & FRT_FLAG_BVH2) && bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
-        L = bvh_launcher<kBvh4LdsStack, false, kWorldBvh4, false, MATS>(waves, 0);
+        L = bvh_launcher<kBvh4LdsStack, false, kWorldBvh4, MATS>(waves, 0);
         return FRT_OK;
     }
     // LDS-resident binary tree: the per-octant node copies when they fit
     const bool oct = lds && !(flags & FRT_FLAG_NO_OCT) && c->scene_lds_bytes_oct <= kLdsOctBytes;
     if (oct) {
-        L = d < 8 ? bvh_launcher<8, true, kWorldBvh2Oct, false, MATS>(waves, c->scene_lds_bytes_oct)
-                  : bvh_launcher<16, true, kWorldBvh2Oct, false, MATS>(waves, c->scene_lds_bytes_oct);
+        L = d < 8 ? bvh_launcher<8, true, kWorldBvh2Oct, MATS>(waves, c->scene_lds_bytes_oct)
+                  : bvh_launcher<16, true, kWorldBvh2Oct, MATS>(waves, c->scene_lds_bytes_oct);
         return FRT_OK;
     }
-    if (d < 8) L = lds ? bvh_launcher<8, true, FRT_WORLD_BVH, false, MATS>(waves, sb)
-                       : bvh_launcher<8, false, FRT_WORLD_BVH, false, MATS>(waves, 0);
-    else if (d < 16) L = lds ? bvh_launcher<16, true, FRT_WORLD_BVH, false, MATS>(waves, sb)
-                             : bvh_launcher<16, false, FRT_WORLD_BVH, false, MATS>(waves, 0);
-    else if (d < 24) L = bvh_launcher<24, false, FRT_WORLD_BVH, false, MATS>(waves, 0);
-    else if (d < 32) L = bvh_launcher<32, false, FRT_WORLD_BVH, false, MATS>(waves, 0);
-    else if (d < 64) L = make_launcher<64, FRT_WORLD_BVH, false, 1, false, MATS>(0);
+    if (d < 8) L = lds ? bvh_launcher<8, true, FRT_WORLD_BVH, MATS>(waves, sb)
+                       : bvh_launcher<8, false, FRT_WORLD_BVH, MATS>(waves, 0);
+    else if (d < 16) L = lds ? bvh_launcher<16, true, FRT_WORLD_BVH, MATS>(waves, sb)
+                             : bvh_launcher<16, false, FRT_WORLD_BVH, MATS>(waves, 0);
+    else if (d < 24) L = bvh_launcher<24, false, FRT_WORLD_BVH, MATS>(waves, 0);
+    else if (d < 32) L = bvh_launcher<32, false, FRT_WORLD_BVH, MATS>(waves, 0);
+    else if (d < 64) L = make_launcher<64, FRT_WORLD_BVH, false, 1, MATS>(0);
     else return FRT_E_UNSUPPORTED;
     return FRT_OK;
 }
@@ -978,25 +943,25 @@ template <int KIND>
 static int pick_launcher_kind(const frt_ctx *c, int flags, Launcher &L)
 {
     constexpr int M = KIND == FRT_INTEGRATOR_AO ? kMatsAll : kMatsNone;
-    if (c->world_kind == FRT_WORLD_LIST) { L = make_launcher<16, FRT_WORLD_LIST, false, 1, false, M, KIND>(0); return FRT_OK; }
+    if (c->world_kind == FRT_WORLD_LIST) { L = make_launcher<16, FRT_WORLD_LIST, false, 1, M, KIND>(0); return FRT_OK; }
     const int d = c->stack_needed;
     const size_t sb = c->scene_lds_bytes;
     const bool lds = d < kLdsMaxDepth && sb <= kLdsSceneBytes && !(flags & FRT_FLAG_NO_LDS_SCENE);
     const bool oct = lds && !(flags & FRT_FLAG_NO_OCT) && c->scene_lds_bytes_oct <= kLdsOctBytes;
     if (oct) {
-        L = d < 8 ? make_launcher<8, kWorldBvh2Oct, true, 5, false, M, KIND>(c->scene_lds_bytes_oct)
-                  : make_launcher<16, kWorldBvh2Oct, true, 5, false, M, KIND>(c->scene_lds_bytes_oct);
+        L = d < 8 ? make_launcher<8, kWorldBvh2Oct, true, 5, M, KIND>(c->scene_lds_bytes_oct)
+                  : make_launcher<16, kWorldBvh2Oct, true, 5, M, KIND>(c->scene_lds_bytes_oct);
     } else if (lds) {
-        L = d < 8 ? make_launcher<8, FRT_WORLD_BVH, true, 5, false, M, KIND>(sb)
-                  : make_launcher<16, FRT_WORLD_BVH, true, 5, false, M, KIND>(sb);
+        L = d < 8 ? make_launcher<8, FRT_WORLD_BVH, true, 5, M, KIND>(sb)
+                  : make_launcher<16, FRT_WORLD_BVH, true, 5, M, KIND>(sb);
     } else if (c->has_bvh4 && !(flags & FRT_FLAG_BVH2) && bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
-        L = make_launcher<kBvh4LdsStack, kWorldBvh4, false, 6, false, M, KIND>(0);
+        L = make_launcher<kBvh4LdsStack, kWorldBvh4, false, 6, M, KIND>(0);
     } else if (d < 16) {
-        L = make_launcher<16, FRT_WORLD_BVH, false, 6, false, M, KIND>(0);
+        L = make_launcher<16, FRT_WORLD_BVH, false, 6, M, KIND>(0);
     } else if (d < 32) {
-        L = make_launcher<32, FRT_WORLD_BVH, false, 6, false, M, KIND>(0);
+        L = make_launcher<32, FRT_WORLD_BVH, false, 6, M, KIND>(0);
     } else if (d < 64) {
-        L = make_launcher<64, FRT_WORLD_BVH, false, 1, false, M, KIND>(0);
+        L = make_launcher<64, FRT_WORLD_BVH, false, 1, M, KIND>(0);
     } else {
         return FRT_E_UNSUPPORTED;
     }
@@ -1010,12 +975,12 @@ static int pick_launcher_f64_t(const frt_ctx *c, Launcher &L)
 {
     if (c->world_kind == FRT_WORLD_LIST) {
         // (a 2-wave register cap changed nothing: profiles/r03/r03c_ab_veach_listbox_f64waves.jsonl)
-        L = make_launcher<16, FRT_WORLD_LIST, false, 1, false, MATS, FRT_INTEGRATOR_PATH, double>(0);
+        L = make_launcher<16, FRT_WORLD_LIST, false, 1, MATS, FRT_INTEGRATOR_PATH, double>(0);
         return FRT_OK;
     }
     const int d = c->stack_needed;
-    if (d < 32) L = make_launcher<32, FRT_WORLD_BVH, false, 1, false, kMatsAll, FRT_INTEGRATOR_PATH, double>(0);
-    else if (d < 64) L = make_launcher<64, FRT_WORLD_BVH, false, 1, false, kMatsAll, FRT_INTEGRATOR_PATH, double>(0);
+    if (d < 32) L = make_launcher<32, FRT_WORLD_BVH, false, 1, kMatsAll, FRT_INTEGRATOR_PATH, double>(0);
+    else if (d < 64) L = make_launcher<64, FRT_WORLD_BVH, false, 1, kMatsAll, FRT_INTEGRATOR_PATH, double>(0);
     else return FRT_E_UNSUPPORTED;
     return FRT_OK;
 }
@@ -1111,7 +1076,7 @@ extern "C" int frt_create(int hip_device, frt_ctx **out)
     c->n_cu = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc(&c->counter, 64) != hipSuccess) {
+        hipMalloc(&c->counter, kCounterBytes) != hipSuccess) {
         delete c;
         return FRT_E_HIP;
     }
@@ -1202,7 +1167,6 @@ struct FlatScene {
     std::vector<float4> nodes_oct;   // 8 octant copies of `nodes` (DevScene::nodes_oct), LDS plan scenes only
     std::vector<double4> tris64, tshade64, tnorm64, spheres64;   // fp64 records (DevScene::tris64 ...)
     bool has4 = false;           // nodes4 / root4 usable
-    int width = 4;               // nodes4 holds 4-wide (4 uint4 / node) or 8-wide (8 uint4 / node) nodes
     int root4 = 0, depth4 = 0;
     std::vector<int> smat, lights, list;
     std::vector<int> tri_view;      // device triangle id -> scene-view triangle (DevScene::tri_view)
@@ -1238,23 +1202,6 @@ static int min_desc(bool lds_scene)
 // Triangles per leaf: FRT_LEAF_SIZE overrides (1 = the reference's one-prim
 // leaves), else 0 = by plan (see flatten_scene).  A tuning knob of this
 // library, not part of the C-ABI.
-// Width of the HBM plans' wide tree: FRT_WIDE=8 builds the 8-wide nodes of
-// bvh8_step instead of BVH4Q (read at upload; an A/B knob, not part of the C-ABI).
-static int wide_override()
-{
-    const char *e = std::getenv("FRT_WIDE");
-    return e && std::atoi(e) == 8 ? 8 : 4;
-}
-// Order of the wide nodes in memory (FRT_NODE_ORDER, read at upload; an A/B
-// knob, not part of the C-ABI): 0 = depth-first pre-order (a node's first
-// interior child follows it), 1 = sibling blocks (a node's interior children
-// take consecutive indices, the blocks laid out depth-first), 2 = breadth-first.
-// Only addresses change: hits are the same (t, DFS rank) minimum in every order.
-static int node_order_override()
-{
-    const char *e = std::getenv("FRT_NODE_ORDER");
-    return e ? std::min(std::max(std::atoi(e), 0), 2) : 0;
-}
 static int leaf_size_override()
 {
     const char *e = std::getenv("FRT_LEAF_SIZE");
@@ -1323,16 +1270,13 @@ static void collapse_leaves(FlatScene &F, int leaf_max)
 // repeatedly opens the interior child of largest surface area until it holds
 // four.  Child boxes are the binary tree's padded fp32 boxes quantized to 8
 // bits per plane on a per-node power-of-two grid, rounded outward.  Nodes in
-// pre-order.  Returns false (no BVH4; the binary tree is used) when a node's
-// grid would overflow the slab arithmetic.
-// W = 4: BVH4Q (bvh4_step), 4 uint4 per node.  W = 8: the 8-wide nodes of
-// bvh8_step, 8 uint4 per node (6 used), children in octant slots.
-template <int W>
-static bool build_wide(FlatScene &F, int root_ref)
+// depth-first pre-order (a node's first interior child follows it; sibling
+// blocks and a breadth-first order measured the same).
+// Returns false (no BVH4; the binary tree is used) when a node's grid would
+// overflow the slab arithmetic.
+static bool build_bvh4(FlatScene &F, int root_ref)
 {
-    constexpr int NU = W == 4 ? 4 : 8;                // uint4 per node
     F.nodes4.clear();
-    F.width = W;
     F.depth4 = 0;
     F.root4 = root_ref;
     const int nn = (int)(F.nodes.size() / 4);
@@ -1358,26 +1302,21 @@ static bool build_wide(FlatScene &F, int root_ref)
     // answer, and needs no per-child ref compare in the node loop (that
     // compare cost 2 % on cornell_1m).
     const uint32_t empty_ref = (uint32_t)~(F.tris.empty() ? FRT_PRIM_SPHERE : 0);
-    // binary node, wide parent (-1 root), child slot, level, own index (orders 1 and 2)
-    struct Item { int bin, parent, slot, lvl, me; };
-    const int order = node_order_override();
-    std::vector<Item> st{{root_ref, -1, 0, 1, 0}};
-    size_t head = 0;                                   // breadth-first: st is the queue
-    int next_free = 1;
-    while (order == 2 ? head < st.size() : !st.empty()) {
-        const Item it = order == 2 ? st[head++] : st.back();
-        if (order != 2) st.pop_back();
-        const int me = order == 0 ? (int)(F.nodes4.size() / NU) : it.me;
-        if (order == 0 && it.parent >= 0) {
-            uint4 &r = F.nodes4[NU * it.parent + 1 + it.slot / 4];
-            const int q = it.slot & 3;
-            (q == 0 ? r.x : q == 1 ? r.y : q == 2 ? r.z : r.w) = (uint32_t)me;
+    struct Item { int bin, parent, slot, lvl; };   // binary node, wide parent (-1 root), child slot, level
+    std::vector<Item> st{{root_ref, -1, 0, 1}};
+    while (!st.empty()) {
+        const Item it = st.back();
+        st.pop_back();
+        const int me = (int)(F.nodes4.size() / 4);
+        if (it.parent >= 0) {
+            uint4 &r = F.nodes4[4 * it.parent + 1];
+            (it.slot == 0 ? r.x : it.slot == 1 ? r.y : it.slot == 2 ? r.z : r.w) = (uint32_t)me;
         }
         F.depth4 = std::max(F.depth4, it.lvl);
-        Child ch[W];
+        Child ch[4];
         int n = 2;
         kids(it.bin, ch);
-        while (n < W) {                                // open the largest interior child
+        while (n < 4) {                                // open the largest interior child
             int best = -1;
             double best_a = -1.0;
             for (int k = 0; k < n; ++k)
@@ -1390,37 +1329,10 @@ static bool build_wide(FlatScene &F, int root_ref)
             ch[best + 1] = two[1];
             ++n;
         }
-        // slot k of the node: child ch[kid[k]], or empty (-1)
-        int kid[W];
-        for (int k = 0; k < W; ++k) kid[k] = k < n ? k : -1;
-        if constexpr (W == 8) {
-            // octant slots (bvh8_step): child k goes to the slot whose octant of the
-            // node's centre best matches its box centre; greedy over (cost, k, s)
-            double cc[W][3];
-            for (int a = 0; a < 3; ++a) {
-                float lo = ch[0].lo[a], hi = ch[0].hi[a];
-                for (int k = 1; k < n; ++k) { lo = std::min(lo, ch[k].lo[a]); hi = std::max(hi, ch[k].hi[a]); }
-                const double cen = 0.5 * ((double)lo + (double)hi);
-                for (int k = 0; k < n; ++k) cc[k][a] = 0.5 * ((double)ch[k].lo[a] + (double)ch[k].hi[a]) - cen;
-            }
-            struct Cand { double cost; int k, s; };
-            std::vector<Cand> cand;
-            for (int k = 0; k < n; ++k)
-                for (int sl = 0; sl < W; ++sl) {
-                    double c = 0.0;
-                    for (int a = 0; a < 3; ++a) c -= ((sl >> a) & 1) ? cc[k][a] : -cc[k][a];
-                    cand.push_back({c, k, sl});
-                }
-            std::stable_sort(cand.begin(), cand.end(), [](const Cand &x, const Cand &y) { return x.cost < y.cost; });
-            bool placed[W];
-            for (int k = 0; k < W; ++k) { placed[k] = false; kid[k] = -1; }
-            for (const Cand &q : cand)
-                if (!placed[q.k] && kid[q.s] < 0) { placed[q.k] = true; kid[q.s] = q.k; }
-        }
         // per-axis grid: origin = min child lo, step 2^e with every plane within 255 steps
         float org[3];
         int ex[3];
-        uint64_t qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
+        uint32_t qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
         for (int a = 0; a < 3; ++a) {
             float lo = ch[0].lo[a], hi = ch[0].hi[a];
             for (int k = 1; k < n; ++k) { lo = std::min(lo, ch[k].lo[a]); hi = std::max(hi, ch[k].hi[a]); }
@@ -1436,10 +1348,10 @@ static bool build_wide(FlatScene &F, int root_ref)
             if (e < -100) return false;                // 2^e / |d| must stay a normal float for the empty-slot
                                                        // test (padded boxes are never this thin)
             ex[a] = e;
-            for (int s = 0; s < W; ++s) {
+            for (int s = 0; s < 4; ++s) {
                 double ql = 255.0, qh = 0.0;           // empty slot: the inverted box
-                if (kid[s] >= 0) {
-                    const Child &c = ch[kid[s]];
+                if (s < n) {
+                    const Child &c = ch[s];
                     ql = std::floor(((double)c.lo[a] - lo) / std::ldexp(1.0, e));
                     qh = std::ceil(((double)c.hi[a] - lo) / std::ldexp(1.0, e));
                     ql = std::min(std::max(ql, 0.0), 255.0);
@@ -1448,43 +1360,21 @@ static bool build_wide(FlatScene &F, int root_ref)
                     while (ql > 0.0 && (double)lo + ql * std::ldexp(1.0, e) > (double)c.lo[a]) ql -= 1.0;
                     while (qh < 255.0 && (double)lo + qh * std::ldexp(1.0, e) < (double)c.hi[a]) qh += 1.0;
                 }
-                qlo[a] |= (uint64_t)ql << (8 * s);
-                qhi[a] |= (uint64_t)qh << (8 * s);
+                qlo[a] |= (uint32_t)ql << (8 * s);
+                qhi[a] |= (uint32_t)qh << (8 * s);
             }
         }
-        uint32_t refs[W];
-        int own[W];                                    // orders 1 and 2: the interior children's indices
-        for (int s = 0; s < W; ++s) {
-            refs[s] = kid[s] >= 0 ? (uint32_t)ch[kid[s]].ref : empty_ref;
-            own[s] = -1;
-            if (order != 0 && kid[s] >= 0 && ch[kid[s]].ref >= 0) { own[s] = next_free++; refs[s] = (uint32_t)own[s]; }
-        }
-        if (F.nodes4.size() < (size_t)(me + 1) * NU) F.nodes4.resize((size_t)(me + 1) * NU);
-        uint4 *out = F.nodes4.data() + (size_t)me * NU;
-        uint4 w0;
-        w0.x = (uint32_t)f2i(org[0]); w0.y = (uint32_t)f2i(org[1]); w0.z = (uint32_t)f2i(org[2]);
-        w0.w = (uint32_t)(ex[0] + 127) | ((uint32_t)(ex[1] + 127) << 8) | ((uint32_t)(ex[2] + 127) << 16);
-        out[0] = w0;
-        if constexpr (W == 4) {
-            out[1] = make_uint4(refs[0], refs[1], refs[2], refs[3]);
-            out[2] = make_uint4((uint32_t)qlo[0], (uint32_t)qhi[0], (uint32_t)qlo[1], (uint32_t)qhi[1]);
-            out[3] = make_uint4((uint32_t)qlo[2], (uint32_t)qhi[2], 0u, 0u);
-        } else {   // refs 0-3 | 4-7, then per axis (lo 0-3, lo 4-7, hi 0-3, hi 4-7), padding to 128 B
-            out[1] = make_uint4(refs[0], refs[1], refs[2], refs[3]);
-            out[2] = make_uint4(refs[4], refs[5], refs[6], refs[7]);
-            for (int a = 0; a < 3; ++a)
-                out[3 + a] = make_uint4((uint32_t)qlo[a], (uint32_t)(qlo[a] >> 32), (uint32_t)qhi[a],
-                                        (uint32_t)(qhi[a] >> 32));
-            out[6] = make_uint4(0u, 0u, 0u, 0u);
-            out[7] = make_uint4(0u, 0u, 0u, 0u);
-        }
-        if (order == 2) {                               // interior children, slot order (queue)
-            for (int s = 0; s < W; ++s)
-                if (own[s] >= 0) st.push_back({ch[kid[s]].ref, me, s, it.lvl + 1, own[s]});
-        } else {                                        // pre-order (first slot next)
-            for (int s = W - 1; s >= 0; --s)
-                if (kid[s] >= 0 && ch[kid[s]].ref >= 0) st.push_back({ch[kid[s]].ref, me, s, it.lvl + 1, own[s]});
-        }
+        uint32_t refs[4];
+        for (int s = 0; s < 4; ++s) refs[s] = s < n ? (uint32_t)ch[s].ref : empty_ref;
+        F.nodes4.resize((size_t)(me + 1) * 4);
+        uint4 *out = F.nodes4.data() + (size_t)me * 4;
+        out[0] = make_uint4((uint32_t)f2i(org[0]), (uint32_t)f2i(org[1]), (uint32_t)f2i(org[2]),
+                            (uint32_t)(ex[0] + 127) | ((uint32_t)(ex[1] + 127) << 8) | ((uint32_t)(ex[2] + 127) << 16));
+        out[1] = make_uint4(refs[0], refs[1], refs[2], refs[3]);
+        out[2] = make_uint4(qlo[0], qhi[0], qlo[1], qhi[1]);
+        out[3] = make_uint4(qlo[2], qhi[2], 0u, 0u);
+        for (int s = n - 1; s >= 0; --s)               // pre-order: the first slot next
+            if (ch[s].ref >= 0) st.push_back({ch[s].ref, me, s, it.lvl + 1});
     }
     F.root4 = 0;
     return true;
@@ -1781,8 +1671,7 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
             d[3] = n[3];
         }
     S.root = (sv->world_kind == FRT_WORLD_BVH) ? ((sv->root >= 0) ? 0 : ~dev_ref(~sv->root)) : 0;
-    F.has4 = sv->world_kind == FRT_WORLD_BVH &&
-             (wide_override() == 8 ? build_wide<8>(F, S.root) : build_wide<4>(F, S.root));
+    F.has4 = sv->world_kind == FRT_WORLD_BVH && build_bvh4(F, S.root);
     if (!F.has4) F.nodes4.clear();
     S.root4 = F.has4 ? F.root4 : S.root;
     S.n_lights = sv->n_lights;
@@ -1790,7 +1679,7 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     S.n_nodes = (int)(F.nodes.size() / 4);
     S.n_tris = nt;
     S.n_mats = nm;
-    S.n_nodes4 = (int)(F.nodes4.size() / (F.width == 8 ? 8 : 4));
+    S.n_nodes4 = (int)(F.nodes4.size() / 4);
     S.node_es = 4; S.node_ps = 1;
     S.node4_es = 4; S.node4_ps = 1;
     S.tri_es = 3; S.tri_ps = 1;
@@ -1854,8 +1743,7 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
         return rc;
     c->world_kind = S.world_kind;
     c->stack_needed = F.depth;
-    c->has_bvh4 = F.has4 && F.width == 4;
-    c->has_bvh8 = F.has4 && F.width == 8;
+    c->has_bvh4 = F.has4;
     c->n_tris = S.n_tris;
     c->n_spheres = (int)F.spheres.size();
     c->has_spec_mats = false;
@@ -1871,7 +1759,6 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
     c->has_spec_mats = c->mats != kMatsNone;
     c->depth4 = F.depth4;
     c->scene_lds_bytes = sizeof(float4) * (F.nodes.size() + F.tris.size() + F.tshade.size() + F.mats.size());
-    c->scene_lds_bytes4 = sizeof(float4) * (F.nodes4.size() + F.tris.size() + F.tshade.size() + F.mats.size());
     c->scene_lds_bytes_oct = F.nodes_oct.empty() ? SIZE_MAX
                              : sizeof(float4) * (F.nodes_oct.size() + F.tris.size() + F.tshade.size() + F.mats.size());
     c->has_f64 = want_f64;
@@ -1899,7 +1786,7 @@ static DevScene host_scene(const FlatScene &F)
 // the self-test's per-pixel loop in precision R (fp64: the binary tree or the list)
 template <typename R>
 static void selftest_pixels(const DevScene &S, const FlatScene &F, const frt_render_params *p, const int32_t *pixels,
-                            int npix, bool brute, bool wide, std::vector<int> &stack, float *out_rgb, uint64_t cnt[3])
+                            int npix, bool wide, std::vector<int> &stack, float *out_rgb, uint64_t cnt[3])
 {
     uint32_t n_ext = 0, n_sh = 0;
     for (int i = 0; i < npix; ++i) {
@@ -1912,16 +1799,11 @@ static void selftest_pixels(const DevScene &S, const FlatScene &F, const frt_ren
             ++cnt[0];
             for (;;) {
                 Hit<R> h;
-                if (brute) {
-                    Trav<R> T;
-                    if (trav_begin(T, S, S.root, P.ro, P.rd, P.rtmax)) brute_all(T, S, P.ro, P.rd, P.shadow);
-                    h = T.h;
-                } else if (S.world_kind == FRT_WORLD_LIST) {
+                if (S.world_kind == FRT_WORLD_LIST) {
                     h = trace<FRT_WORLD_LIST, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data());
                 } else if constexpr (!kIsF64<R>) {
-                    h = wide && F.width == 8 ? trace<kWorldBvh8, 1, kSelftestStack>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data())
-                        : wide ? trace<kWorldBvh4, 1, kSelftestStack>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data())
-                               : trace<FRT_WORLD_BVH, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data());
+                    h = wide ? trace<kWorldBvh4, 1, kSelftestStack>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data())
+                             : trace<FRT_WORLD_BVH, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data());
                 } else {
                     h = trace<FRT_WORLD_BVH, 1>(S, P.ro, P.rd, P.rtmax, P.shadow, stack.data());
                 }
@@ -1959,12 +1841,11 @@ extern "C" int frt_selftest_path_host(const frt_scene_view *sv, const frt_render
             if (sv->materials[i].type == FRT_MAT_METAL) return FRT_E_UNSUPPORTED;
     const DevScene S = host_scene(F);
     std::vector<int> stack(std::max(F.depth + 1, kSelftestStack));
-    const bool brute = !f64 && S.world_kind == FRT_WORLD_BVH && (p->flags & FRT_FLAG_BRUTE) && F.spheres.empty();
-    const bool wide = !f64 && !brute && S.world_kind == FRT_WORLD_BVH && F.has4 && !(p->flags & FRT_FLAG_BVH2) &&
-                      (F.width == 8 ? bvh8_stack_fits(F.depth4, kSelftestStack) : bvh4_stack_fits(F.depth4, kSelftestStack));
+    const bool wide = !f64 && S.world_kind == FRT_WORLD_BVH && F.has4 && !(p->flags & FRT_FLAG_BVH2) &&
+                      bvh4_stack_fits(F.depth4, kSelftestStack);
     uint64_t cnt[3] = {0, 0, 0};   // camera, extension, shadow
-    if (f64) selftest_pixels<double>(S, F, p, pixels, npix, brute, wide, stack, out_rgb, cnt);
-    else selftest_pixels<float>(S, F, p, pixels, npix, brute, wide, stack, out_rgb, cnt);
+    if (f64) selftest_pixels<double>(S, F, p, pixels, npix, wide, stack, out_rgb, cnt);
+    else selftest_pixels<float>(S, F, p, pixels, npix, wide, stack, out_rgb, cnt);
     if (st) {
         memset(st, 0, sizeof(*st));
         st->camera_rays = cnt[0]; st->extension_rays = cnt[1]; st->shadow_rays = cnt[2];
@@ -2074,7 +1955,7 @@ static int pick_launcher(const frt_ctx *c, int integrator, int flags, Launcher &
     if (integrator == FRT_INTEGRATOR_AO || c->mats != kMatsNone || (f64 && c->world_kind != FRT_WORLD_LIST))
         return frt_mats::pick(c, integrator, flags, f64, L);   // every kernel with a material set
     if (f64) {   // a lambertian list world (BVH worlds' fp64 kernels carry every material: the other unit)
-        L = make_launcher<16, FRT_WORLD_LIST, false, 1, false, kMatsNone, FRT_INTEGRATOR_PATH, double>(0);
+        L = make_launcher<16, FRT_WORLD_LIST, false, 1, kMatsNone, FRT_INTEGRATOR_PATH, double>(0);
         return FRT_OK;
     }
     return pick_launcher_t<kMatsNone>(c, flags, L);
@@ -2139,7 +2020,6 @@ extern "C" int frt_trace_device(frt_ctx *c, const float *rays, int64_t n, float 
 {
     const auto t_start = std::chrono::steady_clock::now();
     if (!c || n < 0 || (n > 0 && (!rays || !hits))) return FRT_E_INVALID;
-    if (n >= (int64_t)0xffffffffLL) return set_err(c, FRT_E_UNSUPPORTED, "frt_trace_device: more than 2^32 - 1 rays");
     if (!c->have_scene) return set_err(c, FRT_E_NO_SCENE, "no scene uploaded");
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t stream = hip_stream ? (hipStream_t)hip_stream : c->stream;
@@ -2149,13 +2029,19 @@ extern "C" int frt_trace_device(frt_ctx *c, const float *rays, int64_t n, float 
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, L.fn, kBlock, L.lds) != hipSuccess || bpc <= 0) bpc = 1;
     const int64_t want = std::max<int64_t>(1, (n + kBlock - 1) / kBlock);
     const int grid = (int)std::min<int64_t>((int64_t)c->n_cu * bpc, want);
+    // the 32-bit ray-queue head runs past n by up to one chunk per wave
+    // (render_impl has the same headroom check)
+    if (n + (int64_t)(grid * kBlock / 64) * kTraceChunk >= (int64_t)0xffffffffLL)
+        return set_err(c, FRT_E_UNSUPPORTED, "frt_trace_device: too many rays for one call (2^32 - 1 less the queue headroom)");
     DevRays R{};
     R.ray = reinterpret_cast<const float4 *>(rays);
     R.hit = reinterpret_cast<float4 *>(hits);
     R.n = (uint32_t)n;
     R.min_desc = min_desc(L.lds_scene);
-    R.counter = c->counter;
-    HIPCHK(c, hipMemsetAsync(c->counter, 0, 64, stream));
+    // its own queue word, a cache line away from the render queue's: a trace and
+    // a render of one context on two streams do not share a queue head
+    R.counter = c->counter + kTraceCounterWord;
+    HIPCHK(c, hipMemsetAsync(R.counter, 0, sizeof(unsigned), stream));
     HIPCHK(c, hipEventRecord(c->ev0, stream));
     if (n > 0) {
         DevScene Sarg = c->S;
@@ -2312,6 +2198,50 @@ extern "C" int frt_diag_read(unsigned long long *out)
 }
 #endif
 
+// Work granule of a path / AO / normals render: the frame's samples cut into
+// n_chunks chunks of spi samples (the last one shorter), k = n_chunks chosen
+// for at least about 40 items per resident lane and at most `target` samples
+// an item (about 150 rays: path 24, AO 96, normals 128).  With one queue
+// atomic per refill the first rule alone was best (Cornell 512 spp at 5-6
+// chunks, profiles/r03/samecall/spi_*.jsonl); with 64-item grabs smaller items
+// pay: Cornell 512 spp 289.7 ms at 6 chunks, 281.9 at 23 (flat from 16 to 64
+// chunks), cornell_1m 824.1 -> 810.0 ms, while AO stays best at 6 chunks (1.5
+// rays a sample; profiles/r03/samecall/grab64_spi_*.jsonl).  The target rule
+// grows k with spp, so it is capped at kMaxItemsPerLane items per resident
+// lane: the (chunk, slot) partial sums, 12 B an item, stay below
+// ~1 GB at any spp (1080p 512 spp keeps its 22 chunks, 550 MB), and frames
+// of any spp fit the 32-bit queue.  FRT_SPI_TARGET overrides the target (0:
+// the first rule alone; A/B knob).  spi_req > 0: the caller's samples per item.
+constexpr double kMaxItemsPerLane = 192.0;
+static void work_granule(int integrator, int spp, uint64_t n_slots, long long lanes, int spi_req, int &spi,
+                         int &n_chunks)
+{
+    spi = spi_req;
+    if (spi <= 0) {
+        const char *tgt = std::getenv("FRT_SPI_TARGET");
+        const int target = tgt ? std::atoi(tgt)
+                               : integrator == FRT_INTEGRATOR_PATH ? 24 : integrator == FRT_INTEGRATOR_AO ? 96 : 128;
+        const double slots = std::max((double)n_slots, 1.0);
+        const double k_lanes = std::max(1.0, std::round(40.0 * (double)lanes / slots));
+        double k = k_lanes;
+        if (target > 0) {
+            const double k_cap = std::max(k_lanes, std::floor(kMaxItemsPerLane * (double)lanes / slots));
+            k = std::max(k, std::min(std::ceil((double)spp / (double)target), k_cap));
+        }
+        spi = (int)std::ceil((double)spp / k);
+    }
+    spi = std::max(1, std::min(spi, spp));
+    n_chunks = (spp + spi - 1) / spi;
+}
+// the granule rule for host tests (CPU): internal to libfrt.so, not in include/frt.h
+extern "C" int frt_internal_work_granule(int integrator, int spp, int64_t n_slots, int64_t lanes, int spi_req,
+                                         int *spi, int *n_chunks)
+{
+    if (spp <= 0 || n_slots < 0 || lanes <= 0 || !spi || !n_chunks) return FRT_E_INVALID;
+    work_granule(integrator, spp, (uint64_t)n_slots, (long long)lanes, spi_req, *spi, *n_chunks);
+    return FRT_OK;
+}
+
 static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots, hipStream_t st, frt_stats *stats)
 {
     const auto t_start = std::chrono::steady_clock::now();
@@ -2337,33 +2267,8 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, L.fn, kBlock, L.lds) != hipSuccess || bpc <= 0) bpc = 1;
     const int grid = c->n_cu * bpc;
     const long long lanes = (long long)grid * kBlock;
-    // work granule: the frame's samples cut into k chunks of equal length, k
-    // chosen for at least about 40 items per resident lane and at most
-    // `target` samples an item (about 150 rays: path 24, AO 96, normals 128).
-    // With one queue atomic per refill the first rule alone was best (Cornell
-    // 512 spp at 5-6 chunks, profiles/r03/samecall/spi_*.jsonl); with 64-item
-    // grabs smaller items pay: Cornell 512 spp 289.7 ms at 6 chunks, 281.9 at
-    // 23 (flat from 16 to 64 chunks), cornell_1m 824.1 -> 810.0 ms, while AO
-    // stays best at 6 chunks (1.5 rays a sample; profiles/r03/samecall/grab64_spi_*.jsonl).
-    // FRT_SPI_TARGET overrides the target (0: the first rule alone; A/B knob).
-    int spi = p->samples_per_item;
-    if (spi <= 0) {
-        const char *st = std::getenv("FRT_SPI_TARGET");
-        const int target = st ? std::atoi(st)
-                              : p->integrator == FRT_INTEGRATOR_PATH ? 24 : p->integrator == FRT_INTEGRATOR_AO ? 96 : 128;
-        double k = std::max(1.0, std::round(40.0 * (double)lanes / std::max((double)n_slots, 1.0)));
-        if (target > 0) k = std::max(k, std::ceil((double)p->spp / (double)target));
-        spi = (int)std::ceil((double)p->spp / k);
-        spi = std::max(1, std::min(spi, p->spp));
-    }
-    spi = std::min(spi, p->spp);
-    // FRT_GRANULE=guided (A/B knob): chunk-major items whose lengths fall
-    // linearly, so the last items handed out are the shortest
-    const char *ge = std::getenv("FRT_GRANULE");
-    const bool guided = ge && std::strcmp(ge, "guided") == 0 && p->samples_per_item <= 0;
-    const char *gk = guided ? std::getenv("FRT_GUIDED_CHUNKS") : nullptr;
-    const int n_chunks = guided ? std::min(p->spp, std::max(1, gk ? std::atoi(gk) : (p->spp + spi - 1) / spi))
-                                : (p->spp + spi - 1) / spi;
+    int spi = 0, n_chunks = 0;
+    work_granule(p->integrator, p->spp, n_slots, lanes, p->samples_per_item, spi, n_chunks);
     const unsigned long long n_items = (unsigned long long)n_slots * n_chunks;
     // queue grab: items a wave takes per atomic (FRT_GRAB: A/B knob, not part of the C-ABI)
     const char *gb = std::getenv("FRT_GRAB");
@@ -2392,7 +2297,6 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     W.tile = T; W.ntx = (p->nx + T - 1) / T; W.shard_index = p->shard_index; W.shard_count = p->shard_count;
     W.spi = spi; W.n_chunks = n_chunks; W.n_items = (uint32_t)n_items; W.n_slots = n_slots;
     W.grab = grab;
-    W.guided = guided ? 1 : 0; W.n_tiles = nmt;
     W.partial = c->partial; W.counter = c->counter; W.wave_rays = c->wave_rays;
     W.trav_min = trav_min(L.lds_scene, p->integrator == FRT_INTEGRATOR_PATH);
     W.min_desc = min_desc(L.lds_scene);

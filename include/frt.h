@@ -56,9 +56,8 @@ enum { FRT_FLAG_NO_LDS_SCENE = 1,      /* render_params.flags: keep small scenes
        FRT_FLAG_WAVES6 = 4,            /* register cap for 6 waves/SIMD (A/B timing)                     */
        FRT_FLAG_WAVES4 = 8,            /* the compiler's own allocation, ~4 waves/SIMD (A/B timing)      */
        FRT_FLAG_BVH2 = 16,             /* binary nodes for HBM-resident scenes (A/B timing, self-test)   */
-       FRT_FLAG_BVH4 = 32,             /* 4-wide nodes for LDS-resident scenes too (A/B timing)          */
-       FRT_FLAG_BRUTE = 64,            /* tiny LDS scenes: every triangle in lockstep (A/B timing)       */
-       FRT_FLAG_SPEC = 128,            /* speculative traversal: 4-wide HBM plan, binary LDS plan (A/B)  */
+       /* 32, 64, 128: retired A/B plans (4-wide nodes from LDS, lockstep brute force,
+          speculative traversal), measured slower and removed in round 4; the bits are ignored */
        FRT_FLAG_NO_OCT = 256,          /* LDS binary plan without the per-octant node copies (A/B timing) */
        FRT_FLAG_FP64 = 512,            /* path: the fp64 kernel for this call (self-test: fp64 host replay) */
        FRT_FLAG_FP32 = 1024 };         /* path: the fp32 kernels even where the precision picks fp64      */
@@ -253,7 +252,11 @@ int frt_render_device(frt_ctx *ctx, const frt_render_params *p, float *slots_rgb
  * as int32 bits: the scene view's triangle index or FRT_PRIM_SPHERE | k, -1 =
  * miss; a miss leaves t = t_max).  flags: FRT_FLAG_NO_LDS_SCENE / _BVH2 /
  * _NO_OCT choose the plan as for frt_render.  Returns after the work has
- * completed on `hip_stream` (NULL = the context's stream); st->kernel_ms. */
+ * completed on `hip_stream` (NULL = the context's stream); st->kernel_ms.
+ * The ray queue has its own word in the context, apart from the render's, but
+ * a context is still one stream's worth of state: calls on one context are
+ * issued from one host thread, one at a time (each returns when its work is
+ * done).  n plus a chunk of 256 rays per resident wave must stay below 2^32. */
 int frt_trace_device(frt_ctx *ctx, const float *rays, int64_t n, float *hits, int flags, void *hip_stream,
                      frt_stats *st);
 

@@ -55,6 +55,9 @@ def lib():
         L.ora_render_integrator.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_void_p, ctypes.POINTER(Counters)]
+        L.ora_render_depth.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_void_p, ctypes.POINTER(Counters)]
         L.ora_scene_set_env.argtypes = [ctypes.c_void_p, dp]
         L.ora_scene_set_env.restype = None
         L.ora_scene_ao_tmax.argtypes = [ctypes.c_void_p]
@@ -250,17 +253,18 @@ class OracleScene:
     def ao_tmax(self):
         return lib().ora_scene_ao_tmax(self.ptr)
 
-    def render(self, nx, ny, spp, seed=0, pixels=None, nthreads=None, integrator=0):
+    def render(self, nx, ny, spp, seed=0, pixels=None, nthreads=None, integrator=0, max_depth=33):
         """Mean radiance per pixel (viewer::add_sample semantics) + counters.
-        integrator: 0 path (path.cpp), 2 ao (ao.cpp), 3 normals (debug_renderer.h)."""
+        integrator: 0 path (path.cpp), 2 ao (ao.cpp), 3 normals (debug_renderer.h).
+        max_depth: path::Li's depth cap (path.cpp:36)."""
         if pixels is None:
             pixels = np.arange(nx * ny, dtype=np.int32)
         pixels = np.ascontiguousarray(pixels, dtype=np.int32)
         out = np.zeros((len(pixels), 3))
         cnt = Counters()
         nthreads = nthreads or min(16, os.cpu_count() or 1)
-        rc = lib().ora_render_integrator(self.ptr, integrator, nx, ny, spp, seed, pixels.ctypes.data, len(pixels),
-                                         nthreads, out.ctypes.data, ctypes.byref(cnt))
+        rc = lib().ora_render_depth(self.ptr, integrator, nx, ny, spp, seed, max_depth, pixels.ctypes.data,
+                                    len(pixels), nthreads, out.ctypes.data, ctypes.byref(cnt))
         if rc != 0:
             raise RuntimeError(f"ora_render failed: {rc}")
         return out, cnt

@@ -921,7 +921,7 @@ static inline int pick_sample(double sample, int list_size)
     return index;
 }
 
-typedef struct { const ora_scene *s; rng_key key; ora_counters *cnt; } li_ctx;
+typedef struct { const ora_scene *s; rng_key key; ora_counters *cnt; int max_depth; } li_ctx;   /* max_depth: 33 in path.cpp:36 */
 
 /* path::Li (path.cpp:4-116), recursive like the reference so the
  * association order of every product/sum matches.  Materials: lambertian,
@@ -948,7 +948,7 @@ static v3 Li(li_ctx *c, const ray *r, int depth, const hit_record *prev, double 
         material mtex;
         const material *m = mat_at(s, &hrec, &mtex);
         /* lambertian / modified_phong / dielectric::scatter succeed; diffuse_light's fails (material.h) */
-        if (depth <= 33 && mat_scatters(m->type)) {
+        if (depth <= c->max_depth && mat_scatters(m->type)) {
             const uint32_t base = DIM_BOUNCE(depth);
             const int specular = m->type != MAT_LAMBERT;
             const v3 wi = vneg(unit(r->d));                   /* hrec.wi (triangle.h:108, sphere.h:47) */
@@ -1078,13 +1078,13 @@ static v3 normals_Li(li_ctx *c, const ray *r)
 
 /* one pixel, path.cpp:120-143 (loop over s, add_sample divides by ns: *= 1/ns);
  * ao.h:15-38 and debug_renderer.h:19-45 are the same loop around their Li */
-static void render_pixel(const ora_scene *s, int kind, int nx, int ny, int spp, uint32_t seed, int x, int y,
-                         double *out, ora_counters *cnt)
+static void render_pixel(const ora_scene *s, int kind, int nx, int ny, int spp, uint32_t seed, int max_depth, int x,
+                         int y, double *out, ora_counters *cnt)
 {
     v3 col = mk(0.0, 0.0, 0.0);
     const uint32_t pixel = (uint32_t)y * (uint32_t)nx + (uint32_t)x;
     for (int smp = 0; smp < spp; ++smp) {
-        li_ctx c; c.s = s; c.cnt = cnt; c.key = rng_make(seed, pixel, (uint32_t)smp);
+        li_ctx c; c.s = s; c.cnt = cnt; c.key = rng_make(seed, pixel, (uint32_t)smp); c.max_depth = max_depth;
         double u = (double)(x + rng_u(c.key, 0)) / (double)nx;
         double v = (double)(y + rng_u(c.key, 1)) / (double)ny;
         ray r = camera_get_ray(&s->cam, u, v, rng_u(c.key, 2), rng_u(c.key, 3));
@@ -1100,7 +1100,7 @@ static void render_pixel(const ora_scene *s, int kind, int nx, int ny, int spp, 
 }
 
 typedef struct {
-    const ora_scene *s; int kind, nx, ny, spp; uint32_t seed;
+    const ora_scene *s; int kind, nx, ny, spp, max_depth; uint32_t seed;
     const int32_t *pixels; int npix; int tid, nth;
     double *out; ora_counters cnt;
 } job;
@@ -1110,7 +1110,8 @@ static void *render_worker(void *arg)
     memset(&j->cnt, 0, sizeof(j->cnt));
     for (int i = j->tid; i < j->npix; i += j->nth) {
         int p = j->pixels[i];
-        render_pixel(j->s, j->kind, j->nx, j->ny, j->spp, j->seed, p % j->nx, p / j->nx, &j->out[3 * (size_t)i], &j->cnt);
+        render_pixel(j->s, j->kind, j->nx, j->ny, j->spp, j->seed, j->max_depth, p % j->nx, p / j->nx,
+                     &j->out[3 * (size_t)i], &j->cnt);
     }
     return NULL;
 }
@@ -1121,6 +1122,13 @@ int ora_render(const ora_scene *s, int nx, int ny, int spp, uint32_t seed, const
 }
 int ora_render_integrator(const ora_scene *s, int kind, int nx, int ny, int spp, uint32_t seed,
                           const int32_t *pixels, int npix, int nthreads, double *out_rgb, ora_counters *cnt)
+{
+    return ora_render_depth(s, kind, nx, ny, spp, seed, 33, pixels, npix, nthreads, out_rgb, cnt);
+}
+/* the same with path::Li's depth cap as a parameter (33 in path.cpp:36; the PSS-MLT
+ * comparison uses pssmlt's MaxPathLength 10, pssmlt.h) */
+int ora_render_depth(const ora_scene *s, int kind, int nx, int ny, int spp, uint32_t seed, int max_depth,
+                     const int32_t *pixels, int npix, int nthreads, double *out_rgb, ora_counters *cnt)
 {
     if (!s || nx <= 0 || ny <= 0 || spp <= 0 || npix < 0) return -1;
     if (kind != ORA_INTEGRATOR_PATH && kind != ORA_INTEGRATOR_AO && kind != ORA_INTEGRATOR_NORMALS) return -3;
@@ -1134,6 +1142,7 @@ int ora_render_integrator(const ora_scene *s, int kind, int nx, int ny, int spp,
     pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
     for (int t = 0; t < nthreads; ++t) {
         jobs[t].s = s; jobs[t].kind = kind; jobs[t].nx = nx; jobs[t].ny = ny; jobs[t].spp = spp; jobs[t].seed = seed;
+        jobs[t].max_depth = max_depth;
         jobs[t].pixels = pixels; jobs[t].npix = npix; jobs[t].tid = t; jobs[t].nth = nthreads; jobs[t].out = out_rgb;
         if (nthreads > 1) pthread_create(&th[t], NULL, render_worker, &jobs[t]);
     }

@@ -96,6 +96,10 @@ int  ora_render(const ora_scene *s, int nx, int ny, int spp, uint32_t seed,
 enum { ORA_INTEGRATOR_PATH = 0, ORA_INTEGRATOR_AO = 2, ORA_INTEGRATOR_NORMALS = 3 };
 int  ora_render_integrator(const ora_scene *s, int integrator, int nx, int ny, int spp, uint32_t seed,
                            const int32_t *pixels, int npix, int nthreads, double *out_rgb, ora_counters *cnt);
+/* ... and with path::Li's depth cap (33 in path.cpp:36; MaxPathLength 10 for the
+ * PSS-MLT comparison) */
+int  ora_render_depth(const ora_scene *s, int integrator, int nx, int ny, int spp, uint32_t seed, int max_depth,
+                      const int32_t *pixels, int npix, int nthreads, double *out_rgb, ora_counters *cnt);
 /* constant environment colour (the reference scenes use black) */
 void ora_scene_set_env(ora_scene *s, const double *rgb);
 /* image_texture's decoded image (format 0: nx*ny*3 bytes, sRGB; 1: floats); *index

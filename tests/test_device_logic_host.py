@@ -93,19 +93,13 @@ def test_leaf_size_invariance(kind, objfix, tess, request, tmp_path, monkeypatch
         assert res[leaf][1] == res[1][1]
 
 
-@pytest.mark.parametrize("width,order", [("4", "0"), ("8", "0"), ("4", "1"), ("4", "2"), ("8", "2")])
 @pytest.mark.parametrize("kind,objfix,tess", [("cornell_box_obj", "cornell_obj", 0),
                                               ("cornell_box_obj", "cornell_obj", 12),
                                               ("obj_smooth", "cornell_obj", 5)])
-def test_bvh4_matches_binary(kind, objfix, tess, width, order, request, tmp_path, monkeypatch):
-    """The 4-wide quantized BVH (trace_bvh4) and the 8-wide one with octant-
-    ordered children (trace_bvh8, FRT_WIDE=8), each with an 8-entry stack so
-    the private overflow entries are used, return the binary traversal's hits
-    bit for bit: identical samples and ray counts.  Likewise in every memory
-    order of the wide nodes (FRT_NODE_ORDER: depth-first, sibling blocks,
-    breadth-first), which moves addresses only."""
-    monkeypatch.setenv("FRT_WIDE", width)
-    monkeypatch.setenv("FRT_NODE_ORDER", order)
+def test_bvh4_matches_binary(kind, objfix, tess, request, tmp_path):
+    """The 4-wide quantized BVH (trace_bvh4), with an 8-entry stack so the
+    private overflow entries are used, returns the binary traversal's hits bit
+    for bit: identical samples and ray counts."""
     obj = request.getfixturevalue(objfix)
     if tess:
         obj2 = str(tmp_path / "t.obj")
@@ -119,8 +113,6 @@ def test_bvh4_matches_binary(kind, objfix, tess, width, order, request, tmp_path
     assert np.array_equal(wide, bin2)
     assert st4.rays == st2.rays
     assert st4.stack_entries == 8 and 0 < st4.bvh_depth < st2.bvh_depth   # the wide tree was traversed
-    brute, stb = frt.selftest_path_host(hs, frt.RenderParams.make(nx, ny, 8, seed=13, flags=frt.FRT_FLAG_BRUTE), pix)
-    assert np.array_equal(brute, bin2) and stb.rays == st2.rays                 # every triangle, index order
 
 
 @pytest.mark.parametrize("objfix", ["sphere_obj", "mirror_obj", "glass_obj"])

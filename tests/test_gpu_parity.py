@@ -155,33 +155,28 @@ def test_bvh4_matches_binary(ctx, cornell_obj, tmp_path):
     assert st4.scene_in_lds == 0 and st4.bvh_depth < st2.bvh_depth
     assert np.array_equal(wide, bin2)
     assert st4.rays == st2.rays
-    spec, sts = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21,
-                                                 flags=frt.FRT_FLAG_NO_LDS_SCENE | frt.FRT_FLAG_SPEC))
-    assert np.array_equal(spec, bin2) and sts.rays == st2.rays        # speculative traversal
-    # the 8-wide nodes with octant-ordered children (FRT_WIDE=8 at upload, an A/B plan)
-    import os
-    os.environ["FRT_WIDE"] = "8"
-    try:
-        ctx.upload(frt.HostScene("cornell_box_obj", dst, nx / ny))
-    finally:
-        del os.environ["FRT_WIDE"]
-    w8, st8 = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21, flags=frt.FRT_FLAG_NO_LDS_SCENE))
-    assert 0 < st8.bvh_depth < st4.bvh_depth and np.array_equal(w8, bin2) and st8.rays == st2.rays
-    # small scene: 4-wide nodes from LDS (FRT_FLAG_BVH4) vs the default binary LDS plan
+    # small scene: the default binary LDS plan
     ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, nx / ny))
-    w_lds, stw = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21, flags=frt.FRT_FLAG_BVH4))
     b_lds, stb = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21))
-    assert stw.scene_in_lds == 1 and stb.scene_in_lds == 1 and stw.stack_entries == 8
-    assert np.array_equal(w_lds, b_lds)
+    assert stb.scene_in_lds == 1
     # LDS binary plan: the per-octant node copies (default) vs the (lo, hi) boxes
     noct, stn = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21, flags=frt.FRT_FLAG_NO_OCT))
     assert stn.scene_in_lds == 1 and np.array_equal(noct, b_lds) and stn.rays == stb.rays
-    # LDS binary plan with speculative (parked-leaf) traversal (FRT_FLAG_SPEC)
-    sp_lds, sts2 = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21, flags=frt.FRT_FLAG_SPEC))
-    assert sts2.scene_in_lds == 1 and np.array_equal(sp_lds, b_lds) and sts2.rays == stb.rays
-    # tiny scene: every triangle in lockstep (FRT_FLAG_BRUTE)
-    br, stbr = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=21, flags=frt.FRT_FLAG_BRUTE))
-    assert stbr.scene_in_lds == 1 and np.array_equal(br, b_lds) and stbr.rays == stb.rays
+
+
+def test_lean_plan_rounding(ctx, cornell_obj):
+    """The HBM lambertian plans keep less per-lane state (kLean, frt_render.hip):
+    each radiance contribution is added to the fp32 item sum as it is found,
+    where the LDS plan sums a sample first.  Same rays, same hits, so the films
+    agree to fp32 summation rounding -- pinned here as a tolerance, not
+    bit-equality."""
+    nx, ny, spp = 64, 48, 16
+    ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, nx / ny))
+    lds, st_l = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=23))
+    hbm, st_h = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=23, flags=frt.FRT_FLAG_NO_LDS_SCENE))
+    assert st_l.scene_in_lds == 1 and st_h.scene_in_lds == 0
+    assert st_l.rays == st_h.rays
+    assert np.allclose(lds, hbm, rtol=1e-5, atol=1e-6)
 
 
 @pytest.mark.parametrize("flags", [0, frt.FRT_FLAG_NO_LDS_SCENE, frt.FRT_FLAG_NO_LDS_SCENE | frt.FRT_FLAG_BVH2])

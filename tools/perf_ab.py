@@ -6,7 +6,7 @@ kernel ms and Grays/s as JSON lines.
   python tools/perf_ab.py [--scene cornell|cornell_1m|veach] [--spp 64] [--rounds 5]
                           [--variants default,waves5,default/leaf1]
 
-A variant is FLAG[+FLAG...][/leafN][/wideN][/orderN][/travN][/descN][/granguided][/gkN][/grabN][/sptN]: render flags (travN sets
+A variant is FLAG[+FLAG...][/leafN][/travN][/descN][/grabN][/sptN][/spiN]: render flags (travN sets
 FRT_TRAV_MIN=N, descN FRT_MIN_DESC=N for its renders), on a scene uploaded with
 FRT_LEAF_SIZE=N (one context per leaf size; default = the library default).
 """
@@ -43,7 +43,6 @@ def main():
     kind, obj, name = scene_spec(args.scene, "/tmp")
     names = {"default": 0, "no_lds": frt.FRT_FLAG_NO_LDS_SCENE, "waves4": frt.FRT_FLAG_WAVES4,
              "waves5": frt.FRT_FLAG_WAVES5, "waves6": frt.FRT_FLAG_WAVES6, "bvh2": frt.FRT_FLAG_BVH2,
-             "bvh4": frt.FRT_FLAG_BVH4, "brute": frt.FRT_FLAG_BRUTE, "spec": frt.FRT_FLAG_SPEC,
              "no_oct": frt.FRT_FLAG_NO_OCT}
     flags = {}
     for v in args.variants.split(","):
@@ -71,27 +70,24 @@ def main():
     if env:
         hs.set_env([float(x) for x in env.split(",")])
     ctxs = {}
-    for v in chosen:   # one context per upload-time option (leaf size, wide-tree width)
-        leaf = (opt(v, "leaf"), opt(v, "wide"), opt(v, "order"))
+    for v in chosen:   # one context per upload-time option (leaf size)
+        leaf = opt(v, "leaf")
         if leaf not in ctxs:
-            for val, env in ((leaf[0], "FRT_LEAF_SIZE"), (leaf[1], "FRT_WIDE"), (leaf[2], "FRT_NODE_ORDER")):
-                if val:
-                    os.environ[env] = val
-                else:
-                    os.environ.pop(env, None)
+            if leaf:
+                os.environ["FRT_LEAF_SIZE"] = leaf
+            else:
+                os.environ.pop("FRT_LEAF_SIZE", None)
             ctxs[leaf] = frt.Context(0)
             ctxs[leaf].upload(hs)
     os.environ.pop("FRT_LEAF_SIZE", None)
-    os.environ.pop("FRT_WIDE", None)
-    os.environ.pop("FRT_NODE_ORDER", None)
     res = {v: [] for v in chosen}
     rays = {}
     films = {}
     for r in range(args.rounds + 1):
         for v in chosen:
-            leaf = (opt(v, "leaf"), opt(v, "wide"), opt(v, "order"))
-            for key, env in (("trav", "FRT_TRAV_MIN"), ("desc", "FRT_MIN_DESC"), ("gran", "FRT_GRANULE"),
-                             ("gk", "FRT_GUIDED_CHUNKS"), ("grab", "FRT_GRAB"), ("spt", "FRT_SPI_TARGET")):
+            leaf = opt(v, "leaf")
+            for key, env in (("trav", "FRT_TRAV_MIN"), ("desc", "FRT_MIN_DESC"), ("grab", "FRT_GRAB"),
+                             ("spt", "FRT_SPI_TARGET")):
                 if opt(v, key):
                     os.environ[env] = opt(v, key)
                 else:
@@ -111,7 +107,7 @@ def main():
     if len(films) > 1:   # upload-time options change addresses only: the films must be identical
         import numpy as np
         keys = list(films)
-        print(json.dumps({"films_identical": {"/".join(k): bool(np.array_equal(np.asarray(films[k]),
+        print(json.dumps({"films_identical": {str(k): bool(np.array_equal(np.asarray(films[k]),
                                                                                np.asarray(films[keys[0]])))
                                               for k in keys[1:]}}), flush=True)
     for c in ctxs.values():
