@@ -109,6 +109,12 @@ struct DevScene {
     const double4 *tshade64; // (n_geo, inv_area) per triangle
     const double4 *tnorm64;  // 3 per triangle: vertex normals (smooth shading only)
     const double4 *spheres64;// (centre, radius)
+    // fp64 list kernels: the list's fp32 filter records in the block's LDS
+    // (list_to_lds; null = read S.list / S.tris / S.spheres): 3 float4 per
+    // entry (a triangle's v0 | e1 | e2 with |.|inf in w, or a sphere's (c, r)),
+    // and the entries' prim refs
+    const float4 *lrec;
+    const int *lref;
     int root;                // node index, or ~prim for a single-leaf world
     int root4;               // 4-wide root node, or the same leaf ref as root
     int n_lights, n_list, world_kind;
@@ -465,10 +471,136 @@ template <typename R> FRT_HD Hit<R> trace_list(const DevScene &S, V3<R> o, V3<R>
     return h;
 }
 
+// ---- list worlds in the fp64 kernels: an fp32 filter in front of the fp64 tests ----
+//
+// The fp64 list kernel (C3, veach_mis) ran every primitive test of the list in
+// fp64 (IEEE division and all): 29 per ray.  The decisions the reference makes
+// in fp64 can be had for about the cost of fp32 tests: each primitive is first
+// tested in fp32 with a rounding-error bound on every quantity the test
+// compares, and only primitives that are not CERTAIN misses (an fp64 hit, or
+// within the bound of one) go through the exact fp64 test, in list order, with
+// the same running t_best as hitable_list::hit (hitable_list.cpp:4-21).  A
+// certain miss is a miss in fp64 for any t_max <= the ray's, so skipping it
+// cannot change the fp64 loop's answer: hits, ties and ray counts are the
+// unfiltered loop's bit for bit (tests/test_precision_host.py,
+// frt_internal_list_filter_check).
+//
+// Error bound (u = 2^-24; every fp32 input is the double rounded, relative
+// error <= u): for Moller-Trumbore's s = o - v0, h = d x e2, a = e1.h,
+// N = s.h, q = s x e1, Nv = d.q, Nt = e2.q, standard forward analysis gives
+// |fl(N) - N| <= 55 u Sm D A2, |fl(a) - a| <= 48 u A1 D A2,
+// |fl(Nv) - Nv| <= 63 u D Sm A1, |fl(Nt) - Nt| <= 63 u A2 Sm A1 with
+// Sm = |o|inf + |v0|inf, D = |d|inf, A1 = |e1|inf, A2 = |e2|inf (the records'
+// w).  The filter uses K = 2^-17 = 128 u in place of each constant; the fp64
+// rounding of the exact test (2^-53 relative) is far inside that slack.  The
+// sphere's perpendicular offset l = oc - (oc.d / d.d) d has per-component
+// error <= ~20 u Mo (Mo = |o|inf + |c|inf + r), so |fl(l.l) - l.l| <=
+// K (2 Mo L + r^2) + (K Mo)^2 with L = |l|inf + K Mo.
+constexpr float kListFilterK = 1.0f / 131072.0f;   // 2^-17
+constexpr float kListFilterT = 1.0f / 1048576.0f;  // 2^-20: slack on the t products
+// verdict of the fp32 test: 0 = certain miss, 1 = maybe (exact test needed),
+// 2 = certain hit with t in [tlo, thi]
+struct ListRay32 { f3 o, d; float O, KD; float tmin, tmax; };
+FRT_HD int list_filter_tri(const ListRay32 &r, float4 a4, float4 b4, float4 c4, float &tlo, float &thi)
+{
+    const f3 v0 = xyz(a4), e1 = xyz(b4), e2 = xyz(c4);
+    const float Sm = r.O + a4.w, A1 = b4.w, A2 = c4.w;
+    const f3 h = cross(r.d, e2);
+    const float a = dot(e1, h);
+    const float Ea = r.KD * A1 * A2;
+    tlo = 0.0f; thi = __builtin_inff();
+    if (!(fabsf(a) > Ea)) return 1;                      // a's sign (or a = 0) is not certain
+    const float sg = a < 0.0f ? -1.0f : 1.0f, aa = fabsf(a);
+    const f3 s = r.o - v0;
+    const float N = sg * dot(s, h), Eu = r.KD * Sm * A2;
+    if (N < -Eu || N - aa > Eu + Ea) return 0;           // u < 0 or u > 1
+    const f3 q = cross(s, e1);
+    const float Nv = sg * dot(r.d, q), Ev = r.KD * Sm * A1;
+    if (Nv < -Ev || N + Nv - aa > Eu + Ev + Ea) return 0;   // v < 0 or u + v > 1
+    const float Nt = sg * dot(e2, q), Et = kListFilterK * A2 * Sm * A1;
+    const float alo = aa - Ea, ahi = aa + Ea;            // a' in [alo, ahi], alo > 0
+    // t = Nt' / a' in [(Nt - Et) / ahi, (Nt + Et) / alo] (t_min >= 0, so a negative
+    // numerator bound stays a lower bound)
+    const float nlo = Nt - Et, nhi = Nt + Et;
+    if (nhi <= r.tmin * alo * (1.0f - kListFilterT)) return 0;          // t <= t_min
+    if (nlo > r.tmax * ahi * (1.0f + kListFilterT)) return 0;           // t > t_max
+    tlo = fdiv(nlo, ahi) * (1.0f - kListFilterT);
+    thi = fdiv(nhi, alo) * (1.0f + kListFilterT);
+    const bool sure = N >= Eu && N + Eu <= alo && Nv >= Ev && N + Nv + Eu + Ev <= alo &&
+                      tlo > r.tmin && thi <= r.tmax * (1.0f - kListFilterT);
+    return sure ? 2 : 1;
+}
+FRT_HD int list_filter_sphere(const ListRay32 &r, float4 s4)
+{
+    const f3 c = xyz(s4);
+    const float rr = s4.w;
+    const f3 oc = r.o - c;
+    const float dd = dot(r.d, r.d);
+    const f3 l = oc - fdiv(dot(oc, r.d), dd) * r.d;
+    const float Mo = r.O + vmax(vabs(c.x), vmax(vabs(c.y), vabs(c.z))) + rr;
+    const float L = vmax(vabs(l.x), vmax(vabs(l.y), vabs(l.z))) + kListFilterK * Mo;
+    const float El = kListFilterK * (2.0f * Mo * L + rr * rr) + (kListFilterK * Mo) * (kListFilterK * Mo);
+    return dot(l, l) - rr * rr > El ? 0 : 1;             // the line misses the sphere
+}
+// hitable_list::hit in fp64 with the fp32 filter.  Certain misses are skipped;
+// the rest (up to 4 per ray, more fall back to the whole list) are tested in
+// fp64 in list order.  Closest hit: a primitive whose t interval lies beyond
+// a certain hit's cannot be the closest (it is farther than a primitive that
+// is hit), so it is dropped too.  Any hit: a certain hit answers the query (the
+// caller reads only whether something was hit: path_after_shadow).
+constexpr int kListLdsMax = 512;                   // list entries the fp64 kernels copy to LDS (26 KiB)
+FRT_HD Hit<double> trace_list_filtered(const DevScene &S, d3 o, d3 d, double tmax, bool anyhit)
+{
+    if (S.n_list > 0xffff) return trace_list(S, o, d, tmax, anyhit);   // candidate indices are 16-bit
+    Hit<double> h{-1, tmax, 0.0, 0.0};
+    ListRay32 r;
+    r.o = mk3((float)o.x, (float)o.y, (float)o.z);
+    r.d = mk3((float)d.x, (float)d.y, (float)d.z);
+    r.O = vmax(vabs(r.o.x), vmax(vabs(r.o.y), vabs(r.o.z)));
+    r.KD = kListFilterK * vmax(vabs(r.d.x), vmax(vabs(r.d.y), vabs(r.d.z)));
+    r.tmin = (float)Cst<double>::eps;                    // rounds below 1e-4: fewer certain misses
+    r.tmax = (float)tmax;                                // the tmax test has its own slack
+    uint64_t cand = 0;
+    int ncand = 0;
+    float t_sure = __builtin_inff();
+    const bool lds = S.lrec != nullptr;                  // the kernel's LDS copy of the list (list_to_lds)
+    for (int i = 0; i < S.n_list; ++i) {
+        const int ref = lds ? S.lref[i] : S.list[i];
+        int verdict;
+        float tlo = 0.0f, thi = __builtin_inff();
+        if (ref & FRT_PRIM_SPHERE) {
+            verdict = list_filter_sphere(r, lds ? S.lrec[3 * i] : S.spheres[ref & ~FRT_PRIM_SPHERE]);
+        } else {
+            const float4 a4 = lds ? S.lrec[3 * i] : S.tris[3 * ref], b4 = lds ? S.lrec[3 * i + 1] : S.tris[3 * ref + 1];
+            const float4 c4 = lds ? S.lrec[3 * i + 2] : S.tris[3 * ref + 2];
+            verdict = list_filter_tri(r, a4, b4, c4, tlo, thi);
+        }
+        if (verdict == 0) continue;
+        if (anyhit && verdict == 2) { h.prim = ref; h.t = (double)thi; return h; }
+        if (tlo > t_sure) continue;                      // beyond a certain hit: never the closest
+        if (verdict == 2) t_sure = vmin(t_sure, thi);
+        if (ncand < 4) cand |= (uint64_t)(uint32_t)i << (16 * ncand);
+        ++ncand;
+    }
+    if (ncand > 4) return trace_list(S, o, d, tmax, anyhit);   // (rare) the whole list in fp64
+    for (int k = 0; k < ncand; ++k) {
+        const int i = (int)((cand >> (16 * k)) & 0xffffu);
+        const int ref = lds ? S.lref[i] : S.list[i];
+        double u, v;
+        const double t = prim_t(S, ref, o, d, Cst<double>::eps, h.t, u, v);
+        if (t > 0.0 && ((ref & FRT_PRIM_SPHERE) || t < h.t)) {
+            h.prim = ref; h.t = t; h.u = u; h.v = v;
+            if (anyhit) return h;
+        }
+    }
+    return h;
+}
+
 template <int WORLD, int STRIDE, int STACK = 0, typename R>
 FRT_HD Hit<R> trace(const DevScene &S, V3<R> o, V3<R> d, R tmax, bool anyhit, int *stk)
 {
-    if constexpr (WORLD == FRT_WORLD_LIST) return trace_list(S, o, d, tmax, anyhit);
+    if constexpr (WORLD == FRT_WORLD_LIST && kIsF64<R>) return trace_list_filtered(S, o, d, tmax, anyhit);
+    else if constexpr (WORLD == FRT_WORLD_LIST) return trace_list(S, o, d, tmax, anyhit);
     else if constexpr (WORLD == kWorldBvh4) return trace_bvh4<STRIDE, STACK, kBvh4Overflow>(S, o, d, tmax, anyhit, stk);
     else return trace_bvh<STRIDE>(S, o, d, tmax, anyhit, stk);
 }
@@ -498,7 +630,8 @@ FRT_HD bool trav_step_world(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, boo
         T.tmin = bvh_tmin(o);
     }
     if constexpr (WORLD == FRT_WORLD_LIST) {
-        T.h = trace_list(S, o, d, T.h.t, anyhit);
+        if constexpr (kIsF64<R>) T.h = trace_list_filtered(S, o, d, T.h.t, anyhit);
+        else T.h = trace_list(S, o, d, T.h.t, anyhit);
         return true;
     } else if constexpr (WORLD == kWorldBvh4) {
         return bvh4_step<STRIDE, STACK>(T, S, o, d, anyhit, stk, ovf, min_desc);

@@ -128,6 +128,29 @@ __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
     S.sh_es = 1; S.sh_ps = S0.n_tris;
 }
 
+// fp64 list kernels: the list's fp32 filter records (trace_list_filtered) in
+// the block's LDS, read with one address per wave (broadcast) in list order;
+// the fp64 records stay in HBM (read only for the filter's candidates).
+__device__ __forceinline__ void list_to_lds(DevScene &S, int *lds_base)
+{
+    float4 *rec = reinterpret_cast<float4 *>(lds_base);
+    int *refs = lds_base + 12 * S.n_list;
+    for (int i = threadIdx.x; i < S.n_list; i += kBlock) {
+        const int ref = S.list[i];
+        refs[i] = ref;
+        if (ref & FRT_PRIM_SPHERE) {
+            rec[3 * i] = S.spheres[ref & ~FRT_PRIM_SPHERE];
+            rec[3 * i + 1] = rec[3 * i + 2] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        } else {
+            rec[3 * i] = S.tris[3 * ref]; rec[3 * i + 1] = S.tris[3 * ref + 1]; rec[3 * i + 2] = S.tris[3 * ref + 2];
+        }
+    }
+    __syncthreads();
+    S.lrec = rec;
+    S.lref = refs;
+}
+constexpr size_t kListLdsEntryBytes = 3 * sizeof(float4) + sizeof(int);
+
 // ------------------------------------------------------------------------
 // the persistent path megakernel
 // ------------------------------------------------------------------------
@@ -160,6 +183,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     DevScene S = S0;
     if constexpr (LDS_SCENE) scene_to_lds<WORLD>(S, lds_mem + kStackInts + kItemInts);
     else scene_strides_hbm(S);
+    if constexpr (WORLD == FRT_WORLD_LIST && kIsF64<R>)
+        if (S.n_list <= kListLdsMax) list_to_lds(S, lds_mem + kStackInts + kItemInts);
     const int lane = threadIdx.x & 63;
     const int T2 = W.tile * W.tile;
 
@@ -794,7 +819,7 @@ struct frt_ctx {
     int world_kind = 0, stack_needed = 0;
     bool has_bvh4 = false;        // nodes4 holds the 4-wide BVH4Q
     int depth4 = 0;               // levels of that wide tree
-    int n_tris = 0, n_spheres = 0;
+    int n_tris = 0, n_spheres = 0, n_list = 0;
     bool has_spec_mats = false;   // a non-lambertian scattering material or a texture: MATS kernels
     int mats = kMatsNone;         // kMats* mask of the scene's material set (pick_launcher)
     bool has_metal = false;       // ao::Li cannot sample metal (constant_pdf::generate throws, pdf.h:195-198)
@@ -832,6 +857,8 @@ struct frt_ctx {
 // count (DESIGN.md "Register-cap hazard").  The lambertian kernels (the
 // bench configurations) stay on the greedy allocator.
 static bool bvh4_stack_fits(int depth4, int lds_entries) { return 3 * depth4 <= lds_entries + kBvh4Overflow; }
+// LDS of an fp64 list kernel's filter records (list_to_lds), 0 for longer lists
+static size_t list_lds_bytes(const frt_ctx *c) { return c->n_list <= kListLdsMax ? c->n_list * kListLdsEntryBytes : 0; }
 struct Launcher {
     const void *fn = nullptr;
     size_t lds = 0;
@@ -848,8 +875,10 @@ static Launcher make_launcher(size_t scene_bytes)
     Launcher L;
     L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES, MATS, KIND, R>);
     L.f64 = kIsF64<R>;
+    // scene_bytes: the LDS scene copy, or (fp64 list kernels) the list's filter records
     L.lds = (WORLD != FRT_WORLD_LIST ? (size_t)STACK * kBlock * sizeof(int) : 0) +
-            (size_t)kItemWords * kBlock * sizeof(int) + (LDS ? scene_bytes : 0);
+            (size_t)kItemWords * kBlock * sizeof(int) +
+            (LDS || (WORLD == FRT_WORLD_LIST && kIsF64<R>) ? scene_bytes : 0);
     L.stack = STACK;
     L.waves = WAVES > 1 ? WAVES : 0;
     L.lds_scene = LDS;
@@ -975,7 +1004,7 @@ static int pick_launcher_f64_t(const frt_ctx *c, Launcher &L)
 {
     if (c->world_kind == FRT_WORLD_LIST) {
         // (a 2-wave register cap changed nothing: profiles/r03/r03c_ab_veach_listbox_f64waves.jsonl)
-        L = make_launcher<16, FRT_WORLD_LIST, false, 1, MATS, FRT_INTEGRATOR_PATH, double>(0);
+        L = make_launcher<16, FRT_WORLD_LIST, false, 1, MATS, FRT_INTEGRATOR_PATH, double>(list_lds_bytes(c));
         return FRT_OK;
     }
     const int d = c->stack_needed;
@@ -1554,9 +1583,12 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
         double ng[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
         const double l = std::sqrt(ng[0] * ng[0] + ng[1] * ng[1] + ng[2] * ng[2]);
         for (int k = 0; k < 3; ++k) ng[k] = ng[k] / l;   // unit_vector(cross(e1, e2)), triangle.h:101
-        F.tris[3 * d + 0] = make_float4((float)v[0], (float)v[1], (float)v[2], 0.0f);
-        F.tris[3 * d + 1] = make_float4((float)e1[0], (float)e1[1], (float)e1[2], 0.0f);
-        F.tris[3 * d + 2] = make_float4((float)e2[0], (float)e2[1], (float)e2[2], 0.0f);
+        // w: |x|_inf of each vector rounded up, the magnitudes the fp64 kernels'
+        // fp32 list filter bounds its rounding with (list_filter_tri)
+        auto mabs = [](const double *x) { return round_up(std::max(std::fabs(x[0]), std::max(std::fabs(x[1]), std::fabs(x[2])))); };
+        F.tris[3 * d + 0] = make_float4((float)v[0], (float)v[1], (float)v[2], mabs(v));
+        F.tris[3 * d + 1] = make_float4((float)e1[0], (float)e1[1], (float)e1[2], mabs(e1));
+        F.tris[3 * d + 2] = make_float4((float)e2[0], (float)e2[1], (float)e2[2], mabs(e2));
         const int mat = sv->tri_material[i];
         if (mat < 0 || mat >= nm) return fail(FRT_E_INVALID, "scene view: bad triangle material");
         const int geo = sv->tri_geometry_normal ? (sv->tri_geometry_normal[i] ? 1 : 0) : 1;
@@ -1746,6 +1778,7 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
     c->has_bvh4 = F.has4;
     c->n_tris = S.n_tris;
     c->n_spheres = (int)F.spheres.size();
+    c->n_list = S.n_list;
     c->has_spec_mats = false;
     c->has_metal = false;
     c->mats = kMatsNone;
@@ -1858,6 +1891,32 @@ extern "C" int frt_selftest_path_host(const frt_scene_view *sv, const frt_render
 }
 
 
+// Self-test hook (CPU tests): the fp64 list query with the fp32 filter
+// (trace_list_filtered) against the plain fp64 loop (trace_list) for n rays
+// (8 doubles each: origin, t_max, direction, any-hit flag).  mismatch[i] = 1
+// when the answers differ: closest hit -- primitive, t, u, v bit for bit;
+// any hit -- whether something was hit.  Internal to libfrt.so.
+extern "C" int frt_internal_list_filter_check(const frt_scene_view *sv, const double *rays, int n, int32_t *mismatch)
+{
+    if (!sv || !rays || !mismatch || n < 0 || sv->world_kind != FRT_WORLD_LIST) return FRT_E_INVALID;
+    FlatScene F;
+    std::string err;
+    const int rc = flatten_scene(sv, F, err, true);
+    if (rc != FRT_OK) return rc;
+    const DevScene S = host_scene(F);
+    for (int i = 0; i < n; ++i) {
+        const double *q = rays + 8 * (size_t)i;
+        const d3 o{q[0], q[1], q[2]}, d{q[4], q[5], q[6]};
+        const bool any = q[7] != 0.0;
+        const Hit<double> a = trace_list(S, o, d, q[3], any), b = trace_list_filtered(S, o, d, q[3], any);
+        mismatch[i] = any ? ((a.prim < 0) != (b.prim < 0))
+                          : !(a.prim == b.prim && (a.prim < 0 || (std::memcmp(&a.t, &b.t, 8) == 0 &&
+                                                                  std::memcmp(&a.u, &b.u, 8) == 0 &&
+                                                                  std::memcmp(&a.v, &b.v, 8) == 0)));
+    }
+    return FRT_OK;
+}
+
 // Self-test hook: n PSS-MLT bootstrap eye paths (fresh primary samples from the
 // bootstrap stream) through frt_mlt.hpp on the host; out6[i] = x, y, r, g, b, sc.
 extern "C" int frt_selftest_mlt_paths_host(const frt_scene_view *sv, int nx, int ny, uint32_t seed, int n,
@@ -1955,7 +2014,7 @@ static int pick_launcher(const frt_ctx *c, int integrator, int flags, Launcher &
     if (integrator == FRT_INTEGRATOR_AO || c->mats != kMatsNone || (f64 && c->world_kind != FRT_WORLD_LIST))
         return frt_mats::pick(c, integrator, flags, f64, L);   // every kernel with a material set
     if (f64) {   // a lambertian list world (BVH worlds' fp64 kernels carry every material: the other unit)
-        L = make_launcher<16, FRT_WORLD_LIST, false, 1, kMatsNone, FRT_INTEGRATOR_PATH, double>(0);
+        L = make_launcher<16, FRT_WORLD_LIST, false, 1, kMatsNone, FRT_INTEGRATOR_PATH, double>(list_lds_bytes(c));
         return FRT_OK;
     }
     return pick_launcher_t<kMatsNone>(c, flags, L);
