@@ -365,6 +365,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     }
 }
 
+#include "frt_pool.hpp"   // path_pool_megakernel: the same loop with a per-wave ray pool
+
 // ------------------------------------------------------------------------
 // ray queries (frt_trace_device): a buffer of rays through the same
 // resumable traversal, Scene::world->hit (path.cpp:10, 50; parallel_bvh.h:39-64,
@@ -888,6 +890,24 @@ static Launcher make_launcher(size_t scene_bytes)
 #ifndef FRT_EXP_W6
 #define FRT_EXP_W6 6   // experiment builds: the register cap behind the "6 waves" plans
 #endif
+// the ray-pool megakernel (frt_pool.hpp) for the LDS binary plans of lambertian scenes
+template <int STACK, int WORLD>
+static Launcher make_pool_launcher(size_t scene_bytes)
+{
+    Launcher L;
+    L.fn = reinterpret_cast<const void *>(&path_pool_megakernel<STACK, WORLD, 5>);
+    L.lds = (size_t)(STACK + kPoolItemWords + kPoolSlotWords) * kBlock * sizeof(int) + scene_bytes;
+    L.stack = STACK;
+    L.waves = 5;
+    L.lds_scene = true;
+    return L;
+}
+// FRT_POOL=1: the ray-pool kernel (A/B knob while it is measured; not part of the C-ABI)
+static bool pool_enabled()
+{
+    const char *e = std::getenv("FRT_POOL");
+    return e && std::atoi(e) == 1;
+}
 template <int STACK, bool LDS, int WORLD = FRT_WORLD_BVH, int MATS = kMatsNone>
 static Launcher bvh_launcher(int waves, size_t sb)
 {
@@ -951,6 +971,14 @@ static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
     }
     // LDS-resident binary tree: the per-octant node copies when they fit
     const bool oct = lds && !(flags & FRT_FLAG_NO_OCT) && c->scene_lds_bytes_oct <= kLdsOctBytes;
+    if constexpr (MATS == kMatsNone) {
+        if (lds && pool_enabled() && d < 16) {
+            if (oct) L = d < 8 ? make_pool_launcher<8, kWorldBvh2Oct>(c->scene_lds_bytes_oct)
+                               : make_pool_launcher<16, kWorldBvh2Oct>(c->scene_lds_bytes_oct);
+            else L = d < 8 ? make_pool_launcher<8, FRT_WORLD_BVH>(sb) : make_pool_launcher<16, FRT_WORLD_BVH>(sb);
+            return FRT_OK;
+        }
+    }
     if (oct) {
         L = d < 8 ? bvh_launcher<8, true, kWorldBvh2Oct, MATS>(waves, c->scene_lds_bytes_oct)
                   : bvh_launcher<16, true, kWorldBvh2Oct, MATS>(waves, c->scene_lds_bytes_oct);
