@@ -58,7 +58,9 @@ __device__ __forceinline__ uint64_t drop_lowest(uint64_t m, uint32_t k)
 }
 __device__ __forceinline__ float bperm(int src4, float x) { return i2f(__builtin_amdgcn_ds_bpermute(src4, f2i(x))); }
 
-template <int STACK, int WORLD, int WAVES>
+// RESLAB: the slab ray (1/d, -o/d) and t_min again from the traced ray at every
+// traversal step instead of kept in Trav (6 VGPRs less across the loop)
+template <int STACK, int WORLD, int WAVES, bool RESLAB = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void path_pool_megakernel(
     const DevScene S0, const DevWork W)
 {
@@ -143,6 +145,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
                 const uint32_t tS = min(nfree, nS);
                 poolS = drop_lowest(poolS, tS);
                 poolE = drop_lowest(poolE, min(nfree - tS, nE));
+            }
+            if constexpr (RESLAB) {
+                if (tracing) { T.sr = slab_ray(to, td); T.tmin = bvh_tmin(to); }
             }
             if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, to, td, t_kind == kRayShadow, stk, ovf, 0)) {
                 tracing = false;

@@ -895,18 +895,21 @@ template <int STACK, int WORLD>
 static Launcher make_pool_launcher(size_t scene_bytes)
 {
     Launcher L;
-    L.fn = reinterpret_cast<const void *>(&path_pool_megakernel<STACK, WORLD, 5>);
+    const char *e = std::getenv("FRT_POOL");
+    L.fn = e && std::atoi(e) == 2 ? reinterpret_cast<const void *>(&path_pool_megakernel<STACK, WORLD, 5, true>)
+                                   : reinterpret_cast<const void *>(&path_pool_megakernel<STACK, WORLD, 5, false>);
     L.lds = (size_t)(STACK + kPoolItemWords + kPoolSlotWords) * kBlock * sizeof(int) + scene_bytes;
     L.stack = STACK;
     L.waves = 5;
     L.lds_scene = true;
     return L;
 }
-// FRT_POOL=1: the ray-pool kernel (A/B knob while it is measured; not part of the C-ABI)
+// FRT_POOL=1 / 2: the ray-pool kernel (2: with the slab ray re-derived per step);
+// an A/B knob while it is measured, not part of the C-ABI
 static bool pool_enabled()
 {
     const char *e = std::getenv("FRT_POOL");
-    return e && std::atoi(e) == 1;
+    return e && std::atoi(e) >= 1;
 }
 template <int STACK, bool LDS, int WORLD = FRT_WORLD_BVH, int MATS = kMatsNone>
 static Launcher bvh_launcher(int waves, size_t sb)
