@@ -335,6 +335,29 @@ FRT_HD float fpow01(float x, float y)
 #endif
 }
 FRT_HD double fpow01(double x, double y) { return pow(x, y); }
+// x^y for x in [0, 1], y > 0 where the result only weights radiance (the phong
+// lobe's pdf value and eval_bsdf; never a direction): the fp32 form as fpow01;
+// in the fp64 kernels log2 on the fp32 unit over the double's mantissa, the
+// exponent kept exact, and 2^(y log2 x) rebuilt in double range -- relative
+// error ~1e-6, no underflow before double's (so pdf == 0, which ends a path,
+// path.cpp:84-86, comes out exactly where the double pow gives 0), and about a
+// tenth of OCML's double pow.  The directions (cosine_power_generate) keep the
+// double pow: they decide what the next ray hits.
+FRT_HD float fpow01_w(float x, float y) { return fpow01(x, y); }
+FRT_HD double fpow01_w(double x, double y)
+{
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(FRT_EXP_IEEE_MATH)
+    if (!(x > 0.0)) return x == 0.0 ? 0.0 : pow(x, y);
+    int k;
+    const double m = frexp(x, &k);                            // x = m 2^k, m in [0.5, 1)
+    const double l = y * ((double)__builtin_amdgcn_logf((float)m) + (double)k);   // y log2 x
+    if (l < -1100.0) return 0.0;
+    const double li = floor(l);
+    return ldexp((double)__builtin_amdgcn_exp2f((float)(l - li)), (int)li);
+#else
+    return pow(x, y);
+#endif
+}
 
 // ---- specular materials (material.h:75-171, pdf.h:99-184, util.h:73-117) ----
 template <typename R> FRT_HD V3<R> reflect(V3<R> v, V3<R> n) { return normalize(v - (R(2) * dot(v, n)) * n); }   // util.h:73-76
@@ -360,7 +383,7 @@ template <typename R> FRT_HD R cosine_power_value(V3<R> n, V3<R> wi, R e, V3<R> 
 {
     if (dot(n, wo) <= R(0) || dot(n, wi) <= R(0)) return R(0);
     const R alpha = vmax(R(0), dot(reflect(-wi, n), wo));
-    return fpow01(alpha, e) * (e + R(1)) * (R(0.5f) * Cst<R>::inv_pi);
+    return fpow01_w(alpha, e) * (e + R(1)) * (R(0.5f) * Cst<R>::inv_pi);
 }
 template <typename R> FRT_HD V3<R> cosine_power_generate(V3<R> n, V3<R> wi, R e, R s0, R s1)
 {
@@ -375,7 +398,7 @@ template <typename R> FRT_HD V3<R> cosine_power_generate(V3<R> n, V3<R> wi, R e,
 template <typename R> FRT_HD V3<R> phong_eval(V3<R> kd, V3<R> ks, R e, V3<R> n, V3<R> wi, V3<R> wo)
 {
     const R alpha = vmax(R(0), dot(normalize(reflect(-wi, n)), wo));
-    const V3<R> result = Cst<R>::inv_pi * kd + ((e + R(2)) * (R(0.5f) * Cst<R>::inv_pi) * fpow01(alpha, e)) * ks;
+    const V3<R> result = Cst<R>::inv_pi * kd + ((e + R(2)) * (R(0.5f) * Cst<R>::inv_pi) * fpow01_w(alpha, e)) * ks;
     return dot(n, wo) * result;
 }
 // dielectric_pdf (pdf.h:138-184) and dielectric::eval_bsdf (material.h:146-171)
