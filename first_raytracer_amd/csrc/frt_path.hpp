@@ -500,7 +500,7 @@ constexpr float kListFilterK = 1.0f / 131072.0f;   // 2^-17
 constexpr float kListFilterT = 1.0f / 1048576.0f;  // 2^-20: slack on the t products
 // verdict of the fp32 test: 0 = certain miss, 1 = maybe (exact test needed),
 // 2 = certain hit with t in [tlo, thi]
-struct ListRay32 { f3 o, d; float O, KD; float tmin, tmax; };
+struct ListRay32 { f3 o, d; float O, D, KD; float tmin, tmax; };
 FRT_HD int list_filter_tri(const ListRay32 &r, float4 a4, float4 b4, float4 c4, float &tlo, float &thi)
 {
     const f3 v0 = xyz(a4), e1 = xyz(b4), e2 = xyz(c4);
@@ -540,57 +540,70 @@ FRT_HD int list_filter_sphere(const ListRay32 &r, float4 s4)
     const float Mo = r.O + vmax(vabs(c.x), vmax(vabs(c.y), vabs(c.z))) + rr;
     const float L = vmax(vabs(l.x), vmax(vabs(l.y), vabs(l.z))) + kListFilterK * Mo;
     const float El = kListFilterK * (2.0f * Mo * L + rr * rr) + (kListFilterK * Mo) * (kListFilterK * Mo);
-    return dot(l, l) - rr * rr > El ? 0 : 1;             // the line misses the sphere
+    if (dot(l, l) - rr * rr > El) return 0;              // the line misses the sphere
+    // both roots lie in tc -+ r / |d| (tc = -oc.d / d.d, the closest approach);
+    // tc's error <= K (3 Mo / D + |tc|) with D = |d|inf (d.d >= D^2)
+    const float tc = -fdiv(dot(oc, r.d), dd);
+    const float hw = rr * frsqrt(dd) * (1.0f + kListFilterK) + kListFilterK * (3.0f * fdiv(Mo, r.D) + fabsf(tc));
+    if (tc + hw < r.tmin) return 0;                      // the sphere lies behind t_min
+    if (tc - hw > r.tmax * (1.0f + kListFilterT)) return 0;   // ... or beyond t_max
+    return 1;
 }
-// hitable_list::hit in fp64 with the fp32 filter.  Certain misses are skipped;
-// the rest (up to 4 per ray, more fall back to the whole list) are tested in
-// fp64 in list order.  Closest hit: a primitive whose t interval lies beyond
-// a certain hit's cannot be the closest (it is farther than a primitive that
-// is hit), so it is dropped too.  Any hit: a certain hit answers the query (the
-// caller reads only whether something was hit: path_after_shadow).
+// hitable_list::hit in fp64 with the fp32 filter, one pass in list order.  A
+// primitive that is a certain miss for a lane is skipped for that lane; the
+// lanes for which it is not run the exact fp64 test with their running t_best
+// -- one primitive for the whole wave (its kind is uniform, so no lane pays
+// for the other kind's code), and none at all when it is a certain miss for
+// every lane.  Closest hit: a primitive whose t interval lies beyond a certain
+// hit's cannot be the closest (it is farther than a primitive that is hit), so
+// it is skipped too.  Any hit: a certain hit answers the query (the caller
+// reads only whether something was hit: path_after_shadow).
+FRT_HD int uniform_i(int x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_readfirstlane(x);
+#else
+    return x;
+#endif
+}
 constexpr int kListLdsMax = 512;                   // list entries the fp64 kernels copy to LDS (26 KiB)
 FRT_HD Hit<double> trace_list_filtered(const DevScene &S, d3 o, d3 d, double tmax, bool anyhit)
 {
-    if (S.n_list > 0xffff) return trace_list(S, o, d, tmax, anyhit);   // candidate indices are 16-bit
     Hit<double> h{-1, tmax, 0.0, 0.0};
     ListRay32 r;
     r.o = mk3((float)o.x, (float)o.y, (float)o.z);
     r.d = mk3((float)d.x, (float)d.y, (float)d.z);
     r.O = vmax(vabs(r.o.x), vmax(vabs(r.o.y), vabs(r.o.z)));
-    r.KD = kListFilterK * vmax(vabs(r.d.x), vmax(vabs(r.d.y), vabs(r.d.z)));
+    r.D = vmax(vabs(r.d.x), vmax(vabs(r.d.y), vabs(r.d.z)));
+    r.KD = kListFilterK * r.D;
     r.tmin = (float)Cst<double>::eps;                    // rounds below 1e-4: fewer certain misses
-    r.tmax = (float)tmax;                                // the tmax test has its own slack
-    uint64_t cand = 0;
-    int ncand = 0;
+    r.tmax = (float)tmax;                                // the tmax tests have their own slack
     float t_sure = __builtin_inff();
+    bool done = false;                                   // any-hit query answered
     const bool lds = S.lrec != nullptr;                  // the kernel's LDS copy of the list (list_to_lds)
     for (int i = 0; i < S.n_list; ++i) {
-        const int ref = lds ? S.lref[i] : S.list[i];
-        int verdict;
+        if (!wave_any(!done)) break;
+        const int ref = uniform_i(lds ? S.lref[i] : S.list[i]);
+        int verdict = 0;
         float tlo = 0.0f, thi = __builtin_inff();
-        if (ref & FRT_PRIM_SPHERE) {
-            verdict = list_filter_sphere(r, lds ? S.lrec[3 * i] : S.spheres[ref & ~FRT_PRIM_SPHERE]);
-        } else {
-            const float4 a4 = lds ? S.lrec[3 * i] : S.tris[3 * ref], b4 = lds ? S.lrec[3 * i + 1] : S.tris[3 * ref + 1];
-            const float4 c4 = lds ? S.lrec[3 * i + 2] : S.tris[3 * ref + 2];
-            verdict = list_filter_tri(r, a4, b4, c4, tlo, thi);
+        if (!done) {
+            if (ref & FRT_PRIM_SPHERE) {
+                verdict = list_filter_sphere(r, lds ? S.lrec[3 * i] : S.spheres[ref & ~FRT_PRIM_SPHERE]);
+            } else {
+                const float4 a4 = lds ? S.lrec[3 * i] : S.tris[3 * ref];
+                const float4 b4 = lds ? S.lrec[3 * i + 1] : S.tris[3 * ref + 1];
+                const float4 c4 = lds ? S.lrec[3 * i + 2] : S.tris[3 * ref + 2];
+                verdict = list_filter_tri(r, a4, b4, c4, tlo, thi);
+            }
         }
-        if (verdict == 0) continue;
-        if (anyhit && verdict == 2) { h.prim = ref; h.t = (double)thi; return h; }
-        if (tlo > t_sure) continue;                      // beyond a certain hit: never the closest
+        if (anyhit && verdict == 2) { h.prim = ref; h.t = (double)thi; done = true; continue; }
+        if (verdict == 0 || tlo > t_sure) continue;      // certain miss / beyond a certain hit
         if (verdict == 2) t_sure = vmin(t_sure, thi);
-        if (ncand < 4) cand |= (uint64_t)(uint32_t)i << (16 * ncand);
-        ++ncand;
-    }
-    if (ncand > 4) return trace_list(S, o, d, tmax, anyhit);   // (rare) the whole list in fp64
-    for (int k = 0; k < ncand; ++k) {
-        const int i = (int)((cand >> (16 * k)) & 0xffffu);
-        const int ref = lds ? S.lref[i] : S.list[i];
         double u, v;
         const double t = prim_t(S, ref, o, d, Cst<double>::eps, h.t, u, v);
         if (t > 0.0 && ((ref & FRT_PRIM_SPHERE) || t < h.t)) {
             h.prim = ref; h.t = t; h.u = u; h.v = v;
-            if (anyhit) return h;
+            if (anyhit) done = true;
         }
     }
     return h;
@@ -599,8 +612,11 @@ FRT_HD Hit<double> trace_list_filtered(const DevScene &S, d3 o, d3 d, double tma
 template <int WORLD, int STRIDE, int STACK = 0, typename R>
 FRT_HD Hit<R> trace(const DevScene &S, V3<R> o, V3<R> d, R tmax, bool anyhit, int *stk)
 {
+#if !defined(FRT_EXP_NO_LIST_FILTER)   // experiment builds: the plain fp64 loop (A/B)
     if constexpr (WORLD == FRT_WORLD_LIST && kIsF64<R>) return trace_list_filtered(S, o, d, tmax, anyhit);
-    else if constexpr (WORLD == FRT_WORLD_LIST) return trace_list(S, o, d, tmax, anyhit);
+    else
+#endif
+    if constexpr (WORLD == FRT_WORLD_LIST) return trace_list(S, o, d, tmax, anyhit);
     else if constexpr (WORLD == kWorldBvh4) return trace_bvh4<STRIDE, STACK, kBvh4Overflow>(S, o, d, tmax, anyhit, stk);
     else return trace_bvh<STRIDE>(S, o, d, tmax, anyhit, stk);
 }
@@ -630,8 +646,11 @@ FRT_HD bool trav_step_world(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, boo
         T.tmin = bvh_tmin(o);
     }
     if constexpr (WORLD == FRT_WORLD_LIST) {
+#if !defined(FRT_EXP_NO_LIST_FILTER)
         if constexpr (kIsF64<R>) T.h = trace_list_filtered(S, o, d, T.h.t, anyhit);
-        else T.h = trace_list(S, o, d, T.h.t, anyhit);
+        else
+#endif
+        T.h = trace_list(S, o, d, T.h.t, anyhit);
         return true;
     } else if constexpr (WORLD == kWorldBvh4) {
         return bvh4_step<STRIDE, STACK>(T, S, o, d, anyhit, stk, ovf, min_desc);

@@ -114,8 +114,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         // empty and at most trav_min lanes still trace ----
         for (;;) {
             const uint64_t fr = __ballot(!tracing);
-            if (fr != 0 && (poolE | poolS) != 0) {
-                const uint32_t nfree = (uint32_t)__popcll(fr), nS = (uint32_t)__popcll(poolS);
+            const uint32_t nfree = (uint32_t)__popcll(fr);
+            // hand out queued rays once pool_min lanes are free (or the wave is
+            // about to shade anyway): the hand-out costs ~60 instructions a trip
+            if (fr != 0 && (poolE | poolS) != 0 && (nfree >= (uint32_t)W.pool_min || 64u - nfree <= (uint32_t)W.trav_min)) {
+                const uint32_t nS = (uint32_t)__popcll(poolS);
                 const uint32_t nE = (uint32_t)__popcll(poolE);
                 const uint32_t r = lane_rank(fr);
                 const bool take = !tracing && r < nS + nE;

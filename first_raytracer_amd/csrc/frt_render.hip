@@ -59,6 +59,7 @@ struct DevWork {
     unsigned *counter;                   // work-queue head
     unsigned long long *wave_rays;       // [n_waves][4]: camera, extension, shadow, samples
     uint32_t grab;                       // items a wave takes per queue atomic (at least those it needs)
+    int pool_min;                        // ray-pool kernel: hand out queued rays once this many lanes are free
 };
 
 // slot -> pixel inside a tile: 8x8 blocks, row-major inside a block
@@ -2357,8 +2358,13 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, L.fn, kBlock, L.lds) != hipSuccess || bpc <= 0) bpc = 1;
     const int grid = c->n_cu * bpc;
     const long long lanes = (long long)grid * kBlock;
+    // the granule follows the whole frame's slots, not the shard's: every
+    // shard cuts its pixels' samples into the same chunks, so the per-pixel
+    // sums (and the film) are byte-identical for any shard count
+    // (tools/shard_balance.py: N = 8 of the bench frame still balances)
+    const int n_tiles_frame = ((p->nx + T - 1) / T) * ((p->ny + T - 1) / T);
     int spi = 0, n_chunks = 0;
-    work_granule(p->integrator, p->spp, n_slots, lanes, p->samples_per_item, spi, n_chunks);
+    work_granule(p->integrator, p->spp, (uint64_t)n_tiles_frame * T * T, lanes, p->samples_per_item, spi, n_chunks);
     const unsigned long long n_items = (unsigned long long)n_slots * n_chunks;
     // queue grab: items a wave takes per atomic (FRT_GRAB: A/B knob, not part of the C-ABI)
     const char *gb = std::getenv("FRT_GRAB");
@@ -2390,6 +2396,10 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     W.partial = c->partial; W.counter = c->counter; W.wave_rays = c->wave_rays;
     W.trav_min = trav_min(L.lds_scene, p->integrator == FRT_INTEGRATOR_PATH);
     W.min_desc = min_desc(L.lds_scene);
+    {   // FRT_POOL_MIN: the ray-pool kernel's hand-out threshold (A/B knob, not part of the C-ABI)
+        const char *e = std::getenv("FRT_POOL_MIN");
+        W.pool_min = std::min(std::max(e ? std::atoi(e) : 1, 1), 64);
+    }
 
     HIPCHK(c, hipMemsetAsync(c->counter, 0, 64, st));
 #if defined(FRT_DIAG)
