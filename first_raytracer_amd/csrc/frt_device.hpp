@@ -67,6 +67,29 @@ template <typename R> FRT_HD V3<R> rgb(float4 v) { return V3<R>{R(v.x), R(v.y), 
 
 // min / max / abs / fma / copysign of either precision (the float forms are
 // the fminf / fmaxf ... the fp32 kernels have always used)
+// max / min for the slab tests, whose operands are never NaN (directions are
+// nudged off zero, slab_ray): gfx950's NaN-propagating v_maximum3 / v_minimum3
+// take them as they are, where fmaxf / fminf (IEEE maxNum) first quiet every
+// operand that is not the result of arithmetic in the same block -- t_min and
+// t_best, once per node.  Equal results for non-NaN operands, so the same hits.
+FRT_HD float smax(float a, float b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_elementwise_maximum(a, b);
+#else
+    return fmaxf(a, b);
+#endif
+}
+FRT_HD float smin(float a, float b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_elementwise_minimum(a, b);
+#else
+    return fminf(a, b);
+#endif
+}
+FRT_HD double smax(double a, double b) { return fmax(a, b); }
+FRT_HD double smin(double a, double b) { return fmin(a, b); }
 FRT_HD float vmin(float a, float b) { return fminf(a, b); }
 FRT_HD double vmin(double a, double b) { return fmin(a, b); }
 FRT_HD float vmax(float a, float b) { return fmaxf(a, b); }
@@ -223,8 +246,8 @@ FRT_HD R slab_entry(R lox, R loy, R loz, R hix, R hiy, R hiz, const SlabRay<R> &
     const R tx0 = vfma(lox, r.invd.x, r.oinv.x), tx1 = vfma(hix, r.invd.x, r.oinv.x);
     const R ty0 = vfma(loy, r.invd.y, r.oinv.y), ty1 = vfma(hiy, r.invd.y, r.oinv.y);
     const R tz0 = vfma(loz, r.invd.z, r.oinv.z), tz1 = vfma(hiz, r.invd.z, r.oinv.z);
-    const R tn = vmax(vmax(vmin(tx0, tx1), vmin(ty0, ty1)), vmax(vmin(tz0, tz1), tmin));
-    const R tf = vmin(vmin(vmax(tx0, tx1), vmax(ty0, ty1)), vmin(vmax(tz0, tz1), tmax));
+    const R tn = smax(smax(smin(tx0, tx1), smin(ty0, ty1)), smax(smin(tz0, tz1), tmin));
+    const R tf = smin(smin(smax(tx0, tx1), smax(ty0, ty1)), smin(smax(tz0, tz1), tmax));
     return (tf < tn) ? R(__builtin_inff()) : tn;
 }
 
@@ -233,10 +256,10 @@ FRT_HD R slab_entry(R lox, R loy, R loz, R hix, R hiy, R hiz, const SlabRay<R> &
 template <typename R>
 FRT_HD R slab_entry_nf(R nx, R ny, R nz, R fx, R fy, R fz, const SlabRay<R> &r, R tmin, R tmax)
 {
-    const R tn = vmax(vmax(vfma(nx, r.invd.x, r.oinv.x), vfma(ny, r.invd.y, r.oinv.y)),
-                      vmax(vfma(nz, r.invd.z, r.oinv.z), tmin));
-    const R tf = vmin(vmin(vfma(fx, r.invd.x, r.oinv.x), vfma(fy, r.invd.y, r.oinv.y)),
-                      vmin(vfma(fz, r.invd.z, r.oinv.z), tmax));
+    const R tn = smax(smax(vfma(nx, r.invd.x, r.oinv.x), vfma(ny, r.invd.y, r.oinv.y)),
+                      smax(vfma(nz, r.invd.z, r.oinv.z), tmin));
+    const R tf = smin(smin(vfma(fx, r.invd.x, r.oinv.x), vfma(fy, r.invd.y, r.oinv.y)),
+                      smin(vfma(fz, r.invd.z, r.oinv.z), tmax));
     return (tf < tn) ? R(__builtin_inff()) : tn;
 }
 

@@ -291,17 +291,18 @@ FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyh
     }
     // (a branch-free body -- speculative stack-top read, predicated push -- was
     // 4.5 % slower on Cornell: profiles/r01_exp1_branchy.txt)
+    const R tmin = T.tmin, tbest = T.h.t;
     while ((unsigned)node < (unsigned)kSentinel) {   // interior node
         FRT_DIAG_TICK(2);
         const float4 n0 = node_part(Sn, node, 0), n1 = node_part(Sn, node, 1);
         const float4 n2 = node_part(Sn, node, 2), n3 = node_part(Sn, node, 3);
         R t0, t1;
         if constexpr (OCT) {
-            t0 = slab_entry_nf<R>(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, T.tmin, T.h.t);
-            t1 = slab_entry_nf<R>(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, T.sr, T.tmin, T.h.t);
+            t0 = slab_entry_nf<R>(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, tmin, tbest);
+            t1 = slab_entry_nf<R>(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, T.sr, tmin, tbest);
         } else {
-            t0 = slab_entry<R>(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, T.tmin, T.h.t);
-            t1 = slab_entry<R>(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, T.sr, T.tmin, T.h.t);
+            t0 = slab_entry<R>(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, tmin, tbest);
+            t1 = slab_entry<R>(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, T.sr, tmin, tbest);
         }
         const int c0 = f2i(n3.x), c1 = f2i(n3.y);
         const bool h0 = t0 != R(__builtin_inff()), h1 = t1 != R(__builtin_inff());
@@ -392,8 +393,8 @@ FRT_HD bool bvh4_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit
             const float txn = fmaf((float)((xn >> sh) & 0xffu), ax, bx), txf = fmaf((float)((xf >> sh) & 0xffu), ax, bx);
             const float tyn = fmaf((float)((yn >> sh) & 0xffu), ay, by), tyf = fmaf((float)((yf >> sh) & 0xffu), ay, by);
             const float tzn = fmaf((float)((zn >> sh) & 0xffu), az, bz), tzf = fmaf((float)((zf >> sh) & 0xffu), az, bz);
-            const float tn = fmaxf(fmaxf(txn, tyn), fmaxf(tzn, T.tmin));
-            const float tf = fminf(fminf(txf, tyf), fminf(tzf, T.h.t));
+            const float tn = smax(smax(txn, tyn), smax(tzn, T.tmin));   // v_maximum3 (slab_entry)
+            const float tf = smin(smin(txf, tyf), smin(tzf, T.h.t));
             t[i] = (tf < tn) ? __builtin_inff() : tn;
         }
         // nearest first: sorting network on (t, child), as selects (no branches)
