@@ -88,6 +88,16 @@ FRT_HD float smin(float a, float b)
     return fminf(a, b);
 #endif
 }
+// a * b for 0 <= a, b < 2^24 as one full-rate v_mul_u32_u24 (an int index times
+// a constant became a 64-bit v_mad_u64_u32 in the LDS address)
+FRT_HD int u24mul(int a, int b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (int)__umul24((unsigned)a, (unsigned)b);
+#else
+    return a * b;
+#endif
+}
 FRT_HD double smax(double a, double b) { return fmax(a, b); }
 FRT_HD double smin(double a, double b) { return fmin(a, b); }
 FRT_HD float vmin(float a, float b) { return fminf(a, b); }

@@ -102,6 +102,8 @@ struct DevScene {
     const uint4 *nodes4;     // 4 x uint4 per 4-wide node (HBM-resident scenes; DESIGN.md "BVH4Q")
     const float4 *nodes_oct; // 8 copies of `nodes`, copy o with each child box as (near xyz, far xyz) for
                              // rays of octant o (bit a set: 1/d_a < 0); LDS plans copy them (kWorldBvh2Oct)
+    const int2 *node_refs;   // kWorldBvh2Oct in LDS: the (child0, child1) refs of node j, shared by the
+                             // 8 copies, whose records there hold only the two boxes (3 float4, 48 B)
     // fp64 records of the fp64 kernels (null when the context uploaded none,
     // frt_set_precision): the same device order as tris / tshade / tnorm /
     // spheres, in the reference's doubles (edges taken in fp64, triangle.h:58-60)
@@ -109,19 +111,15 @@ struct DevScene {
     const double4 *tshade64; // (n_geo, inv_area) per triangle
     const double4 *tnorm64;  // 3 per triangle: vertex normals (smooth shading only)
     const double4 *spheres64;// (centre, radius)
-    // fp64 list kernels: the list's fp32 filter records in the block's LDS
-    // (list_to_lds; null = read S.list / S.tris / S.spheres): 3 float4 per
-    // entry (a triangle's v0 | e1 | e2 with |.|inf in w, or a sphere's (c, r)),
-    // and the entries' prim refs
-    const float4 *lrec;
-    const int *lref;
     int root;                // node index, or ~prim for a single-leaf world
     int root4;               // 4-wide root node, or the same leaf ref as root
     int n_lights, n_list, world_kind;
     int n_nodes, n_tris, n_mats;
     // element i, part k of nodes / tris / tshade lives at [i * es + k * ps]:
-    // interleaved in HBM (es = parts, ps = 1), planar in LDS (es = 1, ps = count)
-    // so that lanes reading distinct elements hit distinct LDS bank slots
+    // interleaved in HBM (es = parts, ps = 1).  In LDS the layout keeps lanes
+    // that read distinct elements on distinct bank slots: 48-B records
+    // (triangles, octant node boxes: es = 3) do so interleaved, 64-B and 32-B
+    // ones (binary nodes, shading records) planar (es = 1, ps = count).
     int node_es, node_ps, tri_es, tri_ps, sh_es, sh_ps, node4_es, node4_ps;
     int n_nodes4;
     float root_lo[3], root_hi[3];
@@ -285,26 +283,31 @@ FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyh
 {
     int node = T.node, sp = T.sp;
     DevScene Sn = S;
-    if constexpr (OCT) {
+    if constexpr (OCT) {   // the ray's copy: n_nodes 48-B box records (scene_to_lds)
         const int oct = (T.sr.invd.x < R(0) ? 1 : 0) | (T.sr.invd.y < R(0) ? 2 : 0) | (T.sr.invd.z < R(0) ? 4 : 0);
-        Sn.nodes = S.nodes + oct * 4 * S.node_ps;
+        Sn.nodes = S.nodes + oct * 3 * S.n_nodes;
     }
     // (a branch-free body -- speculative stack-top read, predicated push -- was
     // 4.5 % slower on Cornell: profiles/r01_exp1_branchy.txt)
     const R tmin = T.tmin, tbest = T.h.t;
     while ((unsigned)node < (unsigned)kSentinel) {   // interior node
         FRT_DIAG_TICK(2);
-        const float4 n0 = node_part(Sn, node, 0), n1 = node_part(Sn, node, 1);
-        const float4 n2 = node_part(Sn, node, 2), n3 = node_part(Sn, node, 3);
         R t0, t1;
-        if constexpr (OCT) {
+        int c0, c1;
+        if constexpr (OCT) {   // one address: the record's parts and the refs at immediate offsets
+            const float4 *rec = Sn.nodes + u24mul(node, 3);   // 32-bit mad (node < 2^24)
+            const float4 n0 = rec[0], n1 = rec[1], n2 = rec[2];
+            const int2 cr = S.node_refs[node];
             t0 = slab_entry_nf<R>(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, tmin, tbest);
             t1 = slab_entry_nf<R>(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, T.sr, tmin, tbest);
+            c0 = cr.x; c1 = cr.y;
         } else {
+            const float4 n0 = node_part(Sn, node, 0), n1 = node_part(Sn, node, 1);
+            const float4 n2 = node_part(Sn, node, 2), n3 = node_part(Sn, node, 3);
             t0 = slab_entry<R>(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, tmin, tbest);
             t1 = slab_entry<R>(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, T.sr, tmin, tbest);
+            c0 = f2i(n3.x); c1 = f2i(n3.y);
         }
-        const int c0 = f2i(n3.x), c1 = f2i(n3.y);
         const bool h0 = t0 != R(__builtin_inff()), h1 = t1 != R(__builtin_inff());
         if (h0 && h1) {
             const bool first0 = t0 <= t1;
@@ -472,151 +475,9 @@ template <typename R> FRT_HD Hit<R> trace_list(const DevScene &S, V3<R> o, V3<R>
     return h;
 }
 
-// ---- list worlds in the fp64 kernels: an fp32 filter in front of the fp64 tests ----
-//
-// The fp64 list kernel (C3, veach_mis) ran every primitive test of the list in
-// fp64 (IEEE division and all): 29 per ray.  The decisions the reference makes
-// in fp64 can be had for about the cost of fp32 tests: each primitive is first
-// tested in fp32 with a rounding-error bound on every quantity the test
-// compares, and only primitives that are not CERTAIN misses (an fp64 hit, or
-// within the bound of one) go through the exact fp64 test, in list order, with
-// the same running t_best as hitable_list::hit (hitable_list.cpp:4-21).  A
-// certain miss is a miss in fp64 for any t_max <= the ray's, so skipping it
-// cannot change the fp64 loop's answer: hits, ties and ray counts are the
-// unfiltered loop's bit for bit (tests/test_precision_host.py,
-// frt_internal_list_filter_check).
-//
-// Error bound (u = 2^-24; every fp32 input is the double rounded, relative
-// error <= u): for Moller-Trumbore's s = o - v0, h = d x e2, a = e1.h,
-// N = s.h, q = s x e1, Nv = d.q, Nt = e2.q, standard forward analysis gives
-// |fl(N) - N| <= 55 u Sm D A2, |fl(a) - a| <= 48 u A1 D A2,
-// |fl(Nv) - Nv| <= 63 u D Sm A1, |fl(Nt) - Nt| <= 63 u A2 Sm A1 with
-// Sm = |o|inf + |v0|inf, D = |d|inf, A1 = |e1|inf, A2 = |e2|inf (the records'
-// w).  The filter uses K = 2^-17 = 128 u in place of each constant; the fp64
-// rounding of the exact test (2^-53 relative) is far inside that slack.  The
-// sphere's perpendicular offset l = oc - (oc.d / d.d) d has per-component
-// error <= ~20 u Mo (Mo = |o|inf + |c|inf + r), so |fl(l.l) - l.l| <=
-// K (2 Mo L + r^2) + (K Mo)^2 with L = |l|inf + K Mo.
-constexpr float kListFilterK = 1.0f / 131072.0f;   // 2^-17
-constexpr float kListFilterT = 1.0f / 1048576.0f;  // 2^-20: slack on the t products
-// verdict of the fp32 test: 0 = certain miss, 1 = maybe (exact test needed),
-// 2 = certain hit with t in [tlo, thi]
-struct ListRay32 { f3 o, d; float O, D, KD; float tmin, tmax; };
-FRT_HD int list_filter_tri(const ListRay32 &r, float4 a4, float4 b4, float4 c4, float &tlo, float &thi)
-{
-    const f3 v0 = xyz(a4), e1 = xyz(b4), e2 = xyz(c4);
-    const float Sm = r.O + a4.w, A1 = b4.w, A2 = c4.w;
-    const f3 h = cross(r.d, e2);
-    const float a = dot(e1, h);
-    const float Ea = r.KD * A1 * A2;
-    tlo = 0.0f; thi = __builtin_inff();
-    if (!(fabsf(a) > Ea)) return 1;                      // a's sign (or a = 0) is not certain
-    const float sg = a < 0.0f ? -1.0f : 1.0f, aa = fabsf(a);
-    const f3 s = r.o - v0;
-    const float N = sg * dot(s, h), Eu = r.KD * Sm * A2;
-    if (N < -Eu || N - aa > Eu + Ea) return 0;           // u < 0 or u > 1
-    const f3 q = cross(s, e1);
-    const float Nv = sg * dot(r.d, q), Ev = r.KD * Sm * A1;
-    if (Nv < -Ev || N + Nv - aa > Eu + Ev + Ea) return 0;   // v < 0 or u + v > 1
-    const float Nt = sg * dot(e2, q), Et = kListFilterK * A2 * Sm * A1;
-    const float alo = aa - Ea, ahi = aa + Ea;            // a' in [alo, ahi], alo > 0
-    // t = Nt' / a' in [(Nt - Et) / ahi, (Nt + Et) / alo] (t_min >= 0, so a negative
-    // numerator bound stays a lower bound)
-    const float nlo = Nt - Et, nhi = Nt + Et;
-    if (nhi <= r.tmin * alo * (1.0f - kListFilterT)) return 0;          // t <= t_min
-    if (nlo > r.tmax * ahi * (1.0f + kListFilterT)) return 0;           // t > t_max
-    tlo = fdiv(nlo, ahi) * (1.0f - kListFilterT);
-    thi = fdiv(nhi, alo) * (1.0f + kListFilterT);
-    const bool sure = N >= Eu && N + Eu <= alo && Nv >= Ev && N + Nv + Eu + Ev <= alo &&
-                      tlo > r.tmin && thi <= r.tmax * (1.0f - kListFilterT);
-    return sure ? 2 : 1;
-}
-FRT_HD int list_filter_sphere(const ListRay32 &r, float4 s4)
-{
-    const f3 c = xyz(s4);
-    const float rr = s4.w;
-    const f3 oc = r.o - c;
-    const float dd = dot(r.d, r.d);
-    const f3 l = oc - fdiv(dot(oc, r.d), dd) * r.d;
-    const float Mo = r.O + vmax(vabs(c.x), vmax(vabs(c.y), vabs(c.z))) + rr;
-    const float L = vmax(vabs(l.x), vmax(vabs(l.y), vabs(l.z))) + kListFilterK * Mo;
-    const float El = kListFilterK * (2.0f * Mo * L + rr * rr) + (kListFilterK * Mo) * (kListFilterK * Mo);
-    if (dot(l, l) - rr * rr > El) return 0;              // the line misses the sphere
-    // both roots lie in tc -+ r / |d| (tc = -oc.d / d.d, the closest approach);
-    // tc's error <= K (3 Mo / D + |tc|) with D = |d|inf (d.d >= D^2)
-    const float tc = -fdiv(dot(oc, r.d), dd);
-    const float hw = rr * frsqrt(dd) * (1.0f + kListFilterK) + kListFilterK * (3.0f * fdiv(Mo, r.D) + fabsf(tc));
-    if (tc + hw < r.tmin) return 0;                      // the sphere lies behind t_min
-    if (tc - hw > r.tmax * (1.0f + kListFilterT)) return 0;   // ... or beyond t_max
-    return 1;
-}
-// hitable_list::hit in fp64 with the fp32 filter, one pass in list order.  A
-// primitive that is a certain miss for a lane is skipped for that lane; the
-// lanes for which it is not run the exact fp64 test with their running t_best
-// -- one primitive for the whole wave (its kind is uniform, so no lane pays
-// for the other kind's code), and none at all when it is a certain miss for
-// every lane.  Closest hit: a primitive whose t interval lies beyond a certain
-// hit's cannot be the closest (it is farther than a primitive that is hit), so
-// it is skipped too.  Any hit: a certain hit answers the query (the caller
-// reads only whether something was hit: path_after_shadow).
-FRT_HD int uniform_i(int x)
-{
-#if defined(__HIP_DEVICE_COMPILE__)
-    return __builtin_amdgcn_readfirstlane(x);
-#else
-    return x;
-#endif
-}
-constexpr int kListLdsMax = 512;                   // list entries the fp64 kernels copy to LDS (26 KiB)
-FRT_HD Hit<double> trace_list_filtered(const DevScene &S, d3 o, d3 d, double tmax, bool anyhit)
-{
-    Hit<double> h{-1, tmax, 0.0, 0.0};
-    ListRay32 r;
-    r.o = mk3((float)o.x, (float)o.y, (float)o.z);
-    r.d = mk3((float)d.x, (float)d.y, (float)d.z);
-    r.O = vmax(vabs(r.o.x), vmax(vabs(r.o.y), vabs(r.o.z)));
-    r.D = vmax(vabs(r.d.x), vmax(vabs(r.d.y), vabs(r.d.z)));
-    r.KD = kListFilterK * r.D;
-    r.tmin = (float)Cst<double>::eps;                    // rounds below 1e-4: fewer certain misses
-    r.tmax = (float)tmax;                                // the tmax tests have their own slack
-    float t_sure = __builtin_inff();
-    bool done = false;                                   // any-hit query answered
-    const bool lds = S.lrec != nullptr;                  // the kernel's LDS copy of the list (list_to_lds)
-    for (int i = 0; i < S.n_list; ++i) {
-        if (!wave_any(!done)) break;
-        const int ref = uniform_i(lds ? S.lref[i] : S.list[i]);
-        int verdict = 0;
-        float tlo = 0.0f, thi = __builtin_inff();
-        if (!done) {
-            if (ref & FRT_PRIM_SPHERE) {
-                verdict = list_filter_sphere(r, lds ? S.lrec[3 * i] : S.spheres[ref & ~FRT_PRIM_SPHERE]);
-            } else {
-                const float4 a4 = lds ? S.lrec[3 * i] : S.tris[3 * ref];
-                const float4 b4 = lds ? S.lrec[3 * i + 1] : S.tris[3 * ref + 1];
-                const float4 c4 = lds ? S.lrec[3 * i + 2] : S.tris[3 * ref + 2];
-                verdict = list_filter_tri(r, a4, b4, c4, tlo, thi);
-            }
-        }
-        if (anyhit && verdict == 2) { h.prim = ref; h.t = (double)thi; done = true; continue; }
-        if (verdict == 0 || tlo > t_sure) continue;      // certain miss / beyond a certain hit
-        if (verdict == 2) t_sure = vmin(t_sure, thi);
-        double u, v;
-        const double t = prim_t(S, ref, o, d, Cst<double>::eps, h.t, u, v);
-        if (t > 0.0 && ((ref & FRT_PRIM_SPHERE) || t < h.t)) {
-            h.prim = ref; h.t = t; h.u = u; h.v = v;
-            if (anyhit) done = true;
-        }
-    }
-    return h;
-}
-
 template <int WORLD, int STRIDE, int STACK = 0, typename R>
 FRT_HD Hit<R> trace(const DevScene &S, V3<R> o, V3<R> d, R tmax, bool anyhit, int *stk)
 {
-#if !defined(FRT_EXP_NO_LIST_FILTER)   // experiment builds: the plain fp64 loop (A/B)
-    if constexpr (WORLD == FRT_WORLD_LIST && kIsF64<R>) return trace_list_filtered(S, o, d, tmax, anyhit);
-    else
-#endif
     if constexpr (WORLD == FRT_WORLD_LIST) return trace_list(S, o, d, tmax, anyhit);
     else if constexpr (WORLD == kWorldBvh4) return trace_bvh4<STRIDE, STACK, kBvh4Overflow>(S, o, d, tmax, anyhit, stk);
     else return trace_bvh<STRIDE>(S, o, d, tmax, anyhit, stk);
@@ -647,10 +508,6 @@ FRT_HD bool trav_step_world(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, boo
         T.tmin = bvh_tmin(o);
     }
     if constexpr (WORLD == FRT_WORLD_LIST) {
-#if !defined(FRT_EXP_NO_LIST_FILTER)
-        if constexpr (kIsF64<R>) T.h = trace_list_filtered(S, o, d, T.h.t, anyhit);
-        else
-#endif
         T.h = trace_list(S, o, d, T.h.t, anyhit);
         return true;
     } else if constexpr (WORLD == kWorldBvh4) {

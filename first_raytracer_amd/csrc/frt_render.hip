@@ -42,6 +42,9 @@ constexpr int kBlock = 256;
 constexpr size_t kLdsSceneBytes = 16 * 1024;   // LDS plan: 5-6 blocks/CU x (stack + scene) must fit 160 KiB
 constexpr size_t kLdsOctBytes = 14 * 1024;     // ... with the octant node copies: 5 x (8 + 10 + 14) KiB
 constexpr int kLdsMaxDepth = 16;                // LDS plan: binary stacks of 8 or 16 entries
+// float4 slots of the octant plan's nodes in LDS (scene_to_lds): 8 x 3 per
+// node for the boxes, then one int2 of child refs per node
+__host__ __device__ constexpr int oct_lds_node_slots(int n_nodes) { return 24 * n_nodes + (n_nodes + 1) / 2; }
 #ifndef FRT_QUEUE_GRAB
 #define FRT_QUEUE_GRAB 64
 #endif
@@ -59,7 +62,6 @@ struct DevWork {
     unsigned *counter;                   // work-queue head
     unsigned long long *wave_rays;       // [n_waves][4]: camera, extension, shadow, samples
     uint32_t grab;                       // items a wave takes per queue atomic (at least those it needs)
-    int pool_min;                        // ray-pool kernel: hand out queued rays once this many lanes are free
 };
 
 // slot -> pixel inside a tile: 8x8 blocks, row-major inside a block
@@ -78,9 +80,16 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t m)
 
 // Small scenes (nodes + triangles + shading records + materials, <=
 // kLdsSceneBytes) are copied into LDS once per block and traversed there
-// (ds_read_b128 instead of L1/L2 round trips).  Planar copies: part k of
-// element i at [k * count + i], so lanes reading different elements of the
-// same part hit different banks.
+// (ds_read_b128 instead of L1/L2 round trips).  A wave's ds_read_b128 is
+// served 16 lanes at a time from 64 banks: lanes reading distinct elements
+// stay conflict-free when the elements' 16-B slots differ mod 16.  48-B
+// records do that interleaved ((3 i + k) mod 16: triangles, the octant copies'
+// node boxes), which puts every part at an immediate offset of one address;
+// 64-B and 32-B records are copied planar (part k of element i at
+// [k * count + i]), since interleaved only 4 or 8 slots would be used.
+// Octant plan: 8 x n_nodes box records (3 float4), then the n_nodes child ref
+// pairs (int2, one set for the 8 copies): 392 B per node instead of 512 B,
+// 2 address VALU per node step instead of 5.
 // HBM-resident scenes: the interleaved strides flatten_scene uses, as
 // constants the compiler folds into the address arithmetic (kernel arguments
 // would cost a quarter-rate v_mul_lo_u32 per node / triangle access).
@@ -98,20 +107,24 @@ __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
     constexpr bool WIDE = WORLD == kWorldBvh4, OCT = WORLD == kWorldBvh2Oct;
     float4 *l4 = reinterpret_cast<float4 *>(lds_base);
     const DevScene S0 = S;
-    const int nn = WIDE ? 4 * S0.n_nodes4 : OCT ? 32 * S0.n_nodes : 4 * S0.n_nodes;
+    const int nn = WIDE ? 4 * S0.n_nodes4 : OCT ? oct_lds_node_slots(S0.n_nodes) : 4 * S0.n_nodes;
     const int nt = 3 * S0.n_tris, ns = 2 * S0.n_tris, nm = kMatStride * S0.n_mats;
     if constexpr (WIDE) {
         const float4 *src = reinterpret_cast<const float4 *>(S0.nodes4);
         for (int i = threadIdx.x; i < nn; i += kBlock) l4[(i & 3) * S0.n_nodes4 + (i >> 2)] = src[i];
-    } else if constexpr (OCT) {   // copy o, node j, part k -> [(4 o + k) * n_nodes + j]
-        for (int i = threadIdx.x; i < nn; i += kBlock) {
-            const int e = i >> 2, o = e / S0.n_nodes, j = e - o * S0.n_nodes;
-            l4[(4 * o + (i & 3)) * S0.n_nodes + j] = S0.nodes_oct[i];
+    } else if constexpr (OCT) {   // node e = o * n_nodes + j, part k < 3 -> [3 e + k]; refs of j -> int2 [j]
+        int2 *refs = reinterpret_cast<int2 *>(l4 + 24 * S0.n_nodes);
+        for (int i = threadIdx.x; i < 32 * S0.n_nodes; i += kBlock) {
+            const int e = i >> 2, k = i & 3;
+            const float4 v = S0.nodes_oct[i];
+            if (k < 3) l4[3 * e + k] = v;
+            else if (e < S0.n_nodes) refs[e] = make_int2(f2i(v.x), f2i(v.y));
         }
+        S.node_refs = refs;
     } else {
         for (int i = threadIdx.x; i < nn; i += kBlock) l4[(i & 3) * S0.n_nodes + (i >> 2)] = S0.nodes[i];
     }
-    for (int i = threadIdx.x; i < nt; i += kBlock) l4[nn + (i % 3) * S0.n_tris + i / 3] = S0.tris[i];
+    for (int i = threadIdx.x; i < nt; i += kBlock) l4[nn + i] = S0.tris[i];   // interleaved (48 B)
     for (int i = threadIdx.x; i < ns; i += kBlock) l4[nn + nt + (i & 1) * S0.n_tris + (i >> 1)] = S0.tshade[i];
     for (int i = threadIdx.x; i < nm; i += kBlock) l4[nn + nt + ns + i] = S0.mats[i];
     __syncthreads();
@@ -125,32 +138,10 @@ __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
     S.tris = l4 + nn;
     S.tshade = l4 + nn + nt;
     S.mats = l4 + nn + nt + ns;
-    S.tri_es = 1; S.tri_ps = S0.n_tris;
+    S.tri_es = 3; S.tri_ps = 1;
     S.sh_es = 1; S.sh_ps = S0.n_tris;
 }
 
-// fp64 list kernels: the list's fp32 filter records (trace_list_filtered) in
-// the block's LDS, read with one address per wave (broadcast) in list order;
-// the fp64 records stay in HBM (read only for the filter's candidates).
-__device__ __forceinline__ void list_to_lds(DevScene &S, int *lds_base)
-{
-    float4 *rec = reinterpret_cast<float4 *>(lds_base);
-    int *refs = lds_base + 12 * S.n_list;
-    for (int i = threadIdx.x; i < S.n_list; i += kBlock) {
-        const int ref = S.list[i];
-        refs[i] = ref;
-        if (ref & FRT_PRIM_SPHERE) {
-            rec[3 * i] = S.spheres[ref & ~FRT_PRIM_SPHERE];
-            rec[3 * i + 1] = rec[3 * i + 2] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        } else {
-            rec[3 * i] = S.tris[3 * ref]; rec[3 * i + 1] = S.tris[3 * ref + 1]; rec[3 * i + 2] = S.tris[3 * ref + 2];
-        }
-    }
-    __syncthreads();
-    S.lrec = rec;
-    S.lref = refs;
-}
-constexpr size_t kListLdsEntryBytes = 3 * sizeof(float4) + sizeof(int);
 
 // ------------------------------------------------------------------------
 // the persistent path megakernel
@@ -184,8 +175,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     DevScene S = S0;
     if constexpr (LDS_SCENE) scene_to_lds<WORLD>(S, lds_mem + kStackInts + kItemInts);
     else scene_strides_hbm(S);
-    if constexpr (WORLD == FRT_WORLD_LIST && kIsF64<R>)
-        if (S.n_list <= kListLdsMax) list_to_lds(S, lds_mem + kStackInts + kItemInts);
     const int lane = threadIdx.x & 63;
     const int T2 = W.tile * W.tile;
 
@@ -236,7 +225,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             if (tracing) FRT_DIAG_TICK(3);
             // (LDS-resident binary plans: no leaf postponing, compiled out)
             if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, P.ro, P.rd, P.shadow, stk, ovf,
-                                                                       LDS_SCENE && WORLD == FRT_WORLD_BVH
+                                                                       LDS_SCENE && (WORLD == FRT_WORLD_BVH || WORLD == kWorldBvh2Oct)
                                                                            ? 0 : W.min_desc)) {
                 if (KIND == FRT_INTEGRATOR_PATH && P.shadow) {   // finish the shadow ray here, keep traversing
                     if (path_after_shadow<MATS>(P, T.h.prim < 0)) {
@@ -366,7 +355,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     }
 }
 
-#include "frt_pool.hpp"   // path_pool_megakernel: the same loop with a per-wave ray pool
 
 // ------------------------------------------------------------------------
 // ray queries (frt_trace_device): a buffer of rays through the same
@@ -461,7 +449,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         }
         if (__ballot(tracing || have_next) == 0) break;
         if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, o, d, anyhit, stk, ovf,
-                                                             LDS_SCENE && WORLD == FRT_WORLD_BVH ? 0 : R.min_desc)) {
+                                                             LDS_SCENE && (WORLD == FRT_WORLD_BVH || WORLD == kWorldBvh2Oct) ? 0 : R.min_desc)) {
             tracing = false;
             finish();
         }
@@ -639,7 +627,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
         for (;;) {
             bool ext = false;
             if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, M.P.ro, M.P.rd, M.P.shadow, stk, ovf,
-                                                                 W.min_desc)) {
+                                                                 LDS_SCENE ? 0 : W.min_desc)) {   // LDS plans: compiled out
                 if (M.P.shadow) {               // finish the shadow ray here (mlt_shade's shadow branch)
                     if (!path_after_shadow<(MATS ? kMatsAll : kMatsNone)>(M.P, T.h.prim < 0)) {   // path ended (P.term)
                         tracing = false;
@@ -860,8 +848,6 @@ struct frt_ctx {
 // count (DESIGN.md "Register-cap hazard").  The lambertian kernels (the
 // bench configurations) stay on the greedy allocator.
 static bool bvh4_stack_fits(int depth4, int lds_entries) { return 3 * depth4 <= lds_entries + kBvh4Overflow; }
-// LDS of an fp64 list kernel's filter records (list_to_lds), 0 for longer lists
-static size_t list_lds_bytes(const frt_ctx *c) { return c->n_list <= kListLdsMax ? c->n_list * kListLdsEntryBytes : 0; }
 struct Launcher {
     const void *fn = nullptr;
     size_t lds = 0;
@@ -878,10 +864,8 @@ static Launcher make_launcher(size_t scene_bytes)
     Launcher L;
     L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES, MATS, KIND, R>);
     L.f64 = kIsF64<R>;
-    // scene_bytes: the LDS scene copy, or (fp64 list kernels) the list's filter records
     L.lds = (WORLD != FRT_WORLD_LIST ? (size_t)STACK * kBlock * sizeof(int) : 0) +
-            (size_t)kItemWords * kBlock * sizeof(int) +
-            (LDS || (WORLD == FRT_WORLD_LIST && kIsF64<R>) ? scene_bytes : 0);
+            (size_t)kItemWords * kBlock * sizeof(int) + (LDS ? scene_bytes : 0);
     L.stack = STACK;
     L.waves = WAVES > 1 ? WAVES : 0;
     L.lds_scene = LDS;
@@ -891,27 +875,6 @@ static Launcher make_launcher(size_t scene_bytes)
 #ifndef FRT_EXP_W6
 #define FRT_EXP_W6 6   // experiment builds: the register cap behind the "6 waves" plans
 #endif
-// the ray-pool megakernel (frt_pool.hpp) for the LDS binary plans of lambertian scenes
-template <int STACK, int WORLD>
-static Launcher make_pool_launcher(size_t scene_bytes)
-{
-    Launcher L;
-    const char *e = std::getenv("FRT_POOL");
-    L.fn = e && std::atoi(e) == 2 ? reinterpret_cast<const void *>(&path_pool_megakernel<STACK, WORLD, 5, true>)
-                                   : reinterpret_cast<const void *>(&path_pool_megakernel<STACK, WORLD, 5, false>);
-    L.lds = (size_t)(STACK + kPoolItemWords + kPoolSlotWords) * kBlock * sizeof(int) + scene_bytes;
-    L.stack = STACK;
-    L.waves = 5;
-    L.lds_scene = true;
-    return L;
-}
-// FRT_POOL=1 / 2: the ray-pool kernel (2: with the slab ray re-derived per step);
-// an A/B knob while it is measured, not part of the C-ABI
-static bool pool_enabled()
-{
-    const char *e = std::getenv("FRT_POOL");
-    return e && std::atoi(e) >= 1;
-}
 template <int STACK, bool LDS, int WORLD = FRT_WORLD_BVH, int MATS = kMatsNone>
 static Launcher bvh_launcher(int waves, size_t sb)
 {
@@ -975,14 +938,6 @@ static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
     }
     // LDS-resident binary tree: the per-octant node copies when they fit
     const bool oct = lds && !(flags & FRT_FLAG_NO_OCT) && c->scene_lds_bytes_oct <= kLdsOctBytes;
-    if constexpr (MATS == kMatsNone) {
-        if (lds && pool_enabled() && d < 16) {
-            if (oct) L = d < 8 ? make_pool_launcher<8, kWorldBvh2Oct>(c->scene_lds_bytes_oct)
-                               : make_pool_launcher<16, kWorldBvh2Oct>(c->scene_lds_bytes_oct);
-            else L = d < 8 ? make_pool_launcher<8, FRT_WORLD_BVH>(sb) : make_pool_launcher<16, FRT_WORLD_BVH>(sb);
-            return FRT_OK;
-        }
-    }
     if (oct) {
         L = d < 8 ? bvh_launcher<8, true, kWorldBvh2Oct, MATS>(waves, c->scene_lds_bytes_oct)
                   : bvh_launcher<16, true, kWorldBvh2Oct, MATS>(waves, c->scene_lds_bytes_oct);
@@ -1036,7 +991,7 @@ static int pick_launcher_f64_t(const frt_ctx *c, Launcher &L)
 {
     if (c->world_kind == FRT_WORLD_LIST) {
         // (a 2-wave register cap changed nothing: profiles/r03/r03c_ab_veach_listbox_f64waves.jsonl)
-        L = make_launcher<16, FRT_WORLD_LIST, false, 1, MATS, FRT_INTEGRATOR_PATH, double>(list_lds_bytes(c));
+        L = make_launcher<16, FRT_WORLD_LIST, false, 1, MATS, FRT_INTEGRATOR_PATH, double>(0);
         return FRT_OK;
     }
     const int d = c->stack_needed;
@@ -1615,12 +1570,9 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
         double ng[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
         const double l = std::sqrt(ng[0] * ng[0] + ng[1] * ng[1] + ng[2] * ng[2]);
         for (int k = 0; k < 3; ++k) ng[k] = ng[k] / l;   // unit_vector(cross(e1, e2)), triangle.h:101
-        // w: |x|_inf of each vector rounded up, the magnitudes the fp64 kernels'
-        // fp32 list filter bounds its rounding with (list_filter_tri)
-        auto mabs = [](const double *x) { return round_up(std::max(std::fabs(x[0]), std::max(std::fabs(x[1]), std::fabs(x[2])))); };
-        F.tris[3 * d + 0] = make_float4((float)v[0], (float)v[1], (float)v[2], mabs(v));
-        F.tris[3 * d + 1] = make_float4((float)e1[0], (float)e1[1], (float)e1[2], mabs(e1));
-        F.tris[3 * d + 2] = make_float4((float)e2[0], (float)e2[1], (float)e2[2], mabs(e2));
+        F.tris[3 * d + 0] = make_float4((float)v[0], (float)v[1], (float)v[2], 0.0f);
+        F.tris[3 * d + 1] = make_float4((float)e1[0], (float)e1[1], (float)e1[2], 0.0f);
+        F.tris[3 * d + 2] = make_float4((float)e2[0], (float)e2[1], (float)e2[2], 0.0f);
         const int mat = sv->tri_material[i];
         if (mat < 0 || mat >= nm) return fail(FRT_E_INVALID, "scene view: bad triangle material");
         const int geo = sv->tri_geometry_normal ? (sv->tri_geometry_normal[i] ? 1 : 0) : 1;
@@ -1712,7 +1664,8 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     // octant copies of the binary nodes: child boxes as (near xyz, far xyz).
     // Only the LDS binary plan reads them, and only when they fit its budget
     // (pick_launcher_t): larger scenes get none (8x the node array otherwise).
-    const size_t oct_bytes = sizeof(float4) * (8 * F.nodes.size() + F.tris.size() + F.tshade.size() + F.mats.size());
+    const size_t oct_bytes = sizeof(float4) * (oct_lds_node_slots((int)(F.nodes.size() / 4)) + F.tris.size() +
+                                               F.tshade.size() + F.mats.size());
     if (sv->world_kind == FRT_WORLD_BVH && F.depth < kLdsMaxDepth && oct_bytes <= kLdsOctBytes)
         F.nodes_oct.resize(8 * F.nodes.size());
     for (int o = 0; o < 8 && !F.nodes_oct.empty(); ++o)
@@ -1825,7 +1778,8 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
     c->depth4 = F.depth4;
     c->scene_lds_bytes = sizeof(float4) * (F.nodes.size() + F.tris.size() + F.tshade.size() + F.mats.size());
     c->scene_lds_bytes_oct = F.nodes_oct.empty() ? SIZE_MAX
-                             : sizeof(float4) * (F.nodes_oct.size() + F.tris.size() + F.tshade.size() + F.mats.size());
+                             : sizeof(float4) * (oct_lds_node_slots(S.n_nodes) + F.tris.size() + F.tshade.size() +
+                                                 F.mats.size());
     c->has_f64 = want_f64;
     c->have_scene = true;
     return FRT_OK;
@@ -1922,32 +1876,6 @@ extern "C" int frt_selftest_path_host(const frt_scene_view *sv, const frt_render
     return FRT_OK;
 }
 
-
-// Self-test hook (CPU tests): the fp64 list query with the fp32 filter
-// (trace_list_filtered) against the plain fp64 loop (trace_list) for n rays
-// (8 doubles each: origin, t_max, direction, any-hit flag).  mismatch[i] = 1
-// when the answers differ: closest hit -- primitive, t, u, v bit for bit;
-// any hit -- whether something was hit.  Internal to libfrt.so.
-extern "C" int frt_internal_list_filter_check(const frt_scene_view *sv, const double *rays, int n, int32_t *mismatch)
-{
-    if (!sv || !rays || !mismatch || n < 0 || sv->world_kind != FRT_WORLD_LIST) return FRT_E_INVALID;
-    FlatScene F;
-    std::string err;
-    const int rc = flatten_scene(sv, F, err, true);
-    if (rc != FRT_OK) return rc;
-    const DevScene S = host_scene(F);
-    for (int i = 0; i < n; ++i) {
-        const double *q = rays + 8 * (size_t)i;
-        const d3 o{q[0], q[1], q[2]}, d{q[4], q[5], q[6]};
-        const bool any = q[7] != 0.0;
-        const Hit<double> a = trace_list(S, o, d, q[3], any), b = trace_list_filtered(S, o, d, q[3], any);
-        mismatch[i] = any ? ((a.prim < 0) != (b.prim < 0))
-                          : !(a.prim == b.prim && (a.prim < 0 || (std::memcmp(&a.t, &b.t, 8) == 0 &&
-                                                                  std::memcmp(&a.u, &b.u, 8) == 0 &&
-                                                                  std::memcmp(&a.v, &b.v, 8) == 0)));
-    }
-    return FRT_OK;
-}
 
 // Self-test hook: n PSS-MLT bootstrap eye paths (fresh primary samples from the
 // bootstrap stream) through frt_mlt.hpp on the host; out6[i] = x, y, r, g, b, sc.
@@ -2046,7 +1974,7 @@ static int pick_launcher(const frt_ctx *c, int integrator, int flags, Launcher &
     if (integrator == FRT_INTEGRATOR_AO || c->mats != kMatsNone || (f64 && c->world_kind != FRT_WORLD_LIST))
         return frt_mats::pick(c, integrator, flags, f64, L);   // every kernel with a material set
     if (f64) {   // a lambertian list world (BVH worlds' fp64 kernels carry every material: the other unit)
-        L = make_launcher<16, FRT_WORLD_LIST, false, 1, kMatsNone, FRT_INTEGRATOR_PATH, double>(list_lds_bytes(c));
+        L = make_launcher<16, FRT_WORLD_LIST, false, 1, kMatsNone, FRT_INTEGRATOR_PATH, double>(0);
         return FRT_OK;
     }
     return pick_launcher_t<kMatsNone>(c, flags, L);
@@ -2396,10 +2324,6 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     W.partial = c->partial; W.counter = c->counter; W.wave_rays = c->wave_rays;
     W.trav_min = trav_min(L.lds_scene, p->integrator == FRT_INTEGRATOR_PATH);
     W.min_desc = min_desc(L.lds_scene);
-    {   // FRT_POOL_MIN: the ray-pool kernel's hand-out threshold (A/B knob, not part of the C-ABI)
-        const char *e = std::getenv("FRT_POOL_MIN");
-        W.pool_min = std::min(std::max(e ? std::atoi(e) : 1, 1), 64);
-    }
 
     HIPCHK(c, hipMemsetAsync(c->counter, 0, 64, st));
 #if defined(FRT_DIAG)

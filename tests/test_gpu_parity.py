@@ -164,25 +164,6 @@ def test_bvh4_matches_binary(ctx, cornell_obj, tmp_path):
     assert stn.scene_in_lds == 1 and np.array_equal(noct, b_lds) and stn.rays == stb.rays
 
 
-@pytest.mark.parametrize("flags", [0, frt.FRT_FLAG_NO_OCT])
-def test_ray_pool_matches(ctx, cornell_obj, monkeypatch, flags):
-    """The ray-pool megakernel (frt_pool.hpp: a path's shadow and extension rays
-    traced at once by any free lanes of the wave, answers through LDS slots)
-    renders path_megakernel's film bit for bit, with the same ray counts: the
-    owner applies each answer in path_after_shadow's order."""
-    nx, ny, spp = 96, 64, 16
-    ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, nx / ny))
-    base, st0 = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=29, flags=flags))
-    for tm in ("0", "28", "60"):
-        monkeypatch.setenv("FRT_POOL", "1")
-        monkeypatch.setenv("FRT_TRAV_MIN", tm)
-        pool, st1 = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=29, flags=flags))
-        assert st1.scene_in_lds == 1
-        assert (st1.camera_rays, st1.extension_rays, st1.shadow_rays, st1.samples) == \
-               (st0.camera_rays, st0.extension_rays, st0.shadow_rays, st0.samples)
-        assert np.array_equal(pool, base)
-
-
 def test_lean_plan_rounding(ctx, cornell_obj):
     """The HBM lambertian plans keep less per-lane state (kLean, frt_render.hip):
     each radiance contribution is added to the fp32 item sum as it is found,

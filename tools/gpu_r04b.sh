@@ -1,6 +1,7 @@
 # Round 4, second call: GPU suite on the current build; the slab tests on
 # v_maximum3 / v_minimum3 (this build) against the previous build
-# (build/exp/libfrt_r04b0.so) on Cornell and cornell_1m; veach (C3) with the
+# (build/exp/libfrt_r04b0.so) and the build with leaf postponing compiled out
+# of the LDS plans (build/exp/libfrt_md.so) on Cornell and cornell_1m; veach (C3) with the
 # single-pass fp32 filter vs the plain fp64 list (build/exp/libfrt_nolf.so);
 # ray-pool hand-out thresholds; shard balance with the whole-frame granule
 # (films identical for every shard count); the veach bench line.  Each GPU
@@ -17,10 +18,13 @@ ab() {  # tag, lib ('' = in-tree), perf_ab args...
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.txt 2>&1 \
  && ab smax "" --scene cornell --spp 512 --rounds 3 --bvh gsah --variants default \
  && ab smax libfrt_r04b0.so --scene cornell --spp 512 --rounds 3 --bvh gsah --variants default \
+ && ab smax libfrt_md.so --scene cornell --spp 512 --rounds 3 --bvh gsah --variants default \
  && ab smax "" --scene cornell_1m --spp 256 --rounds 2 --bvh gsah --variants default \
  && ab smax libfrt_r04b0.so --scene cornell_1m --spp 256 --rounds 2 --bvh gsah --variants default \
+ && ab smax libfrt_md.so --scene cornell_1m --spp 256 --rounds 2 --bvh gsah --variants default \
  && ab smax "" --scene cornell --spp 512 --rounds 3 --bvh gsah --variants default \
  && ab smax libfrt_r04b0.so --scene cornell --spp 512 --rounds 3 --bvh gsah --variants default \
+ && ab smax libfrt_md.so --scene cornell --spp 512 --rounds 3 --bvh gsah --variants default \
  && ab veach "" --scene veach --spp 256 --rounds 3 --variants default \
  && ab veach libfrt_nolf.so --scene veach --spp 256 --rounds 3 --variants default \
  && ab pool "" --scene cornell --spp 512 --rounds 3 --bvh gsah --variants default,default/pool1/pmin8,default/pool1/pmin16,default/pool1/pmin32,default/pool2/pmin16 \

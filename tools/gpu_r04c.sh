@@ -1,0 +1,25 @@
+# Round 4, third call: the GPU suite + smoke on the build with the octant plan's
+# 48-B node records (one LDS address per node step), leaf postponing compiled
+# out of the LDS plans, the list filter and the ray pool removed; same-call A/B
+# against the leaf-postponing-only build (build/exp/libfrt_md.so) on Cornell
+# and cornell_1m, veach against the round-4 plain fp64 list build
+# (build/exp/libfrt_nolf.so); then the default and veach bench lines.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
+O=gpurun_out/r04c; mkdir -p $O
+E=first_raytracer_amd/build/exp
+ab() {  # tag, lib ('' = in-tree), perf_ab args...
+  local t=$1 l=$2; shift 2
+  if [ -n "$l" ]; then FRT_LIB_PATH=$E/$l timeout -k 10 300 python -u tools/perf_ab.py "$@" >> $O/ab_$t.jsonl 2>> $O/ab.log
+  else timeout -k 10 300 python -u tools/perf_ab.py "$@" >> $O/ab_$t.jsonl 2>> $O/ab.log; fi
+}
+C="--scene cornell --spp 512 --rounds 3 --bvh gsah --variants default"
+M="--scene cornell_1m --spp 256 --rounds 2 --bvh gsah --variants default"
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.txt 2>&1 \
+ && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
+ && ab oct48 "" $C && ab oct48 libfrt_md.so $C && ab oct48 "" $C && ab oct48 libfrt_md.so $C \
+ && ab oct48 "" $M && ab oct48 libfrt_md.so $M \
+ && ab veach "" --scene veach --spp 256 --rounds 3 --variants default \
+ && ab veach libfrt_nolf.so --scene veach --spp 256 --rounds 3 --variants default \
+ && timeout -k 10 400 python -u bench.py > $O/bench_default.json 2> $O/bench_default.log \
+ && timeout -k 10 400 python -u bench.py --scene veach --spp 1024 > $O/bench_veach.json 2> $O/bench_veach.log

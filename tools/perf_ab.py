@@ -6,7 +6,7 @@ kernel ms and Grays/s as JSON lines.
   python tools/perf_ab.py [--scene cornell|cornell_1m|veach] [--spp 64] [--rounds 5]
                           [--variants default,waves5,default/leaf1]
 
-A variant is FLAG[+FLAG...][/leafN][/travN][/descN][/grabN][/sptN][/spiN][/poolN][/pminN]: render flags (travN sets
+A variant is FLAG[+FLAG...][/leafN][/travN][/descN][/grabN][/sptN][/spiN]: render flags (travN sets
 FRT_TRAV_MIN=N, descN FRT_MIN_DESC=N for its renders), on a scene uploaded with
 FRT_LEAF_SIZE=N (one context per leaf size; default = the library default).
 """
@@ -87,7 +87,7 @@ def main():
         for v in chosen:
             leaf = opt(v, "leaf")
             for key, env in (("trav", "FRT_TRAV_MIN"), ("desc", "FRT_MIN_DESC"), ("grab", "FRT_GRAB"),
-                             ("spt", "FRT_SPI_TARGET"), ("pool", "FRT_POOL"), ("pmin", "FRT_POOL_MIN")):
+                             ("spt", "FRT_SPI_TARGET")):
                 if opt(v, key):
                     os.environ[env] = opt(v, key)
                 else:
