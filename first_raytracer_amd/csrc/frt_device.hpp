@@ -272,12 +272,36 @@ FRT_HD R slab_entry_nf(R nx, R ny, R nz, R fx, R fy, R fz, const SlabRay<R> &r, 
                       smin(vfma(fz, r.invd.z, r.oinv.z), tmax));
     return (tf < tn) ? R(__builtin_inff()) : tn;
 }
+// ... as the interval itself: the box is hit iff tn <= tf, the same decision
+// as slab_entry_nf's for a finite tmax (then tf is finite, so tn <= tf rules
+// out tn = +inf), without the select to +inf and the compare against it
+template <typename R>
+FRT_HD void slab_nf(R nx, R ny, R nz, R fx, R fy, R fz, const SlabRay<R> &r, R tmin, R tmax, R &tn, R &tf)
+{
+    tn = smax(smax(vfma(nx, r.invd.x, r.oinv.x), vfma(ny, r.invd.y, r.oinv.y)), smax(vfma(nz, r.invd.z, r.oinv.z), tmin));
+    tf = smin(smin(vfma(fx, r.invd.x, r.oinv.x), vfma(fy, r.invd.y, r.oinv.y)), smin(vfma(fz, r.invd.z, r.oinv.z), tmax));
+}
 
 // Moller-Trumbore (triangle.h:69-118): returns t, or -1 on miss.  Accepts
 // t in (tmin, tmax] -- the caller resolves t == tmax with the DFS rank tie rule.
 template <typename R>
 FRT_HD R tri_intersect(V3<R> o, V3<R> d, V3<R> v0, V3<R> e1, V3<R> e2, R tmin, R tmax, R &u, R &v)
 {
+    if constexpr (!kIsF64<R>) {
+        // fp32: straight-line code, the same values and decisions.  In a wave the
+        // early outs below only skip work when every lane fails together; as
+        // branches they cost exec-mask bookkeeping and a branch per test.
+        const V3<R> h = cross(d, e2);
+        const R a = dot(e1, h);
+        const R f = rcp(a);
+        const V3<R> s = o - v0;
+        u = f * dot(s, h);
+        const V3<R> q = cross(s, e1);
+        v = f * dot(d, q);
+        const R t = f * dot(e2, q);
+        const bool ok = a != R(0) && !(u < R(0) || u > R(1)) && v >= R(0) && u + v <= R(1) && t > tmin && t <= tmax;
+        return ok ? t : R(-1);
+    }
     const V3<R> h = cross(d, e2);
     const R a = dot(e1, h);
     if (a == R(0)) return R(-1);

@@ -289,26 +289,31 @@ FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyh
     }
     // (a branch-free body -- speculative stack-top read, predicated push -- was
     // 4.5 % slower on Cornell: profiles/r01_exp1_branchy.txt)
-    const R tmin = T.tmin, tbest = T.h.t;
+    // (OCT: t_best held finite -- a ray query may pass t_max = +inf -- so that
+    // slab_nf's tn <= tf is the hit test)
+    const R tmin = T.tmin, tbest = OCT ? vmin(T.h.t, Cst<R>::tmax) : T.h.t;
     while ((unsigned)node < (unsigned)kSentinel) {   // interior node
         FRT_DIAG_TICK(2);
         R t0, t1;
         int c0, c1;
+        bool h0, h1;
         if constexpr (OCT) {   // one address: the record's parts and the refs at immediate offsets
             const float4 *rec = Sn.nodes + u24mul(node, 3);   // 32-bit mad (node < 2^24)
             const float4 n0 = rec[0], n1 = rec[1], n2 = rec[2];
             const int2 cr = S.node_refs[node];
-            t0 = slab_entry_nf<R>(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, tmin, tbest);
-            t1 = slab_entry_nf<R>(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, T.sr, tmin, tbest);
+            R f0, f1;
+            slab_nf<R>(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, tmin, tbest, t0, f0);
+            slab_nf<R>(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, T.sr, tmin, tbest, t1, f1);
+            h0 = t0 <= f0; h1 = t1 <= f1;
             c0 = cr.x; c1 = cr.y;
         } else {
             const float4 n0 = node_part(Sn, node, 0), n1 = node_part(Sn, node, 1);
             const float4 n2 = node_part(Sn, node, 2), n3 = node_part(Sn, node, 3);
             t0 = slab_entry<R>(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, tmin, tbest);
             t1 = slab_entry<R>(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, T.sr, tmin, tbest);
+            h0 = t0 != R(__builtin_inff()); h1 = t1 != R(__builtin_inff());
             c0 = f2i(n3.x); c1 = f2i(n3.y);
         }
-        const bool h0 = t0 != R(__builtin_inff()), h1 = t1 != R(__builtin_inff());
         if (h0 && h1) {
             const bool first0 = t0 <= t1;
             stk[sp * STRIDE] = first0 ? c1 : c0;
