@@ -284,13 +284,15 @@ FRT_HD void slab_nf(R nx, R ny, R nz, R fx, R fy, R fz, const SlabRay<R> &r, R t
 
 // Moller-Trumbore (triangle.h:69-118): returns t, or -1 on miss.  Accepts
 // t in (tmin, tmax] -- the caller resolves t == tmax with the DFS rank tie rule.
-template <typename R>
+// STRAIGHT (fp32): straight-line code, the same values and decisions.  In a
+// wave the early outs only skip work when every lane fails together; as
+// branches they cost exec-mask bookkeeping and a branch per test.  Measured
+// per plan (same call, profiles/r04/r04c): cornell_1m's 4-wide HBM plan
+// +4.4 %, Cornell's LDS plan -2.4 % -- so only the 4-wide traversal uses it.
+template <bool STRAIGHT = false, typename R>
 FRT_HD R tri_intersect(V3<R> o, V3<R> d, V3<R> v0, V3<R> e1, V3<R> e2, R tmin, R tmax, R &u, R &v)
 {
-    if constexpr (!kIsF64<R>) {
-        // fp32: straight-line code, the same values and decisions.  In a wave the
-        // early outs below only skip work when every lane fails together; as
-        // branches they cost exec-mask bookkeeping and a branch per test.
+    if constexpr (STRAIGHT && !kIsF64<R>) {
         const V3<R> h = cross(d, e2);
         const R a = dot(e1, h);
         const R f = rcp(a);

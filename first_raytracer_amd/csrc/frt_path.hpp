@@ -203,23 +203,33 @@ FRT_HD R prim_t(const DevScene &S, int ref, V3<R> o, V3<R> d, R tmin, R tmax, R 
 // Leaf ~node: one sphere, or triangles [first, first + count) (collapse_leaves;
 // the reference's leaves hold one prim, parallel_bvh.h:129-149).  Updates the
 // closest hit with the DFS-rank tie rule; true = any-hit query satisfied.
-template <typename R>
+template <bool STRAIGHT = false, typename R>   // STRAIGHT: see tri_intersect
 FRT_HD bool leaf_hit(const DevScene &S, int lref, V3<R> o, V3<R> d, R tmin, bool anyhit, Hit<R> &h)
 {
-    const bool is_sph = (lref & FRT_PRIM_SPHERE) != 0;
-    const int first = is_sph ? lref : (lref & kLeafIndexMask);
-    const int count = is_sph ? 1 : (lref >> kLeafCountShift) + 1;
+    if (lref & FRT_PRIM_SPHERE) {   // a sphere leaf (one sphere)
+        FRT_DIAG_TICK(1);
+        R u, v;
+        const R t = prim_t(S, lref, o, d, tmin, h.t, u, v);
+        if (t > R(0) && ((t < h.t) || h.prim >= 0)) {
+            h.prim = lref; h.t = t; h.u = u; h.v = v;
+            return anyhit;
+        }
+        return false;
+    }
+    // triangles [first, first + count): no sphere test in the loop.  A hit has
+    // t <= h.t (tri_intersect's t_max); at t == h.t the lower DFS rank wins,
+    // and a triangle rank is below every sphere ref and never below -1 (no hit)
+    const int first = lref & kLeafIndexMask;
+    const int count = (lref >> kLeafCountShift) + 1;
     for (int k = 0; k < count; ++k) {
         FRT_DIAG_TICK(1);
         const int ref = first + k;
         R u, v;
-        const R t = prim_t(S, ref, o, d, tmin, h.t, u, v);
-        if (t > R(0)) {
-            const bool better = (t < h.t) || (h.prim >= 0 && (is_sph || ref < h.prim));
-            if (better) {
-                h.prim = ref; h.t = t; h.u = u; h.v = v;
-                if (anyhit) return true;
-            }
+        const V3<R> a = tri_vec<R>(S, ref, 0), b = tri_vec<R>(S, ref, 1), c = tri_vec<R>(S, ref, 2);
+        const R t = tri_intersect<STRAIGHT>(o, d, a, b, c, tmin, h.t, u, v);
+        if (t > R(0) && ((t < h.t) || ref < h.prim)) {
+            h.prim = ref; h.t = t; h.u = u; h.v = v;
+            if (anyhit) return true;
         }
     }
     return false;
@@ -432,7 +442,7 @@ FRT_HD bool bvh4_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit
         T.sp = sp;
         return false;
     }
-    bool done = node == kSentinel || leaf_hit(S, ~node, o, d, T.tmin, anyhit, T.h);
+    bool done = node == kSentinel || leaf_hit<true>(S, ~node, o, d, T.tmin, anyhit, T.h);
     if (!done) {
         node = pop();
         done = node == kSentinel;

@@ -32,7 +32,9 @@ def main():
     ap.add_argument("--bvh", default="sah", choices=["host", "sah", "ploc", "lbvh", "gsah"],
                     help="sah: binned SAH tree (bench default); host: the reference topology; "
                          "ploc / lbvh: the GPU builders")
-    ap.add_argument("--integrator", default="path", choices=["path", "ao", "normals"])
+    ap.add_argument("--integrator", default="path", choices=["path", "ao", "normals", "pssmlt"],
+                    help="pssmlt: --spp = mutations per pixel, --chains chains")
+    ap.add_argument("--chains", type=int, default=1 << 18)
     ap.add_argument("--env", default="", help="constant environment r,g,b (AO: 1,1,1 unless given)")
     args = ap.parse_args()
     import torch  # noqa: F401  (single HIP runtime)
@@ -65,7 +67,8 @@ def main():
                               "depth": hs.info.bvh_depth}), file=sys.stderr, flush=True)
     else:
         hs = frt.HostScene(kind, obj, nx / ny)
-    integ = {"path": 0, "ao": frt.FRT_INTEGRATOR_AO, "normals": frt.FRT_INTEGRATOR_NORMALS}[args.integrator]
+    integ = {"path": 0, "ao": frt.FRT_INTEGRATOR_AO, "normals": frt.FRT_INTEGRATOR_NORMALS,
+             "pssmlt": None}[args.integrator]
     env = args.env or ("1,1,1" if args.integrator == "ao" else "")
     if env:
         hs.set_env([float(x) for x in env.split(",")])
@@ -93,8 +96,12 @@ def main():
                 else:
                     os.environ.pop(env, None)
             spi = int(opt(v, "spi") or 0)       # samples per work item (0: automatic)
-            p = frt.RenderParams.make(nx, ny, args.spp, seed=0, flags=flags[v.split("/")[0]], samples_per_item=spi,
-                                       integrator=integ)
+            if integ is None:
+                p = frt.RenderParams.pssmlt(nx, ny, args.spp, args.chains, seed=0)
+                p.flags = flags[v.split("/")[0]]
+            else:
+                p = frt.RenderParams.make(nx, ny, args.spp, seed=0, flags=flags[v.split("/")[0]],
+                                           samples_per_item=spi, integrator=integ)
             films[leaf], st = ctxs[leaf].render(p, films.get(leaf))
             if r > 0:
                 res[v].append(st.kernel_ms)
