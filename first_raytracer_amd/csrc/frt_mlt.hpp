@@ -60,7 +60,25 @@ struct PrndSource {
         if (fresh) return r;
         return mlt_mutate(U[(size_t)chain * kMltDims + d], r, d, s2p, logp);
     }
+    // The chain's current values of dims [d0, d0 + 4 N) in N 16-B loads issued
+    // together (d0 % 4 == 0; rows are 368 B = 23 x 16 B), for at().  One per
+    // dimension, each behind the previous dimension's hash and mutation,
+    // exposed the load latency once per primary sample.  Fresh sources read none.
+    template <int N> FRT_HD void fetch(int d0, float4 (&c)[N]) const
+    {
+        if (fresh) return;
+        const float4 *row = reinterpret_cast<const float4 *>(U + (size_t)chain * kMltDims + d0);
+        for (int k = 0; k < N; ++k) c[k] = row[k];
+    }
+    // get(d) with the current value already fetched
+    FRT_HD float at(int d, float cur) const
+    {
+        const float r = rng_u(key, dim0 + (uint32_t)d);
+        if (fresh) return r;
+        return mlt_mutate(cur, r, d, s2p, logp);
+    }
 };
+FRT_HD float f4_at(const float4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 
 struct MltPath {
     PathState<float> P;    // ro, rd, rtmax, shadow, beta, L, nee, nxt_d, depth, prev_spec (prev_p unused)
@@ -72,7 +90,9 @@ struct MltPath {
 // (pssmlt.cpp:115-138 with PixelWidth/Height = nx/ny, dist = ny/(2 half_height)).
 FRT_HD void mlt_begin(MltPath &M, const DevScene &S, const PrndSource &src, int nx, int ny)
 {
-    const float s = src.get(0), t = src.get(1), l0 = src.get(2), l1 = src.get(3);
+    float4 c[1] = {make_float4(0.0f, 0.0f, 0.0f, 0.0f)};
+    src.fetch<1>(0, c);
+    const float s = src.at(0, c[0].x), t = src.at(1, c[0].y), l0 = src.at(2, c[0].z), l1 = src.at(3, c[0].w);
     f3 off = mk3(0, 0, 0);
     if (S.lens_r != 0.0f) {
         const float a = l0 * 2.0f - 1.0f, b = l1 * 2.0f - 1.0f;
@@ -132,7 +152,17 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit<float> &h, const 
     float4 m0 = S.mats[kMatStride * mat], m1 = S.mats[kMatStride * mat + 1];
     const int mtype = f2i(m0.w);
     if constexpr (MATS) apply_texture(S, mat, mtype, h.prim, p, h.u, h.v, m0, m1);
-    const float sc0 = src.get(M.off), sc1 = src.get(M.off + 1);   // scatter rnd (pssmlt.cpp:159-163)
+    // this vertex's primary samples, dims v0 + k (lambertian-only kernels: v0 =
+    // 4 + 8 * vertex, so the 8 dims are two aligned float4; with specular
+    // vertices, which consume 6, each is read on its own)
+    const int v0 = M.off;
+    float4 cur[2] = {make_float4(0.0f, 0.0f, 0.0f, 0.0f), make_float4(0.0f, 0.0f, 0.0f, 0.0f)};
+    if constexpr (!MATS) src.fetch<2>(v0, cur);
+    auto pr = [&](int k) -> float {
+        if constexpr (!MATS) return src.at(v0 + k, f4_at(cur[k >> 2], k & 3));
+        else return src.get(v0 + k);
+    };
+    const float sc0 = pr(0), sc1 = pr(1);               // scatter rnd (pssmlt.cpp:159-163)
     M.off += 3;                                         // consumed at every hit
     if (mtype == FRT_MAT_DIFFUSE_LIGHT && dot(n, P.rd) < 0.0f) {
         const f3 Le = xyz(m1);
@@ -152,13 +182,13 @@ FRT_HD bool mlt_shade(MltPath &M, const DevScene &S, const Hit<float> &h, const 
     if (!(lamb || spec)) return true;                   // diffuse_light seen from behind
     const f3 wi = -normalize(P.rd);
     // NEE prnds (pssmlt.cpp:190-195); the bsdf prnds follow only for the diffuse branch
-    const float rnd0 = src.get(M.off), rnd1 = src.get(M.off + 1), rnd2 = src.get(M.off + 2);
+    const float rnd0 = pr(3), rnd1 = pr(4), rnd2 = pr(5);   // = M.off + 0, 1, 2
     M.off += 3;
     f3 wo, beta_next;
     float pdf;
     SpecMat SM{};
     if (!MATS || lamb) {
-        const float b0 = src.get(M.off), b1 = src.get(M.off + 1);
+        const float b0 = pr(6), b1 = pr(7);             // = M.off + 0, 1
         M.off += 2;
         const Onb<float> uvw = onb_from_w(n);
         wo = onb_local(uvw, cosine_direction(b0, b1));
