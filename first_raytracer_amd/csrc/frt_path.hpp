@@ -186,7 +186,7 @@ template <typename R> FRT_HD CamView<R> cam_view(const DevScene &S)
     else return CamView<R>{S.cam_o, S.cam_llc, S.cam_h, S.cam_v, S.cam_u, S.cam_vv, S.lens_r};
 }
 
-template <typename R>
+template <bool STRAIGHT = false, typename R>
 FRT_HD R prim_t(const DevScene &S, int ref, V3<R> o, V3<R> d, R tmin, R tmax, R &u, R &v)
 {
     if (ref & FRT_PRIM_SPHERE) {
@@ -197,7 +197,7 @@ FRT_HD R prim_t(const DevScene &S, int ref, V3<R> o, V3<R> d, R tmin, R tmax, R 
         return sphere_intersect(o, d, c, r, tmin, tmax);
     }
     const V3<R> a = tri_vec<R>(S, ref, 0), b = tri_vec<R>(S, ref, 1), c = tri_vec<R>(S, ref, 2);
-    return tri_intersect(o, d, a, b, c, tmin, tmax, u, v);
+    return tri_intersect<STRAIGHT>(o, d, a, b, c, tmin, tmax, u, v);
 }
 
 // Leaf ~node: one sphere, or triangles [first, first + count) (collapse_leaves;
@@ -206,6 +206,22 @@ FRT_HD R prim_t(const DevScene &S, int ref, V3<R> o, V3<R> d, R tmin, R tmax, R 
 template <bool STRAIGHT = false, typename R>   // STRAIGHT: see tri_intersect
 FRT_HD bool leaf_hit(const DevScene &S, int lref, V3<R> o, V3<R> d, R tmin, bool anyhit, Hit<R> &h)
 {
+    if constexpr (STRAIGHT) {   // 4-wide traversal: one loop for both kinds (-1.1 % on cornell_1m split, r04d)
+        const bool is_sph = (lref & FRT_PRIM_SPHERE) != 0;
+        const int first = is_sph ? lref : (lref & kLeafIndexMask);
+        const int count = is_sph ? 1 : (lref >> kLeafCountShift) + 1;
+        for (int k = 0; k < count; ++k) {
+            FRT_DIAG_TICK(1);
+            const int ref = first + k;
+            R u, v;
+            const R t = prim_t<STRAIGHT>(S, ref, o, d, tmin, h.t, u, v);
+            if (t > R(0) && ((t < h.t) || (h.prim >= 0 && (is_sph || ref < h.prim)))) {
+                h.prim = ref; h.t = t; h.u = u; h.v = v;
+                if (anyhit) return true;
+            }
+        }
+        return false;
+    }
     if (lref & FRT_PRIM_SPHERE) {   // a sphere leaf (one sphere)
         FRT_DIAG_TICK(1);
         R u, v;
