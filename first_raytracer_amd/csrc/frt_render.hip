@@ -2231,7 +2231,10 @@ extern "C" int frt_diag_read(unsigned long long *out)
 // ~1 GB at any spp (1080p 512 spp keeps its 22 chunks, 550 MB), and frames
 // of any spp fit the 32-bit queue.  FRT_SPI_TARGET overrides the target (0:
 // the first rule alone; A/B knob).  spi_req > 0: the caller's samples per item.
-constexpr double kMaxItemsPerLane = 192.0;
+#ifndef FRT_EXP_ITEMS_CAP
+#define FRT_EXP_ITEMS_CAP 192.0   // experiment builds vary it
+#endif
+constexpr double kMaxItemsPerLane = FRT_EXP_ITEMS_CAP;
 static void work_granule(int integrator, int spp, uint64_t n_slots, long long lanes, int spi_req, int &spi,
                          int &n_chunks)
 {
