@@ -590,8 +590,10 @@ __global__ void mlt_film_to_float(const unsigned long long *__restrict__ acc, fl
 // state, then one proposal per mutation); traversal steps interleave with
 // shading as in path_megakernel
 #ifndef FRT_EXP_MLT_WAVES
-#define FRT_EXP_MLT_WAVES 5      // register cap of the chain kernel: 5 waves/SIMD, +17 % over the
-#endif                           // compiler's 4 (profiles/r01_expmlt1.txt); experiment builds vary it
+#define FRT_EXP_MLT_WAVES 4      // register cap of the chain kernel: 4 waves/SIMD.  Round 1 measured 5
+#endif                           // +17 % over the compiler's own allocation (profiles/r01_expmlt1.txt);
+                                 // round 4's kernel: 4 waves 690.8 ms, 5 waves 700.5, 6 waves 783.9
+                                 // (same call, profiles/r04/r04g); experiment builds vary it
 template <int STACK, int WORLD, bool LDS_SCENE, bool MATS>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_MLT_WAVES))) void mlt_megakernel(
     const DevScene S0, const MltWork W)
@@ -2231,10 +2233,14 @@ extern "C" int frt_diag_read(unsigned long long *out)
 // ~1 GB at any spp (1080p 512 spp keeps its 22 chunks, 550 MB), and frames
 // of any spp fit the 32-bit queue.  FRT_SPI_TARGET overrides the target (0:
 // the first rule alone; A/B knob).  spi_req > 0: the caller's samples per item.
-#ifndef FRT_EXP_ITEMS_CAP
-#define FRT_EXP_ITEMS_CAP 192.0   // experiment builds vary it
-#endif
-constexpr double kMaxItemsPerLane = FRT_EXP_ITEMS_CAP;
+// Round 4: the chunks are the whole frame's for every shard count (films
+// identical at any N), so at N = 8 a shard has an eighth of the items.  Path
+// items of 8 samples under a cap of 384 items per lane (1080p 512 spp: 57 / 64
+// chunks, partial sums 1.4 / 1.6 GB) keep ~40 items per lane in an eighth:
+// predicted 8-way speedup of the render Cornell 6.79 -> 7.37, cornell_1m
+// 6.64 -> 7.20 (shards timed alone, tools/shard_balance.py); at N = 1 Cornell
+// +0.5 %, cornell_1m -0.4 % time (profiles/r04/r04g).
+constexpr double kMaxItemsPerLane = 384.0;
 static void work_granule(int integrator, int spp, uint64_t n_slots, long long lanes, int spi_req, int &spi,
                          int &n_chunks)
 {
@@ -2242,7 +2248,7 @@ static void work_granule(int integrator, int spp, uint64_t n_slots, long long la
     if (spi <= 0) {
         const char *tgt = std::getenv("FRT_SPI_TARGET");
         const int target = tgt ? std::atoi(tgt)
-                               : integrator == FRT_INTEGRATOR_PATH ? 24 : integrator == FRT_INTEGRATOR_AO ? 96 : 128;
+                               : integrator == FRT_INTEGRATOR_PATH ? 8 : integrator == FRT_INTEGRATOR_AO ? 96 : 128;
         const double slots = std::max((double)n_slots, 1.0);
         const double k_lanes = std::max(1.0, std::round(40.0 * (double)lanes / slots));
         double k = k_lanes;
