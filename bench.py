@@ -188,8 +188,8 @@ def mlt_block_rmse(kind, obj, nx, ny, film, threads, seconds, spp=256, block=8, 
     contribution of N_Init = 10^4 bootstrap paths (pssmlt.cpp:303-312): the
     whole image inherits b's sampling error (several % on Cornell, where
     camera paths that see the light score ~17).  The oracle recomputes the b
-    this render used (same bootstrap streams) and a reference b from 10^6
-    paths of another stream; `b_factor` = b_ref / b_used undoes the
+    this render used (same bootstrap streams) and a reference b from 10^7
+    paths of other streams; `b_factor` = b_ref / b_used undoes the
     normalisation noise, so the remaining error is the chains' own.  The light's
     blocks (radiance ~17) carry most of the squared error of both estimators,
     so the gates are on the b-corrected film: the median per-block relative
@@ -223,7 +223,15 @@ def mlt_block_rmse(kind, obj, nx, ny, film, threads, seconds, spp=256, block=8, 
             break
         nb = int(min(bx * by, nb * min(16.0, max(2.0, seconds / max(dt, 1e-3)))))
     b_used = sc.mlt_bootstrap(nx, ny, seed=seed, n_init=n_init)
-    b_ref = sc.mlt_bootstrap(nx, ny, seed=seed ^ 0x5EEDB00F, n_init=1000000)
+    # reference b: 16 x 625,000 paths of independent streams on `threads` host
+    # threads (the oracle call releases the GIL): relative noise ~0.4 %
+    # (a single path's sc has relative std ~13 on Cornell), against 1.3 % at 10^6
+    from concurrent.futures import ThreadPoolExecutor
+    n_ref_parts, n_ref_each = 16, 625000
+    with ThreadPoolExecutor(max_workers=max(1, min(threads, n_ref_parts))) as ex:
+        parts = list(ex.map(lambda k: sc.mlt_bootstrap(nx, ny, seed=(seed ^ 0x5EEDB00F) + 7919 * k,
+                                                       n_init=n_ref_each), range(n_ref_parts)))
+    b_ref = float(np.mean(parts))
     bf = b_ref / b_used
     ref = 0.5 * (h1 + h2)
     rmse = float(np.sqrt(np.mean((g - ref) ** 2)))
@@ -237,6 +245,7 @@ def mlt_block_rmse(kind, obj, nx, ny, film, threads, seconds, spp=256, block=8, 
             "mean_rel_err": float(g.mean() / ref.mean() - 1.0),
             "mean_rel_err_b_corrected": float(gc.mean() / ref.mean() - 1.0),
             "b_used": b_used, "b_ref": b_ref, "b_factor": bf, "n_init": n_init,
+            "b_ref_paths": n_ref_parts * n_ref_each, "b_ref_rel_noise": float(np.std(parts) / np.mean(parts) / 4.0),
             "blocks": int(len(ids)), "block": block, "block_frac": round(len(ids) / (bx * by), 4),
             "oracle_spp": spp, "max_depth": MLT_MAX_PATH, "seconds": round(dt, 1),
             "tolerance": {"rel_block_err_median": 0.05, "mean_rel_err_b_corrected": 0.02}}

@@ -129,7 +129,7 @@ def test_block_means_match_oracle_path(ctx, cornell_obj):
     mutations/pixel over 1536 chains = 4096 mutations a chain, the bench's
     chain length (start-up bias ~0 there).  The film is first corrected for
     the noise of PSS-MLT's normaliser b (10^4 bootstrap paths, pssmlt.cpp:303-
-    312) with the oracle's b from 10^6 paths.  Tolerance: median per-block
+    312) with the oracle's b from 10^7 paths.  Tolerance: median per-block
     relative error <= 0.05, mean over the blocks within 2 %."""
     import bench
     nx, ny = 128, 96
