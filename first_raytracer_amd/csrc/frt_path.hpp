@@ -142,7 +142,7 @@ template <typename R> struct Hit {
 constexpr int kLeafCountShift = 27, kLeafIndexMask = (1 << kLeafCountShift) - 1, kLeafIndexLimit = 1 << kLeafCountShift;
 constexpr int kLeafMax = 8, kLeafDefault = 4, kLeafSmallScene = 2;
 constexpr int kTravMinLds = 12, kTravMinHbm = 32;           // PSS-MLT, AO, normals: see trav_min()
-constexpr int kTravMinLdsPath = 28, kTravMinHbmPath = 40;   // path::Li
+constexpr int kTravMinLdsPath = 20, kTravMinHbmPath = 40;   // path::Li
 constexpr int kMinDescLds = 0, kMinDescHbm = 8;     // leaf postponing: see min_desc()
 
 FRT_HD float4 node_part(const DevScene &S, int i, int k) { return S.nodes[i * S.node_es + k * S.node_ps]; }

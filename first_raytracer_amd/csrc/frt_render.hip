@@ -1197,7 +1197,9 @@ struct FlatScene {
 // bench's 1080p / 512 spp (same call, profiles/r02/r02_ab_trav_min_512spp.txt):
 // path 28 from LDS (Cornell 308.0 -> 301.4 ms; 12 was round 1's 64-spp
 // optimum, profiles/r01_ab_perf6.jsonl) and 40 from HBM (cornell_1m 863.5 ->
-// 857.3 ms); PSS-MLT and AO keep 12 / 32 (28 costs them 4-5 %).
+// 857.3 ms); PSS-MLT and AO keep 12 / 32 (28 costs them 4-5 %).  Round 4's
+// cheaper LDS node loop moved the LDS path optimum to 20 (Cornell 245.3 ->
+// 242.5 ms; 16 / 24: 243.4 / 243.7; profiles/r04/r04{h,i}/ab_*.jsonl).
 // FRT_TRAV_MIN overrides (tuning knob of this library, not part of the C-ABI).
 static int trav_min(bool lds_scene, bool path = false)
 {
