@@ -125,19 +125,27 @@ def test_block_means_match_oracle_path(ctx, cornell_obj):
     """C5's RMSE gate at a reduced size (bench.py mlt_block_rmse, the same
     comparison the bench line reports at 1080p): the GPU's PSS-MLT film in
     8x8-block means against the oracle's fp64 path::Li at pssmlt's depth cap
-    (max_depth 10), 256 spp in two independent halves.  128x96 at 512
-    mutations/pixel over 1536 chains = 4096 mutations a chain, the bench's
-    chain length (start-up bias ~0 there).  The film is first corrected for
-    the noise of PSS-MLT's normaliser b (10^4 bootstrap paths, pssmlt.cpp:303-
-    312) with the oracle's b from 10^7 paths.  Tolerance: median per-block
-    relative error <= 0.05, mean over the blocks within 2 %."""
+    (max_depth 10), 256 spp in two independent halves.  128x96 at 1024
+    mutations/pixel over 1536 chains = 8192 mutations a chain.  Each film is
+    first corrected for the noise of PSS-MLT's normaliser b (10^4 bootstrap
+    paths, pssmlt.cpp:303-312) with the oracle's b from 10^7 paths.  One
+    run's mean still carries the chains' own noise and start-up transient
+    (a single seed at 512 mutations/pixel read +2.6 % with b's noise out,
+    profiles/r04/r04j), so the mean is taken over four
+    independent runs (seeds 3..6).  Tolerance: median per-block relative error
+    <= 0.05 in every run, mean over the blocks and runs within 2 %."""
     import bench
     nx, ny = 128, 96
     ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, nx / ny))
-    film = np.zeros((ny, nx, 3), np.float32)
-    film, st = ctx.render(frt.RenderParams.pssmlt(nx, ny, 512, 1536, seed=3), film)
-    r = bench.mlt_block_rmse("cornell_box_obj", cornell_obj, nx, ny, film.reshape(-1), 16, 0.0, spp=256, seed=3)
-    print("pssmlt vs oracle path blocks:", r)
-    assert r["blocks"] == (nx // 8) * (ny // 8)
-    assert r["rel_block_err_median"] <= r["tolerance"]["rel_block_err_median"]
-    assert abs(r["mean_rel_err_b_corrected"]) <= r["tolerance"]["mean_rel_err_b_corrected"]
+    errs = []
+    for seed in (3, 4, 5, 6):
+        film = np.zeros((ny, nx, 3), np.float32)
+        film, st = ctx.render(frt.RenderParams.pssmlt(nx, ny, 1024, 1536, seed=seed), film)
+        r = bench.mlt_block_rmse("cornell_box_obj", cornell_obj, nx, ny, film.reshape(-1), 16, 0.0, spp=256,
+                                 seed=seed)
+        print("seed", seed, "pssmlt vs oracle path blocks:", r)
+        assert r["blocks"] == (nx // 8) * (ny // 8)
+        assert r["rel_block_err_median"] <= r["tolerance"]["rel_block_err_median"]
+        errs.append(r["mean_rel_err_b_corrected"])
+    print("mean_rel_err_b_corrected per seed", errs, "mean", float(np.mean(errs)))
+    assert abs(float(np.mean(errs))) <= r["tolerance"]["mean_rel_err_b_corrected"]
