@@ -19,10 +19,11 @@ V="--scene veach --spp 256 --rounds 3 --variants default"
  && FRT_LIB_PATH=$E/libfrt_f64fast.so timeout -k 10 300 python -u tools/perf_ab.py $V >> $O/ab_f64div.jsonl 2>> $O/ab.log \
  && FRT_LIB_PATH=$E/libfrt_f64ref.so timeout -k 10 300 python -u tools/perf_ab.py $V >> $O/ab_f64div.jsonl 2>> $O/ab.log \
  && FRT_LIB_PATH=$E/libfrt_f64fast.so timeout -k 10 300 python -u tools/perf_ab.py $V >> $O/ab_f64div.jsonl 2>> $O/ab.log
+rc=$?
 # timing build with one mix32 round per path random number (invalid against the
 # oracle, timing only: build/exp/libfrt_rngcheap.so vs libfrt_rngref.so)
 C="--scene cornell --spp 512 --rounds 3 --bvh gsah --variants default"
 M="--scene cornell_1m --spp 256 --rounds 2 --bvh gsah --variants default"
 ab() { local l=$1; shift; FRT_LIB_PATH=$E/$l timeout -k 10 300 python -u tools/perf_ab.py "$@" >> $O/ab_rng.jsonl 2>> $O/ab.log; }
-[ $? = 0 ] && ab libfrt_rngref.so $C && ab libfrt_rngcheap.so $C && ab libfrt_rngref.so $C && ab libfrt_rngcheap.so $C \
+[ $rc = 0 ] && ab libfrt_rngref.so $C && ab libfrt_rngcheap.so $C && ab libfrt_rngref.so $C && ab libfrt_rngcheap.so $C \
  && ab libfrt_rngref.so $M && ab libfrt_rngcheap.so $M
