@@ -10,12 +10,13 @@ timeout -k 10 400 python -u tools/perf_ab.py --scene cornell_1m --spp 512 --roun
       --variants default,default/leaf3,default/leaf5 > $O/ab_1m_leaf.jsonl 2>> $O/ab.log \
  && timeout -k 10 300 python -u tools/perf_ab.py --scene cornell --spp 512 --rounds 3 --bvh gsah --integrator ao \
       --variants default,default/trav6,default/trav20,default/trav28 > $O/ab_ao_trav.jsonl 2>> $O/ab.log
+rc0=$?
 # C3 timing build: fp64 reciprocal / division as v_rcp_f64 + two Newton steps
 # instead of the IEEE sequence (not correctly rounded; timing only):
 # build/exp/libfrt_f64fast.so vs libfrt_f64ref.so (the same source)
 E=first_raytracer_amd/build/exp
 V="--scene veach --spp 256 --rounds 3 --variants default"
-[ $? = 0 ] && FRT_LIB_PATH=$E/libfrt_f64ref.so timeout -k 10 300 python -u tools/perf_ab.py $V >> $O/ab_f64div.jsonl 2>> $O/ab.log \
+[ $rc0 = 0 ] && FRT_LIB_PATH=$E/libfrt_f64ref.so timeout -k 10 300 python -u tools/perf_ab.py $V >> $O/ab_f64div.jsonl 2>> $O/ab.log \
  && FRT_LIB_PATH=$E/libfrt_f64fast.so timeout -k 10 300 python -u tools/perf_ab.py $V >> $O/ab_f64div.jsonl 2>> $O/ab.log \
  && FRT_LIB_PATH=$E/libfrt_f64ref.so timeout -k 10 300 python -u tools/perf_ab.py $V >> $O/ab_f64div.jsonl 2>> $O/ab.log \
  && FRT_LIB_PATH=$E/libfrt_f64fast.so timeout -k 10 300 python -u tools/perf_ab.py $V >> $O/ab_f64div.jsonl 2>> $O/ab.log
