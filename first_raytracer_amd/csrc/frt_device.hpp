@@ -134,10 +134,14 @@ FRT_HD RngKey rng_key(uint32_t seed, uint32_t pixel, uint32_t sample)
     k.k1 = mix32(mix32(a + pixel * 0x632BE5ABU) ^ (sample * 0x85157AF5U + 0x5851F42DU));
     return k;
 }
-// uniform in [0,1) with 24 bits: exact in fp32 and fp64
+// uniform in [0,1) with 24 bits: exact in fp32 and fp64.  One mix32 round
+// per dimension over the (pixel, sample) key, which is itself two rounds
+// deep; a second round per dimension (rounds 1-3) cost Cornell 1.9 % and the
+// PSS-MLT chain kernel 3 % (two quarter-rate multiplies per random number;
+// same-call timing builds, profiles/r04/r04{k,m}).
 FRT_HD float rng_u(RngKey k, uint32_t dim)
 {
-    const uint32_t h = mix32(mix32(k.k0 ^ (dim * 0x85EBCA77U + 0xC2B2AE3DU)) + k.k1);
+    const uint32_t h = mix32((k.k0 ^ (dim * 0x85EBCA77U + 0xC2B2AE3DU)) + k.k1);
     return (float)(h >> 8) * (1.0f / 16777216.0f);
 }
 template <typename R> FRT_HD R rng_r(RngKey k, uint32_t dim) { return R(rng_u(k, dim)); }

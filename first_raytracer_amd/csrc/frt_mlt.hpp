@@ -46,18 +46,6 @@ FRT_HD float mlt_mutate(float cur, float r, int d, float s2p, float logp)
     return mlt_perturb(cur, 1.0f / 64.0f, 2.77258872223978123767f /* log(16) */, r);
 }
 
-// PSS-MLT primary samples (chain states, proposals, bootstrap paths): one
-// mix32 round per dimension over the (chain, step) key, which is itself two
-// rounds deep (rng_key).  rng_u's second round per dimension cost 3 % of the
-// chain kernel (two quarter-rate multiplies per primary sample; same-call
-// timing build, profiles/r04/r04k); the path kernels keep rng_u.  Identical to
-// oracle/frt_oracle.c rng_u_mlt (DESIGN.md "PSS-MLT streams").
-FRT_HD float rng_u_mlt(RngKey k, uint32_t dim)
-{
-    const uint32_t h = mix32((k.k0 ^ (dim * 0x85EBCA77U + 0xC2B2AE3DU)) + k.k1);
-    return (float)(h >> 8) * (1.0f / 16777216.0f);
-}
-
 // Source of primary samples for one eye path.
 struct PrndSource {
     const float *U;        // chain states [n_chains][dim] (null: bootstrap / fresh)
@@ -68,7 +56,7 @@ struct PrndSource {
     float s2p, logp;       // pixel dims (0,1): s1 = 2/(nx+ny), s2 = 0.1f
     FRT_HD float get(int d) const
     {
-        const float r = rng_u_mlt(key, dim0 + (uint32_t)d);
+        const float r = rng_u(key, dim0 + (uint32_t)d);
         if (fresh) return r;
         return mlt_mutate(U[(size_t)chain * kMltDims + d], r, d, s2p, logp);
     }
@@ -85,7 +73,7 @@ struct PrndSource {
     // get(d) with the current value already fetched
     FRT_HD float at(int d, float cur) const
     {
-        const float r = rng_u_mlt(key, dim0 + (uint32_t)d);
+        const float r = rng_u(key, dim0 + (uint32_t)d);
         if (fresh) return r;
         return mlt_mutate(cur, r, d, s2p, logp);
     }

@@ -730,7 +730,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
                 if (e < total) {
                     const int d = (int)(e - r * (uint32_t)kMltDims);
                     float *row = W.U + (size_t)(jl & 0x7fffffffu) * kMltDims;   // j < 2^31: bit 31 = fresh
-                    const float u = rng_u_mlt(kl, 2u + (uint32_t)d);
+                    const float u = rng_u(kl, 2u + (uint32_t)d);
                     row[d] = (jl >> 31) ? u : mlt_mutate(row[d], u, d, W.s2p, W.logp);
                 }
             }

@@ -66,8 +66,6 @@ def lib():
                                     ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(Counters)]
         L.ora_rng_uniform.argtypes = [ctypes.c_uint32] * 4
         L.ora_rng_uniform.restype = ctypes.c_double
-        L.ora_rng_uniform_mlt.argtypes = [ctypes.c_uint32] * 4
-        L.ora_rng_uniform_mlt.restype = ctypes.c_double
         L.ora_kat_tri_hit.argtypes = [dp, dp, ctypes.c_int, dp, dp, ctypes.c_double, ctypes.c_double, dp]
         L.ora_kat_sphere_hit.argtypes = [dp, ctypes.c_double, dp, dp, ctypes.c_double, ctypes.c_double, dp]
         L.ora_kat_texture_sphere.argtypes = [dp, ctypes.c_double, dp, dp, ctypes.c_double, ctypes.c_double, dp]
@@ -296,7 +294,3 @@ class OracleScene:
 def rng_uniform(seed, pixel, sample, dim):
     return lib().ora_rng_uniform(seed, pixel, sample, dim)
 
-
-def rng_uniform_mlt(seed, pixel, sample, dim):
-    """PSS-MLT primary samples (one mix32 round per dimension; frt_oracle.c rng_u_mlt)."""
-    return lib().ora_rng_uniform_mlt(seed, pixel, sample, dim)

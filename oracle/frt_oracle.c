@@ -48,24 +48,12 @@ static inline rng_key rng_make(uint32_t seed, uint32_t pixel, uint32_t sample)
 }
 static inline double rng_u(rng_key k, uint32_t dim)
 {
-    uint32_t h = mix32(mix32(k.k0 ^ (dim * 0x85EBCA77U + 0xC2B2AE3DU)) + k.k1);
+    uint32_t h = mix32((k.k0 ^ (dim * 0x85EBCA77U + 0xC2B2AE3DU)) + k.k1);   /* one round per dimension (round 4) */
     return (double)(h >> 8) * (1.0 / 16777216.0);
 }
 double ora_rng_uniform(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t dim)
 {
     return rng_u(rng_make(seed, pixel, sample), dim);
-}
-/* PSS-MLT primary samples (chain states, proposals, bootstrap paths): one mix32
- * round per dimension over the (chain, step) key -- the key itself is already
- * two rounds deep (csrc/frt_mlt.hpp rng_u_mlt; DESIGN.md "PSS-MLT streams") */
-static inline double rng_u_mlt(rng_key k, uint32_t dim)
-{
-    uint32_t h = mix32((k.k0 ^ (dim * 0x85EBCA77U + 0xC2B2AE3DU)) + k.k1);
-    return (double)(h >> 8) * (1.0 / 16777216.0);
-}
-double ora_rng_uniform_mlt(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t dim)
-{
-    return rng_u_mlt(rng_make(seed, pixel, sample), dim);
 }
 /* dimension layout: camera 0..3 (path.cpp:131-133); bounce at depth d uses
  * base = 4 + 8 d: scatter get3d +0..2 (path.cpp:36), light pick get1d +3
@@ -1346,18 +1334,18 @@ static void *mlt_worker(void *arg)
     memset(&j->cnt, 0, sizeof j->cnt);
     for (int c = j->c0; c < j->c1; ++c) {
         rng_key k0 = rng_make(j->seed ^ 0x3C6EF372U, (uint32_t)c, 0u);
-        for (int d = 0; d < MLT_DIMS; ++d) cur[d] = rng_u_mlt(k0, (uint32_t)(2 + d));
+        for (int d = 0; d < MLT_DIMS; ++d) cur[d] = rng_u(k0, (uint32_t)(2 + d));
         mlt_contrib C = mlt_eye_path(j->s, cur, j->nx, j->ny, &j->cnt);
         for (long long t = 0; t < j->steps; ++t) {
             rng_key k = rng_make(j->seed ^ 0x3C6EF372U, (uint32_t)c, (uint32_t)(t + 1));
             double large;
             if (rng_u(k, 0) < MLT_LARGE_STEP_PROB) {
-                for (int d = 0; d < MLT_DIMS; ++d) prop[d] = rng_u_mlt(k, (uint32_t)(2 + d));
+                for (int d = 0; d < MLT_DIMS; ++d) prop[d] = rng_u(k, (uint32_t)(2 + d));
                 large = 1.0;
             } else {
-                prop[0] = mlt_perturb(cur[0], s1p, s2p, rng_u_mlt(k, 2));
-                prop[1] = mlt_perturb(cur[1], s1p, s2p, rng_u_mlt(k, 3));
-                for (int d = 2; d < MLT_DIMS; ++d) prop[d] = mlt_perturb(cur[d], 1.0 / 1024.0, 1.0 / 64.0, rng_u_mlt(k, (uint32_t)(2 + d)));
+                prop[0] = mlt_perturb(cur[0], s1p, s2p, rng_u(k, 2));
+                prop[1] = mlt_perturb(cur[1], s1p, s2p, rng_u(k, 3));
+                for (int d = 2; d < MLT_DIMS; ++d) prop[d] = mlt_perturb(cur[d], 1.0 / 1024.0, 1.0 / 64.0, rng_u(k, (uint32_t)(2 + d)));
                 large = 0.0;
             }
             mlt_contrib P = mlt_eye_path(j->s, prop, j->nx, j->ny, &j->cnt);
@@ -1381,7 +1369,7 @@ double ora_mlt_bootstrap(const ora_scene *s, int nx, int ny, uint32_t seed, int 
     double b = 0.0;
     for (int i = 0; i < n_init; ++i) {
         rng_key k = rng_make(seed ^ 0xB5297A4DU, (uint32_t)i, 0u);
-        for (int d = 0; d < MLT_DIMS; ++d) prnds[d] = rng_u_mlt(k, (uint32_t)d);
+        for (int d = 0; d < MLT_DIMS; ++d) prnds[d] = rng_u(k, (uint32_t)d);
         b += mlt_eye_path(s, prnds, nx, ny, &cnt).sc;
     }
     return b / n_init;

@@ -125,7 +125,6 @@ int  ora_world_hit(const ora_scene *s, const double *o, const double *d, double 
 
 /* RNG stream spec (shared with the HIP kernels). */
 double   ora_rng_uniform(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t dim);
-double   ora_rng_uniform_mlt(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t dim);   /* PSS-MLT primary samples */
 
 /* ---- component known-answer entry points (checked against oracle/_ref) ---- */
 /* tri: 9 doubles v0 v1 v2; geo=1 geometric normal, else normals n9.

@@ -57,7 +57,7 @@ def test_pssmlt_eye_paths(kind, objfix, request):
     osc = oracle.OracleScene(kind, obj, nx / ny)
     ref = np.zeros((n, 6))
     for i in range(n):
-        pr = oracle.darr([oracle.rng_uniform_mlt(seed ^ 0xB5297A4D, i, 0, d) for d in range(92)])
+        pr = oracle.darr([oracle.rng_uniform(seed ^ 0xB5297A4D, i, 0, d) for d in range(92)])
         out = oracle.darr(np.zeros(6))
         oracle.lib().ora_mlt_eye_path(osc.ptr, nx, ny, pr[1], out[1])
         ref[i] = out[0]
