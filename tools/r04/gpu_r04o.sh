@@ -23,3 +23,11 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
  && ab m "" $M && ab m libfrt_rng1.so $M \
  && ab mlt "" $P && ab mlt libfrt_rng1.so $P \
  && ab ao "" $A && ab ao libfrt_rng1.so $A && ab nrm "" $N && ab nrm libfrt_rng1.so $N
+rc=$?
+# the 4-wide node test's plane pairs as packed FMAs too (build/exp/libfrt_pk4.so:
+# this source + 3 v_pk_fma_f32 per child instead of 6 v_fma_f32; round 3 measured
+# a similar build 3 % slower)
+[ $rc = 0 ] && ab m4 "" --scene cornell_1m --spp 256 --rounds 2 --bvh gsah --variants default \
+ && ab m4 libfrt_pk4.so --scene cornell_1m --spp 256 --rounds 2 --bvh gsah --variants default \
+ && ab m4 "" --scene cornell_1m --spp 256 --rounds 2 --bvh gsah --variants default \
+ && ab m4 libfrt_pk4.so --scene cornell_1m --spp 256 --rounds 2 --bvh gsah --variants default
