@@ -265,10 +265,26 @@ FRT_HD R slab_entry(R lox, R loy, R loz, R hix, R hiy, R hiz, const SlabRay<R> &
     return (tf < tn) ? R(__builtin_inff()) : tn;
 }
 
-// two fp32 lanes for packed math (v_pk_fma_f32 on gfx950: two FMAs per lane
-// and instruction, each rounded once like the scalar v_fma_f32)
-typedef float float2v __attribute__((ext_vector_type(2)));
-FRT_HD float2v pk_fma(float2v a, float2v b, float2v c) { return __builtin_elementwise_fma(a, b, c); }
+// the same test on a box stored as (near, far) planes for the ray's octant
+// (bvh2_step OCT): bit-identical to slab_entry on the (lo, hi) box
+template <typename R>
+FRT_HD R slab_entry_nf(R nx, R ny, R nz, R fx, R fy, R fz, const SlabRay<R> &r, R tmin, R tmax)
+{
+    const R tn = smax(smax(vfma(nx, r.invd.x, r.oinv.x), vfma(ny, r.invd.y, r.oinv.y)),
+                      smax(vfma(nz, r.invd.z, r.oinv.z), tmin));
+    const R tf = smin(smin(vfma(fx, r.invd.x, r.oinv.x), vfma(fy, r.invd.y, r.oinv.y)),
+                      smin(vfma(fz, r.invd.z, r.oinv.z), tmax));
+    return (tf < tn) ? R(__builtin_inff()) : tn;
+}
+// ... as the interval itself: the box is hit iff tn <= tf, the same decision
+// as slab_entry_nf's for a finite tmax (then tf is finite, so tn <= tf rules
+// out tn = +inf), without the select to +inf and the compare against it
+template <typename R>
+FRT_HD void slab_nf(R nx, R ny, R nz, R fx, R fy, R fz, const SlabRay<R> &r, R tmin, R tmax, R &tn, R &tf)
+{
+    tn = smax(smax(vfma(nx, r.invd.x, r.oinv.x), vfma(ny, r.invd.y, r.oinv.y)), smax(vfma(nz, r.invd.z, r.oinv.z), tmin));
+    tf = smin(smin(vfma(fx, r.invd.x, r.oinv.x), vfma(fy, r.invd.y, r.oinv.y)), smin(vfma(fz, r.invd.z, r.oinv.z), tmax));
+}
 
 // Moller-Trumbore (triangle.h:69-118): returns t, or -1 on miss.  Accepts
 // t in (tmin, tmax] -- the caller resolves t == tmax with the DFS rank tie rule.

@@ -316,7 +316,7 @@ FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyh
     // (a branch-free body -- speculative stack-top read, predicated push -- was
     // 4.5 % slower on Cornell: profiles/r01_exp1_branchy.txt)
     // (OCT: t_best held finite -- a ray query may pass t_max = +inf -- so that
-    // tn <= tf is the hit test)
+    // slab_nf's tn <= tf is the hit test)
     const R tmin = T.tmin, tbest = OCT ? vmin(T.h.t, Cst<R>::tmax) : T.h.t;
     while ((unsigned)node < (unsigned)kSentinel) {   // interior node
         FRT_DIAG_TICK(2);
@@ -327,20 +327,15 @@ FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyh
             const float4 *rec = Sn.nodes + u24mul(node, 3);   // 32-bit mad (node < 2^24)
             const float4 n0 = rec[0], n1 = rec[1], n2 = rec[2];
             const int2 cr = S.node_refs[node];
-            // record (scene_to_lds): (near x0, y0, far x0, y0) | (near z0, far z0, near z1, far z1) |
-            // (near x1, y1, far x1, y1): every plane pair shares its axis scale, so the 12 plane
-            // distances are 6 packed FMAs (v_pk_fma_f32, the same roundings as 12 scalar ones)
-            const float2v ixy = {T.sr.invd.x, T.sr.invd.y}, oxy = {T.sr.oinv.x, T.sr.oinv.y};
-            const float2v izz = {T.sr.invd.z, T.sr.invd.z}, ozz = {T.sr.oinv.z, T.sr.oinv.z};
-            const float2v tn0 = pk_fma(float2v{n0.x, n0.y}, ixy, oxy), tf0 = pk_fma(float2v{n0.z, n0.w}, ixy, oxy);
-            const float2v tz0 = pk_fma(float2v{n1.x, n1.y}, izz, ozz), tz1 = pk_fma(float2v{n1.z, n1.w}, izz, ozz);
-            const float2v tn1 = pk_fma(float2v{n2.x, n2.y}, ixy, oxy), tf1 = pk_fma(float2v{n2.z, n2.w}, ixy, oxy);
-            t0 = smax(smax(tn0.x, tn0.y), smax(tz0.x, tmin));
-            t1 = smax(smax(tn1.x, tn1.y), smax(tz1.x, tmin));
-            const R f0 = smin(smin(tf0.x, tf0.y), smin(tz0.y, tbest));
-            const R f1 = smin(smin(tf1.x, tf1.y), smin(tz1.y, tbest));
+            R f0, f1;
+            slab_nf<R>(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, tmin, tbest, t0, f0);
+            slab_nf<R>(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, T.sr, tmin, tbest, t1, f1);
             h0 = t0 <= f0; h1 = t1 <= f1;
             c0 = cr.x; c1 = cr.y;
+            // (the 12 plane distances as 6 v_pk_fma_f32 over same-axis plane pairs: 19 VALU
+            // per node instead of 25 and 4 fewer spills, yet Cornell 237.3 -> 241.8 ms, and
+            // the 4-wide test's pairs 385 -> 396 ms on cornell_1m: profiles/r04/r04o.  Packed
+            // f32 is no throughput lever on gfx950, MI355X_MICROARCH.md's issue-cost table.)
         } else {
             const float4 n0 = node_part(Sn, node, 0), n1 = node_part(Sn, node, 1);
             const float4 n2 = node_part(Sn, node, 2), n3 = node_part(Sn, node, 3);

@@ -112,20 +112,13 @@ __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
     if constexpr (WIDE) {
         const float4 *src = reinterpret_cast<const float4 *>(S0.nodes4);
         for (int i = threadIdx.x; i < nn; i += kBlock) l4[(i & 3) * S0.n_nodes4 + (i >> 2)] = src[i];
-    } else if constexpr (OCT) {   // node e = o * n_nodes + j -> 3 float4 at [3 e]; refs of j -> int2 [j]
-        // HBM copy o, node j: (nx0 ny0 nz0 fx0) (fy0 fz0 nx1 ny1) (nz1 fx1 fy1 fz1) [child refs];
-        // in LDS regrouped as plane pairs of one axis scale for bvh2_step's packed FMAs:
-        // (nx0 ny0 fx0 fy0) (nz0 fz0 nz1 fz1) (nx1 ny1 fx1 fy1)
+    } else if constexpr (OCT) {   // node e = o * n_nodes + j, part k < 3 -> [3 e + k]; refs of j -> int2 [j]
         int2 *refs = reinterpret_cast<int2 *>(l4 + 24 * S0.n_nodes);
-        for (int e = threadIdx.x; e < 8 * S0.n_nodes; e += kBlock) {
-            const float4 a = S0.nodes_oct[4 * e], b = S0.nodes_oct[4 * e + 1], c = S0.nodes_oct[4 * e + 2];
-            l4[3 * e] = make_float4(a.x, a.y, a.w, b.x);
-            l4[3 * e + 1] = make_float4(a.z, b.y, c.x, c.w);
-            l4[3 * e + 2] = make_float4(b.z, b.w, c.y, c.z);
-            if (e < S0.n_nodes) {
-                const float4 r = S0.nodes_oct[4 * e + 3];
-                refs[e] = make_int2(f2i(r.x), f2i(r.y));
-            }
+        for (int i = threadIdx.x; i < 32 * S0.n_nodes; i += kBlock) {
+            const int e = i >> 2, k = i & 3;
+            const float4 v = S0.nodes_oct[i];
+            if (k < 3) l4[3 * e + k] = v;
+            else if (e < S0.n_nodes) refs[e] = make_int2(f2i(v.x), f2i(v.y));
         }
         S.node_refs = refs;
     } else {
@@ -1219,7 +1212,7 @@ static int trav_min(bool lds_scene, bool path = false)
 // Leaf postponing (bvh2_step): a wave's descent stops once fewer than this
 // many of its lanes still descend.  0 = every lane reaches its leaf first.
 // HBM plans 12 since round 4 (cornell_1m 512 spp 767.5 -> 760.9 ms over 8, 16:
-// 761.6, same call, profiles/r04/r04n; round 3's 8 was within 0.4 %).
+// 761.6, same call, profiles/r04/r04n; confirmed 765.4 -> 759.2 in r04o).
 // FRT_MIN_DESC overrides (tuning knob, not part of the C-ABI).
 static int min_desc(bool lds_scene)
 {
