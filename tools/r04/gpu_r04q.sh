@@ -13,3 +13,12 @@ TAG=r04q/roofb PART=b bash tools/gpu_roofline.sh \
  && pmc sq_ao "$SQ" --integrator ao && pmc fetch_ao FETCH_SIZE --integrator ao && pmc write_ao WRITE_SIZE --integrator ao \
  && pmc sq_normals "$SQ" --integrator normals && pmc fetch_normals FETCH_SIZE --integrator normals \
  && pmc write_normals WRITE_SIZE --integrator normals
+rc=$?
+# veach's fp64 list kernel (modified_phong set: 248 VGPRs, 2 waves/SIMD) under a
+# 3-wave cap (168 VGPRs, 70 spilled): build/exp/libfrt_f64w3.so vs libfrt_f64w1.so
+E=first_raytracer_amd/build/exp
+V="--scene veach --spp 256 --rounds 3 --variants default"
+[ $rc = 0 ] && FRT_LIB_PATH=$E/libfrt_f64w1.so timeout -k 10 300 python -u tools/perf_ab.py $V >> $O/ab_f64w.jsonl 2>> $O/ab.log \
+ && FRT_LIB_PATH=$E/libfrt_f64w3.so timeout -k 10 300 python -u tools/perf_ab.py $V >> $O/ab_f64w.jsonl 2>> $O/ab.log \
+ && FRT_LIB_PATH=$E/libfrt_f64w1.so timeout -k 10 300 python -u tools/perf_ab.py $V >> $O/ab_f64w.jsonl 2>> $O/ab.log \
+ && FRT_LIB_PATH=$E/libfrt_f64w3.so timeout -k 10 300 python -u tools/perf_ab.py $V >> $O/ab_f64w.jsonl 2>> $O/ab.log
