@@ -22,3 +22,7 @@ V="--scene veach --spp 256 --rounds 3 --variants default"
  && FRT_LIB_PATH=$E/libfrt_f64w3.so timeout -k 10 300 python -u tools/perf_ab.py $V >> $O/ab_f64w.jsonl 2>> $O/ab.log \
  && FRT_LIB_PATH=$E/libfrt_f64w1.so timeout -k 10 300 python -u tools/perf_ab.py $V >> $O/ab_f64w.jsonl 2>> $O/ab.log \
  && FRT_LIB_PATH=$E/libfrt_f64w3.so timeout -k 10 300 python -u tools/perf_ab.py $V >> $O/ab_f64w.jsonl 2>> $O/ab.log
+rc=$?
+# rehearsal of the N-rank bench path (tools/gpu_multirank.sh: 2 ranks on the one
+# GPU, gloo collectives) on the final build
+[ $rc = 0 ] && TAG=r04q/mr bash tools/gpu_multirank.sh
