@@ -24,6 +24,7 @@ import json
 import math
 import os
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -360,7 +361,7 @@ class Runner:
         synchronize on both sides, max over ranks)."""
         torch, frt = self.torch, self.frt
         nx, ny = (int(x) for x in args.res.lower().split("x"))
-        workdir = os.path.join(ROOT, "gpurun_out") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else "/tmp"
+        workdir = tempfile.gettempdir()   # the generated 1M-triangle OBJ (33 MB) stays out of gpurun_out/
         kind, obj, scene_name = scene_spec(scene, workdir, tag=f"_r{self.rank}")
         t0 = time.perf_counter()
         gpu_build_ms = None

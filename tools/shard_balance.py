@@ -22,6 +22,7 @@ import argparse
 import json
 import os
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -43,7 +44,7 @@ def main():
     import bench
     import first_raytracer_amd as frt
     nx, ny = (int(v) for v in a.res.split("x"))
-    workdir = os.path.join(ROOT, "gpurun_out") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else "/tmp"
+    workdir = tempfile.gettempdir()   # the generated 1M-triangle OBJ (33 MB) stays out of gpurun_out/
     kind, obj, name = bench.scene_spec(a.scene, workdir)
     hs = frt.HostScene.from_spec({"objects": [{"obj": obj, "geo": True}], "camera": frt.CORNELL_CAMERA,
                                   "world": "list"}, nx / ny)
