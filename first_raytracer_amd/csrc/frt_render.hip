@@ -988,12 +988,15 @@ static int pick_launcher_kind(const frt_ctx *c, int flags, Launcher &L)
 // fp64 kernels (path only; DESIGN.md "Precision"): the list world with the
 // scene's material set, or the binary tree from HBM with every material
 // compiled in (the debugging build; no register cap, stack 32 or 64)
+#ifndef FRT_EXP_F64_LIST_WAVES
+#define FRT_EXP_F64_LIST_WAVES 1   // experiment builds: register cap of the fp64 list kernels (1 = the compiler's own)
+#endif
 template <int MATS>
 static int pick_launcher_f64_t(const frt_ctx *c, Launcher &L)
 {
     if (c->world_kind == FRT_WORLD_LIST) {
         // (a 2-wave register cap changed nothing: profiles/r03/r03c_ab_veach_listbox_f64waves.jsonl)
-        L = make_launcher<16, FRT_WORLD_LIST, false, 1, MATS, FRT_INTEGRATOR_PATH, double>(0);
+        L = make_launcher<16, FRT_WORLD_LIST, false, FRT_EXP_F64_LIST_WAVES, MATS, FRT_INTEGRATOR_PATH, double>(0);
         return FRT_OK;
     }
     const int d = c->stack_needed;
