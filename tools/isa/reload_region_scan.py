@@ -1,3 +1,9 @@
+"""Register-cap reproducer (DESIGN.md \"Register-cap hazard\"): scratch reloads inside an
+s_and_saveexec region whose register is read after the region's s_or_b64 exec join, in
+straight-line code (stops at the first branch).  Input: a kernel's assembly (-S).
+
+    python tools/isa/reload_region_scan.py kernel.s
+"""
 import re, sys
 L = open(sys.argv[1]).read().split("\n")
 def vset(tok):

@@ -1,3 +1,9 @@
+"""Register-cap reproducer (DESIGN.md \"Register-cap hazard\"): forward data flow over a
+kernel's disassembly (llvm-objdump -d, with encodings) on its real control-flow graph:
+does any v_mul_lo_u32 read SGPR <reg> at a point where it may not hold <const>?
+
+    python tools/isa/sgpr_const_flow.py kernel.s s80 0x846ca68b
+"""
 import re, sys
 L = open(sys.argv[1]).read().split('\n')
 REG = sys.argv[2] if len(sys.argv) > 2 else 's80'
