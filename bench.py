@@ -49,6 +49,66 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n, argv, script=None, env=None, poll_s=0.5):
+    """`bench.py --gpus N` without a launcher (no WORLD_SIZE in the
+    environment): start N rank processes of this script with RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT, as torchrun
+    would, and wait for them.  The parent never touches the GPU (it only counts
+    devices, which does not initialise HIP on this image), so the children are
+    fresh processes, not exec'd replacements.  Returns 0 when every rank exits
+    0; when one fails, the others are terminated (by their own PIDs) and its
+    exit code is returned, so a run with fewer than N working ranks cannot print
+    a line."""
+    import subprocess
+    script = script or os.path.abspath(__file__)
+    base = dict(os.environ if env is None else env)
+    base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n))
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, script, *argv], env=e))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(poll_s)
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                log(f"bench: rank {procs.index(p)} exited with {code}; stopping the other ranks")
+                for q in live:
+                    q.terminate()
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def check_world(gpus, world, backend, n_devices):
+    """The rank set must be the one asked for: WORLD_SIZE == --gpus, and with
+    RCCL one device per rank (gloo rehearsals may share devices).  Returns an
+    error message or None."""
+    if world != gpus:
+        return f"--gpus {gpus} but WORLD_SIZE {world}: refusing to measure a different rank count"
+    if n_devices < 1:
+        return "no GPU visible"
+    if backend == "nccl" and n_devices < world:
+        return f"--gpus {world} needs {world} GPUs for RCCL, {n_devices} visible"
+    return None
+
+
 def host_cpus():
     """CPUs this process may use: its affinity mask, capped by the cgroup CPU
     quota (a GPU box shares a large host; nproc reports the whole machine)."""
@@ -252,7 +312,7 @@ def mlt_block_rmse(kind, obj, nx, ny, film, threads, seconds, spp=256, block=8, 
             "tolerance": {"rel_block_err_median": 0.05, "mean_rel_err_b_corrected": 0.02}}
 
 
-def roofline(integrator, key, world, res, V, T):
+def roofline(integrator, key, world, res, V, T, shared_device=False):
     """Roofline of the dominant kernel (the megakernel) for this config.
 
     The bound follows where the scene lives (DESIGN.md §7 "Roofline"):
@@ -306,6 +366,10 @@ def roofline(integrator, key, world, res, V, T):
                         "algorithmic_over_traffic": None if algo is None else round(algo / hbm_gbs, 3)})
             if issue is not None:
                 out["valu_issue_frac"] = round(rays * issue / launch_s / 1e9 / VALU_PEAK_GINST, 4)
+    if shared_device and out.get("frac") is not None:
+        # ranks sharing one device (gloo rehearsal): a rank's launch time is not
+        # the time of a launch that has the chip, so no fraction of its peak
+        out.update({"achieved": None, "frac": None, "basis": "ranks share one device (rehearsal): no roofline"})
     if "bound" not in out:
         # no counter profile for this config: no roofline.  The algorithmic bytes
         # (algorithmic_GBps above) are not one: L1 / L2 / the Infinity Cache / LDS
@@ -325,11 +389,18 @@ class Runner:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         local = int(os.environ.get("LOCAL_RANK", "0"))
-        if self.world != args.gpus:
-            log(f"note: --gpus {args.gpus} but WORLD_SIZE {self.world}; using WORLD_SIZE")
+        n_dev = torch.cuda.device_count()
+        err = check_world(args.gpus, self.world, args.backend, n_dev)
+        if err:
+            log(f"bench: {err}")
+            sys.exit(2)
         self.gloo = args.backend == "gloo"
+        # ranks sharing one device (a gloo rehearsal on a smaller box): the
+        # timings are real, but each rank has only part of the chip, so no
+        # roofline fraction is reported
+        self.shared_device = self.world > n_dev
         if self.gloo:
-            local = local % torch.cuda.device_count()
+            local = local % n_dev
         if self.world > 1:
             torch.cuda.set_device(local)
             if self.gloo:
@@ -497,7 +568,18 @@ def main():
     ap.add_argument("--chains", type=int, default=1 << 18, help="PSS-MLT chains (all ranks)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the N-rank path with host-staged collectives (e.g. ranks sharing one GPU)")
+    ap.add_argument("--rmse-pixels-multi", type=int, default=32768,
+                    help="N > 1: oracle pixel sample for rank 0's RMSE (no CPU timing at N > 1)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start the N ranks here, before anything touches the GPU
+        import torch
+        err = check_world(args.gpus, args.gpus, args.backend, torch.cuda.device_count())
+        if err:
+            log(f"bench: {err}")
+            sys.exit(2)
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
 
     R = Runner(args)
     world, rank = R.world, R.rank
@@ -512,16 +594,20 @@ def main():
         key = f"{args.scene}:{nx}x{ny}"
         threads = args.cpu_threads or host_cpus()
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        timed_cpu = world == 1          # the CPU baseline is timed at N = 1 only; the RMSE is computed at every N
+        if not args.no_cpu_baseline:
             if args.integrator == "pssmlt":
                 cpu = cpu_baseline_mlt(res["kind"], res["obj"], nx, ny, args.seed, threads, args.cpu_seconds)
                 cpu["mlt_rmse"] = mlt_block_rmse(res["kind"], res["obj"], nx, ny, res["film"], threads,
                                                  args.cpu_seconds, seed=args.seed)
                 cpu["rmse"] = cpu["mlt_rmse"]["rmse"]
-            else:
+            elif timed_cpu:
                 cpu = cpu_baseline(res["kind"], res["obj"], nx, ny, args.spp, args.seed, args.cpu_pixels, threads,
                                     res["film"], args.cpu_seconds, integrator=res["integ"], env=res["env"],
                                     min_frac=args.rmse_min_frac)
+            else:
+                cpu = cpu_baseline(res["kind"], res["obj"], nx, ny, args.spp, args.seed, args.rmse_pixels_multi,
+                                    threads, res["film"], 0.0, integrator=res["integ"], env=res["env"])
         ts = load_profile("traversal_stats.json", key)
         V, T = (cpu["V"], cpu["T"]) if cpu is not None else (ts["V"], ts["T"]) if ts is not None else (None, None)
         li_name = {"path": "path::Li", "ao": "ao::Li", "normals": "normals_renderer::Li"}.get(args.integrator)
@@ -558,8 +644,8 @@ def main():
             "gpu_build_ms": None if res["gpu_build_ms"] is None else round(res["gpu_build_ms"], 3),
             "value_per_gpu": round(res["value"] / world, 1),
             "image_mean": [round(float(x), 6) for x in film_np.reshape(-1, 3).mean(0)],
-            "roofline": roofline(args.integrator, key, world, res, V, T),
-            "cpu_baseline": None if cpu is None else {
+            "roofline": roofline(args.integrator, key, world, res, V, T, R.shared_device),
+            "cpu_baseline": None if (cpu is None or not timed_cpu) else {
                 "value": round(cpu["mrays"], 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
                 "host_nproc": nproc,
                 "sample": (f"{cpu['npix']} evenly spaced pixels of the same {nx}x{ny} frame at {args.spp} spp "
@@ -584,7 +670,7 @@ def main():
         if ns is not None:
             nkey = f"cornell_1m:{ns['nx']}x{ns['ny']}"
             ncpu = None
-            if world == 1 and not args.no_cpu_baseline:
+            if not args.no_cpu_baseline:      # a fixed pixel sample: RMSE at every N, no CPU timing
                 ncpu = cpu_baseline(ns["kind"], ns["obj"], ns["nx"], ns["ny"], 512, args.seed, args.ns_pixels,
                                      threads, ns["film"], 0.0)
             nts = load_profile("traversal_stats.json", nkey)
@@ -605,7 +691,7 @@ def main():
                     "rmse_converged": ncpu["rmse_converged"], "diverged_threshold": 1e-3,
                     "oracle_mrays": round(ncpu["mrays"], 3), "oracle_threads": threads},
                 "image_mean": [round(float(x), 6) for x in ns["film"].reshape(-1, 3).mean(0)],
-                "roofline": roofline("path", nkey, world, ns, nV, nT),
+                "roofline": roofline("path", nkey, world, ns, nV, nT, R.shared_device),
             }
         if R.gloo:
             line["config"]["parallelism"] += " (gloo host-staged rehearsal)"
