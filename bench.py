@@ -206,28 +206,86 @@ def cpu_baseline(kind, obj, nx, ny, spp, seed, npix, threads, film, seconds, int
     }
 
 
-def cpu_baseline_mlt(kind, obj, nx, ny, seed, threads, seconds):
-    """The oracle's PSS-MLT on a bounded sample of the same frame: chains x 512
-    mutations, the chain count grown (from 256) until a run takes about
-    `seconds` of CPU work."""
-    import oracle
-    sc = oracle.OracleScene(kind, obj, nx / ny)
-    steps = 512
-
-    def run(chains):
-        t0 = time.perf_counter()
-        _, _, cnt = sc.mlt_render(nx, ny, chains, steps, seed=seed, n_init=10000, nthreads=threads)
-        return cnt, time.perf_counter() - t0
-
-    chains = 256
-    while True:                             # grow the sample until it takes >= seconds/2
-        cnt, dt = run(chains)
-        if dt >= 0.5 * seconds or chains >= 1 << 20:
+def cpu_baseline_mlt(ctx, kind, obj, nx, ny, mpp, n_chains, seed, threads, seconds):
+    """C5's CPU baseline and path-exact parity in one: the oracle's PSS-MLT
+    (pssmlt.cpp restated in fp64) on the chains of shard (0, K) of the config
+    itself -- every one of them runs the config's full mutation count -- with K
+    halved from 1024 (a power of two, at least 16) until the oracle's run takes
+    about `seconds`; the GPU renders the same shard for the comparison
+    (mlt_shard_parity)."""
+    K = 1024
+    while True:
+        par = mlt_shard_parity(ctx, kind, obj, nx, ny, mpp, n_chains, K, seed, threads)
+        dt = par["oracle_seconds"]
+        if dt >= 0.5 * seconds or K <= 16 or K >= n_chains:
             break
-        chains = int(min(1 << 20, chains * min(16.0, max(2.0, seconds / max(dt, 1e-3)))))
-    return {"mrays": cnt.rays / dt / 1e6, "seconds": dt, "rays": cnt.rays, "npix": 0,
-            "V": cnt.node_visits / cnt.rays, "T": (cnt.tri_tests + cnt.sphere_tests) / cnt.rays,
-            "rmse": None, "sample": f"{chains} chains x {steps} mutations"}
+        K = max(16, K >> max(1, min(4, int(math.ceil(math.log2(seconds / max(dt, 1e-3)))))))
+    par.pop("gpu_film")
+    return {"mrays": par["oracle_mrays"], "seconds": dt, "rays": par["rays_oracle"], "npix": 0,
+            "V": par["oracle_counters"]["V"], "T": par["oracle_counters"]["T"], "parity": par,
+            "sample": (f"the {par['chains']} chains c = 0 mod {K} of the config's {n_chains}, "
+                       f"{par['steps_per_chain']} mutations each")}
+
+
+def mlt_shard_parity(ctx, kind, obj, nx, ny, mpp, n_chains, shard_count, seed, threads, shard_index=0,
+                     n_init=10000, flags=0):
+    """C5 path-exact parity at the config itself: the GPU
+    renders shard (shard_index, shard_count) of the PSS-MLT request -- the
+    chains c = shard_index + j * shard_count of n_chains, each with the
+    config's full mutation count -- and the oracle's pssmlt.cpp restatement
+    (ora_mlt_render_shard, fp64) runs the same chains on the same counter-RNG
+    streams.  Returns the comparison and the oracle's CPU timing (the C5 CPU
+    baseline: the reference algorithm on a bounded sample of the same chains).
+
+    * chains: a chain is path-exact when its trajectory fingerprint (accepted
+      proposals, sum of the accepted steps' indices) equals the oracle's.
+      fp32 rounding can flip one accept or one hit decision and send a chain
+      elsewhere until both copies accept the same large step (whose state is
+      the RNG's alone), so `diverged_chains` counts the chains whose
+      fingerprints differ;
+    * film: the shard films (splats scaled as in the full render) compared
+      per pixel and in 8x8-block means, with their means;
+    * rays: camera + extension + shadow counts."""
+    import oracle
+    import first_raytracer_amd as frt
+    film = np.zeros((ny, nx, 3), np.float32)
+    film, st = ctx.render(frt.RenderParams.pssmlt(nx, ny, mpp, n_chains, seed=seed, bootstrap=n_init,
+                                                  shard_index=shard_index, shard_count=shard_count, flags=flags), film)
+    n_local = int(st.work_items)
+    u_gpu, fp_gpu = ctx.mlt_chain_state(0, n_local)
+    steps = mpp * nx * ny // n_chains
+    sc = oracle.OracleScene(kind, obj, nx / ny)
+    t0 = time.perf_counter()
+    ref, b, cnt, fp_ora, u_ora = sc.mlt_render_shard(nx, ny, n_chains, steps, shard_index, shard_count, seed=seed,
+                                                     n_init=n_init, nthreads=threads)
+    dt = time.perf_counter() - t0
+    same = np.all(fp_gpu == fp_ora, axis=1)
+    g, o = film.astype(np.float64), ref
+    du = np.abs(u_gpu.astype(np.float64) - u_ora).max(axis=1) if n_local else np.zeros(0)
+    bs = 8
+    gb = g[: ny // bs * bs, : nx // bs * bs].reshape(ny // bs, bs, nx // bs, bs, 3).mean(axis=(1, 3))
+    ob = o[: ny // bs * bs, : nx // bs * bs].reshape(ny // bs, bs, nx // bs, bs, 3).mean(axis=(1, 3))
+    peak = float(np.abs(o).max())
+    rmse = float(np.sqrt(np.mean((g - o) ** 2)))
+    return {
+        "shard": [shard_index, shard_count], "chains": n_local, "n_chains": n_chains, "steps_per_chain": steps,
+        "samples_gpu": int(st.samples), "samples_oracle": int(cnt.samples),
+        "rays_gpu": int(st.rays), "rays_oracle": int(cnt.rays),
+        "rays_rel_diff": float(abs(int(st.rays) - int(cnt.rays)) / max(1, int(cnt.rays))),
+        "path_exact_chains": int(same.sum()), "diverged_chains": int((~same).sum()),
+        "diverged_frac": float((~same).mean()) if n_local else 0.0,
+        "accepts_gpu": int(fp_gpu[:, 0].astype(np.int64).sum()), "accepts_oracle": int(fp_ora[:, 0].astype(np.int64).sum()),
+        "state_maxdiff_path_exact": float(du[same].max()) if same.any() else None,
+        "film_rmse": rmse, "film_peak": peak, "film_rmse_over_peak": rmse / max(1.0, peak),
+        "film_rel_l2": float(np.linalg.norm(g - o) / max(np.linalg.norm(o), 1e-30)),
+        "block8_rel_l2": float(np.linalg.norm(gb - ob) / max(np.linalg.norm(ob), 1e-30)),
+        "mean_gpu": [float(x) for x in g.reshape(-1, 3).mean(0)], "mean_oracle": [float(x) for x in o.reshape(-1, 3).mean(0)],
+        "mean_rel_diff": float(g.mean() / o.mean() - 1.0) if o.mean() > 0 else None,
+        "b_oracle": float(b),
+        "oracle_seconds": dt, "oracle_mrays": cnt.rays / dt / 1e6, "oracle_threads": threads,
+        "oracle_counters": {"V": cnt.node_visits / max(1, cnt.rays), "T": (cnt.tri_tests + cnt.sphere_tests) / max(1, cnt.rays)},
+        "gpu_film": film,
+    }
 
 
 MLT_MAX_PATH = 10     # pssmlt.h MaxPathLength: pssmlt::Li traces depths 0..10 (pssmlt.cpp:151)
@@ -597,7 +655,8 @@ def main():
         timed_cpu = world == 1          # the CPU baseline is timed at N = 1 only; the RMSE is computed at every N
         if not args.no_cpu_baseline:
             if args.integrator == "pssmlt":
-                cpu = cpu_baseline_mlt(res["kind"], res["obj"], nx, ny, args.seed, threads, args.cpu_seconds)
+                cpu = cpu_baseline_mlt(R.ctx, res["kind"], res["obj"], nx, ny, args.spp, args.chains, args.seed,
+                                       threads, args.cpu_seconds)
                 cpu["mlt_rmse"] = mlt_block_rmse(res["kind"], res["obj"], nx, ny, res["film"], threads,
                                                  args.cpu_seconds, seed=args.seed)
                 cpu["rmse"] = cpu["mlt_rmse"]["rmse"]
@@ -631,7 +690,7 @@ def main():
                        "parallelism": (f"chains-interleaved x{world} + rccl all-reduce" if args.integrator == "pssmlt"
                                        else f"tiles-interleaved x{world} + rccl gather to rank 0")},
             "rmse": None if cpu is None else cpu["rmse"],
-            "rmse_detail": None if cpu is None else cpu["mlt_rmse"] if "mlt_rmse" in cpu else {
+            "rmse_detail": None if cpu is None else dict(cpu["mlt_rmse"], path_exact=cpu["parity"]) if "mlt_rmse" in cpu else {
                 "pixels": cpu["rmse_pixels"], "pixel_frac": round(cpu["rmse_pixels"] / (nx * ny), 4),
                 "diverged_pixels": cpu["diverged_pixels"],
                 "rmse_converged": cpu["rmse_converged"], "diverged_threshold": 1e-3,

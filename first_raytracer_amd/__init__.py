@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("FRT_LIB_PATH") or os.path.join(HERE, "libfrt.so")
 FRT_WORLD_BVH, FRT_WORLD_LIST = 0, 1
 FRT_MAT_LAMBERTIAN, FRT_MAT_DIFFUSE_LIGHT = 0, 1
 FRT_PRIM_SPHERE = 1 << 30
-ABI_VERSION = 8                 # include/frt.h FRT_ABI_VERSION (frt_stats / frt_material layout)
+ABI_VERSION = 9                 # include/frt.h FRT_ABI_VERSION (frt_stats / frt_material layout)
 FRT_MAT_LAMBERTIAN, FRT_MAT_DIFFUSE_LIGHT, FRT_MAT_MODIFIED_PHONG, FRT_MAT_METAL, FRT_MAT_DIELECTRIC = 0, 1, 2, 3, 4
 FRT_MAT_ROUGH_CONDUCTOR = 5
 FRT_DIST_GGX, FRT_DIST_BECKMANN = 0, 1
@@ -176,6 +176,7 @@ _lib = None
 # every symbol include/frt.h declares
 EXPORTS = ("frt_get_abi_version", "frt_create", "frt_destroy", "frt_last_error", "frt_set_precision", "frt_upload_scene",
            "frt_shard_slot_count", "frt_shard_slots", "frt_render", "frt_render_multi", "frt_render_device", "frt_trace_device",
+           "frt_mlt_chain_state",
            "frt_scene_create", "frt_scene_new", "frt_scene_add_obj", "frt_scene_add_sphere", "frt_scene_set_camera",
            "frt_scene_set_env", "frt_scene_add_image", "frt_scene_finish", "frt_scene_build_bvh_gpu",
            "frt_scene_build_bvh_sah", "frt_scene_build_bvh_gpu_algo",
@@ -215,6 +216,7 @@ def lib():
     L.frt_render.argtypes = [vp, ctypes.POINTER(RenderParams), vp, ctypes.POINTER(Stats)]
     L.frt_render_device.argtypes = [vp, ctypes.POINTER(RenderParams), vp, vp, ctypes.POINTER(Stats)]
     L.frt_trace_device.argtypes = [vp, vp, ctypes.c_int64, vp, ctypes.c_int, vp, ctypes.POINTER(Stats)]
+    L.frt_mlt_chain_state.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64, vp, vp]
     L.frt_render_multi.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.POINTER(RenderParams), vp,
                                    ctypes.POINTER(Stats)]
     L.frt_scene_create.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_double, ctypes.POINTER(vp)]
@@ -415,6 +417,16 @@ class Context:
                                        ctypes.c_void_p(stream_ptr) if stream_ptr else None, ctypes.byref(st)),
                "frt_render_device", self.ptr)
         return st
+
+    def mlt_chain_state(self, first, n):
+        """Local chains [first, first + n) of the last PSS-MLT render: (final
+        states n x 92 float32, fingerprints n x 2 uint32 = accepted proposals,
+        sum of the accepted steps' 1-based indices mod 2^32)."""
+        u = np.zeros((max(n, 1), 92), np.float32)
+        fp = np.zeros((max(n, 1), 2), np.uint32)
+        _check(lib().frt_mlt_chain_state(self.ptr, int(first), int(n), u.ctypes.data, fp.ctypes.data),
+               "frt_mlt_chain_state", self.ptr)
+        return u[:n], fp[:n]
 
     def trace_device(self, rays_ptr, n, hits_ptr, flags=0, stream_ptr=None):
         """Batched Scene::world->hit on device buffers: rays n x 8 floats (origin, t_max,

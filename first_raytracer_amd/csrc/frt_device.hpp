@@ -388,32 +388,42 @@ template <typename R> FRT_HD V3<R> random_to_sphere(R radius, R dist2, R r1, R r
     const R s = fsqrt(R(1) - z * z);
     return V3<R>{cp * s, sp * s, z};
 }
-// x^y for x in [0, 1], y > 0 (phong lobes): exp2(y log2 x) on the hardware units
+// x^y for x in [0, 1], y >= 0 (phong lobes): exp2(y log2 x) on the hardware
+// units; y = 0 gives 1 for every x, std::pow's answer (0^0 = 1; the MTL
+// default Ns is 0, so veach_mi's plates have y = 0 and see alpha = 0 often --
+// exp2(0 * -inf) would be NaN)
 FRT_HD float fpow01(float x, float y)
 {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(FRT_EXP_IEEE_MATH)
-    return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
+    return y == 0.0f ? 1.0f : __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
 #else
     return powf(x, y);
 #endif
 }
 FRT_HD double fpow01(double x, double y) { return pow(x, y); }
-// x^y for x in [0, 1], y > 0 where the result only weights radiance (the phong
-// lobe's pdf value and eval_bsdf; never a direction): the fp32 form as fpow01;
-// in the fp64 kernels log2 on the fp32 unit over the double's mantissa, the
-// exponent kept exact, and 2^(y log2 x) rebuilt in double range -- relative
-// error ~1e-6, no underflow before double's (so pdf == 0, which ends a path,
-// path.cpp:84-86, comes out exactly where the double pow gives 0), and about a
-// tenth of OCML's double pow.  The directions (cosine_power_generate) keep the
-// double pow: they decide what the next ray hits.
+// x^y for x in [0, 1], y >= 0 where the result only weights radiance (the
+// phong lobe's pdf value and eval_bsdf; never a direction): the fp32 form as
+// fpow01.  In the fp64 kernels, for y <= 64: log2 of the double's mantissa m
+// on the fp32 unit with m's fp32 rounding residual carried to first order, the
+// exponent kept exact, and 2^(y log2 x) rebuilt in double range.  What is left
+// is v_log_f32's error, ~2^-22 absolute in log2 m, times y: relative error
+// <= 64 * 2^-22 * ln 2 ~ 1.1e-5 at y = 64, 1.7e-7 at y = 1 (without
+// the bound, Ns 1000-1024 reached ~1e-4).  No underflow before double's, so
+// pdf == 0, which ends a path (path.cpp:84-86), comes out exactly where the
+// double pow gives 0.  Larger exponents, x = 0 and y = 0 take OCML's double
+// pow, as the host replay and the reference do.  The directions
+// (cosine_power_generate) keep the double pow: they decide what the next ray
+// hits.
 FRT_HD float fpow01_w(float x, float y) { return fpow01(x, y); }
 FRT_HD double fpow01_w(double x, double y)
 {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(FRT_EXP_IEEE_MATH)
-    if (!(x > 0.0)) return x == 0.0 ? 0.0 : pow(x, y);
+    if (!(x > 0.0) || !(y > 0.0) || y > 64.0) return pow(x, y);
     int k;
     const double m = frexp(x, &k);                            // x = m 2^k, m in [0.5, 1)
-    const double l = y * ((double)__builtin_amdgcn_logf((float)m) + (double)k);   // y log2 x
+    const float mf = (float)m;
+    const double lm = (double)__builtin_amdgcn_logf(mf) + (m - (double)mf) * (1.4426950408889634 / (double)mf);
+    const double l = y * (lm + (double)k);                    // y log2 x
     if (l < -1100.0) return 0.0;
     const double li = floor(l);
     return ldexp((double)__builtin_amdgcn_exp2f((float)(l - li)), (int)li);

@@ -8,7 +8,7 @@
 //   Render (chain loop)     pssmlt.cpp:301-365, AccumulatePathContribution :19-38
 //
 // Primary samples: a chain's current state u[0..91] lives in HBM chain-major,
-// U[chain][dim] (one 368-B row per chain).  A proposal is never stored: its
+// U[chain][dim] (one 384-B row per chain, kMltRow).  A proposal is never stored: its
 // dimension d is computed when the path reads it -- a fresh uniform on a large
 // step, else perturb(U[c][d], r) -- and written back for all 92 dimensions
 // only when the proposal is accepted (by the whole wave, one chain's row at a
@@ -20,6 +20,12 @@ namespace frt {
 
 constexpr int kMltMaxPath = 10;                              // MaxPathLength (pssmlt.h:11)
 constexpr int kMltDims = 4 + (kMltMaxPath + 1) * 8;          // 92 prnds a path can read
+// U row stride: the 92 primary samples, then the chain's trajectory
+// fingerprint (word 92: accepted proposals, word 93: sum of the accepted steps'
+// 1-based indices mod 2^32; ora_mlt_render_shard keeps the same) and 2 pad
+// words: 384 B = three 128-B lines per row
+constexpr int kMltRow = 96;
+constexpr int kMltFp = kMltDims;
 constexpr float kMltLargeStep = 0.3f;                        // LargeStepProb (pssmlt.h:13)
 constexpr uint32_t kMltChainSalt = 0x3C6EF372U, kMltBootSalt = 0xB5297A4DU;
 
@@ -58,16 +64,17 @@ struct PrndSource {
     {
         const float r = rng_u(key, dim0 + (uint32_t)d);
         if (fresh) return r;
-        return mlt_mutate(U[(size_t)chain * kMltDims + d], r, d, s2p, logp);
+        return mlt_mutate(U[(size_t)chain * kMltRow + d], r, d, s2p, logp);
     }
     // The chain's current values of dims [d0, d0 + 4 N) in N 16-B loads issued
-    // together (d0 % 4 == 0; rows are 368 B = 23 x 16 B), for at().  One per
+    // together (d0 % 4 == 0), for at().  One per
     // dimension, each behind the previous dimension's hash and mutation,
     // exposed the load latency once per primary sample.  Fresh sources read none.
+    // (d0 % 4 == 0 and rows of 96 floats: 16-B aligned)
     template <int N> FRT_HD void fetch(int d0, float4 (&c)[N]) const
     {
         if (fresh) return;
-        const float4 *row = reinterpret_cast<const float4 *>(U + (size_t)chain * kMltDims + d0);
+        const float4 *row = reinterpret_cast<const float4 *>(U + (size_t)chain * kMltRow + d0);
         for (int k = 0; k < N; ++k) c[k] = row[k];
     }
     // get(d) with the current value already fetched

@@ -24,6 +24,7 @@ FRT_HD float i2f(int i) { return __builtin_bit_cast(float, i); }
 // colour, texture kind), m4 = (u_scale, v_scale, -, -)
 constexpr int kMatStride = 5;
 FRT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
+FRT_HD uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
 // true if the predicate holds on any active lane of the wave (the host self-test is one lane)
 FRT_HD bool wave_any(bool x)
 {
@@ -80,6 +81,12 @@ __device__ __forceinline__ unsigned long long *diag_slot()
 #endif
 
 constexpr int kSentinel = 0x7fffffff;   // "stack empty"; never a node index
+// Octant plan (kWorldBvh2Oct): 16-bit child refs, so that a stack entry also
+// holds the child's entry distance (bvh2_step).  Interior node j < kOctLeaf is
+// j; a leaf is kOctLeaf | sphere << 13 | (count - 1) << 10 | first (first and
+// sphere index < 1024, count <= 8); kOctSent = empty stack.  The host keeps the
+// plan to scenes whose refs fit (oct_refs_fit).
+constexpr int kOctLeaf = 0x4000, kOctSent = 0x8000;
 constexpr int kWorldBvh4 = 2;           // internal world kind: 4-wide quantized BVH
 constexpr int kWorldBvh2Oct = 4;        // internal world kind: binary nodes from LDS, one copy per ray octant
 constexpr int kBvh4Overflow = 40;       // private stack entries after the LDS ones
@@ -141,6 +148,17 @@ template <typename R> struct Hit {
 // (count - 1 in bits 27..29 below the sphere flag: up to 8 triangles, 2^27 triangles per scene)
 constexpr int kLeafCountShift = 27, kLeafIndexMask = (1 << kLeafCountShift) - 1, kLeafIndexLimit = 1 << kLeafCountShift;
 constexpr int kLeafMax = 8, kLeafDefault = 4, kLeafSmallScene = 2;
+// octant plan refs (kOctLeaf above): a child ref as its 16-bit code, and a
+// leaf code back to leaf_hit's x
+FRT_HD int oct_code(int ref)
+{
+    if (ref >= 0) return ref;
+    const int x = ~ref;
+    return kOctLeaf | ((x >> 17) & 0x2000) | (((x >> kLeafCountShift) & 7) << 10) | (x & 0x3ff);
+}
+FRT_HD int oct_leaf(int code) { return ((code & 0x2000) << 17) | (((code >> 10) & 7) << kLeafCountShift) | (code & 0x3ff); }
+// true when the ref survives the 16-bit code (host check before the octant plan is offered)
+FRT_HD bool oct_ref_fits(int ref) { return ref >= 0 ? ref < kOctLeaf : oct_leaf(oct_code(ref)) == ~ref; }
 constexpr int kTravMinLds = 12, kTravMinHbm = 32;           // PSS-MLT, AO, normals: see trav_min()
 constexpr int kTravMinLdsPath = 20, kTravMinHbmPath = 40;   // path::Li
 constexpr int kMinDescLds = 0, kMinDescHbm = 12;    // leaf postponing: see min_desc()
@@ -304,10 +322,32 @@ template <typename R> FRT_HD bool trav_begin(Trav<R> &T, const DevScene &S, int 
 // descending while other lanes of its wave have none yet, Aila & Laine 2009 --
 // was measured on both plans and removed: +1 % on cornell_1m in round 1,
 // -0.4 % on Cornell and -14 % on cornell_1m at 512 spp in round 3, DESIGN.md.)
+//
+// OCT stacks hold 16-bit refs (oct_code) with the entry distance of the pushed
+// child in the upper half (its fp32 bits truncated to 16, so rounded toward 0:
+// never above the true entry).  A pop skips entries whose entry distance is
+// already beyond the closest hit (pop culling): such a node cannot hold a hit
+// with t <= t_best (padded boxes), so hits are unchanged, but
+// without the distance every such pop cost a node visit or a leaf test.
 template <int STRIDE, bool OCT = false, typename R>
 FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyhit, int *stk, int min_desc = 0)
 {
     int node = T.node, sp = T.sp;
+    // interior node?  (OCT codes: interior < kOctLeaf <= leaf < kOctSent)
+    auto interior = [](int n) { return OCT ? n < kOctLeaf : (unsigned)n < (unsigned)kSentinel; };
+    // OCT pop with culling against t_best (tb); the other plans pop bare refs
+    auto pop = [&](R tb) -> int {
+        if constexpr (OCT) {
+            while (sp > 0) {
+                const int e = stk[--sp * STRIDE];
+                if (!(u2f((uint32_t)e & 0xffff0000u) > tb)) return e & 0xffff;
+                FRT_DIAG_TICK(7);                       // culled (diagnostic build: lanes that skip an entry)
+            }
+            return kOctSent;
+        } else {
+            return (sp > 0) ? stk[--sp * STRIDE] : kSentinel;
+        }
+    };
     DevScene Sn = S;
     if constexpr (OCT) {   // the ray's copy: n_nodes 48-B box records (scene_to_lds)
         const int oct = (T.sr.invd.x < R(0) ? 1 : 0) | (T.sr.invd.y < R(0) ? 2 : 0) | (T.sr.invd.z < R(0) ? 4 : 0);
@@ -318,7 +358,7 @@ FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyh
     // (OCT: t_best held finite -- a ray query may pass t_max = +inf -- so that
     // slab_nf's tn <= tf is the hit test)
     const R tmin = T.tmin, tbest = OCT ? vmin(T.h.t, Cst<R>::tmax) : T.h.t;
-    while ((unsigned)node < (unsigned)kSentinel) {   // interior node
+    while (interior(node)) {
         FRT_DIAG_TICK(2);
         R t0, t1;
         int c0, c1;
@@ -346,7 +386,8 @@ FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyh
         }
         if (h0 && h1) {
             const bool first0 = t0 <= t1;
-            stk[sp * STRIDE] = first0 ? c1 : c0;
+            if constexpr (OCT) stk[sp * STRIDE] = (int)((f2u(float(first0 ? t1 : t0)) & 0xffff0000u) | (uint32_t)(first0 ? c1 : c0));
+            else stk[sp * STRIDE] = first0 ? c1 : c0;
             ++sp;
             node = first0 ? c0 : c1;
         } else if (h0) {
@@ -354,19 +395,20 @@ FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyh
         } else if (h1) {
             node = c1;
         } else {
-            node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel;
+            node = pop(tbest);
         }
-        if (min_desc > 0 && wave_count((unsigned)node < (unsigned)kSentinel) < min_desc) break;
+        if (min_desc > 0 && wave_count(interior(node)) < min_desc) break;
     }
-    if ((unsigned)node < (unsigned)kSentinel) {          // postponed: still descending
+    if (interior(node)) {                                // postponed: still descending
         T.node = node;
         T.sp = sp;
         return false;
     }
-    bool done = node == kSentinel || leaf_hit(S, ~node, o, d, T.tmin, anyhit, T.h);
+    const int sent = OCT ? kOctSent : kSentinel;
+    bool done = node == sent || leaf_hit(S, OCT ? oct_leaf(node) : ~node, o, d, T.tmin, anyhit, T.h);
     if (!done) {
-        node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel;
-        done = node == kSentinel;
+        node = pop(OCT ? vmin(T.h.t, Cst<R>::tmax) : T.h.t);
+        done = node == sent;
     }
     T.node = node;
     T.sp = sp;

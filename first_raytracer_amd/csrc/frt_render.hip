@@ -104,23 +104,23 @@ __device__ __forceinline__ void scene_strides_hbm(DevScene &S)
 template <int WORLD>
 __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
 {
-    constexpr bool WIDE = WORLD == kWorldBvh4, OCT = WORLD == kWorldBvh2Oct;
+    // the LDS plans are binary (BVH4Q from LDS was 13 % slower on Cornell and was removed in round 4)
+    static_assert(WORLD == FRT_WORLD_BVH || WORLD == kWorldBvh2Oct, "LDS plans hold a binary tree");
+    constexpr bool OCT = WORLD == kWorldBvh2Oct;
     float4 *l4 = reinterpret_cast<float4 *>(lds_base);
     const DevScene S0 = S;
-    const int nn = WIDE ? 4 * S0.n_nodes4 : OCT ? oct_lds_node_slots(S0.n_nodes) : 4 * S0.n_nodes;
+    const int nn = OCT ? oct_lds_node_slots(S0.n_nodes) : 4 * S0.n_nodes;
     const int nt = 3 * S0.n_tris, ns = 2 * S0.n_tris, nm = kMatStride * S0.n_mats;
-    if constexpr (WIDE) {
-        const float4 *src = reinterpret_cast<const float4 *>(S0.nodes4);
-        for (int i = threadIdx.x; i < nn; i += kBlock) l4[(i & 3) * S0.n_nodes4 + (i >> 2)] = src[i];
-    } else if constexpr (OCT) {   // node e = o * n_nodes + j, part k < 3 -> [3 e + k]; refs of j -> int2 [j]
+    if constexpr (OCT) {   // node e = o * n_nodes + j, part k < 3 -> [3 e + k]; refs of j -> int2 [j]
         int2 *refs = reinterpret_cast<int2 *>(l4 + 24 * S0.n_nodes);
         for (int i = threadIdx.x; i < 32 * S0.n_nodes; i += kBlock) {
             const int e = i >> 2, k = i & 3;
             const float4 v = S0.nodes_oct[i];
             if (k < 3) l4[3 * e + k] = v;
-            else if (e < S0.n_nodes) refs[e] = make_int2(f2i(v.x), f2i(v.y));
+            else if (e < S0.n_nodes) refs[e] = make_int2(oct_code(f2i(v.x)), oct_code(f2i(v.y)));
         }
         S.node_refs = refs;
+        S.root = oct_code(S0.root);   // 16-bit refs (bvh2_step's OCT stack)
     } else {
         for (int i = threadIdx.x; i < nn; i += kBlock) l4[(i & 3) * S0.n_nodes + (i >> 2)] = S0.nodes[i];
     }
@@ -128,13 +128,8 @@ __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
     for (int i = threadIdx.x; i < ns; i += kBlock) l4[nn + nt + (i & 1) * S0.n_tris + (i >> 1)] = S0.tshade[i];
     for (int i = threadIdx.x; i < nm; i += kBlock) l4[nn + nt + ns + i] = S0.mats[i];
     __syncthreads();
-    if constexpr (WIDE) {
-        S.nodes4 = reinterpret_cast<const uint4 *>(l4);
-        S.node4_es = 1; S.node4_ps = S0.n_nodes4;
-    } else {
-        S.nodes = l4;
-        S.node_es = 1; S.node_ps = S0.n_nodes;
-    }
+    S.nodes = l4;
+    S.node_es = 1; S.node_ps = S0.n_nodes;
     S.tris = l4 + nn;
     S.tshade = l4 + nn + nt;
     S.mats = l4 + nn + nt + ns;
@@ -520,7 +515,7 @@ struct MltWork {
     float b, scale, s2p, logp;           // normaliser, nx*ny/ns, pixel-dim perturb constants
     int trav_min;                        // see path_megakernel / trav_min()
     int min_desc;                        // leaf postponing: see bvh2_step
-    float *U;                            // [n_local][kMltDims] current primary samples (one row per chain)
+    float *U;                            // [n_local][kMltRow] current primary samples + fingerprint (frt_mlt.hpp)
     unsigned long long *film;            // [nx*ny*3] splat accumulation, fixed point (kSplatFix)
     unsigned *counter;
     unsigned long long *wave_rays;
@@ -687,6 +682,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
                 if (csc > 0.0f) cw += (1.0f - a) / (csc / W.b + kMltLargeStep);
                 if (rng_u(key, 1) <= a) {               // accept: splat the old state's weight, move
                     if (csc > 0.0f && cw != 0.0f) mlt_splat(W, cx, cy, cc, cw);
+                    uint2 *fp = reinterpret_cast<uint2 *>(W.U + (size_t)j * kMltRow + kMltFp);
+                    uint2 f = *fp;                      // trajectory fingerprint: (accepts, sum of 1-based steps)
+                    f.x += 1u; f.y += t + 1u;
+                    *fp = f;
                     cw = 0.0f;
                     mat = true; mat_fresh = large;
                     cx = M.x; cy = M.y; cc = L; csc = sc;
@@ -729,7 +728,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
                 const RngKey kl{(uint32_t)__shfl((int)rk0, (int)r), (uint32_t)__shfl((int)rk1, (int)r)};
                 if (e < total) {
                     const int d = (int)(e - r * (uint32_t)kMltDims);
-                    float *row = W.U + (size_t)(jl & 0x7fffffffu) * kMltDims;   // j < 2^31: bit 31 = fresh
+                    float *row = W.U + (size_t)(jl & 0x7fffffffu) * kMltRow;   // j < 2^31: bit 31 = fresh
                     const float u = rng_u(kl, 2u + (uint32_t)d);
                     row[d] = (jl >> 31) ? u : mlt_mutate(row[d], u, d, W.s2p, W.logp);
                 }
@@ -758,6 +757,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
                     have = true;
                     init = true;
                     j = w;
+                    *reinterpret_cast<uint2 *>(W.U + (size_t)w * kMltRow + kMltFp) = make_uint2(0u, 0u);
                     const uint32_t c = (uint32_t)W.shard_index + w * (uint32_t)W.shard_count;
                     C.set(kCsC, (int)c);
                     C.set(kCsT, 0);
@@ -821,6 +821,7 @@ struct frt_ctx {
     int precision = FRT_PRECISION_AUTO;                 // frt_set_precision
     bool has_f64 = false;                               // the scene's fp64 records are in HBM
     double last_mlt_b = 0.0;
+    uint64_t mlt_rows = 0;        // chains whose state rows the last PSS-MLT render left in `partial`
     std::vector<void *> scene_bufs;
     // workspace
     float *partial = nullptr; size_t partial_bytes = 0;
@@ -1045,6 +1046,8 @@ int frt_mats::mlt(int stack, int world, bool lds, const void **boot, const void 
 {
     if (world == FRT_WORLD_LIST) mlt_kernels_t<16, FRT_WORLD_LIST, false, true>(boot, chains);
     else if (world == kWorldBvh4) mlt_kernels_t<kBvh4LdsStack, kWorldBvh4, false, true>(boot, chains);
+    else if (world == kWorldBvh2Oct && stack == 8) mlt_kernels_t<8, kWorldBvh2Oct, true, true>(boot, chains);
+    else if (world == kWorldBvh2Oct && stack == 16) mlt_kernels_t<16, kWorldBvh2Oct, true, true>(boot, chains);
     else if (lds && stack == 8) mlt_kernels_t<8, FRT_WORLD_BVH, true, true>(boot, chains);
     else if (lds && stack == 16) mlt_kernels_t<16, FRT_WORLD_BVH, true, true>(boot, chains);
     else if (!lds && stack == 16) mlt_kernels_t<16, FRT_WORLD_BVH, false, true>(boot, chains);
@@ -1675,8 +1678,11 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     // (pick_launcher_t): larger scenes get none (8x the node array otherwise).
     const size_t oct_bytes = sizeof(float4) * (oct_lds_node_slots((int)(F.nodes.size() / 4)) + F.tris.size() +
                                                F.tshade.size() + F.mats.size());
-    if (sv->world_kind == FRT_WORLD_BVH && F.depth < kLdsMaxDepth && oct_bytes <= kLdsOctBytes)
-        F.nodes_oct.resize(8 * F.nodes.size());
+    bool oct_fit = sv->world_kind == FRT_WORLD_BVH && F.depth < kLdsMaxDepth && oct_bytes <= kLdsOctBytes &&
+                   (sv->root >= 0 || oct_ref_fits(~dev_ref(~sv->root)));
+    for (size_t i = 0; oct_fit && i < F.nodes.size() / 4; ++i)   // refs as 16-bit codes (oct_code)
+        oct_fit = oct_ref_fits(f2i(F.nodes[4 * i + 3].x)) && oct_ref_fits(f2i(F.nodes[4 * i + 3].y));
+    if (oct_fit) F.nodes_oct.resize(8 * F.nodes.size());
     for (int o = 0; o < 8 && !F.nodes_oct.empty(); ++o)
         for (size_t i = 0; i < F.nodes.size() / 4; ++i) {
             const float4 *n = &F.nodes[4 * i];
@@ -1919,6 +1925,7 @@ extern "C" int frt_selftest_mlt_paths_host(const frt_scene_view *sv, int nx, int
 
 // ---- shard geometry ----
 static int eff_tile(const frt_render_params *p) { return p->tile_size > 0 ? p->tile_size : 32; }
+constexpr int kRetiredFlags = 32 | 64 | 128;   // frt.h: the round-4 plans measured slower and removed
 static bool params_ok(const frt_render_params *p)
 {
     const int T = eff_tile(p);
@@ -1926,6 +1933,7 @@ static bool params_ok(const frt_render_params *p)
           p->shard_index >= 0 && p->shard_index < p->shard_count && p->max_depth >= -1 && p->max_depth < 100000))
         return false;
     if (p->sample_offset < 0 || (int64_t)p->sample_offset + p->spp > (int64_t)0xffffffffLL) return false;
+    if (p->flags & kRetiredFlags) return false;         // removed A/B plans: fail loudly, not silently
     if (p->integrator == FRT_INTEGRATOR_PATH || p->integrator == FRT_INTEGRATOR_AO ||
         p->integrator == FRT_INTEGRATOR_NORMALS)
         return true;
@@ -2110,11 +2118,15 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
     const int d = c->stack_needed;
     const bool lds_scene = c->world_kind == FRT_WORLD_BVH && d < kLdsMaxDepth && c->scene_lds_bytes <= kLdsSceneBytes &&
                            !(p->flags & FRT_FLAG_NO_LDS_SCENE);
+    // the octant node copies when they fit, as the path kernels (round 5: the chain kernel used the planar tree)
+    const bool oct = lds_scene && !(p->flags & FRT_FLAG_NO_OCT) && c->scene_lds_bytes_oct <= kLdsOctBytes;
     if (c->world_kind == FRT_WORLD_LIST) { stack = 0; mlt_kernels<16, FRT_WORLD_LIST>(c->has_spec_mats, &kboot, &kchain); }
     else if (!lds_scene && c->has_bvh4 && !(p->flags & FRT_FLAG_BVH2) && bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
         stack = kBvh4LdsStack;
         mlt_kernels<kBvh4LdsStack, kWorldBvh4>(c->has_spec_mats, &kboot, &kchain);
     }
+    else if (oct && d < 8) { stack = 8; mlt_kernels<8, kWorldBvh2Oct, true>(c->has_spec_mats, &kboot, &kchain); }
+    else if (oct) { stack = 16; mlt_kernels<16, kWorldBvh2Oct, true>(c->has_spec_mats, &kboot, &kchain); }
     else if (lds_scene && d < 8) { stack = 8; mlt_kernels<8, FRT_WORLD_BVH, true>(c->has_spec_mats, &kboot, &kchain); }
     else if (lds_scene) { stack = 16; mlt_kernels<16, FRT_WORLD_BVH, true>(c->has_spec_mats, &kboot, &kchain); }
     else if (d < 16) { stack = 16; mlt_kernels<16, FRT_WORLD_BVH>(c->has_spec_mats, &kboot, &kchain); }
@@ -2122,7 +2134,8 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
     else if (d < 64) { stack = 64; mlt_kernels<64, FRT_WORLD_BVH>(c->has_spec_mats, &kboot, &kchain); }
     else return set_err(c, FRT_E_UNSUPPORTED, "BVH deeper than 63 levels");
     const size_t lds_boot = (size_t)stack * kBlock * sizeof(int);
-    const size_t lds = lds_boot + (size_t)kChainWords * kBlock * sizeof(int) + (lds_scene ? c->scene_lds_bytes : 0);
+    const size_t lds = lds_boot + (size_t)kChainWords * kBlock * sizeof(int) +
+                       (oct ? c->scene_lds_bytes_oct : lds_scene ? c->scene_lds_bytes : 0);
     const uint32_t n_chains = (uint32_t)p->mlt_chains;
     const uint32_t n_local = (n_chains > (uint32_t)p->shard_index)
                                  ? (n_chains - 1 - (uint32_t)p->shard_index) / (uint32_t)p->shard_count + 1 : 0;
@@ -2131,7 +2144,7 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
     if (steps >= 0xffffffffULL) return set_err(c, FRT_E_UNSUPPORTED, "pssmlt: more than 2^32 - 1 mutations per chain");
     // bootstrap normaliser (identical on every shard: same streams, fixed-order host sum)
     const int n_init = p->mlt_bootstrap;
-    const size_t need = std::max<size_t>((size_t)n_init * sizeof(float), (size_t)kMltDims * n_local * sizeof(float));
+    const size_t need = std::max<size_t>((size_t)n_init * sizeof(float), (size_t)kMltRow * n_local * sizeof(float));
     if (need > c->partial_bytes) {
         if (c->partial) HIPCHK(c, hipFree(c->partial));
         c->partial = nullptr;
@@ -2213,6 +2226,28 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
         stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     }
     c->last_mlt_b = b;
+    c->mlt_rows = (n_local > 0 && steps > 0) ? n_local : 0;
+    return FRT_OK;
+}
+
+// The chain states of the last PSS-MLT render (test / diagnostic read-back):
+// local chains [first, first + n) of that render's shard, chain c = shard_index
+// + j * shard_count.  u_out (n x 92): final primary samples; fp_out (n x 2): the
+// trajectory fingerprint (accepted proposals, sum of the accepted steps' 1-based
+// indices mod 2^32), which ora_mlt_render_shard computes the same way.
+extern "C" int frt_mlt_chain_state(frt_ctx *c, uint64_t first, uint64_t n, float *u_out, uint32_t *fp_out)
+{
+    if (!c) return FRT_E_INVALID;
+    if (c->mlt_rows == 0 || first + n > c->mlt_rows || first + n < first)
+        return set_err(c, FRT_E_INVALID, "frt_mlt_chain_state: no such chains in the last PSS-MLT render");
+    if (n == 0) return FRT_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    std::vector<float> rows(n * kMltRow);
+    HIPCHK(c, hipMemcpy(rows.data(), c->partial + first * kMltRow, rows.size() * sizeof(float), hipMemcpyDeviceToHost));
+    for (uint64_t k = 0; k < n; ++k) {
+        if (u_out) memcpy(u_out + k * kMltDims, rows.data() + k * kMltRow, kMltDims * sizeof(float));
+        if (fp_out) memcpy(fp_out + 2 * k, rows.data() + k * kMltRow + kMltFp, 2 * sizeof(uint32_t));
+    }
     return FRT_OK;
 }
 
@@ -2237,8 +2272,8 @@ extern "C" int frt_diag_read(unsigned long long *out)
 // rays a sample; profiles/r03/samecall/grab64_spi_*.jsonl).  The target rule
 // grows k with spp, so it is capped at kMaxItemsPerLane items per resident
 // lane: the (chunk, slot) partial sums, 12 B an item, stay below
-// ~1 GB at any spp (1080p 512 spp keeps its 22 chunks, 550 MB), and frames
-// of any spp fit the 32-bit queue.  FRT_SPI_TARGET overrides the target (0:
+// kMaxItemsPerLane x the resident lanes x 12 B (~1.8 GB on MI355X) at any spp,
+// and frames of any spp fit the 32-bit queue.  FRT_SPI_TARGET overrides the target (0:
 // the first rule alone; A/B knob).  spi_req > 0: the caller's samples per item.
 // Round 4: the chunks are the whole frame's for every shard count (films
 // identical at any N), so at N = 8 a shard has an eighth of the items.  Path
@@ -2284,6 +2319,7 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     if (!params_ok(p)) return set_err(c, FRT_E_INVALID, "bad render params");
     if (!c->have_scene) return set_err(c, FRT_E_NO_SCENE, "no scene uploaded");
     HIPCHK(c, hipSetDevice(c->device));
+    c->mlt_rows = 0;                                   // `partial` is about to be reused
     if (p->integrator == FRT_INTEGRATOR_PSSMLT) return render_mlt(c, p, dev_slots, st, stats);
     if (p->integrator == FRT_INTEGRATOR_AO && c->has_metal)   // ao::Li -> constant_pdf::generate throws (pdf.h:195-198)
         return set_err(c, FRT_E_UNSUPPORTED, "ao integrator: metal has no sampling pdf (constant_pdf::generate)");

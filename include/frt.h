@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FRT_ABI_VERSION 8
+#define FRT_ABI_VERSION 9
 
 enum {
     FRT_OK = 0,
@@ -57,7 +57,7 @@ enum { FRT_FLAG_NO_LDS_SCENE = 1,      /* render_params.flags: keep small scenes
        FRT_FLAG_WAVES4 = 8,            /* the compiler's own allocation, ~4 waves/SIMD (A/B timing)      */
        FRT_FLAG_BVH2 = 16,             /* binary nodes for HBM-resident scenes (A/B timing, self-test)   */
        /* 32, 64, 128: retired A/B plans (4-wide nodes from LDS, lockstep brute force,
-          speculative traversal), measured slower and removed in round 4; the bits are ignored */
+          speculative traversal), measured slower and removed in round 4; FRT_E_INVALID since round 5 */
        FRT_FLAG_NO_OCT = 256,          /* LDS binary plan without the per-octant node copies (A/B timing) */
        FRT_FLAG_FP64 = 512,            /* path: the fp64 kernel for this call (self-test: fp64 host replay) */
        FRT_FLAG_FP32 = 1024 };         /* path: the fp32 kernels even where the precision picks fp64      */
@@ -243,6 +243,16 @@ int frt_render_multi(frt_ctx **ctxs, int n, const frt_render_params *p, float *f
 int frt_render_device(frt_ctx *ctx, const frt_render_params *p, float *slots_rgb, void *hip_stream,
                       frt_stats *st);
 
+/* PSS-MLT chain states of this context's last PSS-MLT render (parity tests and
+ * diagnostics; pssmlt.cpp:301-365 keeps them in TMarkovChain): its local chains
+ * [first, first + n), local chain j = global chain shard_index + j *
+ * shard_count.  u_out (n x 92 floats, or NULL): the chain's final primary
+ * samples; fp_out (n x 2, or NULL): its trajectory fingerprint = (accepted
+ * proposals, sum of the accepted mutations' 1-based step indices mod 2^32).
+ * FRT_E_INVALID when the last render of the context was not PSS-MLT or the
+ * range is outside its chains. */
+int frt_mlt_chain_state(frt_ctx *ctx, uint64_t first, uint64_t n, float *u_out, uint32_t *fp_out);
+
 /* Ray queries on the uploaded scene: Scene::world->hit (path.cpp:10, 50;
  * parallel_bvh_node::hit parallel_bvh.h:39-64, hitable_list::hit
  * hitable_list.cpp:4-21) for a batch of rays, with the world's own t_min
@@ -256,7 +266,14 @@ int frt_render_device(frt_ctx *ctx, const frt_render_params *p, float *slots_rgb
  * The ray queue has its own word in the context, apart from the render's, but
  * a context is still one stream's worth of state: calls on one context are
  * issued from one host thread, one at a time (each returns when its work is
- * done).  n plus a chunk of 256 rays per resident wave must stay below 2^32. */
+ * done).  n plus a chunk of 256 rays per resident wave must stay below 2^32.
+ * Input domain: finite origins, directions and t_max, directions not zero,
+ * and |origin| and the scene's coordinates below 1e8 on every axis.  (A
+ * direction component below 1e-30 is nudged to +-1e-30 for the slab test;
+ * with both an origin and a box plane beyond ~3.4e8 on that axis the slab
+ * distances would be inf - inf = NaN, and the NaN-propagating min / max of
+ * the box test would then cull the box.)  The rays a render makes stay inside
+ * this domain for every scene the reference builds. */
 int frt_trace_device(frt_ctx *ctx, const float *rays, int64_t n, float *hits, int flags, void *hip_stream,
                      frt_stats *st);
 

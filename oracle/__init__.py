@@ -93,6 +93,10 @@ def lib():
         L.ora_mlt_render.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_longlong, ctypes.c_int, ctypes.c_void_p,
                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(Counters)]
+        L.ora_mlt_render_shard.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_longlong, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(Counters),
+                                           ctypes.c_void_p, ctypes.c_void_p]
         L.ora_mlt_eye_path.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, dp, dp]
         L.ora_mlt_eye_path.restype = None
         L.ora_write_pfm.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, dp]
@@ -280,6 +284,27 @@ class OracleScene:
         if rc != 0:
             raise RuntimeError(f"ora_mlt_render failed: {rc}")
         return film, b.value, cnt
+
+    def mlt_render_shard(self, nx, ny, n_chains, steps, shard_index, shard_count, seed=0, n_init=10000,
+                         nthreads=None):
+        """The chains c = shard_index + j * shard_count of an n_chains PSS-MLT
+        render (the GPU's shard rule): (film, b, counters, fingerprints, final
+        states).  fingerprints[j] = (accepted proposals, sum of the accepted
+        steps' 1-based indices mod 2^32); states[j] = the chain's final 92
+        primary samples."""
+        n_local = (n_chains - 1 - shard_index) // shard_count + 1 if shard_index < n_chains else 0
+        film = np.zeros((ny, nx, 3))
+        fp = np.zeros((max(n_local, 1), 2), np.uint32)
+        u = np.zeros((max(n_local, 1), 92))
+        b = ctypes.c_double()
+        cnt = Counters()
+        nthreads = nthreads or min(16, os.cpu_count() or 1)
+        rc = lib().ora_mlt_render_shard(self.ptr, nx, ny, seed, n_init, n_chains, steps, shard_index, shard_count,
+                                        nthreads, film.ctypes.data, ctypes.byref(b), ctypes.byref(cnt),
+                                        fp.ctypes.data, u.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"ora_mlt_render_shard failed: {rc}")
+        return film, b.value, cnt, fp[:n_local], u[:n_local]
 
     def mlt_bootstrap(self, nx, ny, seed=0, n_init=10000):
         return lib().ora_mlt_bootstrap(self.ptr, nx, ny, seed, n_init)

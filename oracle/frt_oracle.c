@@ -1313,8 +1313,9 @@ static inline double mlt_perturb(double value, double s1, double s2, double r)
 
 typedef struct {
     const ora_scene *s; int nx, ny; uint32_t seed; double b, scale;
-    int c0, c1; long long steps;
-    double *film; ora_counters cnt; pthread_mutex_t *mu;
+    int j0, j1, shard_index, shard_count; long long steps;    /* chains c = shard_index + j * shard_count */
+    double *film; ora_counters cnt;
+    uint32_t *fp; double *u;                                 /* per local chain: fingerprint, final state */
 } mlt_job;
 
 static void mlt_splat(double *film, int nx, int ny, const mlt_contrib *pc, double w, double scale)
@@ -1332,7 +1333,9 @@ static void *mlt_worker(void *arg)
     double cur[MLT_DIMS], prop[MLT_DIMS];
     const double s1p = 2.0 / (double)(j->nx + j->ny), s2p = (double)0.1f;
     memset(&j->cnt, 0, sizeof j->cnt);
-    for (int c = j->c0; c < j->c1; ++c) {
+    for (int jl = j->j0; jl < j->j1; ++jl) {
+        const int c = j->shard_index + jl * j->shard_count;
+        uint32_t n_acc = 0, acc_sum = 0;                     /* chain fingerprint (see ora_mlt_render_shard) */
         rng_key k0 = rng_make(j->seed ^ 0x3C6EF372U, (uint32_t)c, 0u);
         for (int d = 0; d < MLT_DIMS; ++d) cur[d] = rng_u(k0, (uint32_t)(2 + d));
         mlt_contrib C = mlt_eye_path(j->s, cur, j->nx, j->ny, &j->cnt);
@@ -1354,8 +1357,13 @@ static void *mlt_worker(void *arg)
             if (C.sc > 0.0) { a = P.sc / C.sc; a = a < 1.0 ? a : 1.0; a = a > 0.0 ? a : 0.0; }
             if (P.sc > 0.0) mlt_splat(j->film, j->nx, j->ny, &P, (a + large) / (P.sc / j->b + MLT_LARGE_STEP_PROB), j->scale);
             if (C.sc > 0.0) mlt_splat(j->film, j->nx, j->ny, &C, (1.0 - a) / (C.sc / j->b + MLT_LARGE_STEP_PROB), j->scale);
-            if (rng_u(k, 1) <= a) { memcpy(cur, prop, sizeof cur); C = P; }
+            if (rng_u(k, 1) <= a) {
+                memcpy(cur, prop, sizeof cur); C = P;
+                n_acc += 1u; acc_sum += (uint32_t)(t + 1);
+            }
         }
+        if (j->fp) { j->fp[2 * (size_t)jl] = n_acc; j->fp[2 * (size_t)jl + 1] = acc_sum; }
+        if (j->u) memcpy(j->u + (size_t)jl * MLT_DIMS, cur, sizeof cur);
     }
     return NULL;
 }
@@ -1375,17 +1383,28 @@ double ora_mlt_bootstrap(const ora_scene *s, int nx, int ny, uint32_t seed, int 
     return b / n_init;
 }
 
-/* pssmlt::Render (pssmlt.cpp:301-365): n_chains chains of `steps` mutations
- * each; film (nx*ny*3, zeroed by the caller) receives the splats scaled by
- * nx*ny/(n_chains*steps) as AccumulatePathContribution does with ns. */
-int ora_mlt_render(const ora_scene *s, int nx, int ny, uint32_t seed, int n_init, int n_chains, long long steps,
-                   int nthreads, double *film, double *b_out, ora_counters *cnt)
+/* pssmlt::Render (pssmlt.cpp:301-365) for the chains of one shard: of
+ * n_chains chains of `steps` mutations each, the n_local chains
+ * c = shard_index + j * shard_count (j = 0, 1, ...), the GPU's shard rule
+ * (frt_render.hip MltWork).  film (nx*ny*3, zeroed by the caller) receives
+ * their splats scaled by nx*ny/(n_chains*steps) as AccumulatePathContribution
+ * does with ns, so the shard films of all shards sum to the full render.
+ * Per local chain j (optional): fp[2j] = accepted proposals, fp[2j+1] = the
+ * sum of the accepted steps' 1-based indices mod 2^32 -- the trajectory's
+ * fingerprint, which the GPU keeps too -- and u[92 j ..] = its final state. */
+int ora_mlt_render_shard(const ora_scene *s, int nx, int ny, uint32_t seed, int n_init, int n_chains, long long steps,
+                         int shard_index, int shard_count, int nthreads, double *film, double *b_out,
+                         ora_counters *cnt, uint32_t *fp, double *u)
 {
     if (!s || nx <= 0 || ny <= 0 || n_chains <= 0 || steps <= 0 || n_init <= 0) return -1;
+    if (shard_count < 1 || shard_index < 0 || shard_index >= shard_count) return -1;
+    const int n_local = shard_index < n_chains ? (n_chains - 1 - shard_index) / shard_count + 1 : 0;
     const double b = ora_mlt_bootstrap(s, nx, ny, seed, n_init);
     if (b_out) *b_out = b;
+    if (cnt) memset(cnt, 0, sizeof *cnt);
+    if (n_local == 0) return 0;
     if (nthreads < 1) nthreads = 1;
-    if (nthreads > n_chains) nthreads = n_chains;
+    if (nthreads > n_local) nthreads = n_local;
     mlt_job *jobs = (mlt_job *)calloc((size_t)nthreads, sizeof(mlt_job));
     pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
     double **films = (double **)calloc((size_t)nthreads, sizeof(double *));
@@ -1393,8 +1412,9 @@ int ora_mlt_render(const ora_scene *s, int nx, int ny, uint32_t seed, int n_init
     for (int t = 0; t < nthreads; ++t) {
         films[t] = (double *)calloc((size_t)nx * ny * 3, sizeof(double));
         jobs[t].s = s; jobs[t].nx = nx; jobs[t].ny = ny; jobs[t].seed = seed; jobs[t].b = b; jobs[t].scale = scale;
-        jobs[t].c0 = (int)((long long)n_chains * t / nthreads); jobs[t].c1 = (int)((long long)n_chains * (t + 1) / nthreads);
-        jobs[t].steps = steps; jobs[t].film = films[t];
+        jobs[t].j0 = (int)((long long)n_local * t / nthreads); jobs[t].j1 = (int)((long long)n_local * (t + 1) / nthreads);
+        jobs[t].shard_index = shard_index; jobs[t].shard_count = shard_count;
+        jobs[t].steps = steps; jobs[t].film = films[t]; jobs[t].fp = fp; jobs[t].u = u;
         pthread_create(&th[t], NULL, mlt_worker, &jobs[t]);
     }
     ora_counters tot; memset(&tot, 0, sizeof tot);
@@ -1410,6 +1430,13 @@ int ora_mlt_render(const ora_scene *s, int nx, int ny, uint32_t seed, int n_init
     if (cnt) *cnt = tot;
     free(jobs); free(th); free(films);
     return 0;
+}
+
+/* every chain (shard 0 of 1) */
+int ora_mlt_render(const ora_scene *s, int nx, int ny, uint32_t seed, int n_init, int n_chains, long long steps,
+                   int nthreads, double *film, double *b_out, ora_counters *cnt)
+{
+    return ora_mlt_render_shard(s, nx, ny, seed, n_init, n_chains, steps, 0, 1, nthreads, film, b_out, cnt, NULL, NULL);
 }
 
 /* one PSS-MLT eye path for given primary samples (92 doubles): out x, y, r, g, b, sc */

@@ -117,6 +117,13 @@ double ora_scene_ao_tmax(const ora_scene *s);
 double ora_mlt_bootstrap(const ora_scene *s, int nx, int ny, uint32_t seed, int n_init);
 int  ora_mlt_render(const ora_scene *s, int nx, int ny, uint32_t seed, int n_init, int n_chains, long long steps,
                     int nthreads, double *film, double *b_out, ora_counters *cnt);
+/* the chains c = shard_index + j * shard_count of an n_chains render (the GPU's
+ * shard rule); per local chain, optionally: fp[2j] = accepted proposals,
+ * fp[2j+1] = sum of the accepted steps' 1-based indices mod 2^32, u[92 j ..]
+ * = final state */
+int  ora_mlt_render_shard(const ora_scene *s, int nx, int ny, uint32_t seed, int n_init, int n_chains, long long steps,
+                          int shard_index, int shard_count, int nthreads, double *film, double *b_out,
+                          ora_counters *cnt, uint32_t *fp, double *u);
 void ora_mlt_eye_path(const ora_scene *s, int nx, int ny, const double *prnds, double *out6);
 
 /* Single query of the world (closest or any hit) with reference counters. */

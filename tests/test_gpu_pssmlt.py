@@ -39,6 +39,14 @@ def test_short_chains_match_oracle(ctx, kind, objfix, request):
     assert abs(st.rays - cnt.rays) / cnt.rays < 2e-3
     scale = max(1.0, float(np.abs(ref).max()))
     assert e <= 1e-3 * scale
+    # the chains' trajectory fingerprints and final states (frt_mlt_chain_state)
+    u, fp = ctx.mlt_chain_state(0, chains)
+    _, _, _, fp_o, u_o = oracle.OracleScene(kind, obj, nx / ny).mlt_render_shard(nx, ny, chains, steps, 0, 1, seed=7,
+                                                                                 n_init=2000)
+    same = np.all(fp == fp_o, axis=1)
+    print(kind, "path-exact chains", int(same.sum()), "of", chains, "accepts", int(fp[:, 0].sum()), int(fp_o[:, 0].sum()))
+    assert same.mean() >= 0.99
+    assert np.abs(u[same] - u_o[same]).max() <= 1e-5
 
 
 @pytest.mark.parametrize("flags", [frt.FRT_FLAG_NO_LDS_SCENE, frt.FRT_FLAG_NO_LDS_SCENE | frt.FRT_FLAG_BVH2])
@@ -149,3 +157,50 @@ def test_block_means_match_oracle_path(ctx, cornell_obj):
         errs.append(r["mean_rel_err_b_corrected"])
     print("mean_rel_err_b_corrected per seed", errs, "mean", float(np.mean(errs)))
     assert abs(float(np.mean(errs))) <= r["tolerance"]["mean_rel_err_b_corrected"]
+
+
+def test_chain_state_needs_a_pssmlt_render(ctx, cornell_obj):
+    ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, 1.0))
+    ctx.render(frt.RenderParams.make(16, 16, 1, seed=1))
+    with pytest.raises(frt.FrtError):
+        ctx.mlt_chain_state(0, 1)
+    f = np.zeros((16, 16, 3), np.float32)
+    ctx.render(frt.RenderParams.pssmlt(16, 16, 4, 64, seed=1, bootstrap=100, shard_index=1, shard_count=2), f)
+    u, fp = ctx.mlt_chain_state(0, 32)                     # shard (1, 2) holds 32 chains
+    assert u.shape == (32, 92) and ((u >= 0) & (u <= 1)).all()
+    with pytest.raises(frt.FrtError):
+        ctx.mlt_chain_state(0, 33)
+
+
+def test_c5_chain_shard_matches_oracle(ctx, cornell_obj):
+    """C5 at its own config: CornellBox-Original 1920x1080,
+    512 mutations per pixel over 2^18 chains = 4050 mutations a chain.  The GPU
+    renders shard (0, 256) -- the 1024 chains c = 0 mod 256, each for the full
+    4050 mutations -- and the oracle's fp64 restatement of pssmlt.cpp runs the
+    same chains on the same streams (ora_mlt_render_shard).  A chain is
+    path-exact when its trajectory fingerprint (accepted proposals, sum of the
+    accepted steps' indices) equals the oracle's; fp32 rounding can flip one
+    accept or hit decision, after which the two copies walk apart until both
+    accept the same large step (`diverged_chains`).  Gates: samples equal, ray
+    counts within 2e-3, >= 90 % of the chains path-exact, their final states
+    within 1e-4, shard-film means within 1 % and 8x8-block means within 5 %
+    (relative L2).  It also prints the start-up bias of both against the GPU
+    path tracer at pssmlt's depth cap: the GPU's chains and the oracle's carry
+    the same bias."""
+    import bench
+    nx, ny, mpp, n_chains, K = 1920, 1080, 512, 1 << 18, 256
+    ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, nx / ny))
+    r = bench.mlt_shard_parity(ctx, "cornell_box_obj", cornell_obj, nx, ny, mpp, n_chains, K, 0, 16)
+    r.pop("gpu_film")
+    pt, _ = ctx.render(frt.RenderParams.make(nx, ny, 32, seed=11, max_depth=10))
+    ptm = float(pt.mean())
+    print("C5 shard parity:", r)
+    print("start-up bias vs path tracer (depth 10, 32 spp, mean %.6f): gpu %+.4f oracle %+.4f"
+          % (ptm, K * np.mean(r["mean_gpu"]) / ptm - 1.0, K * np.mean(r["mean_oracle"]) / ptm - 1.0))
+    assert r["samples_gpu"] == r["samples_oracle"] == r["chains"] * r["steps_per_chain"]
+    assert r["steps_per_chain"] == 4050 and r["chains"] == 1024
+    assert r["rays_rel_diff"] < 2e-3
+    assert r["path_exact_chains"] >= 0.9 * r["chains"]
+    assert r["state_maxdiff_path_exact"] <= 1e-4
+    assert abs(r["mean_rel_diff"]) <= 1e-2
+    assert r["block8_rel_l2"] <= 0.05

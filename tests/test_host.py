@@ -21,7 +21,7 @@ def test_library_exports_every_declared_symbol():
     L = frt.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert L.frt_get_abi_version() == frt.ABI_VERSION == 8
+    assert L.frt_get_abi_version() == frt.ABI_VERSION == 9
 
 
 def test_create_without_device_fails_cleanly():

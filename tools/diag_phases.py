@@ -7,7 +7,9 @@
 Counter pairs (wave trips, active lanes summed over trips): 0 BVH4Q node
 iterations, 1 leaf primitive tests, 2 binary node iterations, 3 step-loop
 iterations (tracing lanes), 4 shading passes (lanes shading), 6 outer-loop
-iterations; cycles (s_memtime, per wave, summed): 16 step loop, 17 shading,
+iterations, 7 octant-plan stack entries skipped by pop culling (entry
+distance beyond the closest hit: each was a node visit or a leaf test before
+round 5); cycles (s_memtime, per wave, summed): 16 step loop, 17 shading,
 18 refill + ray setup.  Timing under instrumentation is perturbed; the lane
 counts are exact.
 """
@@ -47,7 +49,7 @@ def main():
     buf = (ctypes.c_ulonglong * 24)()
     frt.lib().frt_diag_read(buf)
     v = list(buf)
-    names = {0: "bvh4_node", 1: "leaf_prim", 2: "bvh2_node", 3: "step", 4: "shade", 6: "outer"}
+    names = {0: "bvh4_node", 1: "leaf_prim", 2: "bvh2_node", 3: "step", 4: "shade", 6: "outer", 7: "culled_pop"}
     out = {"scene": args.scene, "spp": args.spp, "rays": st.rays, "kernel_ms": st.kernel_ms,
            "waves_cap": st.waves_cap, "stack": st.stack_entries}
     for k, n in names.items():

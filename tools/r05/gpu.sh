@@ -1,0 +1,42 @@
+# Round-5 GPU calls: one stage per gpurun call, `bash tools/r05/gpu.sh <stage>`,
+# run from the repository root on the GPU box.  Every GPU step has its own time
+# limit and the steps are chained with &&, so the first failure ends the call.
+# Outputs go to gpurun_out/r05<stage>/; the ones kept are copied to
+# profiles/r05/r05<stage>/.  (One indexed file instead of round 4's one script
+# per call; the stage letter is the record's name.)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
+S=$1; O=gpurun_out/r05$S; mkdir -p $O
+pt() {  # name, seconds, pytest args...
+  local n=$1 s=$2; shift 2
+  timeout -k 10 $s python -u -m pytest -x -v --timeout 600 --timeout-method thread "$@" > $O/pytest_$n.txt 2>&1
+}
+b() {  # name, seconds, bench args...
+  local n=$1 s=$2; shift 2
+  timeout -k 10 $s python -u bench.py "$@" > $O/bench_$n.json 2> $O/bench_$n.log
+}
+E=first_raytracer_amd/build/exp
+ab() {  # tag, lib ('' = in-tree), perf_ab args...
+  local t=$1 l=$2; shift 2
+  if [ -n "$l" ]; then FRT_LIB_PATH=$E/$l timeout -k 10 300 python -u tools/perf_ab.py "$@" >> $O/ab_$t.jsonl 2>> $O/ab.log
+  else timeout -k 10 300 python -u tools/perf_ab.py "$@" >> $O/ab_$t.jsonl 2>> $O/ab.log; fi
+}
+C="--scene cornell --spp 512 --rounds 3 --bvh gsah --variants default"
+P="--scene cornell --spp 512 --rounds 2 --bvh gsah --integrator pssmlt --variants default"
+case $S in
+a)  # the GPU suite (C5 chain-shard parity is new) + smoke on the build with
+    # octant-plan pop culling and the octant plan for PSS-MLT, then the PSS-MLT line
+    pt gpu 1100 tests -m gpu \
+     && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
+     && b pssmlt 500 --integrator pssmlt ;;
+b)  # the default line, the launcher's gloo rehearsal (two ranks, one GPU, no
+    # torchrun), the diagnostic build's phase counters, and same-call A/B of the
+    # pop culling (Cornell) and the octant plan for PSS-MLT against the r05 base
+    # build (build/exp/libfrt_base.so: before both)
+    b default 500 \
+     && b gloo2 400 --gpus 2 --backend gloo --steps 2 --north-star off \
+     && FRT_LIB_PATH=$E/libfrt_diag.so timeout -k 10 200 python tools/diag_phases.py --scene cornell --spp 32 > $O/diag_cornell.json 2> $O/diag.log \
+     && ab c "" $C && ab c libfrt_base.so $C && ab c "" $C && ab c libfrt_base.so $C \
+     && ab mlt "" $P && ab mlt libfrt_base.so $P && ab mlt "" $P && ab mlt libfrt_base.so $P ;;
+*) echo "unknown stage $S"; exit 2 ;;
+esac
