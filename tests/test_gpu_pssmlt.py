@@ -181,12 +181,14 @@ def test_c5_chain_shard_matches_oracle(ctx, cornell_obj):
     path-exact when its trajectory fingerprint (accepted proposals, sum of the
     accepted steps' indices) equals the oracle's; fp32 rounding can flip one
     accept or hit decision, after which the two copies walk apart until both
-    accept the same large step (`diverged_chains`).  Gates: samples equal, ray
-    counts within 2e-3, >= 90 % of the chains path-exact, their final states
-    within 1e-4, shard-film means within 1 % and 8x8-block means within 5 %
-    (relative L2).  It also prints the start-up bias of both against the GPU
-    path tracer at pssmlt's depth cap: the GPU's chains and the oracle's carry
-    the same bias."""
+    accept the same large step (`diverged_chains`; 133 of 16,384 = 0.8 % in the
+    bench's shard of 16, profiles/r05/r05a).  Gates: samples equal, ray counts
+    within 2e-3, >= 97 % of the chains path-exact, their final states within
+    1e-4, shard-film means within 1e-3 and 8x8-block means within 1 % (relative
+    L2), and the full-frame RMSE estimate sqrt(K) x shard RMSE <= 1e-3 (the
+    north star's gate).  It also prints the start-up bias of both against the
+    GPU path tracer at pssmlt's depth cap: the GPU's chains and the oracle's
+    carry the same bias."""
     import bench
     nx, ny, mpp, n_chains, K = 1920, 1080, 512, 1 << 18, 256
     ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, nx / ny))
@@ -200,7 +202,8 @@ def test_c5_chain_shard_matches_oracle(ctx, cornell_obj):
     assert r["samples_gpu"] == r["samples_oracle"] == r["chains"] * r["steps_per_chain"]
     assert r["steps_per_chain"] == 4050 and r["chains"] == 1024
     assert r["rays_rel_diff"] < 2e-3
-    assert r["path_exact_chains"] >= 0.9 * r["chains"]
+    assert r["path_exact_chains"] >= 0.97 * r["chains"]
     assert r["state_maxdiff_path_exact"] <= 1e-4
-    assert abs(r["mean_rel_diff"]) <= 1e-2
-    assert r["block8_rel_l2"] <= 0.05
+    assert abs(r["mean_rel_diff"]) <= 1e-3
+    assert r["block8_rel_l2"] <= 0.01
+    assert r["full_frame_rmse_est"] <= 1e-3
