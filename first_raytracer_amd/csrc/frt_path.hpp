@@ -424,28 +424,58 @@ FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyh
 // so culling stays conservative and the hit equals the binary traversal's
 // bit for bit (the (t, DFS rank) minimum does not depend on visit order).
 // fp32 only: the fp64 kernels traverse the binary tree.
-template <int STRIDE, int LSTACK>
-FRT_HD bool bvh4_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int *ovf, int min_desc = 0)
+// Entry distances of the 4-wide stack (TQ, the path kernels): one byte per LDS
+// entry in a column beside the stack (tq[k * STRIDE]), the distance's fp32 bits
+// >> 20 (exponent and 3 mantissa bits) over [2^-16, 2^16): q = 0 stands for
+// "no bound" (0), so dq(q) never exceeds the true entry distance.  Entries in
+// the private overflow carry none.
+FRT_HD uint32_t tq8(float t) { return (uint32_t)min(max((int)(f2u(t) >> 20) - (111 << 3), 0), 255); }
+FRT_HD float tq8_lo(uint32_t q) { return q == 0u ? 0.0f : u2f((q + (111u << 3)) << 20); }
+
+template <int STRIDE, int LSTACK, bool TQ = false>
+FRT_HD bool bvh4_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int *ovf, int min_desc = 0,
+                      uint8_t *tq = nullptr)
 {
     int node = T.node, sp = T.sp;
     // Entries below LSTACK live in the lane's LDS column, deeper ones in `ovf`
     // (scratch).  A wave-uniform test keeps the common case on plain LDS
     // accesses: a per-lane select between the two would make the compiler
     // branch per push and pop through a generic (flat) pointer.
-    auto push = [&](int v) {
+    auto push = [&](int v, float t) {
         if (!wave_any(sp >= LSTACK)) {
             stk[sp * STRIDE] = v;
+            if constexpr (TQ) tq[sp * STRIDE] = (uint8_t)tq8(t);
         } else {
-            if (sp < LSTACK) stk[sp * STRIDE] = v;
-            else ovf[sp - LSTACK] = v;
+            if (sp < LSTACK) {
+                stk[sp * STRIDE] = v;
+                if constexpr (TQ) tq[sp * STRIDE] = (uint8_t)tq8(t);
+            } else {
+                ovf[sp - LSTACK] = v;
+            }
         }
         ++sp;
     };
-    auto pop = [&]() -> int {
-        if (sp == 0) return kSentinel;
-        --sp;
-        if (!wave_any(sp >= LSTACK)) return stk[sp * STRIDE];
-        return sp < LSTACK ? stk[sp * STRIDE] : ovf[sp - LSTACK];
+    // TQ: entries whose entry distance lies beyond t_best (tb) are skipped (pop
+    // culling, as bvh2_step's octant plan): a node or leaf entered beyond the
+    // closest hit cannot hold a hit with t <= t_best (boxes are padded outward)
+    auto pop = [&](float tb) -> int {
+        while (sp > 0) {
+            --sp;
+            int v;
+            uint32_t q = 0;
+            if (!wave_any(sp >= LSTACK)) {
+                v = stk[sp * STRIDE];
+                if constexpr (TQ) q = tq[sp * STRIDE];
+            } else if (sp < LSTACK) {
+                v = stk[sp * STRIDE];
+                if constexpr (TQ) q = tq[sp * STRIDE];
+            } else {
+                v = ovf[sp - LSTACK];
+            }
+            if (!TQ || !(tq8_lo(q) > tb)) return v;
+            FRT_DIAG_TICK(7);
+        }
+        return kSentinel;
     };
     while ((unsigned)node < (unsigned)kSentinel) {
         FRT_DIAG_TICK(0);
@@ -488,15 +518,18 @@ FRT_HD bool bvh4_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit
         cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
         // hit children are sorted first; the far ones go on the stack, farthest first
         if (!wave_any(sp > LSTACK - 3)) {               // wave-uniform: every push stays in LDS
-            if (t[3] != __builtin_inff()) stk[sp++ * STRIDE] = c[3];
-            if (t[2] != __builtin_inff()) stk[sp++ * STRIDE] = c[2];
-            if (t[1] != __builtin_inff()) stk[sp++ * STRIDE] = c[1];
+#pragma unroll
+            for (int i = 3; i >= 1; --i)
+                if (t[i] != __builtin_inff()) {
+                    if constexpr (TQ) tq[sp * STRIDE] = (uint8_t)tq8(t[i]);
+                    stk[sp++ * STRIDE] = c[i];
+                }
         } else {
-            if (t[3] != __builtin_inff()) push(c[3]);
-            if (t[2] != __builtin_inff()) push(c[2]);
-            if (t[1] != __builtin_inff()) push(c[1]);
+            if (t[3] != __builtin_inff()) push(c[3], t[3]);
+            if (t[2] != __builtin_inff()) push(c[2], t[2]);
+            if (t[1] != __builtin_inff()) push(c[1], t[1]);
         }
-        node = (t[0] != __builtin_inff()) ? c[0] : pop();
+        node = (t[0] != __builtin_inff()) ? c[0] : pop(T.h.t);
         if (min_desc > 0 && wave_count((unsigned)node < (unsigned)kSentinel) < min_desc) break;
     }
     if ((unsigned)node < (unsigned)kSentinel) {          // postponed (min_desc): still descending
@@ -506,7 +539,7 @@ FRT_HD bool bvh4_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit
     }
     bool done = node == kSentinel || leaf_hit<true>(S, ~node, o, d, T.tmin, anyhit, T.h);
     if (!done) {
-        node = pop();
+        node = pop(T.h.t);
         done = node == kSentinel;
     }
     T.node = node;
@@ -571,9 +604,10 @@ FRT_HD bool trav_begin_world(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, R 
         return trav_begin(T, S, WORLD == kWorldBvh4 ? S.root4 : S.root, o, d, tmax);
     }
 }
-template <int WORLD, int STRIDE, int STACK, typename R>
+// TQ: the 4-wide stack keeps entry distances in `tq` (bvh4_step; the path kernels)
+template <int WORLD, int STRIDE, int STACK, bool TQ = false, typename R>
 FRT_HD bool trav_step_world(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyhit, int *stk, int *ovf,
-                            int min_desc = 0)
+                            int min_desc = 0, uint8_t *tq = nullptr)
 {
     // 4-wide (HBM-resident scenes): the slab ray and t_min again from (o, d)
     // (the values trav_begin set), so that they are not live across the
@@ -588,7 +622,7 @@ FRT_HD bool trav_step_world(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, boo
         T.h = trace_list(S, o, d, T.h.t, anyhit);
         return true;
     } else if constexpr (WORLD == kWorldBvh4) {
-        return bvh4_step<STRIDE, STACK>(T, S, o, d, anyhit, stk, ovf, min_desc);
+        return bvh4_step<STRIDE, STACK, TQ>(T, S, o, d, anyhit, stk, ovf, min_desc, tq);
     } else {
         return bvh2_step<STRIDE, WORLD == kWorldBvh2Oct>(T, S, o, d, anyhit, stk, min_desc);
     }

@@ -147,8 +147,11 @@ __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
 // spilled to scratch -- across every traversal and shading phase (spilled
 // VGPRs at the register cap: cornell_1m 51 -> 24, Cornell 31 -> 6; same-call
 // A/B +4.5 % / +1 %).
-constexpr int kItemWords = 10;
-enum { kIsCur, kIsEnd, kIsSlot, kIsChunk, kIsPix, kIsPx, kIsPy, kIsAcc };   // kIsAcc..+2: r, g, b
+// Round 5: 7 words (was 10): the item's end follows from its chunk, and the
+// pixel is one packed word (px | py << 16; the linear index py * nx + px is
+// one mad), which leaves LDS for the stack entries' distances (bvh4_step).
+constexpr int kItemWords = 7;
+enum { kIsCur, kIsSlot, kIsChunk, kIsPxy, kIsAcc };   // kIsAcc..+2: r, g, b
 struct ItemState {
     int *b;      // the lane's column
     __device__ int get(int k) const { return b[k * kBlock]; }
@@ -163,10 +166,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     const DevScene S0, const DevWork W)
 {
     // [STACK][kBlock] stack, [kItemWords][kBlock] item state, then the scene
+    // (LDS plans) or the 4-wide stack's entry distances ([STACK][kBlock] bytes)
     extern __shared__ __attribute__((aligned(16))) int lds_mem[];
     int *stk = lds_mem + threadIdx.x;                                 // one LDS column per lane
     constexpr int kStackInts = WORLD != FRT_WORLD_LIST ? STACK * kBlock : 0;
     constexpr int kItemInts = kItemWords * kBlock;
+    constexpr bool kTQ = WORLD == kWorldBvh4;                         // pop culling on the 4-wide stack
+    uint8_t *tq = reinterpret_cast<uint8_t *>(lds_mem + kStackInts + kItemInts) + threadIdx.x;
     DevScene S = S0;
     if constexpr (LDS_SCENE) scene_to_lds<WORLD>(S, lds_mem + kStackInts + kItemInts);
     else scene_strides_hbm(S);
@@ -178,6 +184,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     // the wave's own item range [q_cur, q_end) from its last queue atomic (wave-uniform)
     uint32_t q_cur = 0, q_end = 0;
     const ItemState I{lds_mem + kStackInts + (int)threadIdx.x};
+    auto item_end = [&]() { return min(W.spp, (I.get(kIsChunk) + 1) * W.spi); };
+    auto item_pix = [&](int &px, int &py) {
+        const int xy = I.get(kIsPxy);
+        px = xy & 0xffff; py = xy >> 16;
+        return py * W.nx + px;
+    };
     PathState<R> P;
     // ray in flight: tracing = traversal steps remain; pending = finished, not yet shaded
     Trav<R> T;
@@ -219,9 +231,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             bool shadow_done = false;
             if (tracing) FRT_DIAG_TICK(3);
             // (LDS-resident binary plans: no leaf postponing, compiled out)
-            if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, P.ro, P.rd, P.shadow, stk, ovf,
+            if (tracing && trav_step_world<WORLD, kBlock, STACK, kTQ>(T, S, P.ro, P.rd, P.shadow, stk, ovf,
                                                                        LDS_SCENE && (WORLD == FRT_WORLD_BVH || WORLD == kWorldBvh2Oct)
-                                                                           ? 0 : W.min_desc)) {
+                                                                           ? 0 : W.min_desc, tq)) {
                 if (KIND == FRT_INTEGRATOR_PATH && P.shadow) {   // finish the shadow ray here, keep traversing
                     if (path_after_shadow<MATS>(P, T.h.prim < 0)) {
                         if constexpr (kLean) flush_L();
@@ -249,7 +261,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             FRT_DIAG_TICK(4);
             pending = false;
             if constexpr (kLean)
-                P.key = rng_key(W.seed, (uint32_t)I.get(kIsPix), (uint32_t)(I.get(kIsCur) - 1) + W.s_off);
+            {
+                int px, py;
+                P.key = rng_key(W.seed, (uint32_t)item_pix(px, py), (uint32_t)(I.get(kIsCur) - 1) + W.s_off);
+            }
             const bool done = shade_kind<KIND, MATS>(P, S, T.h, W.max_depth, ne, ns);
             if (done || kLean) flush_L();   // fp32 chunk sums in either precision
             active = !done;
@@ -260,7 +275,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         const unsigned long long diag_t2 = FRT_DIAG_CLOCK();
         FRT_DIAG_CYC(17, diag_t2 - diag_t1);
         // ---- retire a finished item: its chunk sum goes to its own slot ----
-        if (!active && have_item && I.get(kIsCur) >= I.get(kIsEnd)) {
+        if (!active && have_item && I.get(kIsCur) >= item_end()) {
             float *dst = W.partial + 3ull * ((size_t)(uint32_t)I.get(kIsChunk) * W.n_slots + (uint32_t)I.get(kIsSlot));
             dst[0] = i2f(I.get(kIsAcc + 0)); dst[1] = i2f(I.get(kIsAcc + 1)); dst[2] = i2f(I.get(kIsAcc + 2));
             have_item = false;
@@ -309,22 +324,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
                         have_item = true;
                         const int s_cur = (int)chunk * W.spi;
                         I.set(kIsCur, s_cur);
-                        I.set(kIsEnd, min(W.spp, s_cur + W.spi));
                         I.set(kIsSlot, (int)(t_ord * (uint32_t)T2 + s));
                         I.set(kIsChunk, (int)chunk);
-                        I.set(kIsPix, py * W.nx + px);
-                        I.set(kIsPx, px);
-                        I.set(kIsPy, py);
+                        I.set(kIsPxy, px | (py << 16));   // nx, ny < 2^15 (params_ok)
                         I.set(kIsAcc + 0, 0); I.set(kIsAcc + 1, 0); I.set(kIsAcc + 2, 0);
                     }
                 }
             }
         }
         // ---- next camera sample of the item ----
-        const bool start = !active && have_item && I.get(kIsCur) < I.get(kIsEnd);
+        const bool start = !active && have_item && I.get(kIsCur) < item_end();
         if (start) {
             const int s_cur = I.get(kIsCur);
-            path_begin(P, S, I.get(kIsPx), I.get(kIsPy), W.nx, W.ny, W.seed, (uint32_t)I.get(kIsPix),
+            int px, py;
+            const int pix = item_pix(px, py);
+            path_begin(P, S, px, py, W.nx, W.ny, W.seed, (uint32_t)pix,
                        (uint32_t)s_cur + W.s_off);
             I.set(kIsCur, s_cur + 1);
             active = true;
@@ -619,10 +633,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
     Trav<float> T;
     bool tracing = false, pending = false, beyond = false;
     int ovf[kOverflow<WORLD>];
+    // diagnostic build (FRT_DIAG, tools/diag_phases.py --integrator pssmlt): lane
+    // counts of the traversal (pairs 1, 2, 7 in bvh2_step), step loop (3),
+    // shading (4), accept / reject (5), outer loop (6); cycles of the step loop
+    // (16), shading (17), accept / reject + splats (19), row materialisation
+    // (20), queue + next proposal (18)
+    unsigned long long diag_t0 = FRT_DIAG_CLOCK();
     for (;;) {
+        FRT_DIAG_TICK(6);
         // ---- traversal steps until at most trav_min lanes still traverse ----
         for (;;) {
             bool ext = false;
+            if (tracing) FRT_DIAG_TICK(3);
             if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, M.P.ro, M.P.rd, M.P.shadow, stk, ovf,
                                                                  LDS_SCENE ? 0 : W.min_desc)) {   // LDS plans: compiled out
                 if (M.P.shadow) {               // finish the shadow ray here (mlt_shade's shadow branch)
@@ -647,7 +669,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
             if (__popcll(__ballot(tracing)) <= W.trav_min) break;
         }
         bool next_ray = false, done = false;
+        const unsigned long long diag_t1 = FRT_DIAG_CLOCK();
+        FRT_DIAG_CYC(16, diag_t1 - diag_t0);
         if (pending) {
+            FRT_DIAG_TICK(4);
             pending = false;
             if (beyond) {                               // pssmlt.cpp:151, :276
                 M.P.L = M.P.L + M.P.beta * S.env;
@@ -661,9 +686,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
             }
         }
         // accept / reject (per lane); the accepted proposal's row is written below
+        const unsigned long long diag_t2 = FRT_DIAG_CLOCK();
+        FRT_DIAG_CYC(17, diag_t2 - diag_t1);
         bool mat = false, mat_fresh = false, setup_next = false;
         RngKey mat_key = key;
         if (done) {
+            FRT_DIAG_TICK(5);
             const f3 L = M.P.L;
             const float sc = fmaxf(fmaxf(L.x, L.y), L.z);
             float cx = i2f(C.get(kCsX)), cy = i2f(C.get(kCsY)), csc = i2f(C.get(kCsSc)), cw = i2f(C.get(kCsW));
@@ -714,6 +742,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
         // lanes fill lanes n..63, so it is a permutation).  Coalesced along each
         // row; only the last trip has idle lanes (one chain at a time left 28 of
         // 64 lanes idle on every second trip).  The whole wave is active here. ----
+        const unsigned long long diag_t3 = FRT_DIAG_CLOCK();
+        FRT_DIAG_CYC(19, diag_t3 - diag_t2);
         if (const uint64_t mm = __ballot(mat)) {
             const uint32_t n = (uint32_t)__popcll(mm);
             const int dst = 4 * (int)(mat ? lane_rank(mm) : n + lane_rank(~mm));   // byte address of the target lane
@@ -734,6 +764,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
                 }
             }
         }
+        const unsigned long long diag_t4 = FRT_DIAG_CLOCK();
+        FRT_DIAG_CYC(20, diag_t4 - diag_t3);
         if (setup_next) {                               // next proposal reads the new state
             key = rng_key(W.seed ^ kMltChainSalt, (uint32_t)C.get(kCsC), (uint32_t)C.get(kCsT) + 1u);
             large = rng_u(key, 0) < kMltLargeStep;      // large_step vs mutate (pssmlt.cpp:187-196)
@@ -780,6 +812,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
                 pending = !tracing;
             }
         }
+        diag_t0 = FRT_DIAG_CLOCK();
+        FRT_DIAG_CYC(18, diag_t0 - diag_t4);
         if (__ballot(have || !exhausted) == 0) break;
     }
     unsigned long long cnt[4] = {n_cam, n_ext, n_sh, n_smp};
@@ -868,7 +902,8 @@ static Launcher make_launcher(size_t scene_bytes)
     L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES, MATS, KIND, R>);
     L.f64 = kIsF64<R>;
     L.lds = (WORLD != FRT_WORLD_LIST ? (size_t)STACK * kBlock * sizeof(int) : 0) +
-            (size_t)kItemWords * kBlock * sizeof(int) + (LDS ? scene_bytes : 0);
+            (size_t)kItemWords * kBlock * sizeof(int) + (LDS ? scene_bytes : 0) +
+            (WORLD == kWorldBvh4 ? (size_t)STACK * kBlock : 0);   // the 4-wide stack's entry distances
     L.stack = STACK;
     L.waves = WAVES > 1 ? WAVES : 0;
     L.lds_scene = LDS;
@@ -898,9 +933,11 @@ static Launcher bvh_launcher(int waves, size_t sb)
     return make_launcher<STACK, WORLD, LDS, 1, MATS>(sb);
 }
 #ifndef FRT_EXP_BVH4_LSTACK
-#define FRT_EXP_BVH4_LSTACK 16
+#define FRT_EXP_BVH4_LSTACK 15
 #endif
-constexpr int kBvh4LdsStack = FRT_EXP_BVH4_LSTACK;   // 16 KiB of LDS per block; deeper entries go to scratch
+// LDS entries of the 4-wide stack; deeper entries go to scratch.  15 (was 16 until round 5): 15 KiB of
+// stack + 3.75 KiB of entry distances + 7 KiB of item state per block keep 6 blocks a CU in 160 KiB
+constexpr int kBvh4LdsStack = FRT_EXP_BVH4_LSTACK;
 // MATS: the material set the kernel is compiled for (kMats* mask, frt_path.hpp)
 template <int MATS>
 static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
@@ -1929,7 +1966,8 @@ constexpr int kRetiredFlags = 32 | 64 | 128;   // frt.h: the round-4 plans measu
 static bool params_ok(const frt_render_params *p)
 {
     const int T = eff_tile(p);
-    if (!(p && p->nx > 0 && p->ny > 0 && p->spp > 0 && (T % 8) == 0 && T <= 256 && p->shard_count >= 1 &&
+    // nx, ny < 2^15: the work item packs px | py << 16 (ItemState kIsPxy)
+    if (!(p && p->nx > 0 && p->ny > 0 && p->nx < 32768 && p->ny < 32768 && p->spp > 0 && (T % 8) == 0 && T <= 256 && p->shard_count >= 1 &&
           p->shard_index >= 0 && p->shard_index < p->shard_count && p->max_depth >= -1 && p->max_depth < 100000))
         return false;
     if (p->sample_offset < 0 || (int64_t)p->sample_offset + p->spp > (int64_t)0xffffffffLL) return false;
@@ -2110,6 +2148,40 @@ static void mlt_kernels(bool mats, const void **boot, const void **chains)
     else mlt_kernels_t<STACK, WORLD, LDS, false>(boot, chains);
 }
 
+#if defined(FRT_DIAG)
+// diagnostic builds only: the per-phase counters of the last path or PSS-MLT
+// render, one kDiagSlots row per wave on the device, summed over waves here
+static unsigned long long g_diag_sum[kDiagSlots];
+static unsigned long long *g_diag_buf = nullptr;
+static size_t g_diag_n = 0;
+static int diag_begin(frt_ctx *c, size_t n_waves, hipStream_t st)
+{
+    if (g_diag_n < n_waves * kDiagSlots) {
+        if (g_diag_buf) HIPCHK(c, hipFree(g_diag_buf));
+        g_diag_n = n_waves * kDiagSlots;
+        HIPCHK(c, hipMalloc(&g_diag_buf, g_diag_n * sizeof(unsigned long long)));
+    }
+    HIPCHK(c, hipMemsetAsync(g_diag_buf, 0, g_diag_n * sizeof(unsigned long long), st));
+    HIPCHK(c, hipMemcpyToSymbolAsync(HIP_SYMBOL(frt::frt_diag), &g_diag_buf, sizeof(g_diag_buf), 0,
+                                     hipMemcpyHostToDevice, st));
+    return FRT_OK;
+}
+static int diag_end(frt_ctx *c, size_t n_waves)
+{
+    std::vector<unsigned long long> dv(n_waves * kDiagSlots);
+    HIPCHK(c, hipMemcpy(dv.data(), g_diag_buf, dv.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    for (int k = 0; k < kDiagSlots; ++k) g_diag_sum[k] = 0;
+    for (size_t w = 0; w < n_waves; ++w)
+        for (int k = 0; k < kDiagSlots; ++k) g_diag_sum[k] += dv[w * kDiagSlots + k];
+    return FRT_OK;
+}
+extern "C" int frt_diag_read(unsigned long long *out)
+{
+    for (int k = 0; k < kDiagSlots; ++k) out[k] = g_diag_sum[k];
+    return kDiagSlots;
+}
+#endif
+
 static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, hipStream_t st, frt_stats *stats)
 {
     const auto t_start = std::chrono::steady_clock::now();
@@ -2195,6 +2267,9 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
     W.min_desc = min_desc(lds_scene);
     HIPCHK(c, hipMemsetAsync(c->splat, 0, n_film * sizeof(unsigned long long), st));
     HIPCHK(c, hipMemsetAsync(c->counter, 0, 64, st));
+#if defined(FRT_DIAG)
+    if (const int drc = diag_begin(c, n_waves, st)) return drc;
+#endif
     HIPCHK(c, hipEventRecord(c->ev0, st));
     if (n_local > 0 && steps > 0) {
         DevScene Sarg = c->S;
@@ -2210,6 +2285,9 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
     HIPCHK(c, hipStreamSynchronize(st));
     float ms = 0.0f;
     HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+#if defined(FRT_DIAG)
+    if (const int drc = diag_end(c, n_waves)) return drc;
+#endif
     if (stats) {
         memset(stats, 0, sizeof(*stats));
         for (size_t w = 0; w < n_waves; ++w) {
@@ -2251,15 +2329,6 @@ extern "C" int frt_mlt_chain_state(frt_ctx *c, uint64_t first, uint64_t n, float
     return FRT_OK;
 }
 
-#if defined(FRT_DIAG)
-static unsigned long long g_diag_sum[kDiagSlots];
-// diagnostic builds only: the per-phase counters of the last path render, summed over waves
-extern "C" int frt_diag_read(unsigned long long *out)
-{
-    for (int k = 0; k < kDiagSlots; ++k) out[k] = g_diag_sum[k];
-    return kDiagSlots;
-}
-#endif
 
 // Work granule of a path / AO / normals render: the frame's samples cut into
 // n_chunks chunks of spi samples (the last one shorter), k = n_chunks chosen
@@ -2379,16 +2448,7 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
 
     HIPCHK(c, hipMemsetAsync(c->counter, 0, 64, st));
 #if defined(FRT_DIAG)
-    static unsigned long long *diag_buf = nullptr;
-    static size_t diag_n = 0;
-    if (diag_n < n_waves * kDiagSlots) {
-        if (diag_buf) HIPCHK(c, hipFree(diag_buf));
-        diag_n = n_waves * kDiagSlots;
-        HIPCHK(c, hipMalloc(&diag_buf, diag_n * sizeof(unsigned long long)));
-    }
-    HIPCHK(c, hipMemsetAsync(diag_buf, 0, diag_n * sizeof(unsigned long long), st));
-    HIPCHK(c, hipMemcpyToSymbolAsync(HIP_SYMBOL(frt::frt_diag), &diag_buf, sizeof(diag_buf), 0,
-                                     hipMemcpyHostToDevice, st));
+    if (const int drc = diag_begin(c, n_waves, st)) return drc;
 #endif
     HIPCHK(c, hipEventRecord(c->ev0, st));
     DevScene Sarg = c->S;
@@ -2407,13 +2467,7 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
     float ms = 0.0f;
     HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
 #if defined(FRT_DIAG)
-    {
-        std::vector<unsigned long long> dv(n_waves * kDiagSlots);
-        HIPCHK(c, hipMemcpy(dv.data(), diag_buf, dv.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-        for (int k = 0; k < kDiagSlots; ++k) g_diag_sum[k] = 0;
-        for (size_t w = 0; w < n_waves; ++w)
-            for (int k = 0; k < kDiagSlots; ++k) g_diag_sum[k] += dv[w * kDiagSlots + k];
-    }
+    if (const int drc = diag_end(c, n_waves)) return drc;
 #endif
     if (stats) {
         memset(stats, 0, sizeof(*stats));

@@ -36,6 +36,7 @@ b)  # the default line, the launcher's gloo rehearsal (two ranks, one GPU, no
     b default 500 \
      && b gloo2 400 --gpus 2 --backend gloo --steps 2 --north-star off \
      && FRT_LIB_PATH=$E/libfrt_diag.so timeout -k 10 200 python tools/diag_phases.py --scene cornell --spp 32 > $O/diag_cornell.json 2> $O/diag.log \
+     && FRT_LIB_PATH=$E/libfrt_diag.so timeout -k 10 200 python tools/diag_phases.py --scene cornell --integrator pssmlt --spp 64 > $O/diag_mlt.json 2>> $O/diag.log \
      && ab c "" $C && ab c libfrt_base.so $C && ab c "" $C && ab c libfrt_base.so $C \
      && ab mlt "" $P && ab mlt libfrt_base.so $P && ab mlt "" $P && ab mlt libfrt_base.so $P ;;
 *) echo "unknown stage $S"; exit 2 ;;
