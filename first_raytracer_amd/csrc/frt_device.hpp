@@ -410,15 +410,18 @@ FRT_HD double fpow01(double x, double y) { return pow(x, y); }
 // <= 64 * 2^-22 * ln 2 ~ 1.1e-5 at y = 64, 1.7e-7 at y = 1 (without
 // the bound, Ns 1000-1024 reached ~1e-4).  No underflow before double's, so
 // pdf == 0, which ends a path (path.cpp:84-86), comes out exactly where the
-// double pow gives 0.  Larger exponents, x = 0 and y = 0 take OCML's double
-// pow, as the host replay and the reference do.  The directions
+// double pow gives 0.  y = 0 gives 1 and x = 0 gives 0 (std::pow's values);
+// larger exponents take OCML's double pow, as the host replay and the
+// reference do.  The directions
 // (cosine_power_generate) keep the double pow: they decide what the next ray
 // hits.
 FRT_HD float fpow01_w(float x, float y) { return fpow01(x, y); }
 FRT_HD double fpow01_w(double x, double y)
 {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(FRT_EXP_IEEE_MATH)
-    if (!(x > 0.0) || !(y > 0.0) || y > 64.0) return pow(x, y);
+    if (y == 0.0) return 1.0;                                 // pow(x, 0) = 1 for every x (veach's plates: Ns 0)
+    if (!(x > 0.0)) return x == 0.0 ? 0.0 : pow(x, y);
+    if (y > 64.0) return pow(x, y);
     int k;
     const double m = frexp(x, &k);                            // x = m 2^k, m in [0.5, 1)
     const float mf = (float)m;

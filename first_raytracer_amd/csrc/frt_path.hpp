@@ -49,6 +49,8 @@ FRT_HD int wave_count(bool x)
 // lane occupancy.  FRT_DIAG_TICK(k) adds, for the executing wave, one trip and
 // the number of active lanes to counter pair k of the wave's slot in
 // frt_diag (read back by frt_diag_read); FRT_DIAG_CYC(k, c) adds cycles.
+// Kernels launched without a buffer (frt_diag null: ray queries) count nothing;
+// a launch's grid must fit the buffer the host sized for it (diag_begin).
 // Compiled out of every product build.
 #if defined(FRT_DIAG)
 constexpr int kDiagSlots = 24;
@@ -62,7 +64,7 @@ __device__ __forceinline__ unsigned long long *diag_slot()
 #define FRT_DIAG_TICK(k)                                                                \
     do {                                                                                \
         const uint64_t m_ = __ballot(1);                                                \
-        if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)m_) - 1) {           \
+        if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)m_) - 1 && frt_diag) { \
             unsigned long long *d_ = diag_slot();                                       \
             d_[2 * (k)] += 1;                                                           \
             d_[2 * (k) + 1] += __popcll(m_);                                            \
@@ -71,7 +73,7 @@ __device__ __forceinline__ unsigned long long *diag_slot()
 #define FRT_DIAG_CYC(k, c)                                                              \
     do {                                                                                \
         const uint64_t m_ = __ballot(1);                                                \
-        if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)m_) - 1) diag_slot()[k] += (c); \
+        if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)m_) - 1 && frt_diag) diag_slot()[k] += (c); \
     } while (0)
 #define FRT_DIAG_CLOCK() ((unsigned long long)clock64())
 #else
@@ -87,6 +89,10 @@ constexpr int kSentinel = 0x7fffffff;   // "stack empty"; never a node index
 // sphere index < 1024, count <= 8); kOctSent = empty stack.  The host keeps the
 // plan to scenes whose refs fit (oct_refs_fit).
 constexpr int kOctLeaf = 0x4000, kOctSent = 0x8000;
+#ifndef FRT_EXP_POP_CULL
+#define FRT_EXP_POP_CULL 1       // experiment builds: 0 = pops without the entry-distance test (A/B)
+#endif
+constexpr bool kPopCull = FRT_EXP_POP_CULL != 0;
 constexpr int kWorldBvh4 = 2;           // internal world kind: 4-wide quantized BVH
 constexpr int kWorldBvh2Oct = 4;        // internal world kind: binary nodes from LDS, one copy per ray octant
 constexpr int kBvh4Overflow = 40;       // private stack entries after the LDS ones
@@ -340,7 +346,7 @@ FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyh
         if constexpr (OCT) {
             while (sp > 0) {
                 const int e = stk[--sp * STRIDE];
-                if (!(u2f((uint32_t)e & 0xffff0000u) > tb)) return e & 0xffff;
+                if (!kPopCull || !(u2f((uint32_t)e & 0xffff0000u) > tb)) return e & 0xffff;
                 FRT_DIAG_TICK(7);                       // culled (diagnostic build: lanes that skip an entry)
             }
             return kOctSent;

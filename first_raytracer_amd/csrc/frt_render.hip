@@ -171,7 +171,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     int *stk = lds_mem + threadIdx.x;                                 // one LDS column per lane
     constexpr int kStackInts = WORLD != FRT_WORLD_LIST ? STACK * kBlock : 0;
     constexpr int kItemInts = kItemWords * kBlock;
-    constexpr bool kTQ = WORLD == kWorldBvh4;                         // pop culling on the 4-wide stack
+    constexpr bool kTQ = kPopCull && WORLD == kWorldBvh4;             // pop culling on the 4-wide stack
     uint8_t *tq = reinterpret_cast<uint8_t *>(lds_mem + kStackInts + kItemInts) + threadIdx.x;
     DevScene S = S0;
     if constexpr (LDS_SCENE) scene_to_lds<WORLD>(S, lds_mem + kStackInts + kItemInts);
@@ -903,7 +903,7 @@ static Launcher make_launcher(size_t scene_bytes)
     L.f64 = kIsF64<R>;
     L.lds = (WORLD != FRT_WORLD_LIST ? (size_t)STACK * kBlock * sizeof(int) : 0) +
             (size_t)kItemWords * kBlock * sizeof(int) + (LDS ? scene_bytes : 0) +
-            (WORLD == kWorldBvh4 ? (size_t)STACK * kBlock : 0);   // the 4-wide stack's entry distances
+            (kPopCull && WORLD == kWorldBvh4 ? (size_t)STACK * kBlock : 0);   // the 4-wide stack's entry distances
     L.stack = STACK;
     L.waves = WAVES > 1 ? WAVES : 0;
     L.lds_scene = LDS;
@@ -2223,6 +2223,10 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
         HIPCHK(c, hipMalloc(&c->partial, need));
         c->partial_bytes = need;
     }
+#if defined(FRT_DIAG)
+    // the bootstrap's traversal ticks too: a diagnostic buffer for its grid (zeroed again before the chains)
+    if (const int drc = diag_begin(c, (size_t)(n_init + kBlock - 1) / kBlock * (kBlock / 64), st)) return drc;
+#endif
     {
         int nx = p->nx, ny = p->ny, ni = n_init;
         uint32_t seed = p->seed;

@@ -23,21 +23,31 @@ ab() {  # tag, lib ('' = in-tree), perf_ab args...
 }
 C="--scene cornell --spp 512 --rounds 3 --bvh gsah --variants default"
 P="--scene cornell --spp 512 --rounds 2 --bvh gsah --integrator pssmlt --variants default"
+M="--scene cornell_1m --spp 256 --rounds 2 --bvh gsah --variants default"
 case $S in
 a)  # the GPU suite (C5 chain-shard parity is new) + smoke on the build with
     # octant-plan pop culling and the octant plan for PSS-MLT, then the PSS-MLT line
     pt gpu 1100 tests -m gpu \
      && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
      && b pssmlt 500 --integrator pssmlt ;;
-b)  # the default line, the launcher's gloo rehearsal (two ranks, one GPU, no
-    # torchrun), the diagnostic build's phase counters, and same-call A/B of the
-    # pop culling (Cornell) and the octant plan for PSS-MLT against the r05 base
-    # build (build/exp/libfrt_base.so: before both)
+b)  # (ran with the diag build's PSS-MLT bootstrap ticking into an unset
+    # buffer: GPU fault in diag_mlt, fixed in the next build; the default and
+    # gloo2 lines above it completed)
     b default 500 \
      && b gloo2 400 --gpus 2 --backend gloo --steps 2 --north-star off \
      && FRT_LIB_PATH=$E/libfrt_diag.so timeout -k 10 200 python tools/diag_phases.py --scene cornell --spp 32 > $O/diag_cornell.json 2> $O/diag.log \
+     && FRT_LIB_PATH=$E/libfrt_diag.so timeout -k 10 200 python tools/diag_phases.py --scene cornell --integrator pssmlt --spp 64 > $O/diag_mlt.json 2>> $O/diag.log ;;
+c)  # same-call A/B: in-tree (octant + 4-wide pop culling, 7-word items, 15-entry
+    # 4-wide LDS stack, PSS-MLT on the octant plan) / nocull (the same without
+    # the entry-distance tests) / cull2 (octant culling + PSS-MLT octant plan,
+    # 10-word items) / base (round-5 start); then the diagnostic build (path and
+    # PSS-MLT) and the parity tests of the in-tree build
+    for k in 1 2; do ab c "" $C && ab c libfrt_nocull.so $C && ab c libfrt_cull2.so $C && ab c libfrt_base.so $C || exit 1; done \
+     && for k in 1 2; do ab m "" $M && ab m libfrt_nocull.so $M && ab m libfrt_base.so $M || exit 1; done \
+     && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_base.so $P || exit 1; done \
+     && FRT_LIB_PATH=$E/libfrt_diag.so timeout -k 10 200 python tools/diag_phases.py --scene cornell --spp 32 > $O/diag_cornell.json 2> $O/diag.log \
      && FRT_LIB_PATH=$E/libfrt_diag.so timeout -k 10 200 python tools/diag_phases.py --scene cornell --integrator pssmlt --spp 64 > $O/diag_mlt.json 2>> $O/diag.log \
-     && ab c "" $C && ab c libfrt_base.so $C && ab c "" $C && ab c libfrt_base.so $C \
-     && ab mlt "" $P && ab mlt libfrt_base.so $P && ab mlt "" $P && ab mlt libfrt_base.so $P ;;
+     && FRT_LIB_PATH=$E/libfrt_diag.so timeout -k 10 200 python tools/diag_phases.py --scene cornell_1m --spp 32 > $O/diag_1m.json 2>> $O/diag.log \
+     && pt parity 600 tests/test_gpu_parity.py tests/test_gpu_c4.py tests/test_gpu_trace.py tests/test_gpu_pssmlt.py -m gpu ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
