@@ -24,7 +24,6 @@ FRT_HD float i2f(int i) { return __builtin_bit_cast(float, i); }
 // colour, texture kind), m4 = (u_scale, v_scale, -, -)
 constexpr int kMatStride = 5;
 FRT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
-FRT_HD uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
 // true if the predicate holds on any active lane of the wave (the host self-test is one lane)
 FRT_HD bool wave_any(bool x)
 {
@@ -83,16 +82,6 @@ __device__ __forceinline__ unsigned long long *diag_slot()
 #endif
 
 constexpr int kSentinel = 0x7fffffff;   // "stack empty"; never a node index
-// Octant plan (kWorldBvh2Oct): 16-bit child refs, so that a stack entry also
-// holds the child's entry distance (bvh2_step).  Interior node j < kOctLeaf is
-// j; a leaf is kOctLeaf | sphere << 13 | (count - 1) << 10 | first (first and
-// sphere index < 1024, count <= 8); kOctSent = empty stack.  The host keeps the
-// plan to scenes whose refs fit (oct_refs_fit).
-constexpr int kOctLeaf = 0x4000, kOctSent = 0x8000;
-#ifndef FRT_EXP_POP_CULL
-#define FRT_EXP_POP_CULL 1       // experiment builds: 0 = pops without the entry-distance test (A/B)
-#endif
-constexpr bool kPopCull = FRT_EXP_POP_CULL != 0;
 constexpr int kWorldBvh4 = 2;           // internal world kind: 4-wide quantized BVH
 constexpr int kWorldBvh2Oct = 4;        // internal world kind: binary nodes from LDS, one copy per ray octant
 constexpr int kBvh4Overflow = 40;       // private stack entries after the LDS ones
@@ -154,17 +143,6 @@ template <typename R> struct Hit {
 // (count - 1 in bits 27..29 below the sphere flag: up to 8 triangles, 2^27 triangles per scene)
 constexpr int kLeafCountShift = 27, kLeafIndexMask = (1 << kLeafCountShift) - 1, kLeafIndexLimit = 1 << kLeafCountShift;
 constexpr int kLeafMax = 8, kLeafDefault = 4, kLeafSmallScene = 2;
-// octant plan refs (kOctLeaf above): a child ref as its 16-bit code, and a
-// leaf code back to leaf_hit's x
-FRT_HD int oct_code(int ref)
-{
-    if (ref >= 0) return ref;
-    const int x = ~ref;
-    return kOctLeaf | ((x >> 17) & 0x2000) | (((x >> kLeafCountShift) & 7) << 10) | (x & 0x3ff);
-}
-FRT_HD int oct_leaf(int code) { return ((code & 0x2000) << 17) | (((code >> 10) & 7) << kLeafCountShift) | (code & 0x3ff); }
-// true when the ref survives the 16-bit code (host check before the octant plan is offered)
-FRT_HD bool oct_ref_fits(int ref) { return ref >= 0 ? ref < kOctLeaf : oct_leaf(oct_code(ref)) == ~ref; }
 constexpr int kTravMinLds = 12, kTravMinHbm = 32;           // PSS-MLT, AO, normals: see trav_min()
 constexpr int kTravMinLdsPath = 20, kTravMinHbmPath = 40;   // path::Li
 constexpr int kMinDescLds = 0, kMinDescHbm = 12;    // leaf postponing: see min_desc()
@@ -328,32 +306,10 @@ template <typename R> FRT_HD bool trav_begin(Trav<R> &T, const DevScene &S, int 
 // descending while other lanes of its wave have none yet, Aila & Laine 2009 --
 // was measured on both plans and removed: +1 % on cornell_1m in round 1,
 // -0.4 % on Cornell and -14 % on cornell_1m at 512 spp in round 3, DESIGN.md.)
-//
-// OCT stacks hold 16-bit refs (oct_code) with the entry distance of the pushed
-// child in the upper half (its fp32 bits truncated to 16, so rounded toward 0:
-// never above the true entry).  A pop skips entries whose entry distance is
-// already beyond the closest hit (pop culling): such a node cannot hold a hit
-// with t <= t_best (padded boxes), so hits are unchanged, but
-// without the distance every such pop cost a node visit or a leaf test.
 template <int STRIDE, bool OCT = false, typename R>
 FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyhit, int *stk, int min_desc = 0)
 {
     int node = T.node, sp = T.sp;
-    // interior node?  (OCT codes: interior < kOctLeaf <= leaf < kOctSent)
-    auto interior = [](int n) { return OCT ? n < kOctLeaf : (unsigned)n < (unsigned)kSentinel; };
-    // OCT pop with culling against t_best (tb); the other plans pop bare refs
-    auto pop = [&](R tb) -> int {
-        if constexpr (OCT) {
-            while (sp > 0) {
-                const int e = stk[--sp * STRIDE];
-                if (!kPopCull || !(u2f((uint32_t)e & 0xffff0000u) > tb)) return e & 0xffff;
-                FRT_DIAG_TICK(7);                       // culled (diagnostic build: lanes that skip an entry)
-            }
-            return kOctSent;
-        } else {
-            return (sp > 0) ? stk[--sp * STRIDE] : kSentinel;
-        }
-    };
     DevScene Sn = S;
     if constexpr (OCT) {   // the ray's copy: n_nodes 48-B box records (scene_to_lds)
         const int oct = (T.sr.invd.x < R(0) ? 1 : 0) | (T.sr.invd.y < R(0) ? 2 : 0) | (T.sr.invd.z < R(0) ? 4 : 0);
@@ -364,7 +320,7 @@ FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyh
     // (OCT: t_best held finite -- a ray query may pass t_max = +inf -- so that
     // slab_nf's tn <= tf is the hit test)
     const R tmin = T.tmin, tbest = OCT ? vmin(T.h.t, Cst<R>::tmax) : T.h.t;
-    while (interior(node)) {
+    while ((unsigned)node < (unsigned)kSentinel) {   // interior node
         FRT_DIAG_TICK(2);
         R t0, t1;
         int c0, c1;
@@ -392,8 +348,7 @@ FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyh
         }
         if (h0 && h1) {
             const bool first0 = t0 <= t1;
-            if constexpr (OCT) stk[sp * STRIDE] = (int)((f2u(float(first0 ? t1 : t0)) & 0xffff0000u) | (uint32_t)(first0 ? c1 : c0));
-            else stk[sp * STRIDE] = first0 ? c1 : c0;
+            stk[sp * STRIDE] = first0 ? c1 : c0;
             ++sp;
             node = first0 ? c0 : c1;
         } else if (h0) {
@@ -401,20 +356,19 @@ FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyh
         } else if (h1) {
             node = c1;
         } else {
-            node = pop(tbest);
+            node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel;
         }
-        if (min_desc > 0 && wave_count(interior(node)) < min_desc) break;
+        if (min_desc > 0 && wave_count((unsigned)node < (unsigned)kSentinel) < min_desc) break;
     }
-    if (interior(node)) {                                // postponed: still descending
+    if ((unsigned)node < (unsigned)kSentinel) {          // postponed: still descending
         T.node = node;
         T.sp = sp;
         return false;
     }
-    const int sent = OCT ? kOctSent : kSentinel;
-    bool done = node == sent || leaf_hit(S, OCT ? oct_leaf(node) : ~node, o, d, T.tmin, anyhit, T.h);
+    bool done = node == kSentinel || leaf_hit(S, ~node, o, d, T.tmin, anyhit, T.h);
     if (!done) {
-        node = pop(OCT ? vmin(T.h.t, Cst<R>::tmax) : T.h.t);
-        done = node == sent;
+        node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel;
+        done = node == kSentinel;
     }
     T.node = node;
     T.sp = sp;
@@ -430,58 +384,28 @@ FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyh
 // so culling stays conservative and the hit equals the binary traversal's
 // bit for bit (the (t, DFS rank) minimum does not depend on visit order).
 // fp32 only: the fp64 kernels traverse the binary tree.
-// Entry distances of the 4-wide stack (TQ, the path kernels): one byte per LDS
-// entry in a column beside the stack (tq[k * STRIDE]), the distance's fp32 bits
-// >> 20 (exponent and 3 mantissa bits) over [2^-16, 2^16): q = 0 stands for
-// "no bound" (0), so dq(q) never exceeds the true entry distance.  Entries in
-// the private overflow carry none.
-FRT_HD uint32_t tq8(float t) { return (uint32_t)min(max((int)(f2u(t) >> 20) - (111 << 3), 0), 255); }
-FRT_HD float tq8_lo(uint32_t q) { return q == 0u ? 0.0f : u2f((q + (111u << 3)) << 20); }
-
-template <int STRIDE, int LSTACK, bool TQ = false>
-FRT_HD bool bvh4_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int *ovf, int min_desc = 0,
-                      uint8_t *tq = nullptr)
+template <int STRIDE, int LSTACK>
+FRT_HD bool bvh4_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit, int *stk, int *ovf, int min_desc = 0)
 {
     int node = T.node, sp = T.sp;
     // Entries below LSTACK live in the lane's LDS column, deeper ones in `ovf`
     // (scratch).  A wave-uniform test keeps the common case on plain LDS
     // accesses: a per-lane select between the two would make the compiler
     // branch per push and pop through a generic (flat) pointer.
-    auto push = [&](int v, float t) {
+    auto push = [&](int v) {
         if (!wave_any(sp >= LSTACK)) {
             stk[sp * STRIDE] = v;
-            if constexpr (TQ) tq[sp * STRIDE] = (uint8_t)tq8(t);
         } else {
-            if (sp < LSTACK) {
-                stk[sp * STRIDE] = v;
-                if constexpr (TQ) tq[sp * STRIDE] = (uint8_t)tq8(t);
-            } else {
-                ovf[sp - LSTACK] = v;
-            }
+            if (sp < LSTACK) stk[sp * STRIDE] = v;
+            else ovf[sp - LSTACK] = v;
         }
         ++sp;
     };
-    // TQ: entries whose entry distance lies beyond t_best (tb) are skipped (pop
-    // culling, as bvh2_step's octant plan): a node or leaf entered beyond the
-    // closest hit cannot hold a hit with t <= t_best (boxes are padded outward)
-    auto pop = [&](float tb) -> int {
-        while (sp > 0) {
-            --sp;
-            int v;
-            uint32_t q = 0;
-            if (!wave_any(sp >= LSTACK)) {
-                v = stk[sp * STRIDE];
-                if constexpr (TQ) q = tq[sp * STRIDE];
-            } else if (sp < LSTACK) {
-                v = stk[sp * STRIDE];
-                if constexpr (TQ) q = tq[sp * STRIDE];
-            } else {
-                v = ovf[sp - LSTACK];
-            }
-            if (!TQ || !(tq8_lo(q) > tb)) return v;
-            FRT_DIAG_TICK(7);
-        }
-        return kSentinel;
+    auto pop = [&]() -> int {
+        if (sp == 0) return kSentinel;
+        --sp;
+        if (!wave_any(sp >= LSTACK)) return stk[sp * STRIDE];
+        return sp < LSTACK ? stk[sp * STRIDE] : ovf[sp - LSTACK];
     };
     while ((unsigned)node < (unsigned)kSentinel) {
         FRT_DIAG_TICK(0);
@@ -524,18 +448,15 @@ FRT_HD bool bvh4_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit
         cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
         // hit children are sorted first; the far ones go on the stack, farthest first
         if (!wave_any(sp > LSTACK - 3)) {               // wave-uniform: every push stays in LDS
-#pragma unroll
-            for (int i = 3; i >= 1; --i)
-                if (t[i] != __builtin_inff()) {
-                    if constexpr (TQ) tq[sp * STRIDE] = (uint8_t)tq8(t[i]);
-                    stk[sp++ * STRIDE] = c[i];
-                }
+            if (t[3] != __builtin_inff()) stk[sp++ * STRIDE] = c[3];
+            if (t[2] != __builtin_inff()) stk[sp++ * STRIDE] = c[2];
+            if (t[1] != __builtin_inff()) stk[sp++ * STRIDE] = c[1];
         } else {
-            if (t[3] != __builtin_inff()) push(c[3], t[3]);
-            if (t[2] != __builtin_inff()) push(c[2], t[2]);
-            if (t[1] != __builtin_inff()) push(c[1], t[1]);
+            if (t[3] != __builtin_inff()) push(c[3]);
+            if (t[2] != __builtin_inff()) push(c[2]);
+            if (t[1] != __builtin_inff()) push(c[1]);
         }
-        node = (t[0] != __builtin_inff()) ? c[0] : pop(T.h.t);
+        node = (t[0] != __builtin_inff()) ? c[0] : pop();
         if (min_desc > 0 && wave_count((unsigned)node < (unsigned)kSentinel) < min_desc) break;
     }
     if ((unsigned)node < (unsigned)kSentinel) {          // postponed (min_desc): still descending
@@ -545,7 +466,7 @@ FRT_HD bool bvh4_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit
     }
     bool done = node == kSentinel || leaf_hit<true>(S, ~node, o, d, T.tmin, anyhit, T.h);
     if (!done) {
-        node = pop(T.h.t);
+        node = pop();
         done = node == kSentinel;
     }
     T.node = node;
@@ -610,10 +531,9 @@ FRT_HD bool trav_begin_world(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, R 
         return trav_begin(T, S, WORLD == kWorldBvh4 ? S.root4 : S.root, o, d, tmax);
     }
 }
-// TQ: the 4-wide stack keeps entry distances in `tq` (bvh4_step; the path kernels)
-template <int WORLD, int STRIDE, int STACK, bool TQ = false, typename R>
+template <int WORLD, int STRIDE, int STACK, typename R>
 FRT_HD bool trav_step_world(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyhit, int *stk, int *ovf,
-                            int min_desc = 0, uint8_t *tq = nullptr)
+                            int min_desc = 0)
 {
     // 4-wide (HBM-resident scenes): the slab ray and t_min again from (o, d)
     // (the values trav_begin set), so that they are not live across the
@@ -628,7 +548,7 @@ FRT_HD bool trav_step_world(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, boo
         T.h = trace_list(S, o, d, T.h.t, anyhit);
         return true;
     } else if constexpr (WORLD == kWorldBvh4) {
-        return bvh4_step<STRIDE, STACK, TQ>(T, S, o, d, anyhit, stk, ovf, min_desc, tq);
+        return bvh4_step<STRIDE, STACK>(T, S, o, d, anyhit, stk, ovf, min_desc);
     } else {
         return bvh2_step<STRIDE, WORLD == kWorldBvh2Oct>(T, S, o, d, anyhit, stk, min_desc);
     }

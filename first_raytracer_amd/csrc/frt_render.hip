@@ -117,10 +117,9 @@ __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
             const int e = i >> 2, k = i & 3;
             const float4 v = S0.nodes_oct[i];
             if (k < 3) l4[3 * e + k] = v;
-            else if (e < S0.n_nodes) refs[e] = make_int2(oct_code(f2i(v.x)), oct_code(f2i(v.y)));
+            else if (e < S0.n_nodes) refs[e] = make_int2(f2i(v.x), f2i(v.y));
         }
         S.node_refs = refs;
-        S.root = oct_code(S0.root);   // 16-bit refs (bvh2_step's OCT stack)
     } else {
         for (int i = threadIdx.x; i < nn; i += kBlock) l4[(i & 3) * S0.n_nodes + (i >> 2)] = S0.nodes[i];
     }
@@ -147,11 +146,8 @@ __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
 // spilled to scratch -- across every traversal and shading phase (spilled
 // VGPRs at the register cap: cornell_1m 51 -> 24, Cornell 31 -> 6; same-call
 // A/B +4.5 % / +1 %).
-// Round 5: 7 words (was 10): the item's end follows from its chunk, and the
-// pixel is one packed word (px | py << 16; the linear index py * nx + px is
-// one mad), which leaves LDS for the stack entries' distances (bvh4_step).
-constexpr int kItemWords = 7;
-enum { kIsCur, kIsSlot, kIsChunk, kIsPxy, kIsAcc };   // kIsAcc..+2: r, g, b
+constexpr int kItemWords = 10;
+enum { kIsCur, kIsEnd, kIsSlot, kIsChunk, kIsPix, kIsPx, kIsPy, kIsAcc };   // kIsAcc..+2: r, g, b
 struct ItemState {
     int *b;      // the lane's column
     __device__ int get(int k) const { return b[k * kBlock]; }
@@ -166,13 +162,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     const DevScene S0, const DevWork W)
 {
     // [STACK][kBlock] stack, [kItemWords][kBlock] item state, then the scene
-    // (LDS plans) or the 4-wide stack's entry distances ([STACK][kBlock] bytes)
     extern __shared__ __attribute__((aligned(16))) int lds_mem[];
     int *stk = lds_mem + threadIdx.x;                                 // one LDS column per lane
     constexpr int kStackInts = WORLD != FRT_WORLD_LIST ? STACK * kBlock : 0;
     constexpr int kItemInts = kItemWords * kBlock;
-    constexpr bool kTQ = kPopCull && WORLD == kWorldBvh4;             // pop culling on the 4-wide stack
-    uint8_t *tq = reinterpret_cast<uint8_t *>(lds_mem + kStackInts + kItemInts) + threadIdx.x;
     DevScene S = S0;
     if constexpr (LDS_SCENE) scene_to_lds<WORLD>(S, lds_mem + kStackInts + kItemInts);
     else scene_strides_hbm(S);
@@ -184,12 +177,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
     // the wave's own item range [q_cur, q_end) from its last queue atomic (wave-uniform)
     uint32_t q_cur = 0, q_end = 0;
     const ItemState I{lds_mem + kStackInts + (int)threadIdx.x};
-    auto item_end = [&]() { return min(W.spp, (I.get(kIsChunk) + 1) * W.spi); };
-    auto item_pix = [&](int &px, int &py) {
-        const int xy = I.get(kIsPxy);
-        px = xy & 0xffff; py = xy >> 16;
-        return py * W.nx + px;
-    };
     PathState<R> P;
     // ray in flight: tracing = traversal steps remain; pending = finished, not yet shaded
     Trav<R> T;
@@ -231,9 +218,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             bool shadow_done = false;
             if (tracing) FRT_DIAG_TICK(3);
             // (LDS-resident binary plans: no leaf postponing, compiled out)
-            if (tracing && trav_step_world<WORLD, kBlock, STACK, kTQ>(T, S, P.ro, P.rd, P.shadow, stk, ovf,
+            if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, P.ro, P.rd, P.shadow, stk, ovf,
                                                                        LDS_SCENE && (WORLD == FRT_WORLD_BVH || WORLD == kWorldBvh2Oct)
-                                                                           ? 0 : W.min_desc, tq)) {
+                                                                           ? 0 : W.min_desc)) {
                 if (KIND == FRT_INTEGRATOR_PATH && P.shadow) {   // finish the shadow ray here, keep traversing
                     if (path_after_shadow<MATS>(P, T.h.prim < 0)) {
                         if constexpr (kLean) flush_L();
@@ -261,10 +248,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             FRT_DIAG_TICK(4);
             pending = false;
             if constexpr (kLean)
-            {
-                int px, py;
-                P.key = rng_key(W.seed, (uint32_t)item_pix(px, py), (uint32_t)(I.get(kIsCur) - 1) + W.s_off);
-            }
+                P.key = rng_key(W.seed, (uint32_t)I.get(kIsPix), (uint32_t)(I.get(kIsCur) - 1) + W.s_off);
             const bool done = shade_kind<KIND, MATS>(P, S, T.h, W.max_depth, ne, ns);
             if (done || kLean) flush_L();   // fp32 chunk sums in either precision
             active = !done;
@@ -275,7 +259,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         const unsigned long long diag_t2 = FRT_DIAG_CLOCK();
         FRT_DIAG_CYC(17, diag_t2 - diag_t1);
         // ---- retire a finished item: its chunk sum goes to its own slot ----
-        if (!active && have_item && I.get(kIsCur) >= item_end()) {
+        if (!active && have_item && I.get(kIsCur) >= I.get(kIsEnd)) {
             float *dst = W.partial + 3ull * ((size_t)(uint32_t)I.get(kIsChunk) * W.n_slots + (uint32_t)I.get(kIsSlot));
             dst[0] = i2f(I.get(kIsAcc + 0)); dst[1] = i2f(I.get(kIsAcc + 1)); dst[2] = i2f(I.get(kIsAcc + 2));
             have_item = false;
@@ -324,21 +308,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
                         have_item = true;
                         const int s_cur = (int)chunk * W.spi;
                         I.set(kIsCur, s_cur);
+                        I.set(kIsEnd, min(W.spp, s_cur + W.spi));
                         I.set(kIsSlot, (int)(t_ord * (uint32_t)T2 + s));
                         I.set(kIsChunk, (int)chunk);
-                        I.set(kIsPxy, px | (py << 16));   // nx, ny < 2^15 (params_ok)
+                        I.set(kIsPix, py * W.nx + px);
+                        I.set(kIsPx, px);
+                        I.set(kIsPy, py);
                         I.set(kIsAcc + 0, 0); I.set(kIsAcc + 1, 0); I.set(kIsAcc + 2, 0);
                     }
                 }
             }
         }
         // ---- next camera sample of the item ----
-        const bool start = !active && have_item && I.get(kIsCur) < item_end();
+        const bool start = !active && have_item && I.get(kIsCur) < I.get(kIsEnd);
         if (start) {
             const int s_cur = I.get(kIsCur);
-            int px, py;
-            const int pix = item_pix(px, py);
-            path_begin(P, S, px, py, W.nx, W.ny, W.seed, (uint32_t)pix,
+            path_begin(P, S, I.get(kIsPx), I.get(kIsPy), W.nx, W.ny, W.seed, (uint32_t)I.get(kIsPix),
                        (uint32_t)s_cur + W.s_off);
             I.set(kIsCur, s_cur + 1);
             active = true;
@@ -902,8 +887,7 @@ static Launcher make_launcher(size_t scene_bytes)
     L.fn = reinterpret_cast<const void *>(&path_megakernel<STACK, WORLD, LDS, WAVES, MATS, KIND, R>);
     L.f64 = kIsF64<R>;
     L.lds = (WORLD != FRT_WORLD_LIST ? (size_t)STACK * kBlock * sizeof(int) : 0) +
-            (size_t)kItemWords * kBlock * sizeof(int) + (LDS ? scene_bytes : 0) +
-            (kPopCull && WORLD == kWorldBvh4 ? (size_t)STACK * kBlock : 0);   // the 4-wide stack's entry distances
+            (size_t)kItemWords * kBlock * sizeof(int) + (LDS ? scene_bytes : 0);
     L.stack = STACK;
     L.waves = WAVES > 1 ? WAVES : 0;
     L.lds_scene = LDS;
@@ -933,11 +917,9 @@ static Launcher bvh_launcher(int waves, size_t sb)
     return make_launcher<STACK, WORLD, LDS, 1, MATS>(sb);
 }
 #ifndef FRT_EXP_BVH4_LSTACK
-#define FRT_EXP_BVH4_LSTACK 15
+#define FRT_EXP_BVH4_LSTACK 16
 #endif
-// LDS entries of the 4-wide stack; deeper entries go to scratch.  15 (was 16 until round 5): 15 KiB of
-// stack + 3.75 KiB of entry distances + 7 KiB of item state per block keep 6 blocks a CU in 160 KiB
-constexpr int kBvh4LdsStack = FRT_EXP_BVH4_LSTACK;
+constexpr int kBvh4LdsStack = FRT_EXP_BVH4_LSTACK;   // 16 KiB of LDS per block; deeper entries go to scratch
 // MATS: the material set the kernel is compiled for (kMats* mask, frt_path.hpp)
 template <int MATS>
 static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
@@ -1715,11 +1697,8 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     // (pick_launcher_t): larger scenes get none (8x the node array otherwise).
     const size_t oct_bytes = sizeof(float4) * (oct_lds_node_slots((int)(F.nodes.size() / 4)) + F.tris.size() +
                                                F.tshade.size() + F.mats.size());
-    bool oct_fit = sv->world_kind == FRT_WORLD_BVH && F.depth < kLdsMaxDepth && oct_bytes <= kLdsOctBytes &&
-                   (sv->root >= 0 || oct_ref_fits(~dev_ref(~sv->root)));
-    for (size_t i = 0; oct_fit && i < F.nodes.size() / 4; ++i)   // refs as 16-bit codes (oct_code)
-        oct_fit = oct_ref_fits(f2i(F.nodes[4 * i + 3].x)) && oct_ref_fits(f2i(F.nodes[4 * i + 3].y));
-    if (oct_fit) F.nodes_oct.resize(8 * F.nodes.size());
+    if (sv->world_kind == FRT_WORLD_BVH && F.depth < kLdsMaxDepth && oct_bytes <= kLdsOctBytes)
+        F.nodes_oct.resize(8 * F.nodes.size());
     for (int o = 0; o < 8 && !F.nodes_oct.empty(); ++o)
         for (size_t i = 0; i < F.nodes.size() / 4; ++i) {
             const float4 *n = &F.nodes[4 * i];
@@ -1966,8 +1945,7 @@ constexpr int kRetiredFlags = 32 | 64 | 128;   // frt.h: the round-4 plans measu
 static bool params_ok(const frt_render_params *p)
 {
     const int T = eff_tile(p);
-    // nx, ny < 2^15: the work item packs px | py << 16 (ItemState kIsPxy)
-    if (!(p && p->nx > 0 && p->ny > 0 && p->nx < 32768 && p->ny < 32768 && p->spp > 0 && (T % 8) == 0 && T <= 256 && p->shard_count >= 1 &&
+    if (!(p && p->nx > 0 && p->ny > 0 && p->spp > 0 && (T % 8) == 0 && T <= 256 && p->shard_count >= 1 &&
           p->shard_index >= 0 && p->shard_index < p->shard_count && p->max_depth >= -1 && p->max_depth < 100000))
         return false;
     if (p->sample_offset < 0 || (int64_t)p->sample_offset + p->spp > (int64_t)0xffffffffLL) return false;

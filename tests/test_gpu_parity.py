@@ -235,17 +235,17 @@ def test_launch_plan(ctx, cornell_obj, mirror_obj, sphere_obj, tmp_path):
     assert (st.scene_in_lds, st.waves_cap) == (1, 4)
     ctx.upload(frt.HostScene("cornell_box_obj", sphere_obj, 1.0))            # 2,188 triangles: HBM, 4-wide
     _, st = ctx.render(frt.RenderParams.make(16, 16, 1))
-    assert (st.scene_in_lds, st.waves_cap, st.stack_entries) == (0, 5, 15)
+    assert (st.scene_in_lds, st.waves_cap, st.stack_entries) == (0, 5, 16)
     ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, 1.0))
     _, st = ctx.render(frt.RenderParams.make(16, 16, 1, flags=frt.FRT_FLAG_NO_LDS_SCENE))
-    assert (st.scene_in_lds, st.waves_cap, st.stack_entries) == (0, 6, 15)
+    assert (st.scene_in_lds, st.waves_cap, st.stack_entries) == (0, 6, 16)
     _, st = ctx.render(frt.RenderParams.make(16, 16, 1, flags=frt.FRT_FLAG_NO_LDS_SCENE | frt.FRT_FLAG_BVH2))
     assert (st.scene_in_lds, st.waves_cap, st.stack_entries) == (0, 6, 8)
     dst = str(tmp_path / "tess.obj")
     frt.write_tessellated_obj(cornell_obj, 60, dst)            # ~40k triangles: no longer fits LDS
     ctx.upload(frt.HostScene("cornell_box_obj", dst, 1.0))
     _, st = ctx.render(frt.RenderParams.make(16, 16, 1))
-    assert (st.scene_in_lds, st.waves_cap, st.stack_entries) == (0, 6, 15)
+    assert (st.scene_in_lds, st.waves_cap, st.stack_entries) == (0, 6, 16)
     assert st.scene_bytes > 16 * 1024
 
 
