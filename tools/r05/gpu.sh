@@ -49,5 +49,27 @@ c)  # same-call A/B: in-tree (octant + 4-wide pop culling, 7-word items, 15-entr
      && FRT_LIB_PATH=$E/libfrt_diag.so timeout -k 10 200 python tools/diag_phases.py --scene cornell --integrator pssmlt --spp 64 > $O/diag_mlt.json 2>> $O/diag.log \
      && FRT_LIB_PATH=$E/libfrt_diag.so timeout -k 10 200 python tools/diag_phases.py --scene cornell_1m --spp 32 > $O/diag_1m.json 2>> $O/diag.log \
      && pt parity 600 tests/test_gpu_parity.py tests/test_gpu_c4.py tests/test_gpu_trace.py tests/test_gpu_pssmlt.py -m gpu ;;
+d)  # same-call A/B of the node-or-leaf ("if-if") loop on the octant plan
+    # (ifif20 / ifif8: the wave leaves at 20 / 8 working lanes) against the
+    # in-tree descend-then-test step, on Cornell and PSS-MLT; PSS-MLT trav_min
+    for k in 1 2; do ab c "" $C && ab c libfrt_ifif20.so $C && ab c libfrt_ifif8.so $C || exit 1; done \
+     && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_ifif20.so $P && ab mlt libfrt_ifif8.so $P || exit 1; done \
+     && ab mltt "" --scene cornell --spp 512 --rounds 2 --bvh gsah --integrator pssmlt \
+          --variants default,default/trav6,default/trav20,default/trav28,default ;;
+e)  # the build after the round's A/Bs (pop culling, 7-word items, if-if
+    # removed; PSS-MLT on the octant plan): GPU suite + smoke, the PSS-MLT
+    # line under rocprofv3 kernel-trace + stats, its three PMC passes
+    SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY"
+    pmc() {  # name, counters, bench args...
+      local n=$1 c=$2; shift 2
+      timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $O/$n -o run -- \
+          python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --north-star off "$@" > $O/$n.json 2> $O/$n.log
+    }
+    pt gpu 900 tests -m gpu \
+     && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
+     && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_pssmlt -o run -- \
+          python3 bench.py --integrator pssmlt --steps 3 --warmup 1 > $O/bench_pssmlt.json 2> $O/bench_pssmlt.log \
+     && pmc sq_pssmlt "$SQ" --integrator pssmlt && pmc fetch_pssmlt FETCH_SIZE --integrator pssmlt \
+     && pmc write_pssmlt WRITE_SIZE --integrator pssmlt ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
