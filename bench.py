@@ -414,6 +414,11 @@ def roofline(integrator, key, world, res, V, T, shared_device=False):
         issue = pmc.get("valu_issue_per_ray", pmc.get("valu_insts_per_ray"))
         if pmc.get("l2_hit_rate") is not None:
             out["l2_hit_rate"] = round(pmc["l2_hit_rate"], 4)
+        if pmc.get("write_bytes_per_ray") is not None and integrator != "pssmlt":
+            # WRITE_SIZE per launch (scratch spills included) against the launch's algorithmic
+            # output: one 12-B (chunk, slot) partial sum per work item
+            out["written_bytes_per_launch"] = int(rays * pmc["write_bytes_per_ray"])
+            out["output_bytes_per_launch"] = int(res.get("work_items", 0)) * 12
         if valu_bound and issue is not None:
             ach = rays * issue / launch_s / 1e9
             out.update({"bound": "valu", "achieved": round(ach, 1), "peak": VALU_PEAK_GINST, "unit": "Ginst/s",
@@ -581,7 +586,7 @@ class Runner:
             "integ": integ, "env": env, "bvh": bvh, "gpu_build_ms": gpu_build_ms,
             "setup_s": t2 - t0, "build_s": t1 - t0, "upload_s": t2 - t1,
             "avg_kernel_ms": float(np.mean(kernel_ms)), "rays_per_launch": last.rays,
-            "samples_per_launch": last.samples, "scene_in_lds": last.scene_in_lds,
+            "samples_per_launch": last.samples, "work_items": int(last.work_items), "scene_in_lds": last.scene_in_lds,
             "scene_bytes": last.scene_bytes,
             "launch": {"waves_cap": int(last.waves_cap), "stack": int(last.stack_entries),
                        "bvh_depth": int(last.bvh_depth)},
