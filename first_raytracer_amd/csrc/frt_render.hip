@@ -96,7 +96,7 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t m)
 __device__ __forceinline__ void scene_strides_hbm(DevScene &S)
 {
     S.node_es = 4; S.node_ps = 1;
-    S.node4_es = 4; S.node4_ps = 1;
+    S.node4_es = kNode4Parts; S.node4_ps = 1;
     S.tri_es = 3; S.tri_ps = 1;
     S.sh_es = 2; S.sh_ps = 1;
 }
@@ -1354,9 +1354,9 @@ static bool build_bvh4(FlatScene &F, int root_ref)
     while (!st.empty()) {
         const Item it = st.back();
         st.pop_back();
-        const int me = (int)(F.nodes4.size() / 4);
+        const int me = (int)(F.nodes4.size() / kNode4Parts);
         if (it.parent >= 0) {
-            uint4 &r = F.nodes4[4 * it.parent + 1];
+            uint4 &r = F.nodes4[(size_t)kNode4Parts * it.parent + 1];
             (it.slot == 0 ? r.x : it.slot == 1 ? r.y : it.slot == 2 ? r.z : r.w) = (uint32_t)me;
         }
         F.depth4 = std::max(F.depth4, it.lvl);
@@ -1413,13 +1413,23 @@ static bool build_bvh4(FlatScene &F, int root_ref)
         }
         uint32_t refs[4];
         for (int s = 0; s < 4; ++s) refs[s] = s < n ? (uint32_t)ch[s].ref : empty_ref;
-        F.nodes4.resize((size_t)(me + 1) * 4);
-        uint4 *out = F.nodes4.data() + (size_t)me * 4;
+        F.nodes4.resize((size_t)(me + 1) * kNode4Parts);
+        uint4 *out = F.nodes4.data() + (size_t)me * kNode4Parts;
         out[0] = make_uint4((uint32_t)f2i(org[0]), (uint32_t)f2i(org[1]), (uint32_t)f2i(org[2]),
                             (uint32_t)(ex[0] + 127) | ((uint32_t)(ex[1] + 127) << 8) | ((uint32_t)(ex[2] + 127) << 16));
         out[1] = make_uint4(refs[0], refs[1], refs[2], refs[3]);
+#if FRT_F16_PLANES
+        // per axis: lo planes of children (0, 1), (2, 3), then hi planes, as exact fp16 pairs
+        auto h2 = [](uint32_t q, int s0) {
+            auto h = [](uint32_t v) { return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(float)v); };
+            return h((q >> (8 * s0)) & 0xffu) | (h((q >> (8 * s0 + 8)) & 0xffu) << 16);
+        };
+        for (int a = 0; a < 3; ++a)
+            out[2 + a] = make_uint4(h2(qlo[a], 0), h2(qlo[a], 2), h2(qhi[a], 0), h2(qhi[a], 2));
+#else
         out[2] = make_uint4(qlo[0], qhi[0], qlo[1], qhi[1]);
         out[3] = make_uint4(qlo[2], qhi[2], 0u, 0u);
+#endif
         for (int s = n - 1; s >= 0; --s)               // pre-order: the first slot next
             if (ch[s].ref >= 0) st.push_back({ch[s].ref, me, s, it.lvl + 1});
     }
@@ -1727,9 +1737,9 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
     S.n_nodes = (int)(F.nodes.size() / 4);
     S.n_tris = nt;
     S.n_mats = nm;
-    S.n_nodes4 = (int)(F.nodes4.size() / 4);
+    S.n_nodes4 = (int)(F.nodes4.size() / kNode4Parts);
     S.node_es = 4; S.node_ps = 1;
-    S.node4_es = 4; S.node4_ps = 1;
+    S.node4_es = kNode4Parts; S.node4_ps = 1;
     S.tri_es = 3; S.tri_ps = 1;
     S.sh_es = 2; S.sh_ps = 1;
     S.world_kind = sv->world_kind;

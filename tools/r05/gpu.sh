@@ -71,13 +71,14 @@ e)  # the build after the round's A/Bs (pop culling, 7-word items, if-if
           python3 bench.py --integrator pssmlt --steps 3 --warmup 1 > $O/bench_pssmlt.json 2> $O/bench_pssmlt.log \
      && pmc sq_pssmlt "$SQ" --integrator pssmlt && pmc fetch_pssmlt FETCH_SIZE --integrator pssmlt \
      && pmc write_pssmlt WRITE_SIZE --integrator pssmlt ;;
-f)  # same-call A/B: the compiler's SLP vectorizer off (-fno-slp-vectorize, build/exp/libfrt_noslp.so)
+f)  # same-call A/B: the compiler's SLP vectorizer off (-fno-slp-vectorize, build/exp/libfrt_noslp.so),
+    # and on cornell_1m the BVH4Q planes as fp16 for v_fma_mix_f32 (libfrt_f16.so, FRT_F16_PLANES=1),
     # against the in-tree build (libfrt_cur.so, identical to it): the vectorizer packs float pairs
     # into v_pk_* with register moves around them (115 v_pk / 233 v_mov in the cornell_1m kernel;
     # without: 0 / 168, 20 -> 5 scratch instructions, Cornell 12 -> 0)
     V="--scene veach --spp 256 --rounds 2 --variants default"
     for k in 1 2; do ab c libfrt_cur.so $C && ab c libfrt_noslp.so $C || exit 1; done \
-     && for k in 1 2; do ab m libfrt_cur.so $M && ab m libfrt_noslp.so $M || exit 1; done \
+     && for k in 1 2; do ab m libfrt_cur.so $M && ab m libfrt_noslp.so $M && ab m libfrt_f16.so $M && ab m libfrt_f16noslp.so $M || exit 1; done \
      && for k in 1 2; do ab mlt libfrt_cur.so $P && ab mlt libfrt_noslp.so $P || exit 1; done \
      && for k in 1 2; do ab v libfrt_cur.so $V && ab v libfrt_noslp.so $V || exit 1; done ;;
 *) echo "unknown stage $S"; exit 2 ;;
