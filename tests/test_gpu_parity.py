@@ -222,6 +222,16 @@ def test_lambertian_caps_agree(ctx, cornell_obj, tmp_path):
         assert np.array_equal(f, films[0])
 
 
+@pytest.mark.parametrize("flag", [32, 64, 128])
+def test_retired_flags_rejected(ctx, cornell_obj, flag):
+    """The round-4 A/B plans' flag bits (frt.h: 4-wide nodes from LDS, lockstep
+    brute force, speculative traversal) fail loudly instead of being ignored."""
+    ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, 1.0))
+    with pytest.raises(frt.FrtError):
+        ctx.render(frt.RenderParams.make(16, 16, 1, flags=flag))
+    ctx.render(frt.RenderParams.make(16, 16, 1))        # the context stays usable
+
+
 def test_launch_plan(ctx, cornell_obj, mirror_obj, sphere_obj, tmp_path):
     """The launcher picks the planned kernel: small scenes from LDS with the
     binary BVH at 5 waves/SIMD, HBM-resident scenes on the 4-wide BVH at 6;
