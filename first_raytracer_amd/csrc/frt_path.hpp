@@ -435,9 +435,11 @@ FRT_HD bool bvh4_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit
         const uint4 w0 = node4_part(S, node, 0), w1 = node4_part(S, node, 1);
         const uint4 w2 = node4_part(S, node, 2), w3 = node4_part(S, node, 3);
         const SlabRay<float> &sr = T.sr;
-        const float ax = u2f((w0.w & 0xffu) << 23) * sr.invd.x, bx = fmaf(u2f(w0.x), sr.invd.x, sr.oinv.x);
-        const float ay = u2f(((w0.w >> 8) & 0xffu) << 23) * sr.invd.y, by = fmaf(u2f(w0.y), sr.invd.y, sr.oinv.y);
-        const float az = u2f(((w0.w >> 16) & 0xffu) << 23) * sr.invd.z, bz = fmaf(u2f(w0.z), sr.invd.z, sr.oinv.z);
+        // plane scale 2^e / d per axis: e is a signed byte (v_bfe_i32 + v_ldexp_f32; the same value as
+        // the float 2^e times 1/d, which is exact in the normal range build_bvh4 keeps)
+        const float ax = ldexpf(sr.invd.x, (int)(int8_t)(w0.w & 0xffu)), bx = fmaf(u2f(w0.x), sr.invd.x, sr.oinv.x);
+        const float ay = ldexpf(sr.invd.y, (int)(int8_t)((w0.w >> 8) & 0xffu)), by = fmaf(u2f(w0.y), sr.invd.y, sr.oinv.y);
+        const float az = ldexpf(sr.invd.z, (int)(int8_t)((w0.w >> 16) & 0xffu)), bz = fmaf(u2f(w0.z), sr.invd.z, sr.oinv.z);
         // near / far plane words per axis by the ray's direction sign: a
         // negative 1/d turns the hi plane into the entry plane.  Per child this
         // replaces the per-axis min / max of the two plane distances (the same

@@ -1416,7 +1416,7 @@ static bool build_bvh4(FlatScene &F, int root_ref)
         F.nodes4.resize((size_t)(me + 1) * kNode4Parts);
         uint4 *out = F.nodes4.data() + (size_t)me * kNode4Parts;
         out[0] = make_uint4((uint32_t)f2i(org[0]), (uint32_t)f2i(org[1]), (uint32_t)f2i(org[2]),
-                            (uint32_t)(ex[0] + 127) | ((uint32_t)(ex[1] + 127) << 8) | ((uint32_t)(ex[2] + 127) << 16));
+                            ((uint32_t)ex[0] & 0xffu) | (((uint32_t)ex[1] & 0xffu) << 8) | (((uint32_t)ex[2] & 0xffu) << 16));
         out[1] = make_uint4(refs[0], refs[1], refs[2], refs[3]);
 #if FRT_F16_PLANES
         // per axis: lo planes of children (0, 1), (2, 3), then hi planes, as exact fp16 pairs
