@@ -149,26 +149,11 @@ constexpr int kMinDescLds = 0, kMinDescHbm = 12;    // leaf postponing: see min_
 
 FRT_HD float4 node_part(const DevScene &S, int i, int k) { return S.nodes[i * S.node_es + k * S.node_ps]; }
 FRT_HD uint4 node4_part(const DevScene &S, int i, int k) { return S.nodes4[i * S.node4_es + k * S.node4_ps]; }
-// BVH4Q child planes: bytes (4 x uint4 per node), or the same integers 0..255 as
-// fp16 (FRT_F16_PLANES: 5 x uint4, 80 B), which v_fma_mix_f32 takes directly:
-// one instruction per plane instead of a byte convert and an FMA, the same
-// value bit for bit (q is exact in fp16 and the FMA rounds once either way).
-#ifndef FRT_F16_PLANES
-#define FRT_F16_PLANES 0
-#endif
-constexpr int kNode4Parts = FRT_F16_PLANES ? 5 : 4;
-// fmaf(half HI of h2 as f32, a, b)
-template <int HI> FRT_HD float fma_h16(uint32_t h2, float a, float b)
-{
-#if defined(__HIP_DEVICE_COMPILE__)
-    float r;
-    if constexpr (HI) asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h2), "v"(a), "v"(b));
-    else asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h2), "v"(a), "v"(b));
-    return r;
-#else
-    return fmaf((float)__builtin_bit_cast(_Float16, (uint16_t)(HI ? h2 >> 16 : h2 & 0xffffu)), a, b);
-#endif
-}
+// (BVH4Q child planes as exact fp16 for v_fma_mix_f32 -- one instruction per
+// plane instead of a byte convert and an FMA, 80-B nodes -- measured round 5:
+// node loop 166 -> 149 VALU, cornell_1m 386.3 -> 394.7 ms; not kept,
+// profiles/r05/r05f/ab_m.jsonl)
+constexpr int kNode4Parts = 4;
 FRT_HD float4 tri_part(const DevScene &S, int i, int k) { return S.tris[i * S.tri_es + k * S.tri_ps]; }
 FRT_HD float4 shade_part(const DevScene &S, int i, int k) { return S.tshade[i * S.sh_es + k * S.sh_ps]; }
 
@@ -449,26 +434,6 @@ FRT_HD bool bvh4_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit
         const bool sx = sr.invd.x < 0.0f, sy = sr.invd.y < 0.0f, sz = sr.invd.z < 0.0f;
         float t[4];
         int c[4] = {(int)w1.x, (int)w1.y, (int)w1.z, (int)w1.w};
-#if FRT_F16_PLANES
-        // part 2 + a: (lo of children 0-1, lo 2-3, hi 0-1, hi 2-3) as fp16 pairs, axis a
-        const uint4 w4 = node4_part(S, node, 4);
-        const uint32_t xn0 = sx ? w2.z : w2.x, xn1 = sx ? w2.w : w2.y, xf0 = sx ? w2.x : w2.z, xf1 = sx ? w2.y : w2.w;
-        const uint32_t yn0 = sy ? w3.z : w3.x, yn1 = sy ? w3.w : w3.y, yf0 = sy ? w3.x : w3.z, yf1 = sy ? w3.y : w3.w;
-        const uint32_t zn0 = sz ? w4.z : w4.x, zn1 = sz ? w4.w : w4.y, zf0 = sz ? w4.x : w4.z, zf1 = sz ? w4.y : w4.w;
-        auto child = [&](float txn, float txf, float tyn, float tyf, float tzn, float tzf) {
-            const float tn = smax(smax(txn, tyn), smax(tzn, T.tmin));   // v_maximum3 (slab_entry)
-            const float tf = smin(smin(txf, tyf), smin(tzf, T.h.t));
-            return (tf < tn) ? __builtin_inff() : tn;
-        };
-        t[0] = child(fma_h16<0>(xn0, ax, bx), fma_h16<0>(xf0, ax, bx), fma_h16<0>(yn0, ay, by), fma_h16<0>(yf0, ay, by),
-                     fma_h16<0>(zn0, az, bz), fma_h16<0>(zf0, az, bz));
-        t[1] = child(fma_h16<1>(xn0, ax, bx), fma_h16<1>(xf0, ax, bx), fma_h16<1>(yn0, ay, by), fma_h16<1>(yf0, ay, by),
-                     fma_h16<1>(zn0, az, bz), fma_h16<1>(zf0, az, bz));
-        t[2] = child(fma_h16<0>(xn1, ax, bx), fma_h16<0>(xf1, ax, bx), fma_h16<0>(yn1, ay, by), fma_h16<0>(yf1, ay, by),
-                     fma_h16<0>(zn1, az, bz), fma_h16<0>(zf1, az, bz));
-        t[3] = child(fma_h16<1>(xn1, ax, bx), fma_h16<1>(xf1, ax, bx), fma_h16<1>(yn1, ay, by), fma_h16<1>(yf1, ay, by),
-                     fma_h16<1>(zn1, az, bz), fma_h16<1>(zf1, az, bz));
-#else
         const uint32_t xn = sx ? w2.y : w2.x, xf = sx ? w2.x : w2.y;
         const uint32_t yn = sy ? w2.w : w2.z, yf = sy ? w2.z : w2.w;
         const uint32_t zn = sz ? w3.y : w3.x, zf = sz ? w3.x : w3.y;
@@ -482,7 +447,6 @@ FRT_HD bool bvh4_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit
             const float tf = smin(smin(txf, tyf), smin(tzf, T.h.t));
             t[i] = (tf < tn) ? __builtin_inff() : tn;
         }
-#endif
         // nearest first: sorting network on (t, child), as selects (no branches)
         auto cx = [&](int i, int j) {
             const bool sw = t[j] < t[i];

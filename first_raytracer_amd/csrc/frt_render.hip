@@ -1418,18 +1418,8 @@ static bool build_bvh4(FlatScene &F, int root_ref)
         out[0] = make_uint4((uint32_t)f2i(org[0]), (uint32_t)f2i(org[1]), (uint32_t)f2i(org[2]),
                             ((uint32_t)ex[0] & 0xffu) | (((uint32_t)ex[1] & 0xffu) << 8) | (((uint32_t)ex[2] & 0xffu) << 16));
         out[1] = make_uint4(refs[0], refs[1], refs[2], refs[3]);
-#if FRT_F16_PLANES
-        // per axis: lo planes of children (0, 1), (2, 3), then hi planes, as exact fp16 pairs
-        auto h2 = [](uint32_t q, int s0) {
-            auto h = [](uint32_t v) { return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(float)v); };
-            return h((q >> (8 * s0)) & 0xffu) | (h((q >> (8 * s0 + 8)) & 0xffu) << 16);
-        };
-        for (int a = 0; a < 3; ++a)
-            out[2 + a] = make_uint4(h2(qlo[a], 0), h2(qlo[a], 2), h2(qhi[a], 0), h2(qhi[a], 2));
-#else
         out[2] = make_uint4(qlo[0], qhi[0], qlo[1], qhi[1]);
         out[3] = make_uint4(qlo[2], qhi[2], 0u, 0u);
-#endif
         for (int s = n - 1; s >= 0; --s)               // pre-order: the first slot next
             if (ch[s].ref >= 0) st.push_back({ch[s].ref, me, s, it.lvl + 1});
     }

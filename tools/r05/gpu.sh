@@ -78,8 +78,16 @@ f)  # same-call A/B: the compiler's SLP vectorizer off (-fno-slp-vectorize, buil
     # without: 0 / 168, 20 -> 5 scratch instructions, Cornell 12 -> 0)
     V="--scene veach --spp 256 --rounds 2 --variants default"
     for k in 1 2; do ab c libfrt_cur.so $C && ab c libfrt_noslp.so $C || exit 1; done \
-     && for k in 1 2; do ab m libfrt_cur.so $M && ab m libfrt_noslp.so $M && ab m libfrt_f16.so $M && ab m libfrt_f16noslp.so $M || exit 1; done \
+     && for k in 1 2; do ab m libfrt_cur.so $M && ab m "" $M && ab m libfrt_noslp.so $M && ab m libfrt_f16.so $M && ab m libfrt_f16noslp.so $M || exit 1; done \
      && for k in 1 2; do ab mlt libfrt_cur.so $P && ab mlt libfrt_noslp.so $P || exit 1; done \
      && for k in 1 2; do ab v libfrt_cur.so $V && ab v libfrt_noslp.so $V || exit 1; done ;;
+g)  # the build with -fno-slp-vectorize: GPU suite (incl. the register-cap tables, whose kernels the
+    # flag recompiled) + smoke, then tools/gpu_roofline.sh part a: the default bench line under
+    # rocprofv3 kernel-trace + stats and the Cornell / cornell_1m PMC passes
+    pt gpu 900 tests -m gpu \
+     && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
+     && TAG=r05$S PART=a STEPS=5 timeout -k 10 900 bash tools/gpu_roofline.sh > $O/roofline.log 2>&1 ;;
+h)  # tools/gpu_roofline.sh part b: veach and PSS-MLT lines under rocprofv3, their PMC passes
+    TAG=r05$S PART=b timeout -k 10 1000 bash tools/gpu_roofline.sh > $O/roofline.log 2>&1 ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
