@@ -908,6 +908,8 @@ static Launcher bvh_launcher(int waves, size_t sb)
     // test_register_caps_agree checks every cap and plan).  The defaults stay
     // 4 / 5 waves for the specular sets (faster than 6:
     // profiles/r02/r02_ab_sphere_hbm_mats.jsonl).
+    if constexpr (MATS == kMatsNone && WORLD == kWorldBvh4)   // the lambertian 4-wide HBM plan (round 5)
+        if (waves == 7) return make_launcher<STACK, WORLD, LDS, 7, MATS>(sb);
     if (waves == 6) return make_launcher<STACK, WORLD, LDS, FRT_EXP_W6, MATS>(sb);
     if (waves == 5) return make_launcher<STACK, WORLD, LDS, 5, MATS>(sb);
     if constexpr (MATS != kMatsNone) {
@@ -917,9 +919,14 @@ static Launcher bvh_launcher(int waves, size_t sb)
     return make_launcher<STACK, WORLD, LDS, 1, MATS>(sb);
 }
 #ifndef FRT_EXP_BVH4_LSTACK
-#define FRT_EXP_BVH4_LSTACK 16
+#define FRT_EXP_BVH4_LSTACK 12
 #endif
-constexpr int kBvh4LdsStack = FRT_EXP_BVH4_LSTACK;   // 16 KiB of LDS per block; deeper entries go to scratch
+// LDS entries of the 4-wide stack; deeper ones go to scratch.  12 since round 5
+// (was 16): 12 KiB of stack + 10 KiB of item state a block let 7 blocks share a
+// CU's 160 KiB, and the lambertian 4-wide kernel runs 7 waves/SIMD (72 VGPRs,
+// no spills since the SLP vectorizer is off): cornell_1m 360.3 -> 344.3 ms
+// (+4.6 %, same call, profiles/r05/r05i/ab_m.jsonl)
+constexpr int kBvh4LdsStack = FRT_EXP_BVH4_LSTACK;
 // MATS: the material set the kernel is compiled for (kMats* mask, frt_path.hpp)
 template <int MATS>
 static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
@@ -944,6 +951,9 @@ static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
     // 10 % at the bench's 512 spp -- 337 vs 307 ms, same call --, so the cap stays:
     // profiles/r02/r02_ab_cornell_knobs.jsonl, r02_ab_cornell_512spp.jsonl.)
     int waves = (MATS & kMatsSpecAny) ? (lds ? 4 : 5) : MATS == kMatsTex && lds ? 0 : lds ? 5 : 6;
+    // the lambertian 4-wide HBM plan: 7 waves (round 5; the binary HBM fallback keeps 6)
+    const bool wide = !lds && c->has_bvh4 && !(flags & FRT_FLAG_BVH2) && bvh4_stack_fits(c->depth4, kBvh4LdsStack);
+    if (MATS == kMatsNone && wide) waves = 7;
     if constexpr (MATS != kMatsNone) {   // FRT_MATS_WAVES: register cap of the material kernels (tuning knob, not part of the C-ABI)
         const char *e = std::getenv("FRT_MATS_WAVES");
         if (e) waves = std::atoi(e);
@@ -954,7 +964,7 @@ static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
     // (Measured and removed A/B plans, DESIGN.md section 5: lockstep brute force over tiny
     // scenes, 4-wide nodes from LDS, speculative traversal, an 8-wide HBM tree.)
     // HBM-resident scenes: the 4-wide quantized BVH (half the bytes per box test)
-    if (!lds && c->has_bvh4 && !(flags & FRT_FLAG_BVH2) && bvh4_stack_fits(c->depth4, kBvh4LdsStack)) {
+    if (wide) {
         L = bvh_launcher<kBvh4LdsStack, false, kWorldBvh4, MATS>(waves, 0);
         return FRT_OK;
     }

@@ -74,7 +74,7 @@ def test_c4_1080p_pixel_sample(ctx, c1m, ora, tree):
     assert hs.info.n_tris == N_TRIS
     ctx.upload(hs)
     film, st = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=7))
-    assert st.scene_in_lds == 0 and st.stack_entries == 16          # the HBM BVH4Q plan
+    assert st.scene_in_lds == 0 and st.stack_entries == 12          # the HBM BVH4Q plan
     assert st.samples == nx * ny * spp and st.pixels == nx * ny
     pix = np.unique(np.linspace(0, nx * ny - 1, 4096).astype(np.int32))
     ref, cnt = ora[nx / ny].render(nx, ny, spp, seed=7, pixels=pix)

@@ -89,5 +89,16 @@ g)  # the build with -fno-slp-vectorize: GPU suite (incl. the register-cap table
      && TAG=r05$S PART=a STEPS=5 timeout -k 10 900 bash tools/gpu_roofline.sh > $O/roofline.log 2>&1 ;;
 h)  # tools/gpu_roofline.sh part b: veach and PSS-MLT lines under rocprofv3, their PMC passes
     TAG=r05$S PART=b timeout -k 10 1000 bash tools/gpu_roofline.sh > $O/roofline.log 2>&1 ;;
+i)  # same-call A/B on the -fno-slp-vectorize build (libfrt_cur.so = in-tree): the machine
+    # scheduler's max-ilp and max-memory-clause strategies (libfrt_ilp / _memclause), and a 7-wave
+    # HBM plan (libfrt_w7: 12 LDS stack entries, 22 KiB a block, the 6-wave plans capped at 7)
+    for k in 1 2; do ab c libfrt_cur.so $C && ab c libfrt_ilp.so $C && ab c libfrt_memclause.so $C || exit 1; done \
+     && for k in 1 2; do ab m libfrt_cur.so $M && ab m libfrt_ilp.so $M && ab m libfrt_memclause.so $M && ab m libfrt_w7.so $M || exit 1; done \
+     && for k in 1 2; do ab mlt libfrt_cur.so $P && ab mlt libfrt_ilp.so $P && ab mlt libfrt_memclause.so $P || exit 1; done ;;
+j)  # the build with the 7-wave 4-wide HBM plan: GPU suite + smoke, the default line (Cornell +
+    # north star), the PSS-MLT line with its path-exact parity and CPU baseline
+    pt gpu 900 tests -m gpu \
+     && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
+     && b default 500 && b pssmlt 500 --integrator pssmlt ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
