@@ -100,5 +100,24 @@ j)  # the build with the 7-wave 4-wide HBM plan: GPU suite + smoke, the default 
     pt gpu 900 tests -m gpu \
      && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
      && b default 500 && b pssmlt 500 --integrator pssmlt ;;
+k)  # PMC on the final kernels: the 7-wave cornell_1m plan (bench --scene cornell_1m), AO and
+    # normals (their bench lines under rocprofv3 kernel-trace first)
+    SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY"
+    pmc() {  # name, counters, bench args...
+      local n=$1 c=$2; shift 2
+      timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $O/$n -o run -- \
+          python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --north-star off "$@" > $O/$n.json 2> $O/$n.log
+    }
+    tr() {  # name, bench args...
+      local n=$1; shift
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$n -o run -- \
+          python3 bench.py "$@" > $O/trace_$n.json 2> $O/trace_$n.log
+    }
+    pmc sq_1m "$SQ" --scene cornell_1m && pmc fetch_1m FETCH_SIZE --scene cornell_1m \
+     && pmc write_1m WRITE_SIZE --scene cornell_1m && pmc tcc_1m "TCC_HIT TCC_MISS" --scene cornell_1m \
+     && tr ao --integrator ao --steps 5 --warmup 1 && tr normals --integrator normals --steps 5 --warmup 1 \
+     && pmc sq_ao "$SQ" --integrator ao && pmc fetch_ao FETCH_SIZE --integrator ao && pmc write_ao WRITE_SIZE --integrator ao \
+     && pmc sq_normals "$SQ" --integrator normals && pmc fetch_normals FETCH_SIZE --integrator normals \
+     && pmc write_normals WRITE_SIZE --integrator normals ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
