@@ -119,5 +119,13 @@ k)  # PMC on the final kernels: the 7-wave cornell_1m plan (bench --scene cornel
      && pmc sq_ao "$SQ" --integrator ao && pmc fetch_ao FETCH_SIZE --integrator ao && pmc write_ao WRITE_SIZE --integrator ao \
      && pmc sq_normals "$SQ" --integrator normals && pmc fetch_normals FETCH_SIZE --integrator normals \
      && pmc write_normals WRITE_SIZE --integrator normals ;;
+l)  # same-call A/B: 9-word work items (the linear pixel index derived; libfrt_item9) so that a
+    # 6th 26-KiB octant block fits a CU, at the default 5-wave and the 6-wave cap, against the
+    # in-tree build (libfrt_cur); cornell_1m as a check (7 waves either way); the PSS-MLT chain
+    # kernel at a 5-wave cap (libfrt_mlt5; 105 VGPRs uncapped since the SLP vectorizer is off)
+    C6="--scene cornell --spp 512 --rounds 3 --bvh gsah --variants default,waves6"
+    for k in 1 2; do ab c libfrt_cur.so $C6 && ab c libfrt_item9.so $C6 || exit 1; done \
+     && for k in 1 2; do ab m libfrt_cur.so $M && ab m libfrt_item9.so $M || exit 1; done \
+     && for k in 1 2; do ab mlt libfrt_cur.so $P && ab mlt libfrt_mlt5.so $P || exit 1; done ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
