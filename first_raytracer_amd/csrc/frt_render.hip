@@ -146,19 +146,10 @@ __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
 // spilled to scratch -- across every traversal and shading phase (spilled
 // VGPRs at the register cap: cornell_1m 51 -> 24, Cornell 31 -> 6; same-call
 // A/B +4.5 % / +1 %).
-#ifndef FRT_EXP_ITEM9
-#define FRT_EXP_ITEM9 0
-#endif
-#if FRT_EXP_ITEM9
-// experiment: 9 words, the linear pixel index py * nx + px derived where it is used
-constexpr int kItemWords = 9;
-enum { kIsCur, kIsEnd, kIsSlot, kIsChunk, kIsPx, kIsPy, kIsAcc };   // kIsAcc..+2: r, g, b
-#define FRT_ITEM_PIX(I, W) ((I).get(kIsPy) * (W).nx + (I).get(kIsPx))
-#else
+// (9 words -- the pixel index derived -- fit a 6th octant block per CU: 229.4 vs 229.1 ms at a
+// 6-wave cap, 230.5 vs 230.2 at 5, profiles/r05/r05l; not kept)
 constexpr int kItemWords = 10;
 enum { kIsCur, kIsEnd, kIsSlot, kIsChunk, kIsPix, kIsPx, kIsPy, kIsAcc };   // kIsAcc..+2: r, g, b
-#define FRT_ITEM_PIX(I, W) ((I).get(kIsPix))
-#endif
 struct ItemState {
     int *b;      // the lane's column
     __device__ int get(int k) const { return b[k * kBlock]; }
@@ -259,7 +250,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             FRT_DIAG_TICK(4);
             pending = false;
             if constexpr (kLean)
-                P.key = rng_key(W.seed, (uint32_t)FRT_ITEM_PIX(I, W), (uint32_t)(I.get(kIsCur) - 1) + W.s_off);
+                P.key = rng_key(W.seed, (uint32_t)I.get(kIsPix), (uint32_t)(I.get(kIsCur) - 1) + W.s_off);
             const bool done = shade_kind<KIND, MATS>(P, S, T.h, W.max_depth, ne, ns);
             if (done || kLean) flush_L();   // fp32 chunk sums in either precision
             active = !done;
@@ -322,9 +313,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
                         I.set(kIsEnd, min(W.spp, s_cur + W.spi));
                         I.set(kIsSlot, (int)(t_ord * (uint32_t)T2 + s));
                         I.set(kIsChunk, (int)chunk);
-#if !FRT_EXP_ITEM9
                         I.set(kIsPix, py * W.nx + px);
-#endif
                         I.set(kIsPx, px);
                         I.set(kIsPy, py);
                         I.set(kIsAcc + 0, 0); I.set(kIsAcc + 1, 0); I.set(kIsAcc + 2, 0);
@@ -336,7 +325,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         const bool start = !active && have_item && I.get(kIsCur) < I.get(kIsEnd);
         if (start) {
             const int s_cur = I.get(kIsCur);
-            path_begin(P, S, I.get(kIsPx), I.get(kIsPy), W.nx, W.ny, W.seed, (uint32_t)FRT_ITEM_PIX(I, W),
+            path_begin(P, S, I.get(kIsPx), I.get(kIsPy), W.nx, W.ny, W.seed, (uint32_t)I.get(kIsPix),
                        (uint32_t)s_cur + W.s_off);
             I.set(kIsCur, s_cur + 1);
             active = true;
