@@ -127,5 +127,9 @@ l)  # same-call A/B: 9-word work items (the linear pixel index derived; libfrt_i
     for k in 1 2; do ab c libfrt_cur.so $C6 && ab c libfrt_item9.so $C6 || exit 1; done \
      && for k in 1 2; do ab m libfrt_cur.so $M && ab m libfrt_item9.so $M || exit 1; done \
      && for k in 1 2; do ab mlt libfrt_cur.so $P && ab mlt libfrt_mlt5.so $P || exit 1; done ;;
+m)  # the N-way split's load balance on the final kernels (each shard alone on the GPU), Cornell
+    # and cornell_1m at 1080p 512 spp
+    timeout -k 10 500 python -u tools/shard_balance.py --scene cornell --ns 2,4,8 --reps 2 > $O/shard_cornell.json 2> $O/shard.log \
+     && timeout -k 10 600 python -u tools/shard_balance.py --scene cornell_1m --ns 2,4,8 --reps 1 > $O/shard_1m.json 2>> $O/shard.log ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
