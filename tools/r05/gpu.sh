@@ -131,5 +131,11 @@ m)  # the N-way split's load balance on the final kernels (each shard alone on t
     # and cornell_1m at 1080p 512 spp
     timeout -k 10 500 python -u tools/shard_balance.py --scene cornell --ns 2,4,8 --reps 2 > $O/shard_cornell.json 2> $O/shard.log \
      && timeout -k 10 600 python -u tools/shard_balance.py --scene cornell_1m --ns 2,4,8 --reps 1 > $O/shard_1m.json 2>> $O/shard.log ;;
+n)  # final-build check: GPU suite + smoke, the default line, veach line, and the launcher's
+    # two-rank gloo rehearsal (one GPU) with the north-star block
+    pt gpu 900 tests -m gpu \
+     && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
+     && b default 500 && b veach 400 --scene veach --spp 1024 \
+     && b gloo2 600 --gpus 2 --backend gloo --steps 2 ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
