@@ -137,5 +137,8 @@ n)  # final-build check: GPU suite + smoke, the default line, veach line, and th
      && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
      && b default 500 && b veach 400 --scene veach --spp 1024 \
      && b gloo2 600 --gpus 2 --backend gloo --steps 2 ;;
+o)  # same-call A/B on cornell_1m: unconditional pushes above the 4-wide stack top (libfrt_pushu)
+    # against the in-tree build (libfrt_cur)
+    for k in 1 2; do ab m libfrt_cur.so $M && ab m libfrt_pushu.so $M || exit 1; done ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
