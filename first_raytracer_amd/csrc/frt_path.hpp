@@ -458,17 +458,11 @@ FRT_HD bool bvh4_step(Trav<float> &T, const DevScene &S, f3 o, f3 d, bool anyhit
         cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
         // hit children are sorted first; the far ones go on the stack, farthest first
         if (!wave_any(sp > LSTACK - 3)) {               // wave-uniform: every push stays in LDS
-#if defined(FRT_EXP_PUSHU)
-            // experiment: unconditional writes above the stack top, sp advanced by the hits
-            // (sorted: a hit child's far siblings that missed hold +inf and are overwritten)
-            stk[sp * STRIDE] = c[3]; sp += t[3] != __builtin_inff() ? 1 : 0;
-            stk[sp * STRIDE] = c[2]; sp += t[2] != __builtin_inff() ? 1 : 0;
-            stk[sp * STRIDE] = c[1]; sp += t[1] != __builtin_inff() ? 1 : 0;
-#else
+            // (unconditional writes above the top with sp advanced by the hits: cornell_1m
+            // 343.5 -> 347.2 ms, profiles/r05/r05o; not kept)
             if (t[3] != __builtin_inff()) stk[sp++ * STRIDE] = c[3];
             if (t[2] != __builtin_inff()) stk[sp++ * STRIDE] = c[2];
             if (t[1] != __builtin_inff()) stk[sp++ * STRIDE] = c[1];
-#endif
         } else {
             if (t[3] != __builtin_inff()) push(c[3]);
             if (t[2] != __builtin_inff()) push(c[2]);

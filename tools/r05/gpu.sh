@@ -140,5 +140,9 @@ n)  # final-build check: GPU suite + smoke, the default line, veach line, and th
 o)  # same-call A/B on cornell_1m: unconditional pushes above the 4-wide stack top (libfrt_pushu)
     # against the in-tree build (libfrt_cur)
     for k in 1 2; do ab m libfrt_cur.so $M && ab m libfrt_pushu.so $M || exit 1; done ;;
+p)  # rocprofv3 kernel-trace + stats of the default bench command on the final build (the launch
+    # averages the line's roofline divides by)
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_default -o run -- \
+        python3 bench.py > $O/trace_default.json 2> $O/trace_default.log ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
