@@ -144,5 +144,9 @@ p)  # rocprofv3 kernel-trace + stats of the default bench command on the final b
     # averages the line's roofline divides by)
     timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_default -o run -- \
         python3 bench.py > $O/trace_default.json 2> $O/trace_default.log ;;
+q)  # scheduling knobs re-checked on the final build: Cornell trav_min (default 20), cornell_1m
+    # trav_min / min_desc (defaults 40 / 12) at the 7-wave plan
+    ab ct "" --scene cornell --spp 512 --rounds 3 --bvh gsah --variants default,default/trav12,default/trav16,default/trav24,default/trav28,default \
+     && ab mt "" --scene cornell_1m --spp 256 --rounds 2 --bvh gsah --variants default,default/trav32,default/trav48,default/desc8,default/desc16,default ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
