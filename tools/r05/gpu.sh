@@ -148,5 +148,16 @@ q)  # scheduling knobs re-checked on the final build: Cornell trav_min (default 
     # trav_min / min_desc (defaults 40 / 12) at the 7-wave plan
     ab ct "" --scene cornell --spp 512 --rounds 3 --bvh gsah --variants default,default/trav12,default/trav16,default/trav24,default/trav28,default \
      && ab mt "" --scene cornell_1m --spp 256 --rounds 2 --bvh gsah --variants default,default/trav32,default/trav48,default/desc8,default/desc16,default ;;
+r)  # same-call A/B on cornell_1m: an 8-wave 4-wide HBM plan (libfrt_w8: 10 LDS stack entries,
+    # 20 KiB a block, eight to a CU; 64 VGPRs, 25 spilled) against the in-tree 7-wave plan
+    for k in 1 2; do ab m "" $M && ab m libfrt_w8.so $M || exit 1; done ;;
+s)  # same-call A/B on cornell_1m: the area-optimal 4-wide collapse (libfrt_dp, FRT_EXP_BVH4_DP=1:
+    # per binary node the least summed node area over 1..4 slots; host SAH tree 148603 -> 113784
+    # nodes, node area sum -1.5 %) against the in-tree greedy collapse
+    for k in 1 2; do ab m "" $M && ab m libfrt_dp.so $M || exit 1; done ;;
+t)  # the build with the area-optimal 4-wide collapse: GPU suite + smoke, the default line
+    pt gpu 900 tests -m gpu \
+     && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
+     && b default 500 ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
