@@ -159,5 +159,17 @@ t)  # the build with the area-optimal 4-wide collapse: GPU suite + smoke, the de
     pt gpu 900 tests -m gpu \
      && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
      && b default 500 ;;
+u)  # the area-optimal collapse build: cornell_1m PMC passes (bench --scene cornell_1m), then the
+    # default bench command under rocprofv3 kernel-trace + stats
+    SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY"
+    pmc() {  # name, counters, bench args...
+      local n=$1 c=$2; shift 2
+      timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $O/$n -o run -- \
+          python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --north-star off "$@" > $O/$n.json 2> $O/$n.log
+    }
+    pmc sq_1m "$SQ" --scene cornell_1m && pmc fetch_1m FETCH_SIZE --scene cornell_1m \
+     && pmc write_1m WRITE_SIZE --scene cornell_1m && pmc tcc_1m "TCC_HIT TCC_MISS" --scene cornell_1m \
+     && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_default -o run -- \
+          python3 bench.py > $O/trace_default.json 2> $O/trace_default.log ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
