@@ -171,5 +171,11 @@ u)  # the area-optimal collapse build: cornell_1m PMC passes (bench --scene corn
      && pmc write_1m WRITE_SIZE --scene cornell_1m && pmc tcc_1m "TCC_HIT TCC_MISS" --scene cornell_1m \
      && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_default -o run -- \
           python3 bench.py > $O/trace_default.json 2> $O/trace_default.log ;;
+v)  # same-call A/B on cornell_1m: SAH-terminated leaves of up to 8 triangles (libfrt_lsah,
+    # FRT_EXP_LEAF_SAH=1; FRT_LEAF_SAH = 100 x triangle / binary-node cost) against the in-tree
+    # "every subtree of <= 4 triangles" rule.  Host SAH tree: mean leaf 3.45 (in-tree), 6.27 / 4.63 /
+    # 3.18 at 20 / 35 / 50
+    M8="--scene cornell_1m --spp 256 --rounds 2 --bvh gsah --variants default/leaf8"
+    for k in 1 2; do ab m "" $M && for r in 28 35 42 50; do FRT_LEAF_SAH=$r ab m$r libfrt_lsah.so $M8 || exit 1; done || exit 1; done ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
