@@ -177,5 +177,14 @@ v)  # same-call A/B on cornell_1m: SAH-terminated leaves of up to 8 triangles (l
     # 3.18 at 20 / 35 / 50
     M8="--scene cornell_1m --spp 256 --rounds 2 --bvh gsah --variants default/leaf8"
     for k in 1 2; do ab m "" $M && for r in 28 35 42 50; do FRT_LEAF_SAH=$r ab m$r libfrt_lsah.so $M8 || exit 1; done || exit 1; done ;;
+w)  # leaf size on the LDS octant plan (default 2), Cornell and PSS-MLT, same call
+    ab cl "" --scene cornell --spp 512 --rounds 3 --bvh gsah --variants default,default/leaf1,default/leaf3,default/leaf4,default \
+     && ab mltl "" --scene cornell --spp 512 --rounds 2 --bvh gsah --integrator pssmlt --variants default,default/leaf1,default/leaf3,default ;;
+x)  # same-call A/B: the binary traversal's stack top in a register (libfrt_topreg,
+    # FRT_EXP_TOPREG=1: a pop hands the top over at once and refills it from LDS off the critical
+    # path) against the in-tree build, Cornell and PSS-MLT; then the parity tests on that library
+    for k in 1 2; do ab c "" $C && ab c libfrt_topreg.so $C || exit 1; done \
+     && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_topreg.so $P || exit 1; done \
+     && FRT_LIB_PATH=$E/libfrt_topreg.so pt parity 600 tests/test_gpu_parity.py tests/test_gpu_pssmlt.py -m gpu ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
