@@ -82,6 +82,7 @@ __device__ __forceinline__ unsigned long long *diag_slot()
 #endif
 
 constexpr int kSentinel = 0x7fffffff;   // "stack empty"; never a node index
+constexpr int kStepBranch = 0, kStepStore = 1, kStepSelect = 2;   // bvh2_step's node-visit forms
 constexpr int kWorldBvh4 = 2;           // internal world kind: 4-wide quantized BVH
 constexpr int kWorldBvh2Oct = 4;        // internal world kind: binary nodes from LDS, one copy per ray octant
 constexpr int kBvh4Overflow = 40;       // private stack entries after the LDS ones
@@ -302,6 +303,16 @@ template <typename R> FRT_HD bool trav_begin(Trav<R> &T, const DevScene &S, int 
 // lanes keep their node and stack and resume on the next step, while the lanes
 // that reached a leaf test it now.  A wave then no longer runs its node loop
 // for as many trips as its slowest lane needs to reach a leaf.
+// STEP (octant plan): how a node visit updates node / stack.  kStepBranch:
+// push, descend or pop as branches.  kStepStore: the far child is written to
+// the slot above the top on every visit (the stack keeps it only when both
+// children were hit), the pop keeps its branch.  kStepSelect: also the entry
+// below the top is read on every visit, and node / sp come from selects -- no
+// branch in the loop body.  The octant plan's stack has more slots than the
+// tree has levels (d < STACK), so the slot above the top is always inside the
+// lane's column.  Cornell (path): Store +0.4 %, Select -0.9 %; PSS-MLT: Select
+// +1.1 %, Store -0.2 % (same call, two alternations, profiles/r05/r05z; the
+// node loop issued 0.48 SALU per VALU instruction with its branches, r05y).
 // OCT (kWorldBvh2Oct): S.nodes holds the 8 octant copies; the ray's copy
 // stores every child box as (near xyz, far xyz) for its direction signs, so a
 // box costs 6 FMAs and two 3-way max / min instead of also sorting each
@@ -311,7 +322,7 @@ template <typename R> FRT_HD bool trav_begin(Trav<R> &T, const DevScene &S, int 
 // descending while other lanes of its wave have none yet, Aila & Laine 2009 --
 // was measured on both plans and removed: +1 % on cornell_1m in round 1,
 // -0.4 % on Cornell and -14 % on cornell_1m at 512 spp in round 3, DESIGN.md.)
-template <int STRIDE, bool OCT = false, typename R>
+template <int STRIDE, bool OCT = false, int STEP = kStepBranch, typename R>
 FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyhit, int *stk, int min_desc = 0)
 {
     int node = T.node, sp = T.sp;
@@ -354,7 +365,22 @@ FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyh
             h0 = t0 != R(__builtin_inff()); h1 = t1 != R(__builtin_inff());
             c0 = f2i(n3.x); c1 = f2i(n3.y);
         }
-        if (h0 && h1) {
+        if constexpr (OCT && STEP == kStepSelect) {   // no branches: store above the top, read below it
+            const bool first0 = h0 && (!h1 || t0 <= t1);
+            const int nr = first0 ? c0 : c1, fr = first0 ? c1 : c0;
+            const int below = stk[(sp > 0 ? sp - 1 : 0) * STRIDE];
+            stk[sp * STRIDE] = fr;                 // the slot above the top: kept only when pushed
+            const bool both = h0 && h1, any = h0 || h1;
+            node = any ? nr : (sp > 0 ? below : kSentinel);
+            sp += both ? 1 : (!any && sp > 0 ? -1 : 0);
+        } else if constexpr (OCT && STEP == kStepStore) {   // the store without a branch, the pop with one
+            const bool first0 = h0 && (!h1 || t0 <= t1);
+            const int nr = first0 ? c0 : c1, fr = first0 ? c1 : c0;
+            stk[sp * STRIDE] = fr;
+            sp += (h0 && h1) ? 1 : 0;
+            if (h0 || h1) node = nr;
+            else node = (sp > 0) ? stk[--sp * STRIDE] : kSentinel;
+        } else if (h0 && h1) {
             const bool first0 = t0 <= t1;
             stk[sp * STRIDE] = first0 ? c1 : c0;
             ++sp;
@@ -543,7 +569,7 @@ FRT_HD bool trav_begin_world(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, R 
         return trav_begin(T, S, WORLD == kWorldBvh4 ? S.root4 : S.root, o, d, tmax);
     }
 }
-template <int WORLD, int STRIDE, int STACK, typename R>
+template <int WORLD, int STRIDE, int STACK, int STEP = kStepBranch, typename R>
 FRT_HD bool trav_step_world(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyhit, int *stk, int *ovf,
                             int min_desc = 0)
 {
@@ -562,7 +588,7 @@ FRT_HD bool trav_step_world(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, boo
     } else if constexpr (WORLD == kWorldBvh4) {
         return bvh4_step<STRIDE, STACK>(T, S, o, d, anyhit, stk, ovf, min_desc);
     } else {
-        return bvh2_step<STRIDE, WORLD == kWorldBvh2Oct>(T, S, o, d, anyhit, stk, min_desc);
+        return bvh2_step<STRIDE, WORLD == kWorldBvh2Oct, STEP>(T, S, o, d, anyhit, stk, min_desc);
     }
 }
 

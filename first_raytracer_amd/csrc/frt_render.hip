@@ -221,7 +221,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             bool shadow_done = false;
             if (tracing) FRT_DIAG_TICK(3);
             // (LDS-resident binary plans: no leaf postponing, compiled out)
-            if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, P.ro, P.rd, P.shadow, stk, ovf,
+            if (tracing && trav_step_world<WORLD, kBlock, STACK, kStepStore>(T, S, P.ro, P.rd, P.shadow, stk, ovf,
                                                                        LDS_SCENE && (WORLD == FRT_WORLD_BVH || WORLD == kWorldBvh2Oct)
                                                                            ? 0 : W.min_desc)) {
                 if (KIND == FRT_INTEGRATOR_PATH && P.shadow) {   // finish the shadow ray here, keep traversing
@@ -445,7 +445,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             }
         }
         if (__ballot(tracing || have_next) == 0) break;
-        if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, o, d, anyhit, stk, ovf,
+        if (tracing && trav_step_world<WORLD, kBlock, STACK, kStepStore>(T, S, o, d, anyhit, stk, ovf,
                                                              LDS_SCENE && (WORLD == FRT_WORLD_BVH || WORLD == kWorldBvh2Oct) ? 0 : R.min_desc)) {
             tracing = false;
             finish();
@@ -633,7 +633,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
         for (;;) {
             bool ext = false;
             if (tracing) FRT_DIAG_TICK(3);
-            if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, M.P.ro, M.P.rd, M.P.shadow, stk, ovf,
+            if (tracing && trav_step_world<WORLD, kBlock, STACK, kStepSelect>(T, S, M.P.ro, M.P.rd, M.P.shadow, stk, ovf,
                                                                  LDS_SCENE ? 0 : W.min_desc)) {   // LDS plans: compiled out
                 if (M.P.shadow) {               // finish the shadow ray here (mlt_shade's shadow branch)
                     if (!path_after_shadow<(MATS ? kMatsAll : kMatsNone)>(M.P, T.h.prim < 0)) {   // path ended (P.term)

@@ -186,5 +186,32 @@ x)  # same-call A/B: the binary traversal's stack top in a register (libfrt_topr
     for k in 1 2; do ab c "" $C && ab c libfrt_topreg.so $C || exit 1; done \
      && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_topreg.so $P || exit 1; done \
      && FRT_LIB_PATH=$E/libfrt_topreg.so pt parity 600 tests/test_gpu_parity.py tests/test_gpu_pssmlt.py -m gpu ;;
+y)  # where the Cornell kernel's cycles go: the wave-cycle buckets (WAIT_ANY + WAIT_INST_ANY +
+    # ACTIVE_INST_ANY = WAVE_CYCLES) and the instruction mix, two SQ passes (counters the box
+    # lists only); cornell_1m pass A too
+    timeout -k 10 60 rocprofv3 -L > $O/counters.txt 2>&1 || true
+    have() { local out=""; for c in "$@"; do grep -qw "$c" $O/counters.txt && out="$out $c"; done; echo $out; }
+    A=$(have SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS)
+    B=$(have SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_MISC SQ_INSTS_VMEM)
+    echo "A: $A" > $O/sets.txt; echo "B: $B" >> $O/sets.txt
+    pmc() {  # name, counters, bench args...
+      local n=$1 c=$2; shift 2
+      timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $O/$n -o run -- \
+          python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --north-star off "$@" > $O/$n.json 2> $O/$n.log
+    }
+    pmc sqa_cornell "$A" && pmc sqb_cornell "$B" && pmc sqa_1m "$A" --scene cornell_1m ;;
+z)  # same-call A/B of the octant node step without branches (SQ_INSTS_SALU is 48 % of SQ_INSTS_VALU
+    # on Cornell, r05y): libfrt_bf1 (store above the top and read below it every visit, selects
+    # only), libfrt_bf2 (the store only; the pop keeps its branch); then parity on bf1
+    for k in 1 2; do ab c "" $C && ab c libfrt_bf1.so $C && ab c libfrt_bf2.so $C || exit 1; done \
+     && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_bf1.so $P && ab mlt libfrt_bf2.so $P || exit 1; done \
+     && FRT_LIB_PATH=$E/libfrt_bf1.so pt parity 600 tests/test_gpu_parity.py tests/test_gpu_pssmlt.py -m gpu ;;
+aa) # the build with the node-visit forms (path / ray queries: kStepStore, PSS-MLT: kStepSelect):
+    # GPU suite + smoke, same-call A/B against the previous build (libfrt_prev), the default line
+    pt gpu 900 tests -m gpu \
+     && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
+     && for k in 1 2; do ab c libfrt_prev.so $C && ab c "" $C || exit 1; done \
+     && for k in 1 2; do ab mlt libfrt_prev.so $P && ab mlt "" $P || exit 1; done \
+     && b default 500 ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
