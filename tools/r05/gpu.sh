@@ -213,5 +213,15 @@ aa) # the build with the node-visit forms (path / ray queries: kStepStore, PSS-M
      && for k in 1 2; do ab c libfrt_prev.so $C && ab c "" $C || exit 1; done \
      && for k in 1 2; do ab mlt libfrt_prev.so $P && ab mlt "" $P || exit 1; done \
      && b default 500 ;;
+ab) # control experiment: 16 more LDS bytes per octant node visit (libfrt_ldsx reads the next record's
+    # first part and discards it) -- how much would fewer bytes per visit (fp16 planes) be worth?
+    for k in 1 2; do ab c "" $C && ab c libfrt_ldsx.so $C || exit 1; done \
+     && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_ldsx.so $P || exit 1; done ;;
+ac) # the octant records as fp16 planes in a scene frame + the refs, 32 B (libfrt_oct16; was 48 B +
+    # 8 B of refs): the GPU suite on that library first (parity of every octant-plan test), then the
+    # same-call A/B against the in-tree build on Cornell and PSS-MLT
+    FRT_LIB_PATH=$E/libfrt_oct16.so pt gpu 900 tests -m gpu \
+     && for k in 1 2; do ab c "" $C && ab c libfrt_oct16.so $C || exit 1; done \
+     && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_oct16.so $P || exit 1; done ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
