@@ -311,8 +311,9 @@ template <typename R> FRT_HD bool trav_begin(Trav<R> &T, const DevScene &S, int 
 // branch in the loop body.  The octant plan's stack has more slots than the
 // tree has levels (d < STACK), so the slot above the top is always inside the
 // lane's column.  Cornell (path): Store +0.4 %, Select -0.9 %; PSS-MLT: Select
-// +1.1 %, Store -0.2 % (same call, two alternations, profiles/r05/r05z; the
-// node loop issued 0.48 SALU per VALU instruction with its branches, r05y).
+// +1.1 %, Store -0.2 %; AO / normals: Store -2.4 % / -3 % (same call, two
+// alternations, profiles/r05/r05z, r05af; the Cornell kernel issued 0.48 SALU
+// per VALU instruction with the branches, r05y).
 // OCT (kWorldBvh2Oct): S.nodes holds the 8 octant copies; the ray's copy
 // stores every child box as (near xyz, far xyz) for its direction signs, so a
 // box costs 6 FMAs and two 3-way max / min instead of also sorting each

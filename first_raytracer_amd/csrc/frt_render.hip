@@ -138,6 +138,11 @@ __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
 }
 
 
+// the octant node step of each integrator (bvh2_step's STEP): the path kernels
+// store the far child without a branch (Cornell +0.4 %); AO and normals keep
+// the branches (their rays agree more: Store cost AO 2.4 %, normals 3 %, same
+// call, profiles/r05/r05af); PSS-MLT's chain kernel takes kStepSelect
+template <int KIND> constexpr int kPathStep = KIND == FRT_INTEGRATOR_PATH ? kStepStore : kStepBranch;
 // ------------------------------------------------------------------------
 // the persistent path megakernel
 // ------------------------------------------------------------------------
@@ -221,7 +226,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             bool shadow_done = false;
             if (tracing) FRT_DIAG_TICK(3);
             // (LDS-resident binary plans: no leaf postponing, compiled out)
-            if (tracing && trav_step_world<WORLD, kBlock, STACK, kStepStore>(T, S, P.ro, P.rd, P.shadow, stk, ovf,
+            if (tracing && trav_step_world<WORLD, kBlock, STACK, kPathStep<KIND>>(T, S, P.ro, P.rd, P.shadow, stk, ovf,
                                                                        LDS_SCENE && (WORLD == FRT_WORLD_BVH || WORLD == kWorldBvh2Oct)
                                                                            ? 0 : W.min_desc)) {
                 if (KIND == FRT_INTEGRATOR_PATH && P.shadow) {   // finish the shadow ray here, keep traversing
@@ -445,7 +450,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
             }
         }
         if (__ballot(tracing || have_next) == 0) break;
-        if (tracing && trav_step_world<WORLD, kBlock, STACK, kStepStore>(T, S, o, d, anyhit, stk, ovf,
+        if (tracing && trav_step_world<WORLD, kBlock, STACK>(T, S, o, d, anyhit, stk, ovf,
                                                              LDS_SCENE && (WORLD == FRT_WORLD_BVH || WORLD == kWorldBvh2Oct) ? 0 : R.min_desc)) {
             tracing = false;
             finish();

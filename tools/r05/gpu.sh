@@ -223,5 +223,50 @@ ac) # the octant records as fp16 planes in a scene frame + the refs, 32 B (libfr
     FRT_LIB_PATH=$E/libfrt_oct16.so pt gpu 900 tests -m gpu \
      && for k in 1 2; do ab c "" $C && ab c libfrt_oct16.so $C || exit 1; done \
      && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_oct16.so $P || exit 1; done ;;
+ad) # PMC per-ray figures of the kernels the node-visit forms changed (Cornell, PSS-MLT, AO, normals),
+    # the PSS-MLT line under rocprofv3 kernel-trace, then the default line under kernel-trace
+    SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY"
+    pmc() {  # name, counters, bench args...
+      local n=$1 c=$2; shift 2
+      timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $O/$n -o run -- \
+          python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --north-star off "$@" > $O/$n.json 2> $O/$n.log
+    }
+    tr() {  # name, seconds, bench args...
+      local n=$1 s=$2; shift 2
+      timeout -k 10 $s rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$n -o run -- \
+          python3 bench.py "$@" > $O/trace_$n.json 2> $O/trace_$n.log
+    }
+    pmc sq_cornell "$SQ" && pmc fetch_cornell FETCH_SIZE && pmc write_cornell WRITE_SIZE \
+     && pmc sq_pssmlt "$SQ" --integrator pssmlt && pmc fetch_pssmlt FETCH_SIZE --integrator pssmlt \
+     && pmc write_pssmlt WRITE_SIZE --integrator pssmlt \
+     && pmc sq_ao "$SQ" --integrator ao && pmc fetch_ao FETCH_SIZE --integrator ao && pmc write_ao WRITE_SIZE --integrator ao \
+     && pmc sq_normals "$SQ" --integrator normals && pmc fetch_normals FETCH_SIZE --integrator normals \
+     && pmc write_normals WRITE_SIZE --integrator normals \
+     && tr pssmlt 400 --integrator pssmlt --steps 3 --warmup 1 --no-cpu-baseline --north-star off \
+     && tr default 600 ;;
+ae) # PSS-MLT trav_min re-checked on the branch-free node step (default 12); the AO and normals lines
+    ab mltt "" --scene cornell --spp 512 --rounds 2 --bvh gsah --integrator pssmlt \
+          --variants default,default/trav6,default/trav16,default/trav20,default \
+     && b ao 300 --integrator ao && b normals 300 --integrator normals ;;
+af) # AO / normals lines read slower after the node-visit forms (r05ae vs r05k): same-call A/B of the
+    # path kernels with the branchy step (libfrt_pbranch) against the in-tree kStepStore, AO and normals
+    A="--scene cornell --spp 512 --rounds 3 --bvh gsah --integrator ao --variants default"
+    N="--scene cornell --spp 512 --rounds 3 --bvh gsah --integrator normals --variants default"
+    for k in 1 2; do ab ao "" $A && ab ao libfrt_pbranch.so $A || exit 1; done \
+     && for k in 1 2; do ab nrm "" $N && ab nrm libfrt_pbranch.so $N || exit 1; done ;;
+ag) # the build with the per-integrator node step (path: Store, AO / normals / ray queries: Branch,
+    # PSS-MLT: Select): GPU suite + smoke, AO / normals PMC passes and lines, the default line
+    SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY"
+    pmc() {  # name, counters, bench args...
+      local n=$1 c=$2; shift 2
+      timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $O/$n -o run -- \
+          python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --north-star off "$@" > $O/$n.json 2> $O/$n.log
+    }
+    pt gpu 900 tests -m gpu \
+     && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
+     && pmc sq_ao "$SQ" --integrator ao && pmc fetch_ao FETCH_SIZE --integrator ao && pmc write_ao WRITE_SIZE --integrator ao \
+     && pmc sq_normals "$SQ" --integrator normals && pmc fetch_normals FETCH_SIZE --integrator normals \
+     && pmc write_normals WRITE_SIZE --integrator normals \
+     && b ao 300 --integrator ao && b normals 300 --integrator normals && b default 500 ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
