@@ -268,5 +268,10 @@ ag) # the build with the per-integrator node step (path: Store, AO / normals / r
      && pmc sq_normals "$SQ" --integrator normals && pmc fetch_normals FETCH_SIZE --integrator normals \
      && pmc write_normals WRITE_SIZE --integrator normals \
      && b ao 300 --integrator ao && b normals 300 --integrator normals && b default 500 ;;
+ah) # C3 (veach, list world): the BVH over the list (culling only; trace_list) against the in-order scan
+    # (FRT_LIST_BVH=0), same library, alternated; then the GPU suite on the list-BVH build
+    V="--scene veach --spp 256 --rounds 2 --variants default"
+    for k in 1 2; do ab v "" $V && FRT_LIST_BVH=0 ab vscan "" $V || exit 1; done \
+     && pt gpu 900 tests -m gpu ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
