@@ -239,6 +239,12 @@ template <typename R> FRT_HD V3<R> normalize(V3<R> v) { return rlen(v) * v; }
 // (aabb.h:24-25) keeps the interval unchanged in that case, and so does this
 // (the near-parallel slab spans +-huge).  Device boxes are padded outward, so
 // neither the nudge nor the FMA rounding can cull a hit.
+// a value every active lane holds, moved into a scalar register (plain on the host)
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ int frt_uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+#else
+inline int frt_uniform(int x) { return x; }
+#endif
 template <typename R> struct SlabRay { V3<R> invd, oinv; };
 template <typename R> FRT_HD SlabRay<R> slab_ray(V3<R> o, V3<R> d)
 {

@@ -273,5 +273,35 @@ ah) # C3 (veach, list world): the BVH over the list (culling only; trace_list) a
     V="--scene veach --spp 256 --rounds 2 --variants default"
     for k in 1 2; do ab v "" $V && FRT_LIST_BVH=0 ab vscan "" $V || exit 1; done \
      && pt gpu 900 tests -m gpu ;;
+ai) # C3: the list scan's entry index and prim ref made wave-uniform (readfirstlane; libfrt_luni)
+    V="--scene veach --spp 256 --rounds 2 --variants default"
+    for k in 1 2; do ab v "" $V && ab v libfrt_luni.so $V || exit 1; done ;;
+aj) # C3: the uniform list scan (libfrt_luni: readfirstlane index / ref) and with the fp64 records by
+    # scalar loads from the constant address space (libfrt_luni2) against the in-tree scan
+    V="--scene veach --spp 256 --rounds 2 --variants default"
+    for k in 1 2; do ab v "" $V && ab v libfrt_luni.so $V && ab v libfrt_luni2.so $V || exit 1; done ;;
+ak) # the build with the uniform list scan (scalar loads of the list's records): GPU suite + smoke,
+    # the veach line (C3), its PMC passes (fp64 issue weights)
+    SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY"
+    F64="SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64"
+    pmc() {  # name, counters, bench args...
+      local n=$1 c=$2; shift 2
+      timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $O/$n -o run -- \
+          python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --north-star off "$@" > $O/$n.json 2> $O/$n.log
+    }
+    pt gpu 900 tests -m gpu \
+     && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
+     && b veach 400 --scene veach --spp 1024 \
+     && pmc sq_veach "$SQ" --scene veach --spp 1024 && pmc fetch_veach FETCH_SIZE --scene veach --spp 1024 \
+     && pmc write_veach WRITE_SIZE --scene veach --spp 1024 && pmc f64_veach "$F64" --scene veach --spp 1024 \
+     && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_veach -o run -- \
+          python3 bench.py --scene veach --spp 1024 --steps 3 --warmup 1 --no-cpu-baseline --north-star off \
+          > $O/trace_veach.json 2> $O/trace_veach.log ;;
+al) # the fp64 list scan with the records through the constant address space (the r05aj libfrt_luni2
+    # form; stage ak ran a helper-function form whose loads stayed vector loads): A/B against the
+    # previous build (libfrt_prev), the GPU suite, the veach line
+    V="--scene veach --spp 256 --rounds 2 --variants default"
+    for k in 1 2; do ab v libfrt_prev.so $V && ab v "" $V || exit 1; done \
+     && pt gpu 900 tests -m gpu && b veach 400 --scene veach --spp 1024 ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
