@@ -540,24 +540,31 @@ template <typename R> FRT_HD Hit<R> trace_list(const DevScene &S, V3<R> o, V3<R>
 {
     Hit<R> h{-1, tmax, R(0), R(0)};
     for (int i = 0; i < S.n_list; ++i) {
-        const int ref = frt_uniform(S.list[frt_uniform(i)]);   // every lane tests the same entry
+#if defined(__HIP_DEVICE_COMPILE__)   // every lane tests the same entry: a scalar load
+        const int ref = frt_uniform(((const __attribute__((address_space(4))) int *)S.list)[frt_uniform(i)]);
+#else
+        const int ref = S.list[i];
+#endif
         R u, v;
 #if defined(__HIP_DEVICE_COMPILE__)
-        // fp64 (C3): the uniform entry's record through the constant address space, which
-        // lets the compiler use scalar loads for the triangles' vertex records.  veach
-        // 256 spp, same call: 201.7 / 201.4 ms -> 187.2 / 187.2 (+7.7 %; the uniform index
-        // alone +0.9 %; profiles/r05/r05aj)
+        // fp64 (C3): the uniform entry's records through the constant address space as
+        // indexed base pointers, so that the compiler reads them with scalar loads (the
+        // entry, the sphere and all three vertex records; the form matters -- an offset
+        // pointer left v0 and the sphere as vector loads).  veach 256 spp, same call:
+        // 201.7 / 201.4 ms -> 187.2 / 187.2 with the vertex records v1 / v2 scalar
+        // (profiles/r05/r05aj), -> 174.9 / 174.8 with every load scalar (r05am)
         R t;
         if constexpr (kIsF64<R>) {
             typedef const __attribute__((address_space(4))) double4 *cptr;
             if (ref & FRT_PRIM_SPHERE) {
-                const double4 q = *(cptr)(S.spheres64 + (ref & ~FRT_PRIM_SPHERE));
+                const cptr sb = (cptr)S.spheres64;
+                const double4 q = sb[ref & ~FRT_PRIM_SPHERE];
                 u = v = R(0);
                 t = sphere_intersect(o, d, xyz(q), q.w, Cst<R>::eps, h.t);
             } else {
-                const cptr tp = (cptr)(S.tris64 + 3 * ref);
-                const double4 a = tp[0], b = tp[1], c = tp[2];
-                t = tri_intersect<false>(o, d, xyz(a), xyz(b), xyz(c), Cst<R>::eps, h.t, u, v);
+                const cptr tb = (cptr)S.tris64;
+                const double4 a = tb[3 * ref], b = tb[3 * ref + 1], c = tb[3 * ref + 2];
+                t = tri_intersect(o, d, xyz(a), xyz(b), xyz(c), Cst<R>::eps, h.t, u, v);
             }
         } else {
             t = prim_t(S, ref, o, d, Cst<R>::eps, h.t, u, v);

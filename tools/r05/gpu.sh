@@ -303,5 +303,27 @@ al) # the fp64 list scan with the records through the constant address space (th
     V="--scene veach --spp 256 --rounds 2 --variants default"
     for k in 1 2; do ab v libfrt_prev.so $V && ab v "" $V || exit 1; done \
      && pt gpu 900 tests -m gpu && b veach 400 --scene veach --spp 1024 ;;
+am) # C3: every load of the fp64 list scan scalar (libfrt_lsc: the list entry and all three vertex
+    # records through the constant address space, base-pointer indexing) against the in-tree build
+    # (the vertex records v1 / v2 and the sphere scalar, the entry and v0 vector)
+    V="--scene veach --spp 256 --rounds 2 --variants default"
+    for k in 1 2; do ab v "" $V && ab v libfrt_lsc.so $V || exit 1; done ;;
+an) # the build with every fp64 list-scan load scalar: GPU suite + smoke, the veach line, its PMC
+    # passes and kernel trace (stage ak's steps)
+    SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY"
+    F64="SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64"
+    pmc() {  # name, counters, bench args...
+      local n=$1 c=$2; shift 2
+      timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $O/$n -o run -- \
+          python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --north-star off "$@" > $O/$n.json 2> $O/$n.log
+    }
+    pt gpu 900 tests -m gpu \
+     && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
+     && b veach 400 --scene veach --spp 1024 \
+     && pmc sq_veach "$SQ" --scene veach --spp 1024 && pmc fetch_veach FETCH_SIZE --scene veach --spp 1024 \
+     && pmc write_veach WRITE_SIZE --scene veach --spp 1024 && pmc f64_veach "$F64" --scene veach --spp 1024 \
+     && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_veach -o run -- \
+          python3 bench.py --scene veach --spp 1024 --steps 3 --warmup 1 --no-cpu-baseline --north-star off \
+          > $O/trace_veach.json 2> $O/trace_veach.log ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
