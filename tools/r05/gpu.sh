@@ -325,5 +325,9 @@ an) # the build with every fp64 list-scan load scalar: GPU suite + smoke, the ve
      && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_veach -o run -- \
           python3 bench.py --scene veach --spp 1024 --steps 3 --warmup 1 --no-cpu-baseline --north-star off \
           > $O/trace_veach.json 2> $O/trace_veach.log ;;
+ao) # C3: the fp64 list kernels at a 3-wave register cap (libfrt_f64w3) against the compiler's own
+    # allocation (2 waves), on the scalar-load build
+    V="--scene veach --spp 256 --rounds 2 --variants default"
+    for k in 1 2; do ab v "" $V && ab v libfrt_f64w3.so $V || exit 1; done ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
