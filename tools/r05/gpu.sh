@@ -329,5 +329,10 @@ ao) # C3: the fp64 list kernels at a 3-wave register cap (libfrt_f64w3) against 
     # allocation (2 waves), on the scalar-load build
     V="--scene veach --spp 256 --rounds 2 --variants default"
     for k in 1 2; do ab v "" $V && ab v libfrt_f64w3.so $V || exit 1; done ;;
+ap) # cornell_1m trees on the final kernels: GPU binned SAH (the bench default), host binned SAH, the
+    # reference's create_bvh topology (full-sweep SAH, one-prim leaves before collapse)
+    for k in 1 2; do ab mt "" --scene cornell_1m --spp 256 --rounds 2 --bvh gsah --variants default \
+      && ab mt "" --scene cornell_1m --spp 256 --rounds 2 --bvh sah --variants default \
+      && ab mt "" --scene cornell_1m --spp 256 --rounds 2 --bvh host --variants default || exit 1; done ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
