@@ -334,5 +334,11 @@ ap) # cornell_1m trees on the final kernels: GPU binned SAH (the bench default),
     for k in 1 2; do ab mt "" --scene cornell_1m --spp 256 --rounds 2 --bvh gsah --variants default \
       && ab mt "" --scene cornell_1m --spp 256 --rounds 2 --bvh sah --variants default \
       && ab mt "" --scene cornell_1m --spp 256 --rounds 2 --bvh host --variants default || exit 1; done ;;
+aq) # the octant plan's leaves with the straight-line triangle test (libfrt_ostr; round 4 measured
+    # -2.4 % on Cornell before the SLP vectorizer was turned off), Cornell and PSS-MLT; Cornell trav_min
+    # re-checked on the Store node step
+    for k in 1 2; do ab c "" $C && ab c libfrt_ostr.so $C || exit 1; done \
+     && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_ostr.so $P || exit 1; done \
+     && ab ct "" --scene cornell --spp 512 --rounds 3 --bvh gsah --variants default,default/trav16,default/trav24,default ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
