@@ -340,5 +340,11 @@ aq) # the octant plan's leaves with the straight-line triangle test (libfrt_ostr
     for k in 1 2; do ab c "" $C && ab c libfrt_ostr.so $C || exit 1; done \
      && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_ostr.so $P || exit 1; done \
      && ab ct "" --scene cornell --spp 512 --rounds 3 --bvh gsah --variants default,default/trav16,default/trav24,default ;;
+ar) # final build: GPU suite + smoke, the default line, the PSS-MLT line (path-exact chain-shard parity,
+    # CPU baseline), and the launcher's two-rank gloo rehearsal
+    pt gpu 900 tests -m gpu \
+     && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
+     && b default 500 && b pssmlt 600 --integrator pssmlt \
+     && b gloo2 600 --gpus 2 --backend gloo --steps 2 ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
