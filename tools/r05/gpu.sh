@@ -346,5 +346,8 @@ ar) # final build: GPU suite + smoke, the default line, the PSS-MLT line (path-e
      && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
      && b default 500 && b pssmlt 600 --integrator pssmlt \
      && b gloo2 600 --gpus 2 --backend gloo --steps 2 ;;
+as) # cornell_1m: the 4-wide plan's leaf loop with the next triangle's loads issued ahead of the
+    # current test (libfrt_lpf; 8 VGPRs spilled at the 7-wave cap) against the in-tree serial loop
+    for k in 1 2; do ab m "" $M && ab m libfrt_lpf.so $M || exit 1; done ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
