@@ -349,5 +349,8 @@ ar) # final build: GPU suite + smoke, the default line, the PSS-MLT line (path-e
 as) # cornell_1m: the 4-wide plan's leaf loop with the next triangle's loads issued ahead of the
     # current test (libfrt_lpf; 8 VGPRs spilled at the 7-wave cap) against the in-tree serial loop
     for k in 1 2; do ab m "" $M && ab m libfrt_lpf.so $M || exit 1; done ;;
+at) # PSS-MLT chain kernel at a 5-wave cap (libfrt_mlt5) on the branch-free node step, against the
+    # in-tree 4-wave cap
+    for k in 1 2; do ab mlt "" $P && ab mlt libfrt_mlt5.so $P || exit 1; done ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
