@@ -566,8 +566,18 @@ template <typename R> FRT_HD Hit<R> trace_list(const DevScene &S, V3<R> o, V3<R>
                 const double4 a = tb[3 * ref], b = tb[3 * ref + 1], c = tb[3 * ref + 2];
                 t = tri_intersect(o, d, xyz(a), xyz(b), xyz(c), Cst<R>::eps, h.t, u, v);
             }
-        } else {
-            t = prim_t(S, ref, o, d, Cst<R>::eps, h.t, u, v);
+        } else {   // fp32 list kernels: the same scalar loads of the fp32 records
+            typedef const __attribute__((address_space(4))) float4 *cptr;
+            if (ref & FRT_PRIM_SPHERE) {
+                const cptr sb = (cptr)S.spheres;
+                const float4 q = sb[ref & ~FRT_PRIM_SPHERE];
+                u = v = R(0);
+                t = sphere_intersect(o, d, xyz(q), q.w, Cst<R>::eps, h.t);
+            } else {
+                const cptr tb = (cptr)S.tris;
+                const float4 a = tb[ref * S.tri_es], b = tb[ref * S.tri_es + S.tri_ps], c = tb[ref * S.tri_es + 2 * S.tri_ps];
+                t = tri_intersect(o, d, xyz(a), xyz(b), xyz(c), Cst<R>::eps, h.t, u, v);
+            }
         }
 #else
         const R t = prim_t(S, ref, o, d, Cst<R>::eps, h.t, u, v);

@@ -352,5 +352,10 @@ as) # cornell_1m: the 4-wide plan's leaf loop with the next triangle's loads iss
 at) # PSS-MLT chain kernel at a 5-wave cap (libfrt_mlt5) on the branch-free node step, against the
     # in-tree 4-wave cap
     for k in 1 2; do ab mlt "" $P && ab mlt libfrt_mlt5.so $P || exit 1; done ;;
+au) # the fp32 list kernels with the list scan's scalar loads: veach at fp32 (bench --precision fp32),
+    # the previous build (libfrt_prev) and the in-tree build alternated, then the GPU suite
+    VB="--scene veach --spp 256 --precision fp32 --steps 3 --warmup 1 --no-cpu-baseline --north-star off"
+    for k in 1 2; do FRT_LIB_PATH=$E/libfrt_prev.so b v32prev$k 300 $VB && b v32cur$k 300 $VB || exit 1; done \
+     && pt gpu 900 tests -m gpu ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
