@@ -357,5 +357,8 @@ au) # the fp32 list kernels with the list scan's scalar loads: veach at fp32 (be
     VB="--scene veach --spp 256 --precision fp32 --steps 3 --warmup 1 --no-cpu-baseline --north-star off"
     for k in 1 2; do FRT_LIB_PATH=$E/libfrt_prev.so b v32prev$k 300 $VB && b v32cur$k 300 $VB || exit 1; done \
      && pt gpu 900 tests -m gpu ;;
+av) # cornell_1m: the 4-wide stack's top in a register (libfrt_b4top: a pop hands the next node over at
+    # once, the LDS read refills the register off the critical path; 12 VGPRs spilled at the 7-wave cap)
+    for k in 1 2; do ab m "" $M && ab m libfrt_b4top.so $M || exit 1; done ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
