@@ -360,5 +360,7 @@ au) # the fp32 list kernels with the list scan's scalar loads: veach at fp32 (be
 av) # cornell_1m: the 4-wide stack's top in a register (libfrt_b4top: a pop hands the next node over at
     # once, the LDS read refills the register off the critical path; 12 VGPRs spilled at the 7-wave cap)
     for k in 1 2; do ab m "" $M && ab m libfrt_b4top.so $M || exit 1; done ;;
+aw) # Cornell at N = 1: samples per work item (automatic: 9 on the LDS plan) against larger items
+    ab cs "" --scene cornell --spp 512 --rounds 3 --bvh gsah --variants default,default/spi16,default/spi32,default/spi64,default ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
