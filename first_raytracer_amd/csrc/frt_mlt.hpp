@@ -29,19 +29,18 @@ constexpr int kMltFp = kMltDims;
 constexpr float kMltLargeStep = 0.3f;                        // LargeStepProb (pssmlt.h:13)
 constexpr uint32_t kMltChainSalt = 0x3C6EF372U, kMltBootSalt = 0xB5297A4DU;
 
-// perturb (pssmlt.cpp:6-17) with log(s2/s1) precomputed
+// perturb (pssmlt.cpp:6-17) with log(s2/s1) precomputed.  The two halves as
+// selects around one exp (the same operations and values as the branches,
+// whose FMA the compiler formed as s2 * e + value and -s2 * e + value; as
+// branches a wave ran both halves, two v_exp_f32 and the exec-mask bookkeeping)
 FRT_HD float mlt_perturb(float value, float s2, float log_ratio, float r)
 {
-    float result;
-    if (r < 0.5f) {
-        r = r * 2.0f;
-        result = value + s2 * fexp(-log_ratio * r);
-        if (result > 1.0f) result -= 1.0f;
-    } else {
-        r = (r - 0.5f) * 2.0f;
-        result = value - s2 * fexp(-log_ratio * r);
-        if (result < 0.0f) result += 1.0f;
-    }
+    const bool up = r < 0.5f;
+    const float rr = up ? r * 2.0f : (r - 0.5f) * 2.0f;
+    const float e = fexp(-log_ratio * rr);
+    float result = fmaf(up ? s2 : -s2, e, value);
+    if (up && result > 1.0f) result -= 1.0f;
+    if (!up && result < 0.0f) result += 1.0f;
     return result;
 }
 

@@ -362,5 +362,9 @@ av) # cornell_1m: the 4-wide stack's top in a register (libfrt_b4top: a pop hand
     for k in 1 2; do ab m "" $M && ab m libfrt_b4top.so $M || exit 1; done ;;
 aw) # Cornell at N = 1: samples per work item (automatic: 9 on the LDS plan) against larger items
     ab cs "" --scene cornell --spp 512 --rounds 3 --bvh gsah --variants default,default/spi16,default/spi32,default/spi64,default ;;
+ax) # PSS-MLT: the Kelemen perturbation as selects around one exp (in-tree) against the branches
+    # (libfrt_prev), then the PSS-MLT GPU tests and the PSS-MLT line on the in-tree build
+    for k in 1 2; do ab mlt libfrt_prev.so $P && ab mlt "" $P || exit 1; done \
+     && pt mlt 600 tests/test_gpu_pssmlt.py -m gpu && b pssmlt 600 --integrator pssmlt ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
