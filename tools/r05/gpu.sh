@@ -366,5 +366,20 @@ ax) # PSS-MLT: the Kelemen perturbation as selects around one exp (in-tree) agai
     # (libfrt_prev), then the PSS-MLT GPU tests and the PSS-MLT line on the in-tree build
     for k in 1 2; do ab mlt libfrt_prev.so $P && ab mlt "" $P || exit 1; done \
      && pt mlt 600 tests/test_gpu_pssmlt.py -m gpu && b pssmlt 600 --integrator pssmlt ;;
+ay) # final build (branch-free perturbation): GPU suite + smoke, PSS-MLT PMC passes and its line under
+    # rocprofv3 kernel-trace
+    SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY"
+    pmc() {  # name, counters, bench args...
+      local n=$1 c=$2; shift 2
+      timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $O/$n -o run -- \
+          python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --north-star off "$@" > $O/$n.json 2> $O/$n.log
+    }
+    pt gpu 900 tests -m gpu \
+     && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
+     && pmc sq_pssmlt "$SQ" --integrator pssmlt && pmc fetch_pssmlt FETCH_SIZE --integrator pssmlt \
+     && pmc write_pssmlt WRITE_SIZE --integrator pssmlt \
+     && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_pssmlt -o run -- \
+          python3 bench.py --integrator pssmlt --steps 3 --warmup 1 --no-cpu-baseline --north-star off \
+          > $O/trace_pssmlt.json 2> $O/trace_pssmlt.log ;;
 *) echo "unknown stage $S"; exit 2 ;;
 esac
