@@ -8,7 +8,13 @@ the CPU baseline (the fp64 C restatement, oracle/, timed on this host's cores).
 The same JSON line carries the north-star run (BASELINE.json north_star, SURVEY
 §8(d) C4): the 1,005,858-triangle tessellated Cornell box at 1920x1080 / 512
 spp, sharded the same way, timed the same way, with its own RMSE against the
-oracle and its own roofline ("north_star": {...}).
+oracle and its own roofline ("north_star": {...}).  It also carries BASELINE.json's
+configs[2] and [4] as blocks "c3" (veach_mi 1080p 1024 spp, the fp64 list-world
+kernel) and "c5" (PSS-MLT on CornellBox 1080p, 512 mutations per pixel, 2^18
+chains), each timed the same way (3 frames after 1 warm-up) with its own RMSE
+against the oracle (C5: path-exact on a chain shard of the config), roofline
+and CPU figure, so the driver's default run measures four of the five configs
+(C1 is the reference's own CPU plumbing case).
 
 One "step" = one full frame: every rank renders its tiles (tile t -> rank
 t mod N) into HBM, then the per-rank slot buffers are gathered to rank 0,
@@ -206,16 +212,24 @@ def cpu_baseline(kind, obj, nx, ny, spp, seed, npix, threads, film, seconds, int
     }
 
 
-def cpu_baseline_mlt(ctx, kind, obj, nx, ny, mpp, n_chains, seed, threads, seconds):
+def cpu_baseline_mlt(ctx, r, mpp, n_chains, seed, threads, seconds):
     """C5's CPU baseline and path-exact parity in one: the oracle's PSS-MLT
     (pssmlt.cpp restated in fp64) on the chains of shard (0, K) of the config
     itself -- every one of them runs the config's full mutation count -- with K
     halved from 1024 (a power of two, at least 16) until the oracle's run takes
     about `seconds`; the GPU renders the same shard for the comparison
-    (mlt_shard_parity)."""
+    (mlt_shard_parity).  `r` is the measured render (bench.Runner.measure):
+    its scene must still be the one uploaded to ctx.  A request with fewer
+    mutations than chains (0 steps per chain) has no chain to compare: the
+    parity is None, with a note."""
+    nx, ny = r["nx"], r["ny"]
+    if mpp * nx * ny // n_chains <= 0:
+        return {"mrays": None, "seconds": 0.0, "rays": 0, "npix": 0, "V": None, "T": None, "parity": None,
+                "sample": "none", "note": (f"{mpp} mutations/pixel x {nx}x{ny} < {n_chains} chains: 0 mutations "
+                                           f"per chain, no path-exact parity")}
     K = 1024
     while True:
-        par = mlt_shard_parity(ctx, kind, obj, nx, ny, mpp, n_chains, K, seed, threads)
+        par = mlt_shard_parity(ctx, r["kind"], r["obj"], nx, ny, mpp, n_chains, K, seed, threads, env=r["env"])
         dt = par["oracle_seconds"]
         if dt >= 0.5 * seconds or K <= 16 or K >= n_chains:
             break
@@ -228,7 +242,7 @@ def cpu_baseline_mlt(ctx, kind, obj, nx, ny, mpp, n_chains, seed, threads, secon
 
 
 def mlt_shard_parity(ctx, kind, obj, nx, ny, mpp, n_chains, shard_count, seed, threads, shard_index=0,
-                     n_init=10000, flags=0):
+                     n_init=10000, flags=0, env=None):
     """C5 path-exact parity at the config itself: the GPU
     renders shard (shard_index, shard_count) of the PSS-MLT request -- the
     chains c = shard_index + j * shard_count of n_chains, each with the
@@ -255,6 +269,8 @@ def mlt_shard_parity(ctx, kind, obj, nx, ny, mpp, n_chains, shard_count, seed, t
     u_gpu, fp_gpu = ctx.mlt_chain_state(0, n_local)
     steps = mpp * nx * ny // n_chains
     sc = oracle.OracleScene(kind, obj, nx / ny)
+    if env is not None:                       # the GPU scene's environment (bench --env)
+        sc.set_env(env)
     t0 = time.perf_counter()
     ref, b, cnt, fp_ora, u_ora = sc.mlt_render_shard(nx, ny, n_chains, steps, shard_index, shard_count, seed=seed,
                                                      n_init=n_init, nthreads=threads)
@@ -295,7 +311,7 @@ MLT_MAX_PATH = 10     # pssmlt.h MaxPathLength: pssmlt::Li traces depths 0..10 (
 
 
 def mlt_block_rmse(kind, obj, nx, ny, film, threads, seconds, spp=256, block=8, seed=0, n_init=10000,
-                   max_blocks=None):
+                   max_blocks=None, env=None):
     """C5's "RMSE vs CPU ref".  PSS-MLT (pssmlt.cpp) and path::Li estimate the
     same image with different samples, so no stream is shared and no pixel is
     path-exact at 1080p (chains run ~4000 mutations; pssmlt.cpp has no
@@ -321,6 +337,8 @@ def mlt_block_rmse(kind, obj, nx, ny, film, threads, seconds, spp=256, block=8, 
     `rmse_b_corrected` the same after the b correction."""
     import oracle
     sc = oracle.OracleScene(kind, obj, nx / ny)
+    if env is not None:
+        sc.set_env(env)
     bx, by = nx // block, ny // block
     img = np.asarray(film, np.float64).reshape(ny, nx, 3)
 
@@ -427,15 +445,28 @@ def roofline(integrator, key, world, res, V, T, shared_device=False):
                         "hbm_GBps": None if hbm_gbs is None else round(hbm_gbs, 1),
                         "lds_frac": None if algo is None else round(algo / LDS_PEAK_GBS, 4)})
         elif hbm is not None:
+            # FETCH_SIZE counts L2 misses; on gfx950 those include Infinity-Cache hits
+            # (MI355X_MICROARCH.md), and cornell_1m's 99 MB scene fits the 256 MB
+            # Infinity Cache: the counted bytes are an upper bound on HBM bytes, and
+            # the kernel is latency-bound (wait_frac), not bandwidth-bound
             out.update({"bound": "hbm", "achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(hbm_gbs / HBM_PEAK_GBS, 4), "traffic": int(rays * hbm),
+                        "counts_infinity_cache_hits": True,
+                        "traffic_basis": "2 x FETCH_SIZE + WRITE_SIZE: L2-miss bytes, served by the Infinity "
+                                         "Cache or HBM (the counters do not split them)",
                         "algorithmic_over_traffic": None if algo is None else round(algo / hbm_gbs, 3)})
             if issue is not None:
                 out["valu_issue_frac"] = round(rays * issue / launch_s / 1e9 / VALU_PEAK_GINST, 4)
+        if pmc.get("wait_frac") is not None:
+            # SQ_WAIT_ANY / SQ_WAVE_CYCLES: share of wave cycles spent in s_waitcnt
+            out["wait_frac"] = round(pmc["wait_frac"], 4)
     if shared_device and out.get("frac") is not None:
         # ranks sharing one device (gloo rehearsal): a rank's launch time is not
         # the time of a launch that has the chip, so no fraction of its peak
-        out.update({"achieved": None, "frac": None, "basis": "ranks share one device (rehearsal): no roofline"})
+        for k in ("achieved", "frac", "valu_issue_frac", "lds_frac"):     # every fraction of a chip peak
+            if k in out:
+                out[k] = None
+        out["basis"] = "ranks share one device (rehearsal): no roofline"
     if "bound" not in out:
         # no counter profile for this config: no roofline.  The algorithmic bytes
         # (algorithmic_GBps above) are not one: L1 / L2 / the Infinity Cache / LDS
@@ -493,10 +524,24 @@ class Runner:
         if self.world > 1:
             self.dist.barrier()
 
-    def measure(self, args, scene, spp, steps, warmup, bvh_arg):
+    def gather_ranks(self, x):
+        """Every rank's float x, as a list on every rank (one all-reduce of a
+        world-sized vector; per-rank timings for the line at N > 1)."""
+        torch = self.torch
+        v = torch.zeros(self.world, dtype=torch.float64, device=self.dev)
+        v[self.rank] = float(x)
+        if self.world > 1:
+            self.all_reduce(v)
+        return [float(t) for t in v.cpu()]
+
+    def measure(self, args, scene, spp, steps, warmup, bvh_arg, integrator=None, precision=None, env=None):
         """Build + upload `scene`, then W warmup and K timed frames (barrier +
-        synchronize on both sides, max over ranks)."""
+        synchronize on both sides, max over ranks).  `integrator`, `precision`
+        and `env` default to the command line's (the configuration blocks pass
+        their own)."""
         torch, frt = self.torch, self.frt
+        integrator = integrator or args.integrator
+        precision = precision or args.precision
         nx, ny = (int(x) for x in args.res.lower().split("x"))
         workdir = tempfile.gettempdir()   # the generated 1M-triangle OBJ (33 MB) stays out of gpurun_out/
         kind, obj, scene_name = scene_spec(scene, workdir, tag=f"_r{self.rank}")
@@ -508,17 +553,14 @@ class Runner:
                                           "world": "list"}, nx / ny)
         else:
             hs = frt.HostScene(kind, obj, nx / ny)   # OBJ load + reference-topology BVH build (host)
-        env = None
-        if args.env:
-            env = tuple(float(x) for x in args.env.split(","))
-        elif args.integrator == "ao":
+        if env is None and integrator == "ao":
             env = (1.0, 1.0, 1.0)                    # the scenes' black environment would make every AO sample 0
         if env is not None:
             hs.set_env(env)
         integ = {"path": frt.FRT_INTEGRATOR_PATH, "ao": frt.FRT_INTEGRATOR_AO,
-                 "normals": frt.FRT_INTEGRATOR_NORMALS}.get(args.integrator, frt.FRT_INTEGRATOR_PSSMLT)
+                 "normals": frt.FRT_INTEGRATOR_NORMALS}.get(integrator, frt.FRT_INTEGRATOR_PSSMLT)
         ctx = self.ctx
-        ctx.set_precision(args.precision)           # read by the upload below (fp64 records) and the renders
+        ctx.set_precision(precision)                 # read by the upload below (fp64 records) and the renders
         if bvh == "sah":
             hs.build_bvh_sah()                       # binned SAH on the host (in host_build_s)
         if bvh in ("gpu", "ploc", "lbvh"):
@@ -531,7 +573,7 @@ class Runner:
         ctx.upload(hs)                               # flatten + leaf collapse + BVH4Q + copy to HBM
         t2 = time.perf_counter()
         world, rank = self.world, self.rank
-        if args.integrator == "pssmlt":
+        if integrator == "pssmlt":
             # chains shard over ranks (chain c -> rank c mod N); splat films are summed
             params = frt.RenderParams.pssmlt(nx, ny, spp, args.chains, seed=args.seed,
                                              shard_index=rank, shard_count=world)
@@ -542,15 +584,25 @@ class Runner:
             from first_raytracer_amd.dist import TileGather
             tgather = TileGather(nx, ny, args.tile, world, rank, self.dev, stage_cpu=self.gloo)
         stream = torch.cuda.current_stream(self.dev)
+        ev = []                                      # (start, end) events around each timed step's collective
 
-        def step():
-            if args.integrator == "pssmlt":
+        def step(timed=False):
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            if integrator == "pssmlt":
                 st = ctx.render_device(params, mlt_film.data_ptr(), stream.cuda_stream)
+                if timed:
+                    e0.record(stream)
                 if world > 1:
                     self.all_reduce(mlt_film)        # RCCL sum of the per-rank splat films
-                return st
-            st = ctx.render_device(params, tgather.my_slots.data_ptr(), stream.cuda_stream)
-            tgather.gather()       # RCCL gather of the tile slots to rank 0, which scatters them into its film
+            else:
+                st = ctx.render_device(params, tgather.my_slots.data_ptr(), stream.cuda_stream)
+                if timed:
+                    e0.record(stream)
+                tgather.gather()   # RCCL gather of the tile slots to rank 0, which scatters them into its film
+            if timed:
+                e1.record(stream)
+                ev.append((e0, e1))
             return st
 
         for _ in range(warmup):
@@ -562,14 +614,17 @@ class Runner:
         kernel_ms = []
         last = None
         for k in range(steps):
-            st = step()
+            st = step(timed=True)
             rays += st.rays
             kernel_ms.append(st.kernel_ms)
             last = st
-            log(f"rank {rank} {scene} step {k}: {st.rays / 1e9:.3f} Grays, kernel {st.kernel_ms:.1f} ms")
+            log(f"rank {rank} {scene} {integrator} step {k}: {st.rays / 1e9:.3f} Grays, kernel {st.kernel_ms:.1f} ms")
         torch.cuda.synchronize(self.dev)
         self.barrier()
         elapsed = time.perf_counter() - t_start
+        my_elapsed = elapsed
+        gather_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if ev else 0.0
+        per_rank = None
         if world > 1:
             t = torch.tensor([elapsed], dtype=torch.float64, device=self.dev)
             self.all_reduce(t, op=self.dist.ReduceOp.MAX)
@@ -577,15 +632,20 @@ class Runner:
             r = torch.tensor([float(rays)], dtype=torch.float64, device=self.dev)
             self.all_reduce(r, op=self.dist.ReduceOp.SUM)
             rays = int(r.item())
+            per_rank = {"kernel_ms": [round(x, 3) for x in self.gather_ranks(np.mean(kernel_ms))],
+                        "collective_ms": [round(x, 3) for x in self.gather_ranks(gather_ms)],
+                        "elapsed_s": [round(x, 4) for x in self.gather_ranks(my_elapsed)],
+                        "rays_per_step": [int(x) for x in self.gather_ranks(last.rays)]}
         film = None
         if rank == 0:
-            film = (mlt_film if args.integrator == "pssmlt" else tgather.film).cpu().numpy()
+            film = (mlt_film if integrator == "pssmlt" else tgather.film).cpu().numpy()
         return {
             "scene": scene, "scene_name": scene_name, "kind": kind, "obj": obj, "nx": nx, "ny": ny, "spp": spp,
             "steps": steps, "warmup": warmup, "elapsed": elapsed, "rays": rays, "value": rays / elapsed / 1e6,
-            "integ": integ, "env": env, "bvh": bvh, "gpu_build_ms": gpu_build_ms,
+            "integrator": integrator, "integ": integ, "env": env, "bvh": bvh, "gpu_build_ms": gpu_build_ms,
             "setup_s": t2 - t0, "build_s": t1 - t0, "upload_s": t2 - t1,
             "avg_kernel_ms": float(np.mean(kernel_ms)), "rays_per_launch": last.rays,
+            "collective_ms": gather_ms, "per_rank": per_rank,
             "samples_per_launch": last.samples, "work_items": int(last.work_items), "scene_in_lds": last.scene_in_lds,
             "scene_bytes": last.scene_bytes,
             "launch": {"waves_cap": int(last.waves_cap), "stack": int(last.stack_entries),
@@ -598,6 +658,91 @@ class Runner:
 BVH_NAMES = {"gpu": "binned SAH (GPU, 32 bins per axis)", "ploc": "PLOC (GPU)", "lbvh": "linear BVH (GPU)",
              "sah": "binned SAH (host, 32 bins per axis)",
              "host": "create_bvh (reference topology)"}
+
+
+def parse_env(text):
+    return tuple(float(x) for x in text.split(",")) if text else None
+
+
+def count_devices_no_hip():
+    """GPUs this process may use, counted through amdsmi (torch's own amdsmi
+    count, which honours the *_VISIBLE_DEVICES variables) WITHOUT initialising
+    HIP: the parent of `bench.py --gpus N` starts N rank processes and must
+    not have touched the GPU (torch.cuda.device_count()
+    falls back to hipGetDeviceCount when amdsmi fails).  None when amdsmi
+    cannot count."""
+    import torch
+    try:
+        n = int(torch.cuda._device_count_amdsmi())
+    except Exception:           # no amdsmi, or a torch without that helper
+        return None
+    return n if n >= 0 else None
+
+
+def launch_ranks(args, argv, count=count_devices_no_hip):
+    """`bench.py --gpus N` without a launcher: check the device count with
+    amdsmi only, assert that HIP is still uninitialised, then start the N
+    ranks (spawn_ranks).  Returns the exit code (2 = refused)."""
+    n_dev = count()
+    if n_dev is None:
+        log("bench: cannot count GPUs without initialising HIP (amdsmi unavailable); "
+            "start the ranks with torchrun instead")
+        return 2
+    err = check_world(args.gpus, args.gpus, args.backend, n_dev)
+    if err:
+        log(f"bench: {err}")
+        return 2
+    import torch
+    assert not torch.cuda.is_initialized(), "HIP initialised in the launcher before the ranks start"
+    return spawn_ranks(args.gpus, argv)
+
+
+def cpu_line(cpu, threads, nproc, sample):
+    return {"value": round(cpu["mrays"], 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "host_nproc": nproc, "sample": sample}
+
+
+def path_rmse_detail(cpu, nx, ny):
+    return {"pixels": cpu["rmse_pixels"], "pixel_frac": round(cpu["rmse_pixels"] / (nx * ny), 4),
+            "diverged_pixels": cpu["diverged_pixels"], "rmse_converged": cpu["rmse_converged"],
+            "diverged_threshold": 1e-3, "extra_oracle_seconds": cpu["rmse_extra_seconds"]}
+
+
+def block_common(r, world):
+    """The fields every configuration block shares with the headline line."""
+    out = {"value": round(r["value"], 1), "unit": "Mrays/s", "n_gpus": world, "steps": r["steps"],
+           "warmup": r["warmup"], "ms_per_step": round(r["elapsed"] / r["steps"] * 1e3, 2),
+           "dtype": "f64" if r["fp64"] else "f32", "rays_per_step": int(r["rays"] // r["steps"]),
+           "bvh": BVH_NAMES[r["bvh"]], "setup_s": round(r["setup_s"], 2),
+           "collective_ms": round(r["collective_ms"], 3),
+           "image_mean": [round(float(x), 6) for x in r["film"].reshape(-1, 3).mean(0)]}
+    if r["per_rank"] is not None:
+        out["per_rank"] = r["per_rank"]
+    return out
+
+
+def first_ray_estimate(cpu_mrays):
+    """cpu_baseline / (the port's 1-thread Mrays/s on C1 over first_ray's), or None."""
+    rec = None
+    for rnd in ("r06", "r03"):
+        path = os.path.join(ROOT, "profiles", rnd, "cpu_ratio.json")
+        if os.path.exists(path):
+            with open(path) as f:
+                rec = json.load(f)
+            break
+    if not rec or not rec.get("ratio_port_over_first_ray"):
+        return None
+    ratio = rec["ratio_port_over_first_ray"]
+    return {"value": round(cpu_mrays / ratio, 3), "unit": "Mrays/s", "ratio_port_over_first_ray": ratio,
+            "oracle_mrays_1thread_median": rec.get("oracle_mrays_1thread"),
+            "basis": ("cpu_baseline / ratio; ratio = the oracle's 1-thread Mrays/s on C1 (CornellBox 256x256x16, "
+                      f"median of {len(rec.get('oracle_runs', []))} runs, {rec.get('measured', 'round 3')}) over "
+                      "first_ray's 2.14 Mrays/s (SURVEY.md section 6, the survey's probe build in the same "
+                      "container; tools/cpu_ratio.py). first_ray itself does not run here: path.cpp needs "
+                      "cpp-taskflow and GLFW, which this image lacks, and the task rules forbid building the "
+                      "reference against stand-ins; nothing of the reference travels to the GPU box. Assumes "
+                      "first_ray scales like the port; as written its shared ray counters scale negatively "
+                      "(1.25 Mrays/s on 8 threads, SURVEY section 6)")}
 
 
 def main():
@@ -623,6 +768,13 @@ def main():
                     help="auto: with the default config (cornell, path) also run cornell_1m 1080p/512spp")
     ap.add_argument("--ns-steps", type=int, default=3, help="timed frames of the north-star run")
     ap.add_argument("--ns-pixels", type=int, default=32768, help="oracle pixel sample for the north-star RMSE")
+    ap.add_argument("--configs", default="auto", choices=["auto", "on", "off"],
+                    help="auto: with the default config also run BASELINE's C3 (veach_mi 1080p 1024 spp) and C5 "
+                         "(PSS-MLT on CornellBox 1080p, 512 mutations/pixel) as blocks \"c3\" and \"c5\"")
+    ap.add_argument("--cfg-steps", type=int, default=3, help="timed frames of each configuration block")
+    ap.add_argument("--cfg-cpu-seconds", type=float, default=10.0,
+                    help="target oracle duration of each configuration block's CPU baseline / parity")
+    ap.add_argument("--c3-min-pixels", type=int, default=16384, help="oracle pixels of the C3 block's RMSE (at least)")
     ap.add_argument("--rmse-min-frac", type=float, default=0.25,
                     help="the calibrated CPU sample covers at least this fraction of the frame's pixels")
     ap.add_argument("--precision", default="auto", choices=["auto", "fp32", "fp64"],
@@ -640,43 +792,53 @@ def main():
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # no launcher: start the N ranks here, before anything touches the GPU
-        import torch
-        err = check_world(args.gpus, args.gpus, args.backend, torch.cuda.device_count())
-        if err:
-            log(f"bench: {err}")
-            sys.exit(2)
-        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+        sys.exit(launch_ranks(args, sys.argv[1:]))
 
     R = Runner(args)
     world, rank = R.world, R.rank
-    res = R.measure(args, args.scene, args.spp, args.steps, args.warmup, args.bvh)
-    do_ns = args.north_star == "on" or (args.north_star == "auto" and args.scene == "cornell"
-                                        and args.integrator == "path" and args.res == "1920x1080"
-                                        and args.spp == 512)
-    ns = R.measure(args, "cornell_1m", 512, args.ns_steps, 1, args.bvh) if do_ns else None
+    threads = args.cpu_threads or host_cpus()
+    timed_cpu = world == 1          # the CPU baseline is timed at N = 1 only; the RMSE is computed at every N
+    nproc = os.cpu_count()
+    res = R.measure(args, args.scene, args.spp, args.steps, args.warmup, args.bvh, env=parse_env(args.env))
+    mlt_cpu = None
+    if args.integrator == "pssmlt" and rank == 0 and not args.no_cpu_baseline:
+        # the path-exact parity renders shard chains on R.ctx: it runs now, while R.ctx
+        # still holds this line's scene (not after the north-star upload)
+        mlt_cpu = cpu_baseline_mlt(R.ctx, res, args.spp, args.chains, args.seed, threads, args.cpu_seconds)
+    default = (args.scene == "cornell" and args.integrator == "path" and args.res == "1920x1080"
+               and args.spp == 512)
+    do_ns = args.north_star == "on" or (args.north_star == "auto" and default)
+    ns = R.measure(args, "cornell_1m", 512, args.ns_steps, 1, args.bvh, integrator="path", precision="auto") \
+        if do_ns else None
+    do_cfg = args.configs == "on" or (args.configs == "auto" and default)
+    c3 = c5 = c5_cpu = None
+    if do_cfg:
+        # BASELINE configs[2] and [4]: the driver's default run measures them too
+        c3 = R.measure(args, "veach", 1024, args.cfg_steps, 1, args.bvh, integrator="path", precision="auto")
+        c5 = R.measure(args, "cornell", 512, args.cfg_steps, 1, args.bvh, integrator="pssmlt", precision="auto")
+        if rank == 0 and not args.no_cpu_baseline:
+            c5_cpu = cpu_baseline_mlt(R.ctx, c5, 512, args.chains, args.seed, threads, args.cfg_cpu_seconds)
 
     if rank == 0:
         nx, ny = res["nx"], res["ny"]
         key = f"{args.scene}:{nx}x{ny}"
-        threads = args.cpu_threads or host_cpus()
         cpu = None
-        timed_cpu = world == 1          # the CPU baseline is timed at N = 1 only; the RMSE is computed at every N
         if not args.no_cpu_baseline:
             if args.integrator == "pssmlt":
-                cpu = cpu_baseline_mlt(R.ctx, res["kind"], res["obj"], nx, ny, args.spp, args.chains, args.seed,
-                                       threads, args.cpu_seconds)
-                cpu["mlt_rmse"] = mlt_block_rmse(res["kind"], res["obj"], nx, ny, res["film"], threads,
-                                                 args.cpu_seconds, seed=args.seed)
-                # "RMSE vs CPU ref": the same chains on the oracle (path-exact up to
-                # fp32-diverged chains), as the full-frame estimate from one shard
-                cpu["rmse"] = cpu["parity"]["full_frame_rmse_est"]
+                cpu = mlt_cpu
+                if cpu is not None:
+                    cpu["mlt_rmse"] = mlt_block_rmse(res["kind"], res["obj"], nx, ny, res["film"], threads,
+                                                     args.cpu_seconds, seed=args.seed, env=res["env"])
+                    # "RMSE vs CPU ref": the same chains on the oracle (path-exact up to
+                    # fp32-diverged chains), as the full-frame estimate from one shard
+                    cpu["rmse"] = cpu["parity"]["full_frame_rmse_est"] if cpu["parity"] else None
             elif timed_cpu:
                 cpu = cpu_baseline(res["kind"], res["obj"], nx, ny, args.spp, args.seed, args.cpu_pixels, threads,
-                                    res["film"], args.cpu_seconds, integrator=res["integ"], env=res["env"],
-                                    min_frac=args.rmse_min_frac)
+                                   res["film"], args.cpu_seconds, integrator=res["integ"], env=res["env"],
+                                   min_frac=args.rmse_min_frac)
             else:
                 cpu = cpu_baseline(res["kind"], res["obj"], nx, ny, args.spp, args.seed, args.rmse_pixels_multi,
-                                    threads, res["film"], 0.0, integrator=res["integ"], env=res["env"])
+                                   threads, res["film"], 0.0, integrator=res["integ"], env=res["env"])
         ts = load_profile("traversal_stats.json", key)
         V, T = (cpu["V"], cpu["T"]) if cpu is not None else (ts["V"], ts["T"]) if ts is not None else (None, None)
         li_name = {"path": "path::Li", "ao": "ao::Li", "normals": "normals_renderer::Li"}.get(args.integrator)
@@ -687,7 +849,6 @@ def main():
                     "pssmlt": f"{sname} {nx}x{ny} PSS-MLT {args.spp} mutations/pixel, {args.chains} chains"
                     }[args.integrator]
         film_np = res["film"]
-        nproc = os.cpu_count()
         line = {
             "metric": METRIC, "value": round(res["value"], 1), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(res["elapsed"] / args.steps * 1e3, 2),
@@ -704,11 +865,8 @@ def main():
                 "basis": ("rmse = full_frame_rmse_est of path_exact: the GPU's and the oracle's films of the same "
                           "chain shard (the config's own chains and mutation count), sqrt(K) x the shard-film RMSE; "
                           "statistical = 8x8-block means against the oracle's path tracer (a different estimator)"),
-                "path_exact": cpu["parity"], "statistical": cpu["mlt_rmse"]} if "mlt_rmse" in cpu else {
-                "pixels": cpu["rmse_pixels"], "pixel_frac": round(cpu["rmse_pixels"] / (nx * ny), 4),
-                "diverged_pixels": cpu["diverged_pixels"],
-                "rmse_converged": cpu["rmse_converged"], "diverged_threshold": 1e-3,
-                "extra_oracle_seconds": cpu["rmse_extra_seconds"]},
+                "path_exact": cpu["parity"], "statistical": cpu["mlt_rmse"]} if "mlt_rmse" in cpu else
+            path_rmse_detail(cpu, nx, ny),
             "mutations_per_step": int(res["samples_per_launch"]) if args.integrator == "pssmlt" else None,
             "rays_per_step": int(res["rays"] // args.steps),
             "setup_s": round(res["setup_s"], 2), "host_build_s": round(res["build_s"], 2),
@@ -716,56 +874,98 @@ def main():
             "bvh": BVH_NAMES[res["bvh"]],
             "gpu_build_ms": None if res["gpu_build_ms"] is None else round(res["gpu_build_ms"], 3),
             "value_per_gpu": round(res["value"] / world, 1),
+            "collective_ms": round(res["collective_ms"], 3),
             "image_mean": [round(float(x), 6) for x in film_np.reshape(-1, 3).mean(0)],
             "roofline": roofline(args.integrator, key, world, res, V, T, R.shared_device),
-            "cpu_baseline": None if (cpu is None or not timed_cpu) else {
-                "value": round(cpu["mrays"], 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-                "host_nproc": nproc,
-                "sample": (f"{cpu['npix']} evenly spaced pixels of the same {nx}x{ny} frame at {args.spp} spp "
-                           f"({cpu['rays']} rays, {cpu['seconds']:.1f} s) on {threads} threads (every CPU this "
-                           f"process may use; the host reports {nproc}); fp64 C restatement of {li_name}. "
-                           f"first_ray itself (path.cpp + cpp-taskflow + GLFW) cannot be built here")
+            "cpu_baseline": None if (cpu is None or not timed_cpu or (args.integrator == "pssmlt"
+                                                                      and not cpu["parity"])) else cpu_line(
+                cpu, threads, nproc,
+                (f"{cpu['npix']} evenly spaced pixels of the same {nx}x{ny} frame at {args.spp} spp "
+                 f"({cpu['rays']} rays, {cpu['seconds']:.1f} s) on {threads} threads (every CPU this "
+                 f"process may use; the host reports {nproc}); fp64 C restatement of {li_name}")
                 if args.integrator != "pssmlt" else
-                          (f"PSS-MLT {cpu['sample']} on the same {nx}x{ny} frame ({cpu['rays']} rays, "
-                           f"{cpu['seconds']:.1f} s) on {threads} threads; fp64 C restatement of pssmlt.cpp")},
+                (f"PSS-MLT {cpu['sample']} on the same {nx}x{ny} frame ({cpu['rays']} rays, "
+                 f"{cpu['seconds']:.1f} s) on {threads} threads; fp64 C restatement of pssmlt.cpp")),
         }
-        ratio = load_profile(os.path.join("r03", "cpu_ratio.json"), "ratio_port_over_first_ray")
-        if line["cpu_baseline"] is not None and ratio:
-            # first_ray itself cannot be built here (cpp-taskflow, GLFW); the
-            # port's single-thread speed over first_ray's on C1 in the same container converts
-            line["cpu_baseline"]["first_ray_estimate"] = {
-                "value": round(cpu["mrays"] / ratio, 3), "unit": "Mrays/s", "ratio_port_over_first_ray": ratio,
-                "basis": ("cpu_baseline / ratio; ratio = the oracle's 1-thread Mrays/s on C1 (CornellBox "
-                          "256x256x16) over first_ray's 2.14 (SURVEY.md section 6), same container "
-                          "(profiles/r03/cpu_ratio.json, tools/cpu_ratio.py). Assumes first_ray scales like the "
-                          "port; as written its shared ray counters scale negatively (1.25 Mrays/s on 8 threads, "
-                          "SURVEY section 6)")}
+        if res["per_rank"] is not None:
+            line["per_rank"] = res["per_rank"]
+        if line["cpu_baseline"] is not None:
+            est = first_ray_estimate(cpu["mrays"])
+            if est is not None:
+                line["cpu_baseline"]["first_ray_estimate"] = est
         if ns is not None:
             nkey = f"cornell_1m:{ns['nx']}x{ns['ny']}"
             ncpu = None
-            if not args.no_cpu_baseline:      # a fixed pixel sample: RMSE at every N, no CPU timing
+            if not args.no_cpu_baseline:      # a fixed pixel sample, timed; the RMSE at every N
                 ncpu = cpu_baseline(ns["kind"], ns["obj"], ns["nx"], ns["ny"], 512, args.seed, args.ns_pixels,
-                                     threads, ns["film"], 0.0)
+                                    threads, ns["film"], 0.0)
             nts = load_profile("traversal_stats.json", nkey)
             nV, nT = ((ncpu["V"], ncpu["T"]) if ncpu is not None else (nts["V"], nts["T"]) if nts is not None
                       else (None, None))
-            line["north_star"] = {
-                "workload": f"{ns['scene_name']} {ns['nx']}x{ns['ny']} 512spp path+NEE+MIS",
-                "value": round(ns["value"], 1), "unit": "Mrays/s", "n_gpus": world,
-                "steps": ns["steps"], "warmup": ns["warmup"],
-                "ms_per_step": round(ns["elapsed"] / ns["steps"] * 1e3, 2),
+            blk = {"workload": f"{ns['scene_name']} {ns['nx']}x{ns['ny']} 512spp path+NEE+MIS"}
+            blk.update(block_common(ns, world))
+            blk.update({
                 "target": f">= {NS_TARGET_MRAYS:.0f} Mrays/s on one MI355X",
                 "target_met": bool(ns["value"] / world >= NS_TARGET_MRAYS),
-                "rays_per_step": int(ns["rays"] // ns["steps"]),
-                "bvh": BVH_NAMES[ns["bvh"]], "setup_s": round(ns["setup_s"], 2),
                 "rmse": None if ncpu is None else ncpu["rmse"],
                 "rmse_detail": None if ncpu is None else {
                     "pixels": ncpu["rmse_pixels"], "diverged_pixels": ncpu["diverged_pixels"],
                     "rmse_converged": ncpu["rmse_converged"], "diverged_threshold": 1e-3,
                     "oracle_mrays": round(ncpu["mrays"], 3), "oracle_threads": threads},
-                "image_mean": [round(float(x), 6) for x in ns["film"].reshape(-1, 3).mean(0)],
                 "roofline": roofline("path", nkey, world, ns, nV, nT, R.shared_device),
-            }
+                "cpu_baseline": None if (ncpu is None or not timed_cpu) else cpu_line(
+                    ncpu, threads, nproc,
+                    f"the RMSE sample: {ncpu['npix']} evenly spaced pixels of the same frame at 512 spp "
+                    f"({ncpu['rays']} rays, {ncpu['seconds']:.1f} s) on {threads} threads; fp64 C restatement "
+                    f"of path::Li over the reference-topology BVH")})
+            line["north_star"] = blk
+        if c3 is not None:
+            c3x, c3y = c3["nx"], c3["ny"]
+            ccpu = None
+            if not args.no_cpu_baseline:
+                min_frac = min(1.0, args.c3_min_pixels / (c3x * c3y))
+                if timed_cpu:
+                    ccpu = cpu_baseline(c3["kind"], c3["obj"], c3x, c3y, 1024, args.seed, 0, threads, c3["film"],
+                                        args.cfg_cpu_seconds, integrator=c3["integ"], min_frac=min_frac)
+                else:
+                    ccpu = cpu_baseline(c3["kind"], c3["obj"], c3x, c3y, 1024, args.seed, args.c3_min_pixels,
+                                        threads, c3["film"], 0.0, integrator=c3["integ"])
+            ckey = f"veach:{c3x}x{c3y}"
+            blk = {"workload": f"{c3['scene_name']} {c3x}x{c3y} 1024spp path+NEE+MIS (BASELINE configs[2], "
+                               f"list world, {'fp64' if c3['fp64'] else 'fp32'} kernel: precision auto)"}
+            blk.update(block_common(c3, world))
+            blk.update({
+                "rmse": None if ccpu is None else ccpu["rmse"],
+                "rmse_detail": None if ccpu is None else path_rmse_detail(ccpu, c3x, c3y),
+                "roofline": roofline("path", ckey, world, c3, None if ccpu is None else ccpu["V"],
+                                     None if ccpu is None else ccpu["T"], R.shared_device),
+                "cpu_baseline": None if (ccpu is None or not timed_cpu) else cpu_line(
+                    ccpu, threads, nproc,
+                    f"{ccpu['npix']} evenly spaced pixels of the same frame at 1024 spp ({ccpu['rays']} rays, "
+                    f"{ccpu['seconds']:.1f} s) on {threads} threads; fp64 C restatement of path::Li")})
+            line["c3"] = blk
+        if c5 is not None:
+            par = c5_cpu["parity"] if c5_cpu is not None else None
+            blk = {"workload": f"{c5['scene_name']} {c5['nx']}x{c5['ny']} PSS-MLT 512 mutations/pixel, "
+                               f"{args.chains} chains (BASELINE configs[4])"}
+            blk.update(block_common(c5, world))
+            blk.update({
+                "mutations_per_step": int(c5["samples_per_launch"]),
+                "rmse": None if not par else par["full_frame_rmse_est"],
+                "rmse_detail": None if c5_cpu is None else {
+                    "basis": ("full_frame_rmse_est: the GPU's and the oracle's films of the same chain shard (the "
+                              "config's own chains, each with the config's full mutation count), sqrt(K) x the "
+                              "shard-film RMSE; a chain is path-exact when its trajectory fingerprint equals the "
+                              "oracle's"),
+                    "path_exact": par, "note": c5_cpu.get("note")},
+                "roofline": roofline("pssmlt", f"cornell:{c5['nx']}x{c5['ny']}", world, c5,
+                                     None if not par else par["oracle_counters"]["V"],
+                                     None if not par else par["oracle_counters"]["T"], R.shared_device),
+                "cpu_baseline": None if (not par or not timed_cpu) else cpu_line(
+                    c5_cpu, threads, nproc,
+                    f"PSS-MLT {c5_cpu['sample']} ({c5_cpu['rays']} rays, {c5_cpu['seconds']:.1f} s) on "
+                    f"{threads} threads; fp64 C restatement of pssmlt.cpp")})
+            line["c5"] = blk
         if R.gloo:
             line["config"]["parallelism"] += " (gloo host-staged rehearsal)"
         if args.pfm:

@@ -886,6 +886,7 @@ struct Launcher {
     bool lds_scene = false;
     bool wide = false;      // 4-wide quantized BVH
     bool f64 = false;       // the fp64 kernel
+    size_t scene_lds = 0;   // scene bytes the plan loads into LDS (octant copies or planar tree), 0 = HBM
 };
 template <int STACK, int WORLD, bool LDS, int WAVES = 1, int MATS = kMatsNone,
           int KIND = FRT_INTEGRATOR_PATH, typename R = float>
@@ -896,6 +897,7 @@ static Launcher make_launcher(size_t scene_bytes)
     L.f64 = kIsF64<R>;
     L.lds = (WORLD != FRT_WORLD_LIST ? (size_t)STACK * kBlock * sizeof(int) : 0) +
             (size_t)kItemWords * kBlock * sizeof(int) + (LDS ? scene_bytes : 0);
+    L.scene_lds = LDS ? scene_bytes : 0;
     L.stack = STACK;
     L.waves = WAVES > 1 ? WAVES : 0;
     L.lds_scene = LDS;
@@ -2074,6 +2076,7 @@ struct TraceLauncher {
     size_t lds = 0;
     int waves = 0;
     bool lds_scene = false;
+    size_t scene_lds = 0;   // as Launcher::scene_lds
 };
 template <int STACK, int WORLD, bool LDS, int WAVES>
 static TraceLauncher make_trace(size_t scene_bytes)
@@ -2081,6 +2084,7 @@ static TraceLauncher make_trace(size_t scene_bytes)
     TraceLauncher L;
     L.fn = reinterpret_cast<const void *>(&trace_kernel<STACK, WORLD, LDS, WAVES>);
     L.lds = (WORLD != FRT_WORLD_LIST ? (size_t)STACK * kBlock * sizeof(int) : 0) + (LDS ? scene_bytes : 0);
+    L.scene_lds = LDS ? scene_bytes : 0;
     L.waves = WAVES;
     L.lds_scene = LDS;
     return L;
@@ -2165,7 +2169,7 @@ extern "C" int frt_trace_device(frt_ctx *c, const float *rays, int64_t n, float 
         st->kernel_ms = ms;
         st->scene_in_lds = L.lds_scene ? 1u : 0u;
         st->waves_cap = (uint32_t)L.waves;
-        st->scene_bytes = c->scene_lds_bytes;
+        st->scene_bytes = L.lds_scene ? L.scene_lds : c->scene_lds_bytes;   // what this plan reads
         st->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     }
     return FRT_OK;
@@ -2335,7 +2339,8 @@ static int render_mlt(frt_ctx *c, const frt_render_params *p, float *dev_film, h
         stats->scene_in_lds = lds_scene ? 1u : 0u;
         stats->stack_entries = (uint32_t)stack;
         stats->bvh_depth = (uint32_t)c->stack_needed;
-        stats->scene_bytes = c->scene_lds_bytes;
+        // the LDS copy the chain kernel loads (the octant node copies on that plan)
+        stats->scene_bytes = oct ? c->scene_lds_bytes_oct : c->scene_lds_bytes;
         stats->kernel_ms = ms;
         stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     }
@@ -2523,7 +2528,7 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
         stats->waves_cap = (uint32_t)L.waves;
         stats->stack_entries = (uint32_t)L.stack;
         stats->bvh_depth = (uint32_t)(L.wide ? c->depth4 : c->stack_needed);
-        stats->scene_bytes = c->scene_lds_bytes;
+        stats->scene_bytes = L.lds_scene ? L.scene_lds : c->scene_lds_bytes;   // what this plan reads
         stats->kernel_ms = ms;
         stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
         stats->fp64 = L.f64 ? 1u : 0u;

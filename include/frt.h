@@ -194,7 +194,10 @@ typedef struct frt_stats {
     uint32_t waves_cap;      /* register cap in waves/SIMD, 0 = compiler's own  */
     uint32_t stack_entries;  /* per-lane LDS traversal stack                    */
     uint32_t bvh_depth;      /* levels of the device BVH (after leaf collapse)  */
-    uint64_t scene_bytes;    /* nodes + triangles + shading records + materials */
+    uint64_t scene_bytes;    /* scene bytes the plan reads: its LDS copy when   */
+                             /* scene_in_lds (the octant node copies on that    */
+                             /* plan), else nodes + triangles + shading records */
+                             /* + materials in HBM                              */
     uint32_t fp64;           /* 1: the fp64 kernel ran (ABI 8)                  */
     uint32_t reserved;
 } frt_stats;

@@ -73,3 +73,40 @@ def test_bench_rank_count_mismatch_exits_nonzero():
     assert p.returncode == 2
     assert p.stdout.strip() == ""
     assert "WORLD_SIZE" in p.stderr
+
+
+def test_launch_refuses_when_amdsmi_cannot_count():
+    """the launcher counts devices through amdsmi only; when
+    amdsmi fails it refuses (exit 2) instead of falling back to a HIP call that
+    would initialise the GPU in the parent before it starts the ranks."""
+    import argparse
+    import torch
+    args = argparse.Namespace(gpus=2, backend="nccl")
+    assert bench.launch_ranks(args, [], count=lambda: None) == 2
+    assert bench.launch_ranks(args, [], count=lambda: 1) == 2           # RCCL: one device per rank
+    assert not torch.cuda.is_initialized()
+
+
+def test_count_devices_no_hip_does_not_initialise():
+    import torch
+    n = bench.count_devices_no_hip()
+    assert n is None or n >= 0
+    assert not torch.cuda.is_initialized()
+
+
+def test_mlt_parity_zero_steps_is_reported_not_raised():
+    """fewer mutations than chains leaves 0 steps per chain; the
+    parity is skipped with a note before anything touches the context."""
+    r = {"nx": 256, "ny": 256, "kind": "cornell_box_obj", "obj": "unused", "env": None}
+    out = bench.cpu_baseline_mlt(None, r, 1, 1 << 18, 0, 1, 1.0)
+    assert out["parity"] is None and "0 mutations per chain" in out["note"]
+
+
+def test_shared_device_roofline_has_no_fractions():
+    """a gloo rehearsal with ranks sharing one device reports no
+    fraction of a chip peak, VALU issue included."""
+    res = {"avg_kernel_ms": 100.0, "rays_per_launch": 10 ** 9, "scene_in_lds": False, "scene_bytes": 10 ** 8,
+           "launch": {}, "fp64": False}
+    out = bench.roofline("path", "cornell_1m:1920x1080", 2, res, 50.0, 2.0, shared_device=True)
+    for k in ("achieved", "frac", "valu_issue_frac", "lds_frac"):
+        assert out.get(k) is None, k

@@ -6,8 +6,11 @@ cpu_baseline runs) single-threaded on C1 -- CornellBox-Original 256x256 x 16
 spp, full frame, path::Li -- in this container, and relates it to SURVEY.md
 section 6's measurement of first_ray itself on the same container and config:
 2.14 Mrays/s on one thread (12.60 M rays in 5.89 s; path.cpp:4-116 driven by
-integrator.h:19-45).  Writes profiles/r03/cpu_ratio.json, which bench.py reads
-to put a "first_ray on this host" estimate beside cpu_baseline.
+integrator.h:19-45).  Writes profiles/r06/cpu_ratio.json, which bench.py reads
+to put a "first_ray on this host" estimate beside cpu_baseline.  (Round 6
+re-timed the oracle side on the current RNG; first_ray's side stays the
+survey's probe: first_ray needs cpp-taskflow and GLFW, absent from this image,
+and the task rules forbid building the reference against stand-ins.)
 
     python tools/cpu_ratio.py [--reps 5]
 """
@@ -56,8 +59,10 @@ def main():
         "ratio_port_over_first_ray": round(med / FIRST_RAY_MRAYS_1T, 3),
         "host": {"cpu": cpu, "machine": platform.machine()},
         "source": "SURVEY.md section 6 (first_ray, same container, g++ -O3 -march=native, 1 thread)",
+        "measured": time.strftime("round 6, %Y-%m-%d"),
+        "oracle_spread": [round(min(r["mrays"] for r in runs), 3), round(max(r["mrays"] for r in runs), 3)],
     }
-    dst = os.path.join(ROOT, "profiles", "r03", "cpu_ratio.json")
+    dst = os.path.join(ROOT, "profiles", "r06", "cpu_ratio.json")
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)

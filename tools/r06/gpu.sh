@@ -1,0 +1,43 @@
+# Round-6 GPU calls: one stage per gpurun call, `bash tools/r06/gpu.sh <stage>`,
+# run from the repository root on the GPU box.  Every GPU step has its own time
+# limit and the steps are chained with &&, so the first failure ends the call.
+# Outputs go to gpurun_out/r06<stage>/; the ones kept are copied to
+# profiles/r06/r06<stage>/.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
+S=$1; O=gpurun_out/r06$S; mkdir -p $O
+pt() {  # name, seconds, pytest args...
+  local n=$1 s=$2; shift 2
+  timeout -k 10 $s python -u -m pytest -x -v --timeout 600 --timeout-method thread "$@" > $O/pytest_$n.txt 2>&1
+}
+b() {  # name, seconds, bench args...
+  local n=$1 s=$2; shift 2
+  timeout -k 10 $s python -u bench.py "$@" > $O/bench_$n.json 2> $O/bench_$n.log
+}
+E=first_raytracer_amd/build/exp
+ab() {  # tag, lib ('' = in-tree), perf_ab args...
+  local t=$1 l=$2; shift 2
+  if [ -n "$l" ]; then FRT_LIB_PATH=$E/$l timeout -k 10 300 python -u tools/perf_ab.py "$@" >> $O/ab_$t.jsonl 2>> $O/ab.log
+  else timeout -k 10 300 python -u tools/perf_ab.py "$@" >> $O/ab_$t.jsonl 2>> $O/ab.log; fi
+}
+SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY"
+WT="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
+pmc() {  # name, counters, bench args...
+  local n=$1 c=$2; shift 2
+  timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $O/$n -o run -- \
+      python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --north-star off --configs off "$@" > $O/$n.json 2> $O/$n.log
+}
+C="--scene cornell --spp 512 --rounds 3 --bvh gsah --variants default"
+P="--scene cornell --spp 512 --rounds 2 --bvh gsah --integrator pssmlt --variants default"
+M="--scene cornell_1m --spp 256 --rounds 2 --bvh gsah --variants default"
+case $S in
+a)  # round-6 start: GPU suite + smoke on the build with the plan-read scene_bytes and the
+    # 44-entry 4-wide overflow stack, then the driver's default command (now with the c3 and
+    # c5 blocks) exactly as the driver runs it
+    pt gpu 900 tests -m gpu \
+     && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
+     && b default 600 --gpus 1 --steps 20 --warmup 5 ;;
+esac
+rc=$?
+echo "rc=$rc" > $O/rc.txt
+exit $rc

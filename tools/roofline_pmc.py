@@ -17,6 +17,8 @@ KEY is "<integrator>:<scene>:<nx>x<ny>" (bench.py's key).  From the LAST
                         (rcp/sqrt/rsq_f64) is weighted four; without the pass
                         valu_issue_per_ray = valu_insts_per_ray)
   l2_hit_rate         = TCC_HIT / (TCC_HIT + TCC_MISS)   (--tcc pass)
+  wait_frac           = SQ_WAIT_ANY / SQ_WAVE_CYCLES     (--wait pass: the share of
+                        wave cycles spent waiting in s_waitcnt)
 FETCH_SIZE / WRITE_SIZE are KiB; FETCH_SIZE is doubled as MI355X_MICROARCH.md
 "HBM [CDNA4]" prescribes for gfx950 (it tallies 128-B requests at 64 B).
 The rays per launch come from the bench JSON the passes printed (every pass
@@ -59,6 +61,7 @@ def main():
     ap.add_argument("--bench", required=True)
     ap.add_argument("--f64", default="")
     ap.add_argument("--tcc", default="")
+    ap.add_argument("--wait", default="")
     ap.add_argument("--copy-to", default="")
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "roofline_pmc.json"))
     a = ap.parse_args()
@@ -94,6 +97,10 @@ def main():
         _, tc, p_tc = last_megakernel(a.tcc)
         passes.append(("tcc", p_tc))
         rec.update({"TCC": tc, "l2_hit_rate": tc["TCC_HIT"] / max(1.0, tc["TCC_HIT"] + tc["TCC_MISS"])})
+    if a.wait:
+        _, wt, p_wt = last_megakernel(a.wait)
+        passes.append(("wait", p_wt))
+        rec.update({"WAIT": wt, "wait_frac": wt["SQ_WAIT_ANY"] / max(1.0, wt["SQ_WAVE_CYCLES"])})
     srcs = []
     for tag, p in passes:
         if a.copy_to:
