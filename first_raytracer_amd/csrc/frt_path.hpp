@@ -85,7 +85,10 @@ constexpr int kSentinel = 0x7fffffff;   // "stack empty"; never a node index
 constexpr int kStepBranch = 0, kStepStore = 1, kStepSelect = 2;   // bvh2_step's node-visit forms
 constexpr int kWorldBvh4 = 2;           // internal world kind: 4-wide quantized BVH
 constexpr int kWorldBvh2Oct = 4;        // internal world kind: binary nodes from LDS, one copy per ray octant
-constexpr int kBvh4Overflow = 44;       // private stack entries after the LDS ones: with the 12 LDS
+#ifndef FRT_EXP_BVH4_OVF
+#define FRT_EXP_BVH4_OVF 44             // experiment builds vary it
+#endif
+constexpr int kBvh4Overflow = FRT_EXP_BVH4_OVF;   // private stack entries after the LDS ones: with the 12 LDS
                                         // entries, 4-wide trees to depth 18 (3 pending siblings a level)
 template <int WORLD> constexpr int kOverflow = WORLD == kWorldBvh4 ? kBvh4Overflow : 1;
 

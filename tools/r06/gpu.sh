@@ -37,6 +37,17 @@ a)  # round-6 start: GPU suite + smoke on the build with the plan-read scene_byt
     pt gpu 900 tests -m gpu \
      && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
      && b default 600 --gpus 1 --steps 20 --warmup 5 ;;
+b)  # PSS-MLT round-6 changes (fingerprint in LDS, integer splat conversion, materialisation
+    # loads grouped by 4 trips): the PSS-MLT parity tests on the in-tree build, then a same-call
+    # A/B against the round-5 source (libfrt_base.so) and the group sizes 1 and 2
+    pt mlt 600 tests/test_gpu_pssmlt.py -m gpu \
+     && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_base.so $P && ab mlt libfrt_mg1.so $P && ab mlt libfrt_mg2.so $P || exit 1; done \
+     && for k in 1 2; do ab m "" $M && ab m libfrt_base.so $M || exit 1; done ;;
+c)  # stage b's variants were all ~3 % slower than round 5 (574 -> 590 ms): isolate the change.
+    # none = all three off (11 chain words, the rest as round 5); fponly / splatonly / grouponly =
+    # one change each; base = the round-5 source
+    for k in 1 2; do for v in libfrt_base.so libfrt_none.so libfrt_fponly.so libfrt_splatonly.so libfrt_grouponly.so ""; do
+        ab mlt "$v" $P || exit 1; done; done ;;
 esac
 rc=$?
 echo "rc=$rc" > $O/rc.txt
