@@ -84,33 +84,6 @@ struct PrndSource {
         return mlt_mutate(cur, r, d, s2p, logp);
     }
 };
-// A splat value x (fp32, >= 0) in the film's fixed point: round-to-nearest-
-// even of x * 2^shift, shift = kSplatFix (36), in integer operations.  It equals
-// __double2ll_rn((double)x * 2^shift) -- x * 2^shift is exact in double -- for
-// every x in [0, 2^(63 - shift)) (tests/test_mlt_splat_fix.py runs the host
-// build of this function against that expression), without the fp64 multiply
-// and conversion sequence that cost a splat ~3 x 12 fp64 issue slots.  false:
-// x is negative, NaN, or too large for a signed 64-bit pixel (the splat is
-// dropped, as before).  -0.0 gives 0.
-template <int SHIFT>
-FRT_HD bool splat_fixed(float x, unsigned long long &out)
-{
-    if (!(x >= 0.0f && x < (float)(1ull << (63 - SHIFT)))) return false;
-    const uint32_t b = (uint32_t)f2i(x) & 0x7fffffffu;
-    const uint32_t e = b >> 23;
-    const uint32_t m = (b & 0x7fffffu) | (e ? 0x800000u : 0u);
-    const int sh = (int)(e ? e : 1u) - 150 + SHIFT;      // x = m * 2^(e - 150); denormals e = 1 with no hidden bit
-    if (sh >= 0) {
-        out = (unsigned long long)m << sh;
-        return true;
-    }
-    const int s = -sh;
-    if (s >= 32) { out = 0ull; return true; }           // m < 2^24: below half a quantum
-    const uint32_t q = m >> s, rem = m & ((1u << s) - 1u), half = 1u << (s - 1);
-    out = (unsigned long long)(q + ((rem > half || (rem == half && (q & 1u))) ? 1u : 0u));
-    return true;
-}
-
 FRT_HD float f4_at(const float4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 
 struct MltPath {

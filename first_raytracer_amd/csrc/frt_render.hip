@@ -142,7 +142,13 @@ __device__ __forceinline__ void scene_to_lds(DevScene &S, int *lds_base)
 // store the far child without a branch (Cornell +0.4 %); AO and normals keep
 // the branches (their rays agree more: Store cost AO 2.4 %, normals 3 %, same
 // call, profiles/r05/r05af); PSS-MLT's chain kernel takes kStepSelect
-template <int KIND> constexpr int kPathStep = KIND == FRT_INTEGRATOR_PATH ? kStepStore : kStepBranch;
+#ifndef FRT_EXP_PATH_STEP
+#define FRT_EXP_PATH_STEP kStepStore   // experiment builds vary the path kernels' form
+#endif
+#ifndef FRT_EXP_MLT_STEP
+#define FRT_EXP_MLT_STEP kStepSelect   // ... and the chain kernel's
+#endif
+template <int KIND> constexpr int kPathStep = KIND == FRT_INTEGRATOR_PATH ? FRT_EXP_PATH_STEP : kStepBranch;
 // ------------------------------------------------------------------------
 // the persistent path megakernel
 // ------------------------------------------------------------------------
@@ -510,11 +516,9 @@ __global__ void scatter_shards(const float *__restrict__ gathered, float *__rest
 // ------------------------------------------------------------------------
 // chain state columns (ItemState over kChainWords words): step count, chain
 // index, the current state's film position, scalar contribution, pending
-// weight and colour, the trajectory fingerprint (written to the U row when the
-// chain ends: a global read-modify-write per accept put a load latency in the
-// accept phase)
-constexpr int kChainWords = 11;
-enum { kCsT, kCsC, kCsX, kCsY, kCsSc, kCsW, kCsCc, kCsFa = kCsCc + 3, kCsFs };   // kCsCc..+2: r, g, b
+// weight and colour
+constexpr int kChainWords = 9;
+enum { kCsT, kCsC, kCsX, kCsY, kCsSc, kCsW, kCsCc };   // kCsCc..+2: r, g, b
 struct MltWork {
     int nx, ny;
     uint32_t seed;
@@ -571,29 +575,11 @@ __global__ __launch_bounds__(kBlock) void mlt_bootstrap(const DevScene S0, int n
 // Inf there; none occurs in the test scenes).  mlt_film_to_float converts once
 // at the end.
 constexpr int kSplatFix = 36;
-#ifndef FRT_EXP_MLT_SPLAT_INT
-#define FRT_EXP_MLT_SPLAT_INT 1   // experiment builds: 0 = round 5's fp64 conversion
-#endif
-#ifndef FRT_EXP_MLT_FP_LDS
-#define FRT_EXP_MLT_FP_LDS 1      // experiment builds: 0 = round 5's fingerprint read-modify-write in HBM
-#endif
 __device__ __forceinline__ void mlt_splat(const MltWork &W, float x, float y, f3 c, float w)
 {
     const int pix = mlt_pixel(x, y, W.nx, W.ny);
     if (pix < 0) return;
     const float k = W.scale * w;
-    // (k * c) * 2^36 rounded to nearest even, in integer operations (splat_fixed; the
-    // values of round 5's fp64 multiply + __double2ll_rn, which cost ~36 fp64 slots a splat)
-#if FRT_EXP_MLT_SPLAT_INT
-    unsigned long long v0, v1, v2;
-    const bool ok0 = splat_fixed<kSplatFix>(k * c.x, v0), ok1 = splat_fixed<kSplatFix>(k * c.y, v1);
-    const bool ok2 = splat_fixed<kSplatFix>(k * c.z, v2);
-    if (!(ok0 && ok1 && ok2)) return;
-    unsigned long long *f = W.film + 3 * (size_t)pix;
-    atomicAdd(f + 0, v0);
-    atomicAdd(f + 1, v1);
-    atomicAdd(f + 2, v2);
-#else
     const double q = (double)(1ull << kSplatFix), lim = 9.2233720368547758e18;   // 2^63
     const double v[3] = {(double)(k * c.x) * q, (double)(k * c.y) * q, (double)(k * c.z) * q};
     if (!(v[0] >= 0.0 && v[0] < lim && v[1] >= 0.0 && v[1] < lim && v[2] >= 0.0 && v[2] < lim)) return;
@@ -601,7 +587,6 @@ __device__ __forceinline__ void mlt_splat(const MltWork &W, float x, float y, f3
     atomicAdd(f + 0, (unsigned long long)__double2ll_rn(v[0]));
     atomicAdd(f + 1, (unsigned long long)__double2ll_rn(v[1]));
     atomicAdd(f + 2, (unsigned long long)__double2ll_rn(v[2]));
-#endif
 }
 __global__ void mlt_film_to_float(const unsigned long long *__restrict__ acc, float *__restrict__ film, size_t n)
 {
@@ -659,7 +644,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
         for (;;) {
             bool ext = false;
             if (tracing) FRT_DIAG_TICK(3);
-            if (tracing && trav_step_world<WORLD, kBlock, STACK, kStepSelect>(T, S, M.P.ro, M.P.rd, M.P.shadow, stk, ovf,
+            if (tracing && trav_step_world<WORLD, kBlock, STACK, FRT_EXP_MLT_STEP>(T, S, M.P.ro, M.P.rd, M.P.shadow, stk, ovf,
                                                                  LDS_SCENE ? 0 : W.min_desc)) {   // LDS plans: compiled out
                 if (M.P.shadow) {               // finish the shadow ray here (mlt_shade's shadow branch)
                     if (!path_after_shadow<(MATS ? kMatsAll : kMatsNone)>(M.P, T.h.prim < 0)) {   // path ended (P.term)
@@ -724,16 +709,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
                 if (csc > 0.0f) cw += (1.0f - a) / (csc / W.b + kMltLargeStep);
                 if (rng_u(key, 1) <= a) {               // accept: splat the old state's weight, move
                     if (csc > 0.0f && cw != 0.0f) mlt_splat(W, cx, cy, cc, cw);
-                    // trajectory fingerprint: (accepts, sum of 1-based steps)
-#if FRT_EXP_MLT_FP_LDS
-                    C.set(kCsFa, C.get(kCsFa) + 1);
-                    C.set(kCsFs, (int)((uint32_t)C.get(kCsFs) + t + 1u));
-#else
                     uint2 *fp = reinterpret_cast<uint2 *>(W.U + (size_t)j * kMltRow + kMltFp);
-                    uint2 f = *fp;
+                    uint2 f = *fp;                      // trajectory fingerprint: (accepts, sum of 1-based steps)
                     f.x += 1u; f.y += t + 1u;
                     *fp = f;
-#endif
                     cw = 0.0f;
                     mat = true; mat_fresh = large;
                     cx = M.x; cy = M.y; cc = L; csc = sc;
@@ -744,10 +723,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
             }
             if ((uint64_t)t >= W.steps) {               // chain finished
                 if (csc > 0.0f && cw != 0.0f) mlt_splat(W, cx, cy, cc, cw);
-#if FRT_EXP_MLT_FP_LDS
-                *reinterpret_cast<uint2 *>(W.U + (size_t)j * kMltRow + kMltFp) =
-                    make_uint2((uint32_t)C.get(kCsFa), (uint32_t)C.get(kCsFs));
-#endif
                 have = false;
             } else {
                 setup_next = true;
@@ -775,39 +750,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
             const uint32_t rk0 = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)mat_key.k0);
             const uint32_t rk1 = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)mat_key.k1);
             const uint32_t total = n * (uint32_t)kMltDims;
-            // kMatGroup trips at a time: their current values are loaded together before any
-            // of them is mutated and stored (one trip per loop iteration put one HBM round trip
-            // behind each 64 elements: the compiler cannot move a load above the previous
-            // trip's store; the elements are distinct, so the reordering is safe)
-#ifndef FRT_EXP_MAT_GROUP
-#define FRT_EXP_MAT_GROUP 4   // experiment builds vary it
-#endif
-            constexpr int kMatGroup = FRT_EXP_MAT_GROUP;
-            for (uint32_t e0 = 0; e0 < total; e0 += 64u * kMatGroup) {
-                float cur[kMatGroup];
-                uint32_t jl[kMatGroup], k0[kMatGroup], k1[kMatGroup];
-                int dd[kMatGroup];
-#pragma unroll
-                for (int g = 0; g < kMatGroup; ++g) {
-                    const uint32_t e = e0 + 64u * (uint32_t)g + (uint32_t)lane;
-                    const uint32_t r = min(e / (uint32_t)kMltDims, n - 1u);
-                    jl[g] = (uint32_t)__shfl((int)rj, (int)r);   // every lane active: sources are lanes < n
-                    k0[g] = (uint32_t)__shfl((int)rk0, (int)r);
-                    k1[g] = (uint32_t)__shfl((int)rk1, (int)r);
-                    dd[g] = (int)(e - r * (uint32_t)kMltDims);
-                    cur[g] = 0.0f;
-                    if (e < total && !(jl[g] >> 31))            // j < 2^31: bit 31 = fresh (no read)
-                        cur[g] = W.U[(size_t)(jl[g] & 0x7fffffffu) * kMltRow + dd[g]];
-                }
-#pragma unroll
-                for (int g = 0; g < kMatGroup; ++g) {
-                    const uint32_t e = e0 + 64u * (uint32_t)g + (uint32_t)lane;
-                    if (e < total) {
-                        const RngKey kl{k0[g], k1[g]};
-                        const float u = rng_u(kl, 2u + (uint32_t)dd[g]);
-                        W.U[(size_t)(jl[g] & 0x7fffffffu) * kMltRow + dd[g]] =
-                            (jl[g] >> 31) ? u : mlt_mutate(cur[g], u, dd[g], W.s2p, W.logp);
-                    }
+            for (uint32_t e0 = 0; e0 < total; e0 += 64) {
+                const uint32_t e = e0 + (uint32_t)lane;
+                const uint32_t r = min(e / (uint32_t)kMltDims, n - 1u);
+                const uint32_t jl = (uint32_t)__shfl((int)rj, (int)r);   // every lane active: sources are lanes < n
+                const RngKey kl{(uint32_t)__shfl((int)rk0, (int)r), (uint32_t)__shfl((int)rk1, (int)r)};
+                if (e < total) {
+                    const int d = (int)(e - r * (uint32_t)kMltDims);
+                    float *row = W.U + (size_t)(jl & 0x7fffffffu) * kMltRow;   // j < 2^31: bit 31 = fresh
+                    const float u = rng_u(kl, 2u + (uint32_t)d);
+                    row[d] = (jl >> 31) ? u : mlt_mutate(row[d], u, d, W.s2p, W.logp);
                 }
             }
         }
@@ -836,12 +788,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FRT_EXP_
                     have = true;
                     init = true;
                     j = w;
-#if FRT_EXP_MLT_FP_LDS
-                    C.set(kCsFa, 0);
-                    C.set(kCsFs, 0);
-#else
                     *reinterpret_cast<uint2 *>(W.U + (size_t)w * kMltRow + kMltFp) = make_uint2(0u, 0u);
-#endif
                     const uint32_t c = (uint32_t)W.shard_index + w * (uint32_t)W.shard_count;
                     C.set(kCsC, (int)c);
                     C.set(kCsT, 0);

@@ -48,6 +48,40 @@ c)  # stage b's variants were all ~3 % slower than round 5 (574 -> 590 ms): isol
     # one change each; base = the round-5 source
     for k in 1 2; do for v in libfrt_base.so libfrt_none.so libfrt_fponly.so libfrt_splatonly.so libfrt_grouponly.so ""; do
         ab mlt "$v" $P || exit 1; done; done ;;
+d)  # the N-rank path of the default command (C2 + north star + C3 + C5 blocks) rehearsed with two
+    # ranks sharing the box's one GPU (gloo, host-staged collectives): the driver's SCALE run executes
+    # this command at N = 2, 4, 8 with RCCL
+    b gloo2 600 --gpus 2 --backend gloo --steps 2 --warmup 1 ;;
+e)  # the final build's evidence: the default command under rocprofv3 kernel-trace + stats, then per
+    # config the PMC passes tools/roofline_pmc.py reads (sq, fetch, write, wait; C4 + tcc, C3 + f64),
+    # one counter group per run, and the per-ray table written under gpurun_out
+    F64="SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64"
+    rp() {  # key, extra roofline_pmc args, bench args... (passes named <tag>_<group>)
+      local key=$1 tag=$2 extra=$3; shift 3
+      python tools/roofline_pmc.py $key --sq $O/${tag}_sq --fetch $O/${tag}_fetch --write $O/${tag}_write \
+          --wait $O/${tag}_wait $extra --bench $O/${tag}_sq.json --copy-to $O/pmc --out $O/roofline_pmc.json >> $O/roofline.log 2>&1
+    }
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_default -o run -- \
+        python3 bench.py --steps 5 --warmup 1 > $O/trace_default.json 2> $O/trace_default.log \
+     && cp profiles/roofline_pmc.json $O/roofline_pmc.json \
+     && pmc c2_sq "$SQ" && pmc c2_fetch FETCH_SIZE && pmc c2_write WRITE_SIZE && pmc c2_wait "$WT" \
+     && rp path:cornell:1920x1080 c2 "" \
+     && pmc c4_sq "$SQ" --scene cornell_1m && pmc c4_fetch FETCH_SIZE --scene cornell_1m \
+     && pmc c4_write WRITE_SIZE --scene cornell_1m && pmc c4_wait "$WT" --scene cornell_1m \
+     && pmc c4_tcc "TCC_HIT TCC_MISS" --scene cornell_1m \
+     && rp path:cornell_1m:1920x1080 c4 "--tcc $O/c4_tcc" \
+     && pmc c3_sq "$SQ" --scene veach --spp 1024 && pmc c3_fetch FETCH_SIZE --scene veach --spp 1024 \
+     && pmc c3_write WRITE_SIZE --scene veach --spp 1024 && pmc c3_wait "$WT" --scene veach --spp 1024 \
+     && pmc c3_f64 "$F64" --scene veach --spp 1024 \
+     && rp path:veach:1920x1080:fp64 c3 "--f64 $O/c3_f64" \
+     && pmc c5_sq "$SQ" --integrator pssmlt && pmc c5_fetch FETCH_SIZE --integrator pssmlt \
+     && pmc c5_write WRITE_SIZE --integrator pssmlt && pmc c5_wait "$WT" --integrator pssmlt \
+     && rp pssmlt:cornell:1920x1080 c5 "" ;;
+f)  # the node loop under a wave-uniform trip count (kStepUniform, libfrt_uni.so: path and chain
+    # kernels) against the in-tree forms (Store / Select), then stage d's two-rank rehearsal
+    for k in 1 2; do ab c "" $C && ab c libfrt_uni.so $C || exit 1; done \
+     && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_uni.so $P || exit 1; done \
+     && b gloo2 600 --gpus 2 --backend gloo --steps 2 --warmup 1 ;;
 esac
 rc=$?
 echo "rc=$rc" > $O/rc.txt
