@@ -946,6 +946,24 @@ static Launcher bvh_launcher(int waves, size_t sb)
 // no spills since the SLP vectorizer is off): cornell_1m 360.3 -> 344.3 ms
 // (+4.6 %, same call, profiles/r05/r05i/ab_m.jsonl)
 constexpr int kBvh4LdsStack = FRT_EXP_BVH4_LSTACK;
+// The third unit (frt_render_lds.hip): the lambertian kernels of the octant LDS
+// plan -- the path kernels (C2) and the PSS-MLT chain kernels (C5) -- compiled
+// with the machine scheduler's max-memory-clause strategy (Makefile LDSFLAGS).
+// Whole-library A/B (same call, profiles/r05/r05i): Cornell 229.9 / 230.2 ->
+// 227.1 / 227.1 ms, PSS-MLT 599.7 / 601.3 -> 596.9 / 597.7 ms, while the
+// 4-wide HBM kernel (cornell_1m) lost 1.6 % under it; one unit per strategy
+// takes both.  Diagnostic builds (FRT_DIAG: their counters are a device global
+// of the main unit) keep these kernels in the main unit.
+#if (defined(FRT_DIAG) && !defined(FRT_TU_LDS)) || defined(FRT_EXP_NO_LDS_SPLIT)   // (A/B builds: no split)
+constexpr bool kSplitLds = false;
+#else
+constexpr bool kSplitLds = true;
+#endif
+namespace frt_lds {
+int path_oct(int stack, int waves, size_t scene_bytes, Launcher &L);
+int mlt_oct(int stack, const void **boot, const void **chains);
+}  // namespace frt_lds
+
 // MATS: the material set the kernel is compiled for (kMats* mask, frt_path.hpp)
 template <int MATS>
 static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
@@ -990,9 +1008,13 @@ static int pick_launcher_t(const frt_ctx *c, int flags, Launcher &L)
     // LDS-resident binary tree: the per-octant node copies when they fit
     const bool oct = lds && !(flags & FRT_FLAG_NO_OCT) && c->scene_lds_bytes_oct <= kLdsOctBytes;
     if (oct) {
-        L = d < 8 ? bvh_launcher<8, true, kWorldBvh2Oct, MATS>(waves, c->scene_lds_bytes_oct)
-                  : bvh_launcher<16, true, kWorldBvh2Oct, MATS>(waves, c->scene_lds_bytes_oct);
-        return FRT_OK;
+        if constexpr (MATS == kMatsNone && kSplitLds) {   // the third unit's kernels (frt_lds)
+            return frt_lds::path_oct(d < 8 ? 8 : 16, waves, c->scene_lds_bytes_oct, L);
+        } else {
+            L = d < 8 ? bvh_launcher<8, true, kWorldBvh2Oct, MATS>(waves, c->scene_lds_bytes_oct)
+                      : bvh_launcher<16, true, kWorldBvh2Oct, MATS>(waves, c->scene_lds_bytes_oct);
+            return FRT_OK;
+        }
     }
     if (d < 8) L = lds ? bvh_launcher<8, true, FRT_WORLD_BVH, MATS>(waves, sb)
                        : bvh_launcher<8, false, FRT_WORLD_BVH, MATS>(waves, 0);
@@ -1070,7 +1092,22 @@ int pick(const frt_ctx *c, int integrator, int flags, bool f64, Launcher &L);
 int mlt(int stack, int world, bool lds, const void **boot, const void **chains);
 }  // namespace frt_mats
 
-#ifdef FRT_TU_MATS
+#if defined(FRT_TU_LDS)
+int frt_lds::path_oct(int stack, int waves, size_t scene_bytes, Launcher &L)
+{
+    if (stack == 8) L = bvh_launcher<8, true, kWorldBvh2Oct, kMatsNone>(waves, scene_bytes);
+    else if (stack == 16) L = bvh_launcher<16, true, kWorldBvh2Oct, kMatsNone>(waves, scene_bytes);
+    else return FRT_E_UNSUPPORTED;
+    return FRT_OK;
+}
+int frt_lds::mlt_oct(int stack, const void **boot, const void **chains)
+{
+    if (stack == 8) mlt_kernels_t<8, kWorldBvh2Oct, true, false>(boot, chains);
+    else if (stack == 16) mlt_kernels_t<16, kWorldBvh2Oct, true, false>(boot, chains);
+    else return FRT_E_UNSUPPORTED;
+    return FRT_OK;
+}
+#elif defined(FRT_TU_MATS)
 int frt_mats::pick(const frt_ctx *c, int integrator, int flags, bool f64, Launcher &L)
 {
     if (integrator == FRT_INTEGRATOR_AO) return pick_launcher_kind<FRT_INTEGRATOR_AO>(c, flags, L);
@@ -2187,6 +2224,7 @@ template <int STACK, int WORLD, bool LDS = false>
 static void mlt_kernels(bool mats, const void **boot, const void **chains)
 {
     if (mats) frt_mats::mlt(STACK, WORLD, LDS, boot, chains);
+    else if constexpr (WORLD == kWorldBvh2Oct && kSplitLds) frt_lds::mlt_oct(STACK, boot, chains);
     else mlt_kernels_t<STACK, WORLD, LDS, false>(boot, chains);
 }
 
@@ -2743,4 +2781,4 @@ extern "C" int frt_render_multi(frt_ctx **ctxs, int n, const frt_render_params *
     return FRT_OK;
 }
 
-#endif  // FRT_TU_MATS
+#endif  // FRT_TU_LDS / FRT_TU_MATS / main unit

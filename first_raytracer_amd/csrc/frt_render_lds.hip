@@ -1,0 +1,11 @@
+// The library's third translation unit: the lambertian kernels of the octant
+// LDS plan (path and PSS-MLT chains), reached through frt_lds::path_oct /
+// frt_lds::mlt_oct (frt_render.hip "launch plans").  Built with the machine
+// scheduler's max-memory-clause strategy (Makefile, LDSFLAGS); see the comment
+// at kSplitLds.
+#define FRT_TU_LDS 1
+#undef FRT_DIAG
+#ifndef FRT_RENDER_SRC
+#define FRT_RENDER_SRC "frt_render.hip"
+#endif
+#include FRT_RENDER_SRC

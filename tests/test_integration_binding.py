@@ -98,7 +98,6 @@ def frt_header():
             decl = re.sub(r"\[[^\]]*\]", "", decl).strip()
             if not decl:
                 continue
-            head, _, rest = decl.partition(" ")
             for f in re.split(r"\s*,\s*", decl):
                 w = re.findall(r"\w+", f)
                 if w:

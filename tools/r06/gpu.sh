@@ -79,8 +79,12 @@ e)  # the final build's evidence: the default command under rocprofv3 kernel-tra
      && rp pssmlt:cornell:1920x1080 c5 "" ;;
 f)  # the node loop under a wave-uniform trip count (kStepUniform, libfrt_uni.so: path and chain
     # kernels) against the in-tree forms (Store / Select), then stage d's two-rank rehearsal
-    for k in 1 2; do ab c "" $C && ab c libfrt_uni.so $C || exit 1; done \
-     && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_uni.so $P || exit 1; done \
+    # (round 6 later: in-tree = the octant LDS plan's lambertian kernels in their own unit under the
+    # max-memory-clause scheduler; libfrt_nosplit.so = the same source with them in the main unit;
+    # libfrt_uni.so = the wave-uniform node loop, built before the split)
+    pt benchline 600 tests/test_gpu_bench_line.py -m gpu \
+     && for k in 1 2; do ab c "" $C && ab c libfrt_nosplit.so $C && ab c libfrt_uni.so $C || exit 1; done \
+     && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_nosplit.so $P && ab mlt libfrt_uni.so $P || exit 1; done \
      && b gloo2 600 --gpus 2 --backend gloo --steps 2 --warmup 1 ;;
 esac
 rc=$?
