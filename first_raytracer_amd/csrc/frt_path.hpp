@@ -83,7 +83,6 @@ __device__ __forceinline__ unsigned long long *diag_slot()
 
 constexpr int kSentinel = 0x7fffffff;   // "stack empty"; never a node index
 constexpr int kStepBranch = 0, kStepStore = 1, kStepSelect = 2;   // bvh2_step's node-visit forms
-constexpr int kStepUniform = 3;         // experiment: kStepSelect's body under a wave-uniform loop
 constexpr int kWorldBvh4 = 2;           // internal world kind: 4-wide quantized BVH
 constexpr int kWorldBvh2Oct = 4;        // internal world kind: binary nodes from LDS, one copy per ray octant
 #ifndef FRT_EXP_BVH4_OVF
@@ -345,35 +344,6 @@ FRT_HD bool bvh2_step(Trav<R> &T, const DevScene &S, V3<R> o, V3<R> d, bool anyh
     // tests a leaf until the lane's query is done -- was 60 % slower on Cornell
     // and 50 % on PSS-MLT than this descend-then-test step: profiles/r05/r05d)
     const R tmin = T.tmin, tbest = OCT ? vmin(T.h.t, Cst<R>::tmax) : T.h.t;
-    if constexpr (OCT && STEP == kStepUniform) {
-        // kStepSelect's visit under a wave-uniform loop: the wave runs while any lane
-        // descends, the others compute on node 0 and keep their state (selects), so the
-        // loop costs one ballot a trip instead of the per-lane exit mask bookkeeping.
-        // The store above the top is harmless for a lane that does not descend (the slot
-        // is outside its stack, d < STACK).
-        for (;;) {
-            const bool desc = (unsigned)node < (unsigned)kSentinel;
-            if (!wave_any(desc)) break;
-            FRT_DIAG_TICK(2);
-            const int nd = desc ? node : 0;
-            const float4 *rec = Sn.nodes + u24mul(nd, 3);
-            const float4 n0 = rec[0], n1 = rec[1], n2 = rec[2];
-            const int2 cr = S.node_refs[nd];
-            R t0, t1, f0, f1;
-            slab_nf<R>(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, T.sr, tmin, tbest, t0, f0);
-            slab_nf<R>(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, T.sr, tmin, tbest, t1, f1);
-            const bool h0 = t0 <= f0, h1 = t1 <= f1;
-            const bool first0 = h0 && (!h1 || t0 <= t1);
-            const int nr = first0 ? cr.x : cr.y, fr = first0 ? cr.y : cr.x;
-            const int below = stk[(sp > 0 ? sp - 1 : 0) * STRIDE];
-            stk[sp * STRIDE] = fr;
-            const bool both = h0 && h1, any = h0 || h1;
-            const int nnode = any ? nr : (sp > 0 ? below : kSentinel);
-            const int nsp = sp + (both ? 1 : (!any && sp > 0 ? -1 : 0));
-            node = desc ? nnode : node;
-            sp = desc ? nsp : sp;
-        }
-    } else
     while ((unsigned)node < (unsigned)kSentinel) {   // interior node
         FRT_DIAG_TICK(2);
         R t0, t1;
