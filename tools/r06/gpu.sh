@@ -86,6 +86,11 @@ f)  # the node loop under a wave-uniform trip count (kStepUniform, libfrt_uni.so
      && for k in 1 2; do ab c "" $C && ab c libfrt_nosplit.so $C && ab c libfrt_uni.so $C || exit 1; done \
      && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_nosplit.so $P && ab mlt libfrt_uni.so $P || exit 1; done \
      && b gloo2 600 --gpus 2 --backend gloo --steps 2 --warmup 1 ;;
+h)  # the machine scheduler's iterative strategies: for the octant unit (ldsit*: C2, C5) and, through
+    # DEFS on every unit, for cornell_1m's 4-wide kernel in the main unit (allit*)
+    for k in 1 2; do ab c "" $C && ab c libfrt_ldsitilp.so $C && ab c libfrt_ldsitmaxocc.so $C || exit 1; done \
+     && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_ldsitilp.so $P && ab mlt libfrt_ldsitmaxocc.so $P || exit 1; done \
+     && for k in 1 2; do ab m "" $M && ab m libfrt_allitilp.so $M && ab m libfrt_allitmaxocc.so $M && ab m libfrt_allitminreg.so $M || exit 1; done ;;
 esac
 rc=$?
 echo "rc=$rc" > $O/rc.txt
