@@ -160,8 +160,16 @@ template <int KIND> constexpr int kPathStep = KIND == FRT_INTEGRATOR_PATH ? FRT_
 // A/B +4.5 % / +1 %).
 // (9 words -- the pixel index derived -- fit a 6th octant block per CU: 229.4 vs 229.1 ms at a
 // 6-wave cap, 230.5 vs 230.2 at 5, profiles/r05/r05l; not kept)
+#ifndef FRT_EXP_ITEM7
+#define FRT_EXP_ITEM7 0   // experiment builds: 7-word items (end and pixel coordinates derived)
+#endif
+#if FRT_EXP_ITEM7
+constexpr int kItemWords = 7;
+enum { kIsCur, kIsSlot, kIsChunk, kIsPix, kIsAcc };   // kIsAcc..+2: r, g, b
+#else
 constexpr int kItemWords = 10;
 enum { kIsCur, kIsEnd, kIsSlot, kIsChunk, kIsPix, kIsPx, kIsPy, kIsAcc };   // kIsAcc..+2: r, g, b
+#endif
 struct ItemState {
     int *b;      // the lane's column
     __device__ int get(int k) const { return b[k * kBlock]; }
@@ -273,7 +281,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         const unsigned long long diag_t2 = FRT_DIAG_CLOCK();
         FRT_DIAG_CYC(17, diag_t2 - diag_t1);
         // ---- retire a finished item: its chunk sum goes to its own slot ----
-        if (!active && have_item && I.get(kIsCur) >= I.get(kIsEnd)) {
+#if FRT_EXP_ITEM7
+        auto item_end = [&]() { return min(W.spp, (I.get(kIsChunk) + 1) * W.spi); };
+#else
+        auto item_end = [&]() { return I.get(kIsEnd); };
+#endif
+        if (!active && have_item && I.get(kIsCur) >= item_end()) {
             float *dst = W.partial + 3ull * ((size_t)(uint32_t)I.get(kIsChunk) * W.n_slots + (uint32_t)I.get(kIsSlot));
             dst[0] = i2f(I.get(kIsAcc + 0)); dst[1] = i2f(I.get(kIsAcc + 1)); dst[2] = i2f(I.get(kIsAcc + 2));
             have_item = false;
@@ -322,23 +335,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
                         have_item = true;
                         const int s_cur = (int)chunk * W.spi;
                         I.set(kIsCur, s_cur);
-                        I.set(kIsEnd, min(W.spp, s_cur + W.spi));
                         I.set(kIsSlot, (int)(t_ord * (uint32_t)T2 + s));
                         I.set(kIsChunk, (int)chunk);
                         I.set(kIsPix, py * W.nx + px);
+#if !FRT_EXP_ITEM7
+                        I.set(kIsEnd, min(W.spp, s_cur + W.spi));
                         I.set(kIsPx, px);
                         I.set(kIsPy, py);
+#endif
                         I.set(kIsAcc + 0, 0); I.set(kIsAcc + 1, 0); I.set(kIsAcc + 2, 0);
                     }
                 }
             }
         }
         // ---- next camera sample of the item ----
-        const bool start = !active && have_item && I.get(kIsCur) < I.get(kIsEnd);
+        const bool start = !active && have_item && I.get(kIsCur) < item_end();
         if (start) {
             const int s_cur = I.get(kIsCur);
-            path_begin(P, S, I.get(kIsPx), I.get(kIsPy), W.nx, W.ny, W.seed, (uint32_t)I.get(kIsPix),
-                       (uint32_t)s_cur + W.s_off);
+#if FRT_EXP_ITEM7
+            const int pix = I.get(kIsPix), py = (int)((uint32_t)pix / (uint32_t)W.nx), px = pix - py * W.nx;
+#else
+            const int pix = I.get(kIsPix), px = I.get(kIsPx), py = I.get(kIsPy);
+#endif
+            path_begin(P, S, px, py, W.nx, W.ny, W.seed, (uint32_t)pix, (uint32_t)s_cur + W.s_off);
             I.set(kIsCur, s_cur + 1);
             active = true;
             next_ray = true;
@@ -946,15 +965,18 @@ static Launcher bvh_launcher(int waves, size_t sb)
 // no spills since the SLP vectorizer is off): cornell_1m 360.3 -> 344.3 ms
 // (+4.6 %, same call, profiles/r05/r05i/ab_m.jsonl)
 constexpr int kBvh4LdsStack = FRT_EXP_BVH4_LSTACK;
-// The third unit (frt_render_lds.hip): the lambertian kernels of the octant LDS
-// plan -- the path kernels (C2) and the PSS-MLT chain kernels (C5) -- compiled
-// with the machine scheduler's max-memory-clause strategy (Makefile LDSFLAGS).
-// Whole-library A/B (same call, profiles/r05/r05i): Cornell 229.9 / 230.2 ->
-// 227.1 / 227.1 ms, PSS-MLT 599.7 / 601.3 -> 596.9 / 597.7 ms, while the
-// 4-wide HBM kernel (cornell_1m) lost 1.6 % under it; one unit per strategy
-// takes both.  Diagnostic builds (FRT_DIAG: their counters are a device global
-// of the main unit) keep these kernels in the main unit.
-#if (defined(FRT_DIAG) && !defined(FRT_TU_LDS)) || defined(FRT_EXP_NO_LDS_SPLIT)   // (A/B builds: no split)
+// Two more units for the lambertian kernels of the octant LDS plan, each under
+// the machine scheduling strategy that measured fastest for it (same call, two
+// alternations): frt_render_lds.hip holds the path kernels (C2) under
+// max-memory-clause (Makefile LDSFLAGS; Cornell 229.4 / 229.7 -> 227.5 / 227.5
+// ms, profiles/r06/r06f), frt_render_chain.hip the PSS-MLT chain kernels (C5)
+// under iterative-maxocc (CHAINFLAGS; 576.8 / 576.1 -> 570.6 / 571.6 ms against
+// max-memory-clause, profiles/r06/r06h).  The 4-wide HBM kernel (cornell_1m)
+// loses under every other strategy (max-memory-clause 1.6 %, iterative ones
+// 9-26 %), so it stays in the main unit on the default one.  Diagnostic builds
+// (FRT_DIAG: their counters are a device global of the main unit) keep these
+// kernels in the main unit.
+#if (defined(FRT_DIAG) && !defined(FRT_TU_LDS) && !defined(FRT_TU_CHAIN)) || defined(FRT_EXP_NO_LDS_SPLIT)
 constexpr bool kSplitLds = false;
 #else
 constexpr bool kSplitLds = true;
@@ -1100,6 +1122,7 @@ int frt_lds::path_oct(int stack, int waves, size_t scene_bytes, Launcher &L)
     else return FRT_E_UNSUPPORTED;
     return FRT_OK;
 }
+#elif defined(FRT_TU_CHAIN)
 int frt_lds::mlt_oct(int stack, const void **boot, const void **chains)
 {
     if (stack == 8) mlt_kernels_t<8, kWorldBvh2Oct, true, false>(boot, chains);
@@ -2781,4 +2804,4 @@ extern "C" int frt_render_multi(frt_ctx **ctxs, int n, const frt_render_params *
     return FRT_OK;
 }
 
-#endif  // FRT_TU_LDS / FRT_TU_MATS / main unit
+#endif  // FRT_TU_LDS / FRT_TU_CHAIN / FRT_TU_MATS / main unit

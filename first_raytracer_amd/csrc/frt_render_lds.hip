@@ -1,6 +1,6 @@
-// The library's third translation unit: the lambertian kernels of the octant
-// LDS plan (path and PSS-MLT chains), reached through frt_lds::path_oct /
-// frt_lds::mlt_oct (frt_render.hip "launch plans").  Built with the machine
+// The library's third translation unit: the lambertian path kernels of the
+// octant LDS plan (C2), reached through frt_lds::path_oct (frt_render.hip
+// "launch plans").  Built with the machine
 // scheduler's max-memory-clause strategy (Makefile, LDSFLAGS); see the comment
 // at kSplitLds.
 #define FRT_TU_LDS 1

@@ -91,6 +91,12 @@ h)  # the machine scheduler's iterative strategies: for the octant unit (ldsit*:
     for k in 1 2; do ab c "" $C && ab c libfrt_ldsitilp.so $C && ab c libfrt_ldsitmaxocc.so $C || exit 1; done \
      && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_ldsitilp.so $P && ab mlt libfrt_ldsitmaxocc.so $P || exit 1; done \
      && for k in 1 2; do ab m "" $M && ab m libfrt_allitilp.so $M && ab m libfrt_allitmaxocc.so $M && ab m libfrt_allitminreg.so $M || exit 1; done ;;
+i)  # 7-word work items (end and pixel coordinates derived; libfrt_item7) and with them a 15-entry
+    # LDS stack for the 4-wide plan (22 KiB a block, still 7 to a CU; libfrt_item7ls15), against the
+    # in-tree build (10-word items, 12 entries; PSS-MLT chains now in their own iterative-maxocc unit)
+    for k in 1 2; do ab m "" $M && ab m libfrt_item7.so $M && ab m libfrt_item7ls15.so $M || exit 1; done \
+     && for k in 1 2; do ab c "" $C && ab c libfrt_item7.so $C || exit 1; done \
+     && for k in 1 2; do ab mlt "" $P || exit 1; done ;;
 esac
 rc=$?
 echo "rc=$rc" > $O/rc.txt
