@@ -160,16 +160,10 @@ template <int KIND> constexpr int kPathStep = KIND == FRT_INTEGRATOR_PATH ? FRT_
 // A/B +4.5 % / +1 %).
 // (9 words -- the pixel index derived -- fit a 6th octant block per CU: 229.4 vs 229.1 ms at a
 // 6-wave cap, 230.5 vs 230.2 at 5, profiles/r05/r05l; not kept)
-#ifndef FRT_EXP_ITEM7
-#define FRT_EXP_ITEM7 0   // experiment builds: 7-word items (end and pixel coordinates derived)
-#endif
-#if FRT_EXP_ITEM7
-constexpr int kItemWords = 7;
-enum { kIsCur, kIsSlot, kIsChunk, kIsPix, kIsAcc };   // kIsAcc..+2: r, g, b
-#else
+// (7 words -- the end and the pixel coordinates derived -- measured 1 % slower on Cornell and
+// +-0 on cornell_1m, also with the 4-wide plan's LDS stack grown to 15 entries: profiles/r06/r06i)
 constexpr int kItemWords = 10;
 enum { kIsCur, kIsEnd, kIsSlot, kIsChunk, kIsPix, kIsPx, kIsPy, kIsAcc };   // kIsAcc..+2: r, g, b
-#endif
 struct ItemState {
     int *b;      // the lane's column
     __device__ int get(int k) const { return b[k * kBlock]; }
@@ -281,12 +275,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
         const unsigned long long diag_t2 = FRT_DIAG_CLOCK();
         FRT_DIAG_CYC(17, diag_t2 - diag_t1);
         // ---- retire a finished item: its chunk sum goes to its own slot ----
-#if FRT_EXP_ITEM7
-        auto item_end = [&]() { return min(W.spp, (I.get(kIsChunk) + 1) * W.spi); };
-#else
-        auto item_end = [&]() { return I.get(kIsEnd); };
-#endif
-        if (!active && have_item && I.get(kIsCur) >= item_end()) {
+        if (!active && have_item && I.get(kIsCur) >= I.get(kIsEnd)) {
             float *dst = W.partial + 3ull * ((size_t)(uint32_t)I.get(kIsChunk) * W.n_slots + (uint32_t)I.get(kIsSlot));
             dst[0] = i2f(I.get(kIsAcc + 0)); dst[1] = i2f(I.get(kIsAcc + 1)); dst[2] = i2f(I.get(kIsAcc + 2));
             have_item = false;
@@ -338,26 +327,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES)))
                         I.set(kIsSlot, (int)(t_ord * (uint32_t)T2 + s));
                         I.set(kIsChunk, (int)chunk);
                         I.set(kIsPix, py * W.nx + px);
-#if !FRT_EXP_ITEM7
                         I.set(kIsEnd, min(W.spp, s_cur + W.spi));
                         I.set(kIsPx, px);
                         I.set(kIsPy, py);
-#endif
                         I.set(kIsAcc + 0, 0); I.set(kIsAcc + 1, 0); I.set(kIsAcc + 2, 0);
                     }
                 }
             }
         }
         // ---- next camera sample of the item ----
-        const bool start = !active && have_item && I.get(kIsCur) < item_end();
+        const bool start = !active && have_item && I.get(kIsCur) < I.get(kIsEnd);
         if (start) {
             const int s_cur = I.get(kIsCur);
-#if FRT_EXP_ITEM7
-            const int pix = I.get(kIsPix), py = (int)((uint32_t)pix / (uint32_t)W.nx), px = pix - py * W.nx;
-#else
-            const int pix = I.get(kIsPix), px = I.get(kIsPx), py = I.get(kIsPy);
-#endif
-            path_begin(P, S, px, py, W.nx, W.ny, W.seed, (uint32_t)pix, (uint32_t)s_cur + W.s_off);
+            path_begin(P, S, I.get(kIsPx), I.get(kIsPy), W.nx, W.ny, W.seed, (uint32_t)I.get(kIsPix),
+                       (uint32_t)s_cur + W.s_off);
             I.set(kIsCur, s_cur + 1);
             active = true;
             next_ray = true;

@@ -97,6 +97,15 @@ i)  # 7-word work items (end and pixel coordinates derived; libfrt_item7) and wi
     for k in 1 2; do ab m "" $M && ab m libfrt_item7.so $M && ab m libfrt_item7ls15.so $M || exit 1; done \
      && for k in 1 2; do ab c "" $C && ab c libfrt_item7.so $C || exit 1; done \
      && for k in 1 2; do ab mlt "" $P || exit 1; done ;;
+j)  # compiler flags per unit: AMDGPU register-pressure trackers in the scheduler (ldstrk: the octant
+    # path unit only; alltrk: every unit), relaxed occupancy targets (allrelax: every unit), and the
+    # material unit (C3's fp64 list kernel) under max-memory-clause / iterative-maxocc (matsmem,
+    # matsmaxocc; it keeps the basic SGPR allocator)
+    V="--scene veach --spp 256 --rounds 2 --variants default"
+    for k in 1 2; do for v in "" libfrt_ldstrk.so libfrt_alltrk.so libfrt_allrelax.so; do ab c "$v" $C || exit 1; done; done \
+     && for k in 1 2; do for v in "" libfrt_alltrk.so libfrt_allrelax.so; do ab m "$v" $M || exit 1; done; done \
+     && for k in 1 2; do for v in "" libfrt_alltrk.so libfrt_allrelax.so; do ab mlt "$v" $P || exit 1; done; done \
+     && for k in 1 2; do for v in "" libfrt_matsmem.so libfrt_matsmaxocc.so libfrt_alltrk.so libfrt_allrelax.so; do ab v "$v" $V || exit 1; done; done ;;
 esac
 rc=$?
 echo "rc=$rc" > $O/rc.txt
