@@ -106,6 +106,10 @@ j)  # compiler flags per unit: AMDGPU register-pressure trackers in the schedule
      && for k in 1 2; do for v in "" libfrt_alltrk.so libfrt_allrelax.so; do ab m "$v" $M || exit 1; done; done \
      && for k in 1 2; do for v in "" libfrt_alltrk.so libfrt_allrelax.so; do ab mlt "$v" $P || exit 1; done; done \
      && for k in 1 2; do for v in "" libfrt_matsmem.so libfrt_matsmaxocc.so libfrt_alltrk.so libfrt_allrelax.so; do ab v "$v" $V || exit 1; done; done ;;
+k)  # the final tree as the driver runs it: the GPU suite, smoke, then the default bench command
+    pt gpu 900 tests -m gpu \
+     && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
+     && b default 600 --gpus 1 --steps 20 --warmup 5 ;;
 esac
 rc=$?
 echo "rc=$rc" > $O/rc.txt
