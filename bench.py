@@ -55,6 +55,29 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+class Heartbeat:
+    """A line on stderr every `every` s while rank 0 runs long oracle work (the
+    oracle's C calls release the GIL), so a long CPU phase is not silent."""
+
+    def __init__(self, what, every=30.0):
+        import threading
+        self.what, self.every, self.t0 = what, every, time.perf_counter()
+        self.stop = threading.Event()
+        self.th = threading.Thread(target=self.run, daemon=True)
+
+    def run(self):
+        while not self.stop.wait(self.every):
+            log(f"bench: {self.what} running, {time.perf_counter() - self.t0:.0f} s")
+
+    def __enter__(self):
+        self.th.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        self.th.join()
+
+
 def free_port():
     import socket
     s = socket.socket()
@@ -212,7 +235,7 @@ def cpu_baseline(kind, obj, nx, ny, spp, seed, npix, threads, film, seconds, int
     }
 
 
-def cpu_baseline_mlt(ctx, r, mpp, n_chains, seed, threads, seconds):
+def cpu_baseline_mlt(ctx, r, mpp, n_chains, seed, threads, seconds, shards=0):
     """C5's CPU baseline and path-exact parity in one: the oracle's PSS-MLT
     (pssmlt.cpp restated in fp64) on the chains of shard (0, K) of the config
     itself -- every one of them runs the config's full mutation count -- with K
@@ -227,11 +250,11 @@ def cpu_baseline_mlt(ctx, r, mpp, n_chains, seed, threads, seconds):
         return {"mrays": None, "seconds": 0.0, "rays": 0, "npix": 0, "V": None, "T": None, "parity": None,
                 "sample": "none", "note": (f"{mpp} mutations/pixel x {nx}x{ny} < {n_chains} chains: 0 mutations "
                                            f"per chain, no path-exact parity")}
-    K = 1024
+    K = shards if shards > 0 else 1024      # shards = 1: every chain of the frame (no estimate)
     while True:
         par = mlt_shard_parity(ctx, r["kind"], r["obj"], nx, ny, mpp, n_chains, K, seed, threads, env=r["env"])
         dt = par["oracle_seconds"]
-        if dt >= 0.5 * seconds or K <= 16 or K >= n_chains:
+        if shards > 0 or dt >= 0.5 * seconds or K <= 16 or K >= n_chains:
             break
         K = max(16, K >> max(1, min(4, int(math.ceil(math.log2(seconds / max(dt, 1e-3)))))))
     par.pop("gpu_film")
@@ -784,6 +807,9 @@ def main():
                     help="pssmlt: C5 config, --spp = mutations per pixel; ao (ao.cpp), normals (debug_renderer.h)")
     ap.add_argument("--env", default="", help="constant environment r,g,b (default: the scene's; 1,1,1 for ao)")
     ap.add_argument("--chains", type=int, default=1 << 18, help="PSS-MLT chains (all ranks)")
+    ap.add_argument("--mlt-shards", type=int, default=0,
+                    help="PSS-MLT path-exact parity on shard (0, K) of the chains; 0: K calibrated to "
+                         "--cpu-seconds, 1: every chain (the full-frame RMSE, no estimate)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the N-rank path with host-staged collectives (e.g. ranks sharing one GPU)")
     ap.add_argument("--rmse-pixels-multi", type=int, default=32768,
@@ -804,7 +830,9 @@ def main():
     if args.integrator == "pssmlt" and rank == 0 and not args.no_cpu_baseline:
         # the path-exact parity renders shard chains on R.ctx: it runs now, while R.ctx
         # still holds this line's scene (not after the north-star upload)
-        mlt_cpu = cpu_baseline_mlt(R.ctx, res, args.spp, args.chains, args.seed, threads, args.cpu_seconds)
+        with Heartbeat("PSS-MLT parity (oracle)"):
+            mlt_cpu = cpu_baseline_mlt(R.ctx, res, args.spp, args.chains, args.seed, threads, args.cpu_seconds,
+                                       shards=args.mlt_shards)
     default = (args.scene == "cornell" and args.integrator == "path" and args.res == "1920x1080"
                and args.spp == 512)
     do_ns = args.north_star == "on" or (args.north_star == "auto" and default)
@@ -817,8 +845,12 @@ def main():
         c3 = R.measure(args, "veach", 1024, args.cfg_steps, 1, args.bvh, integrator="path", precision="auto")
         c5 = R.measure(args, "cornell", 512, args.cfg_steps, 1, args.bvh, integrator="pssmlt", precision="auto")
         if rank == 0 and not args.no_cpu_baseline:
-            c5_cpu = cpu_baseline_mlt(R.ctx, c5, 512, args.chains, args.seed, threads, args.cfg_cpu_seconds)
+            with Heartbeat("C5 parity (oracle)"):
+                c5_cpu = cpu_baseline_mlt(R.ctx, c5, 512, args.chains, args.seed, threads, args.cfg_cpu_seconds)
 
+    beat = Heartbeat("oracle RMSE / CPU baseline") if rank == 0 else None
+    if beat is not None:
+        beat.__enter__()
     if rank == 0:
         nx, ny = res["nx"], res["ny"]
         key = f"{args.scene}:{nx}x{ny}"
@@ -970,6 +1002,7 @@ def main():
             line["config"]["parallelism"] += " (gloo host-staged rehearsal)"
         if args.pfm:
             R.frt.write_pfm(args.pfm, film_np.reshape(ny, nx, 3))
+        beat.__exit__()
         print(json.dumps(line), flush=True)
     R.ctx.close()
     if world > 1:

@@ -110,6 +110,11 @@ k)  # the final tree as the driver runs it: the GPU suite, smoke, then the defau
     pt gpu 900 tests -m gpu \
      && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
      && b default 600 --gpus 1 --steps 20 --warmup 5 ;;
+l)  # full-frame parity (no sample, no estimate): C2 and C3 against the oracle on every pixel
+    # (--rmse-min-frac 1), C5 path-exact on every chain of the frame (--mlt-shards 1)
+    b c2full 600 --steps 3 --warmup 1 --north-star off --configs off --rmse-min-frac 1.0 \
+     && b c3full 600 --scene veach --spp 1024 --steps 3 --warmup 1 --configs off --rmse-min-frac 1.0 \
+     && b c5full 900 --integrator pssmlt --steps 3 --warmup 1 --mlt-shards 1 ;;
 esac
 rc=$?
 echo "rc=$rc" > $O/rc.txt
