@@ -328,32 +328,6 @@ FRT_HD R tri_intersect(V3<R> o, V3<R> d, V3<R> v0, V3<R> e1, V3<R> e2, R tmin, R
     return (t > tmin && t <= tmax) ? t : R(-1);
 }
 
-// Unit-triangle test (Woop 2004; the form of Aila & Laine's GPU tracer), fp32
-// kernels under FRT_EXP_WOOP: the triangle's record holds the rows of the
-// inverse of the affine map (e1, e2, e1 x e2, v0), so the ray's w (the unit
-// triangle's normal axis), u and v are three dot products each: t = -w(o) / w'(d),
-// u = u(o) + t u'(d), v likewise.  m0 = (w row, w offset), m1 = (u row, u
-// offset), m2 = (v row, v offset), computed in fp64 at upload.  The same
-// acceptance as tri_intersect: t in (tmin, tmax], u >= 0, v >= 0, u + v <= 1.
-// STRAIGHT: straight-line; else the u / v part only after the t test.
-template <bool STRAIGHT = false>
-FRT_HD float tri_woop(f3 o, f3 d, float4 m0, float4 m1, float4 m2, float tmin, float tmax, float &u, float &v)
-{
-    const float oz = fmaf(o.z, m0.z, fmaf(o.y, m0.y, fmaf(o.x, m0.x, m0.w)));
-    const float dz = fmaf(d.z, m0.z, fmaf(d.y, m0.y, d.x * m0.x));
-    const float t = -oz * rcp(dz);
-    if constexpr (!STRAIGHT)
-        if (!(t > tmin && t <= tmax)) return -1.0f;
-    const float ox = fmaf(o.z, m1.z, fmaf(o.y, m1.y, fmaf(o.x, m1.x, m1.w)));
-    const float dx = fmaf(d.z, m1.z, fmaf(d.y, m1.y, d.x * m1.x));
-    u = fmaf(t, dx, ox);
-    const float oy = fmaf(o.z, m2.z, fmaf(o.y, m2.y, fmaf(o.x, m2.x, m2.w)));
-    const float dy = fmaf(d.z, m2.z, fmaf(d.y, m2.y, d.x * m2.x));
-    v = fmaf(t, dy, oy);
-    const bool ok = (STRAIGHT ? (t > tmin && t <= tmax) : true) && u >= 0.0f && v >= 0.0f && u + v <= 1.0f;
-    return ok ? t : -1.0f;
-}
-
 // sphere::hit (sphere.h:26-56): returns t or -1; accepts t in [tmin, tmax].
 // The discriminant b^2 - a(|oc|^2 - r^2) loses ~|oc|^2/r^2 ulps to
 // cancellation in fp32 (veach's r = 0.03 lights at distance 15: a 2 % error,

@@ -95,9 +95,7 @@ template <int WORLD> constexpr int kOverflow = WORLD == kWorldBvh4 ? kBvh4Overfl
 // device scene (fp32, HBM-resident; DESIGN.md "Data layout")
 struct DevScene {
     const float4 *nodes;     // 4 x float4 per interior node: child0 box | child1 box | (child0, child1) refs
-    const float4 *tris;      // 3 x float4 per triangle: v0 | e1 | e2 (48 B), DFS leaf order; under FRT_EXP_WOOP
-                             // the unit-triangle rows of tri_woop (the intersection records)
-    const float4 *trisv;     // v0 | e1 | e2 in HBM for the light samples (= tris without FRT_EXP_WOOP)
+    const float4 *tris;      // 3 x float4 per triangle: v0 | e1 | e2 (48 B), DFS leaf order
     const float4 *tshade;    // 2 x float4 per triangle: (n_geo, inv_area) | (mat, geo, -, -)
     const float4 *tnorm;     // 3 x float4 per triangle: vertex normals (smooth shading only)
     const float4 *spheres;   // (centre, radius)
@@ -171,27 +169,6 @@ template <typename R> FRT_HD V3<R> tri_vec(const DevScene &S, int i, int k)   //
     if constexpr (kIsF64<R>) return xyz(S.tris64[3 * i + k]);
     else return xyz(tri_part(S, i, k));
 }
-#ifndef FRT_EXP_WOOP
-#define FRT_EXP_WOOP 0   // experiment builds: the fp32 kernels intersect triangles with tri_woop
-#endif
-// the triangle's vertices for light sampling (trisv: HBM, also under FRT_EXP_WOOP)
-template <typename R> FRT_HD V3<R> tri_vert(const DevScene &S, int i, int k)   // v0 | e1 | e2
-{
-    if constexpr (kIsF64<R>) return xyz(S.tris64[3 * i + k]);
-    else if constexpr (FRT_EXP_WOOP) return xyz(S.trisv[3 * i + k]);
-    else return xyz(tri_part(S, i, k));
-}
-// ray / triangle `ref` in the kernel's precision (Moller-Trumbore, or tri_woop under FRT_EXP_WOOP)
-template <bool STRAIGHT = false, typename R>
-FRT_HD R tri_hit(const DevScene &S, int ref, V3<R> o, V3<R> d, R tmin, R tmax, R &u, R &v)
-{
-    if constexpr (FRT_EXP_WOOP && !kIsF64<R>) {
-        return tri_woop<STRAIGHT>(o, d, tri_part(S, ref, 0), tri_part(S, ref, 1), tri_part(S, ref, 2), tmin, tmax, u, v);
-    } else {
-        const V3<R> a = tri_vec<R>(S, ref, 0), b = tri_vec<R>(S, ref, 1), c = tri_vec<R>(S, ref, 2);
-        return tri_intersect<STRAIGHT>(o, d, a, b, c, tmin, tmax, u, v);
-    }
-}
 template <typename R> FRT_HD void sphere_get(const DevScene &S, int k, V3<R> &c, R &r)
 {
     if constexpr (kIsF64<R>) { const double4 q = S.spheres64[k]; c = xyz(q); r = q.w; }
@@ -231,7 +208,8 @@ FRT_HD R prim_t(const DevScene &S, int ref, V3<R> o, V3<R> d, R tmin, R tmax, R 
         u = v = R(0);
         return sphere_intersect(o, d, c, r, tmin, tmax);
     }
-    return tri_hit<STRAIGHT>(S, ref, o, d, tmin, tmax, u, v);
+    const V3<R> a = tri_vec<R>(S, ref, 0), b = tri_vec<R>(S, ref, 1), c = tri_vec<R>(S, ref, 2);
+    return tri_intersect<STRAIGHT>(o, d, a, b, c, tmin, tmax, u, v);
 }
 
 // Leaf ~node: one sphere, or triangles [first, first + count) (collapse_leaves;
@@ -275,7 +253,8 @@ FRT_HD bool leaf_hit(const DevScene &S, int lref, V3<R> o, V3<R> d, R tmin, bool
         FRT_DIAG_TICK(1);
         const int ref = first + k;
         R u, v;
-        const R t = tri_hit<STRAIGHT>(S, ref, o, d, tmin, h.t, u, v);
+        const V3<R> a = tri_vec<R>(S, ref, 0), b = tri_vec<R>(S, ref, 1), c = tri_vec<R>(S, ref, 2);
+        const R t = tri_intersect<STRAIGHT>(o, d, a, b, c, tmin, h.t, u, v);
         if (t > R(0) && ((t < h.t) || ref < h.prim)) {
             h.prim = ref; h.t = t; h.u = u; h.v = v;
             if (anyhit) return true;
@@ -601,8 +580,7 @@ template <typename R> FRT_HD Hit<R> trace_list(const DevScene &S, V3<R> o, V3<R>
             } else {
                 const cptr tb = (cptr)S.tris;
                 const float4 a = tb[ref * S.tri_es], b = tb[ref * S.tri_es + S.tri_ps], c = tb[ref * S.tri_es + 2 * S.tri_ps];
-                if constexpr (FRT_EXP_WOOP) t = tri_woop(o, d, a, b, c, Cst<R>::eps, h.t, u, v);
-                else t = tri_intersect(o, d, xyz(a), xyz(b), xyz(c), Cst<R>::eps, h.t, u, v);
+                t = tri_intersect(o, d, xyz(a), xyz(b), xyz(c), Cst<R>::eps, h.t, u, v);
             }
         }
 #else
@@ -722,7 +700,7 @@ FRT_HD V3<R> prim_sample(const DevScene &S, int ref, V3<R> o, R u0, R u1, V3<R> 
         ln = normalize(p);
         return p;
     }
-    const V3<R> a = tri_vert<R>(S, ref, 0), b = tri_vert<R>(S, ref, 1), c = tri_vert<R>(S, ref, 2);   // triangle.h:145-175
+    const V3<R> a = tri_vec<R>(S, ref, 0), b = tri_vec<R>(S, ref, 1), c = tri_vec<R>(S, ref, 2);   // triangle.h:145-175
     const R su0 = fsqrt(u0);
     const R b0 = R(1) - su0;
     const R b1 = u1 * su0;

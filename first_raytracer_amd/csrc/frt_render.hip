@@ -1277,7 +1277,6 @@ static inline float round_up(double x)
 // host image of the device scene (DESIGN.md "Data layout")
 struct FlatScene {
     std::vector<float4> nodes, tris, tshade, tnorm, spheres, mats, tuv;
-    std::vector<float4> trisv;    // v0 | e1 | e2 when tris holds tri_woop's rows (FRT_EXP_WOOP)
     std::vector<float4> texels;   // image_texture texels (rgb, -), all images back to back
     std::vector<uint4> nodes4;   // 4-wide quantized BVH
     std::vector<float4> nodes_oct;   // 8 octant copies of `nodes` (DevScene::nodes_oct), LDS plan scenes only
@@ -1710,27 +1709,6 @@ static int flatten_scene(const frt_scene_view *sv, FlatScene &F, std::string &er
         F.tris[3 * d + 0] = make_float4((float)v[0], (float)v[1], (float)v[2], 0.0f);
         F.tris[3 * d + 1] = make_float4((float)e1[0], (float)e1[1], (float)e1[2], 0.0f);
         F.tris[3 * d + 2] = make_float4((float)e2[0], (float)e2[1], (float)e2[2], 0.0f);
-        if (FRT_EXP_WOOP) {   // tri_woop's rows: the inverse of [e1 e2 n] (n = e1 x e2) and -row . v0, in fp64
-            if (d == 0) F.trisv.resize(3 * (size_t)nt);
-            for (int k = 0; k < 3; ++k) F.trisv[3 * d + k] = F.tris[3 * d + k];
-            const double n[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
-            const double det = e1[0] * (e2[1] * n[2] - e2[2] * n[1]) - e2[0] * (e1[1] * n[2] - e1[2] * n[1]) +
-                               n[0] * (e1[1] * e2[2] - e1[2] * e2[1]);
-            // rows of inverse([e1 e2 n] as columns) = the cross products of the columns / det
-            double r[3][3] = {{e2[1] * n[2] - e2[2] * n[1], e2[2] * n[0] - e2[0] * n[2], e2[0] * n[1] - e2[1] * n[0]},
-                              {n[1] * e1[2] - n[2] * e1[1], n[2] * e1[0] - n[0] * e1[2], n[0] * e1[1] - n[1] * e1[0]},
-                              {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]}};
-            const int row_of[3] = {2, 0, 1};   // m0 = w row, m1 = u row, m2 = v row
-            for (int k = 0; k < 3; ++k) {
-                const double *q = r[row_of[k]];
-                if (det == 0.0 || !std::isfinite(det)) {   // degenerate: every ray misses (t = NaN)
-                    F.tris[3 * d + k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                    continue;
-                }
-                const double a = q[0] / det, b = q[1] / det, cc = q[2] / det;
-                F.tris[3 * d + k] = make_float4((float)a, (float)b, (float)cc, (float)-(a * v[0] + b * v[1] + cc * v[2]));
-            }
-        }
         const int mat = sv->tri_material[i];
         if (mat < 0 || mat >= nm) return fail(FRT_E_INVALID, "scene view: bad triangle material");
         const int geo = sv->tri_geometry_normal ? (sv->tri_geometry_normal[i] ? 1 : 0) : 1;
@@ -1905,14 +1883,13 @@ extern "C" int frt_upload_scene(frt_ctx *c, const frt_scene_view *sv)
     int rc;
     if ((rc = upload_vec(c, F.nodes, &S.nodes)) || (rc = upload_vec(c, F.nodes4, &S.nodes4)) ||
         (rc = upload_vec(c, F.nodes_oct, &S.nodes_oct)) ||
-        (rc = upload_vec(c, F.tris, &S.tris)) || (rc = upload_vec(c, F.trisv, &S.trisv)) ||
+        (rc = upload_vec(c, F.tris, &S.tris)) ||
         (rc = upload_vec(c, F.tshade, &S.tshade)) || (rc = upload_vec(c, F.tnorm, &S.tnorm)) ||
         (rc = upload_vec(c, F.tuv, &S.tuv)) || (rc = upload_vec(c, F.texels, &S.texels)) ||
         (rc = upload_vec(c, F.spheres, &S.spheres)) || (rc = upload_vec(c, F.smat, &S.sphere_mat)) ||
         (rc = upload_vec(c, F.mats, &S.mats)) || (rc = upload_vec(c, F.lights, &S.lights)) ||
         (rc = upload_vec(c, F.list, &S.list)) || (rc = upload_vec(c, F.tri_view, &S.tri_view)))
         return rc;
-    if (F.trisv.empty()) S.trisv = S.tris;
     S.tris64 = nullptr; S.tshade64 = nullptr; S.tnorm64 = nullptr; S.spheres64 = nullptr;
     if (want_f64 && ((rc = upload_vec(c, F.tris64, &S.tris64)) || (rc = upload_vec(c, F.tshade64, &S.tshade64)) ||
                      (rc = upload_vec(c, F.tnorm64, &S.tnorm64)) || (rc = upload_vec(c, F.spheres64, &S.spheres64))))
@@ -1953,7 +1930,6 @@ static DevScene host_scene(const FlatScene &F)
     DevScene S = F.meta;
     S.nodes = F.nodes.data(); S.nodes4 = F.nodes4.data(); S.nodes_oct = F.nodes_oct.data();
     S.tris = F.tris.data(); S.tshade = F.tshade.data(); S.tnorm = F.tnorm.data();
-    S.trisv = F.trisv.empty() ? F.tris.data() : F.trisv.data();
     S.tuv = F.tuv.data(); S.texels = F.texels.data();
     S.spheres = F.spheres.data(); S.sphere_mat = F.smat.data(); S.mats = F.mats.data();
     S.lights = F.lights.data(); S.list = F.list.data(); S.tri_view = F.tri_view.data();

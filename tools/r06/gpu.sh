@@ -117,7 +117,7 @@ l)  # full-frame parity (no sample, no estimate): C2 and C3 against the oracle o
      && b c5full 900 --integrator pssmlt --steps 3 --warmup 1 --mlt-shards 1 ;;
 m)  # C4 (the north star) against the oracle on every pixel (~9 minutes of oracle on 16 threads)
     b c4full 1150 --scene cornell_1m --steps 3 --warmup 1 --configs off --rmse-min-frac 1.0 ;;
-n)  # the unit-triangle (Woop) test in every fp32 kernel (libfrt_woop.so) against Moller-Trumbore
+n)  # the unit-triangle (Woop) test in every fp32 kernel against Moller-Trumbore (knob removed after this A/B; needs the e32c42c sources)
     for k in 1 2; do ab c "" $C && ab c libfrt_woop.so $C || exit 1; done \
      && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_woop.so $P || exit 1; done \
      && for k in 1 2; do ab m "" $M && ab m libfrt_woop.so $M || exit 1; done ;;
