@@ -35,8 +35,10 @@ def main():
     ap.add_argument("--integrator", default="path", choices=["path", "ao", "normals", "pssmlt"],
                     help="pssmlt: --spp = mutations per pixel, --chains chains")
     ap.add_argument("--chains", type=int, default=1 << 18)
+    ap.add_argument("--save-films", default="", help="npz of each variant's last film (cross-library checks)")
     ap.add_argument("--env", default="", help="constant environment r,g,b (AO: 1,1,1 unless given)")
     args = ap.parse_args()
+    import numpy as np
     import torch  # noqa: F401  (single HIP runtime)
     import first_raytracer_amd as frt
     sys.path.insert(0, ROOT)
@@ -45,7 +47,7 @@ def main():
     kind, obj, name = scene_spec(args.scene, "/tmp")
     names = {"default": 0, "no_lds": frt.FRT_FLAG_NO_LDS_SCENE, "waves4": frt.FRT_FLAG_WAVES4,
              "waves5": frt.FRT_FLAG_WAVES5, "waves6": frt.FRT_FLAG_WAVES6, "bvh2": frt.FRT_FLAG_BVH2,
-             "no_oct": frt.FRT_FLAG_NO_OCT}
+             "no_oct": frt.FRT_FLAG_NO_OCT, "fp32": frt.FRT_FLAG_FP32}
     flags = {}
     for v in args.variants.split(","):
         parts = v.split("/")[0].split("+")
@@ -86,6 +88,7 @@ def main():
     res = {v: [] for v in chosen}
     rays = {}
     films = {}
+    last = {}
     for r in range(args.rounds + 1):
         for v in chosen:
             leaf = opt(v, "leaf")
@@ -103,6 +106,8 @@ def main():
                 p = frt.RenderParams.make(nx, ny, args.spp, seed=0, flags=flags[v.split("/")[0]],
                                            samples_per_item=spi, integrator=integ)
             films[leaf], st = ctxs[leaf].render(p, films.get(leaf))
+            if args.save_films:
+                last[v] = np.array(films[leaf], copy=True)
             if r > 0:
                 res[v].append(st.kernel_ms)
             rays[v] = st.rays
@@ -112,11 +117,12 @@ def main():
                           "min_ms": min(ms), "grays_per_s": rays[v] / (statistics.median(ms) * 1e-3) / 1e9,
                           "rays": rays[v]}), flush=True)
     if len(films) > 1:   # upload-time options change addresses only: the films must be identical
-        import numpy as np
         keys = list(films)
         print(json.dumps({"films_identical": {str(k): bool(np.array_equal(np.asarray(films[k]),
                                                                                np.asarray(films[keys[0]])))
                                               for k in keys[1:]}}), flush=True)
+    if args.save_films:
+        np.savez(args.save_films, **last)
     for c in ctxs.values():
         c.close()
 

@@ -121,6 +121,15 @@ n)  # the unit-triangle (Woop) test in every fp32 kernel against Moller-Trumbore
     for k in 1 2; do ab c "" $C && ab c libfrt_woop.so $C || exit 1; done \
      && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_woop.so $P || exit 1; done \
      && for k in 1 2; do ab m "" $M && ab m libfrt_woop.so $M || exit 1; done ;;
+o)  # list-order records read one entry ahead in trace_list (libfrt_listrec.so) vs the in-tree scan:
+    # veach 256 spp in fp64 (C3's kernel) and fp32, the films of both libraries, the C3 tests on it
+    V="--scene veach --spp 256 --rounds 2 --variants default,fp32"
+    F="--scene veach --spp 64 --res 480x270 --rounds 1 --variants default,fp32"
+    for k in 1 2; do ab v "" $V && ab v libfrt_listrec.so $V || exit 1; done \
+     && timeout -k 10 300 python -u tools/perf_ab.py $F --save-films $O/films_base.npz > /dev/null 2>> $O/ab.log \
+     && FRT_LIB_PATH=$E/libfrt_listrec.so timeout -k 10 300 python -u tools/perf_ab.py $F --save-films $O/films_exp.npz > /dev/null 2>> $O/ab.log \
+     && python -c "import numpy as np; a=np.load('$O/films_base.npz'); b=np.load('$O/films_exp.npz'); print({k: bool(np.array_equal(a[k], b[k])) for k in a.files})" > $O/films_equal.txt \
+     && FRT_LIB_PATH=$E/libfrt_listrec.so pt veach 900 tests/test_gpu_precision.py -m gpu -k veach ;;
 esac
 rc=$?
 echo "rc=$rc" > $O/rc.txt
