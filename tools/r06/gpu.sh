@@ -121,6 +121,11 @@ n)  # the unit-triangle (Woop) test in every fp32 kernel against Moller-Trumbore
     for k in 1 2; do ab c "" $C && ab c libfrt_woop.so $C || exit 1; done \
      && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_woop.so $P || exit 1; done \
      && for k in 1 2; do ab m "" $M && ab m libfrt_woop.so $M || exit 1; done ;;
+p)  # the tree after the round's last experiments (sources as stage k's; bench.py with the
+    # heartbeat and --mlt-shards): the GPU suite, smoke, the default bench command
+    pt gpu 900 tests -m gpu \
+     && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
+     && b default 600 --gpus 1 --steps 20 --warmup 5 ;;
 o)  # list-order records read one entry ahead in trace_list (libfrt_listrec.so) vs the in-tree scan:
     # veach 256 spp in fp64 (C3's kernel) and fp32, the films of both libraries, the C3 tests on it
     V="--scene veach --spp 256 --rounds 2 --variants default,fp32"
