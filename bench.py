@@ -44,7 +44,8 @@ SCENES = os.path.join(ROOT, "tests", "golden", "scenes")
 # VALU instruction issues over 2 cycles -> 1228.8 G wave-instructions/s; LDS
 # aggregate ~150 TB/s for ds_read_b64/b128
 HBM_PEAK_GBS = 8000.0
-VALU_PEAK_GINST = 256 * 4 * 2.4 / 2.0
+VALU_PEAK_CLOCK_GHZ = 2.4
+VALU_PEAK_GINST = 256 * 4 * VALU_PEAK_CLOCK_GHZ / 2.0
 LDS_PEAK_GBS = 150000.0
 L2_XCD_BYTES = 4 << 20          # one XCD's L2 (MI355X_MICROARCH.md)
 NODE_BYTES, TRI_BYTES, RAY_BYTES = 32, 48, 32   # B_ray = 32 V + 48 T + 32
@@ -483,10 +484,19 @@ def roofline(integrator, key, world, res, V, T, shared_device=False):
         if pmc.get("wait_frac") is not None:
             # SQ_WAIT_ANY / SQ_WAVE_CYCLES: share of wave cycles spent in s_waitcnt
             out["wait_frac"] = round(pmc["wait_frac"], 4)
+        if pmc.get("clock_ghz"):
+            # the clock the chip ran this kernel at (GRBM_GUI_ACTIVE, profiled launch): the
+            # VALU peak above is priced at 2.4 GHz; at the running clock the issue rate is
+            # the same fraction of a lower peak (MI355X_MICROARCH.md "DVFS give-back")
+            ck = pmc["clock_ghz"]
+            out["clock_ghz"] = round(ck, 3)
+            vf = out.get("frac") if out.get("bound") == "valu" else out.get("valu_issue_frac")
+            if vf is not None:
+                out["valu_issue_frac_at_clock"] = round(vf * VALU_PEAK_CLOCK_GHZ / ck, 4)
     if shared_device and out.get("frac") is not None:
         # ranks sharing one device (gloo rehearsal): a rank's launch time is not
         # the time of a launch that has the chip, so no fraction of its peak
-        for k in ("achieved", "frac", "valu_issue_frac", "lds_frac"):     # every fraction of a chip peak
+        for k in ("achieved", "frac", "valu_issue_frac", "lds_frac", "valu_issue_frac_at_clock"):   # chip peaks
             if k in out:
                 out[k] = None
         out["basis"] = "ranks share one device (rehearsal): no roofline"

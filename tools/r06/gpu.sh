@@ -121,6 +121,17 @@ n)  # the unit-triangle (Woop) test in every fp32 kernel against Moller-Trumbore
     for k in 1 2; do ab c "" $C && ab c libfrt_woop.so $C || exit 1; done \
      && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_woop.so $P || exit 1; done \
      && for k in 1 2; do ab m "" $M && ab m libfrt_woop.so $M || exit 1; done ;;
+q)  # the clock each config's megakernel runs at (GRBM_GUI_ACTIVE over the dispatch, one pass per
+    # config), merged into a copy of profiles/roofline_pmc.json (bench.py: clock_ghz,
+    # valu_issue_frac_at_clock)
+    CK="GRBM_GUI_ACTIVE GRBM_COUNT"
+    cp profiles/roofline_pmc.json $O/roofline_pmc.json \
+     && pmc c2_clk "$CK" && pmc c4_clk "$CK" --scene cornell_1m && pmc c3_clk "$CK" --scene veach --spp 1024 \
+     && pmc c5_clk "$CK" --integrator pssmlt \
+     && for x in "path:cornell:1920x1080 c2" "path:cornell_1m:1920x1080 c4" "path:veach:1920x1080:fp64 c3" \
+                 "pssmlt:cornell:1920x1080 c5"; do set -- $x; \
+          python tools/roofline_pmc.py $1 --clock $O/$2_clk --clock-only --copy-to $O/pmc --out $O/roofline_pmc.json \
+              >> $O/roofline.log 2>&1 || exit 1; done ;;
 p)  # the tree after the round's last experiments (sources as stage k's; bench.py with the
     # heartbeat and --mlt-shards): the GPU suite, smoke, the default bench command
     pt gpu 900 tests -m gpu \

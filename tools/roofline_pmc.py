@@ -19,6 +19,10 @@ KEY is "<integrator>:<scene>:<nx>x<ny>" (bench.py's key).  From the LAST
   l2_hit_rate         = TCC_HIT / (TCC_HIT + TCC_MISS)   (--tcc pass)
   wait_frac           = SQ_WAIT_ANY / SQ_WAVE_CYCLES     (--wait pass: the share of
                         wave cycles spent waiting in s_waitcnt)
+  clock_ghz           = GRBM_GUI_ACTIVE / 8 / dispatch ns (--clock pass: the clock the chip
+                        ran the launch at; rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs,
+                        MI355X_MICROARCH.md "DVFS give-back")
+  --clock-only: add just the --clock figures to KEY's existing record.
 FETCH_SIZE / WRITE_SIZE are KiB; FETCH_SIZE is doubled as MI355X_MICROARCH.md
 "HBM [CDNA4]" prescribes for gfx950 (it tallies 128-B requests at 64 B).
 The rays per launch come from the bench JSON the passes printed (every pass
@@ -52,19 +56,50 @@ def last_megakernel(d):
     return names[last], dict(per[last]), path
 
 
+def dispatch_ns(path, did=None):
+    """End - Start timestamp of the last megakernel dispatch in a counter CSV."""
+    rows = [r for r in csv.DictReader(open(path)) if "megakernel" in r["Kernel_Name"]]
+    last = max(int(r["Dispatch_Id"]) for r in rows) if did is None else did
+    r = next(r for r in rows if int(r["Dispatch_Id"]) == last)
+    return float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+
+
+def clock_fields(d):
+    _, gr, p = last_megakernel(d)
+    ns = dispatch_ns(p)
+    return {"GRBM": gr, "clock_dispatch_ms": ns * 1e-6, "clock_ghz": gr["GRBM_GUI_ACTIVE"] / 8.0 / ns}, p
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("key")
-    ap.add_argument("--sq", required=True)
-    ap.add_argument("--fetch", required=True)
-    ap.add_argument("--write", required=True)
-    ap.add_argument("--bench", required=True)
+    ap.add_argument("--sq", default="")
+    ap.add_argument("--fetch", default="")
+    ap.add_argument("--write", default="")
+    ap.add_argument("--bench", default="")
+    ap.add_argument("--clock", default="")
+    ap.add_argument("--clock-only", action="store_true")
     ap.add_argument("--f64", default="")
     ap.add_argument("--tcc", default="")
     ap.add_argument("--wait", default="")
     ap.add_argument("--copy-to", default="")
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "roofline_pmc.json"))
     a = ap.parse_args()
+    if a.clock_only:
+        t = json.load(open(a.out))
+        fields, p = clock_fields(a.clock)
+        if a.copy_to:
+            os.makedirs(a.copy_to, exist_ok=True)
+            dst = os.path.join(a.copy_to, f"pmc_{a.key.replace(':', '_')}_clock.csv")
+            shutil.copy(p, dst)
+            p = os.path.relpath(dst, ROOT)
+        t[a.key].update(fields)
+        t[a.key]["source"] = t[a.key]["source"].split(", " + p)[0] + ", " + p
+        json.dump(t, open(a.out, "w"), indent=1, sort_keys=True)
+        print(json.dumps(fields, indent=1))
+        return
+    if not (a.sq and a.fetch and a.write and a.bench):
+        sys.exit("--sq, --fetch, --write and --bench are required (or --clock-only)")
     line = [l for l in open(a.bench) if l.startswith("{")][-1]
     b = json.loads(line)
     rays = b["roofline"]["rays_per_launch"]
@@ -101,6 +136,10 @@ def main():
         _, wt, p_wt = last_megakernel(a.wait)
         passes.append(("wait", p_wt))
         rec.update({"WAIT": wt, "wait_frac": wt["SQ_WAIT_ANY"] / max(1.0, wt["SQ_WAVE_CYCLES"])})
+    if a.clock:
+        fields, p_ck = clock_fields(a.clock)
+        passes.append(("clock", p_ck))
+        rec.update(fields)
     srcs = []
     for tag, p in passes:
         if a.copy_to:
