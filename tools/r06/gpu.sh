@@ -121,6 +121,16 @@ n)  # the unit-triangle (Woop) test in every fp32 kernel against Moller-Trumbore
     for k in 1 2; do ab c "" $C && ab c libfrt_woop.so $C || exit 1; done \
      && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_woop.so $P || exit 1; done \
      && for k in 1 2; do ab m "" $M && ab m libfrt_woop.so $M || exit 1; done ;;
+r)  # (record; the knob was removed after it) LDS-DMA touches on the 4-wide plan (FRT_EXP_TOUCH): the leaf's later lines (libfrt_touch.so),
+    # the second-nearest child (libfrt_touchc.so), both (libfrt_touch3.so) vs the in-tree build:
+    # cornell_1m 256 spp, then every library's film at a small size against the in-tree one
+    F="--scene cornell_1m --spp 16 --res 480x270 --rounds 1 --variants default"
+    for k in 1 2; do ab m "" $M && ab m libfrt_touch.so $M && ab m libfrt_touchc.so $M \
+                     && ab m libfrt_touch3.so $M || exit 1; done \
+     && timeout -k 10 300 python -u tools/perf_ab.py $F --save-films $O/films_base.npz > /dev/null 2>> $O/ab.log \
+     && for l in touch touchc touch3; do FRT_LIB_PATH=$E/libfrt_$l.so timeout -k 10 300 python -u tools/perf_ab.py $F \
+            --save-films $O/films_$l.npz > /dev/null 2>> $O/ab.log || exit 1; done \
+     && python -c "import numpy as np; a=np.load('$O/films_base.npz'); print({l: bool(np.array_equal(a['default'], np.load('$O/films_'+l+'.npz')['default'])) for l in ('touch','touchc','touch3')})" > $O/films_equal.txt ;;
 q)  # the clock each config's megakernel runs at (GRBM_GUI_ACTIVE over the dispatch, one pass per
     # config), merged into a copy of profiles/roofline_pmc.json (bench.py: clock_ghz,
     # valu_issue_frac_at_clock)
