@@ -131,6 +131,9 @@ r)  # (record; the knob was removed after it) LDS-DMA touches on the 4-wide plan
      && for l in touch touchc touch3; do FRT_LIB_PATH=$E/libfrt_$l.so timeout -k 10 300 python -u tools/perf_ab.py $F \
             --save-films $O/films_$l.npz > /dev/null 2>> $O/ab.log || exit 1; done \
      && python -c "import numpy as np; a=np.load('$O/films_base.npz'); print({l: bool(np.array_equal(a['default'], np.load('$O/films_'+l+'.npz')['default'])) for l in ('touch','touchc','touch3')})" > $O/films_equal.txt ;;
+s)  # the AO and shading-normals integrators on this round's build (Cornell 1080p 512 spp lines)
+    b ao 600 --integrator ao --steps 10 --warmup 3 --configs off --north-star off \
+     && b normals 600 --integrator normals --steps 10 --warmup 3 --configs off --north-star off ;;
 q)  # the clock each config's megakernel runs at (GRBM_GUI_ACTIVE over the dispatch, one pass per
     # config), merged into a copy of profiles/roofline_pmc.json (bench.py: clock_ghz,
     # valu_issue_frac_at_clock)
