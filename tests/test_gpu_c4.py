@@ -15,6 +15,9 @@ sampled pixel and channel, nothing excluded.
     oracle renders with the same streams; rays per sample within 0.5 % (the
     GPU counts the whole frame, the oracle the sample).
   * 96x54 at 64 spp, whole frame on both sides: ray counts within 0.2 %.
+  * the configs' own sample counts on the bench tree (GPU binned SAH): 1920x1080
+    at 256 spp (BASELINE.json configs[3]) and 512 spp (north_star), on 8,192
+    evenly spaced pixels.
 """
 import os
 
@@ -103,3 +106,22 @@ def test_c4_small_frame_exact_counts(ctx, c1m, ora, tree):
     assert abs(st.rays - cnt.rays) / cnt.rays < 2e-3
     assert abs(st.shadow_rays - cnt.shadow_rays) / cnt.shadow_rays < 2e-3
     assert e <= RMSE_TOL
+
+
+@pytest.mark.parametrize("spp", [256, 512])
+def test_c4_config_spp(ctx, c1m, ora, spp):
+    nx, ny = 1920, 1080
+    hs = host_scene(ctx, c1m, nx / ny, "gpu")
+    ctx.upload(hs)
+    film, st = ctx.render(frt.RenderParams.make(nx, ny, spp, seed=11))
+    assert st.scene_in_lds == 0 and st.samples == nx * ny * spp
+    pix = np.unique(np.linspace(0, nx * ny - 1, 8192).astype(np.int32))
+    ref, cnt = ora[nx / ny].render(nx, ny, spp, seed=11, pixels=pix)
+    got = film.reshape(-1, 3)[pix]
+    e = rmse(got, ref)
+    print(f"C4 {spp} spp: rmse {e:.3e} over {len(pix)} px, rays/sample gpu {st.rays / st.samples:.5f} "
+          f"oracle {cnt.rays / cnt.samples:.5f}, kernel {st.kernel_ms:.1f} ms, {st.rays / st.kernel_ms / 1e6:.2f} Grays/s")
+    assert np.isfinite(film).all()
+    assert e <= RMSE_TOL
+    assert abs(st.rays / st.samples - cnt.rays / cnt.samples) / (cnt.rays / cnt.samples) < 2e-3
+

@@ -131,6 +131,8 @@ r)  # (record; the knob was removed after it) LDS-DMA touches on the 4-wide plan
      && for l in touch touchc touch3; do FRT_LIB_PATH=$E/libfrt_$l.so timeout -k 10 300 python -u tools/perf_ab.py $F \
             --save-films $O/films_$l.npz > /dev/null 2>> $O/ab.log || exit 1; done \
      && python -c "import numpy as np; a=np.load('$O/films_base.npz'); print({l: bool(np.array_equal(a['default'], np.load('$O/films_'+l+'.npz')['default'])) for l in ('touch','touchc','touch3')})" > $O/films_equal.txt ;;
+t)  # the C4 GPU test at the configs' own sample counts (256 / 512 spp on 8,192 oracle pixels)
+    pt c4 900 tests/test_gpu_c4.py -m gpu -k config_spp -s ;;
 s)  # the AO and shading-normals integrators on this round's build (Cornell 1080p 512 spp lines)
     b ao 600 --integrator ao --steps 10 --warmup 3 --configs off --north-star off \
      && b normals 600 --integrator normals --steps 10 --warmup 3 --configs off --north-star off ;;
