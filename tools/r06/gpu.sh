@@ -131,6 +131,19 @@ r)  # (record; the knob was removed after it) LDS-DMA touches on the 4-wide plan
      && for l in touch touchc touch3; do FRT_LIB_PATH=$E/libfrt_$l.so timeout -k 10 300 python -u tools/perf_ab.py $F \
             --save-films $O/films_$l.npz > /dev/null 2>> $O/ab.log || exit 1; done \
      && python -c "import numpy as np; a=np.load('$O/films_base.npz'); print({l: bool(np.array_equal(a['default'], np.load('$O/films_'+l+'.npz')['default'])) for l in ('touch','touchc','touch3')})" > $O/films_equal.txt ;;
+v)  # (record; the knob was removed after it) the fine tail (FRT_FINE_TAIL=1: the last chunk's samples cut into 8 chunks queued last): same
+    # process at N = 1 (Cornell, cornell_1m), then every shard of N = 8 alone with and without it
+    timeout -k 10 400 python -u tools/perf_ab.py --scene cornell --spp 512 --rounds 3 --bvh gsah \
+        --variants default,default/fine1 > $O/ab_c.jsonl 2>> $O/ab.log \
+     && timeout -k 10 400 python -u tools/perf_ab.py --scene cornell_1m --spp 512 --rounds 2 --bvh gsah \
+        --variants default,default/fine1 > $O/ab_m.jsonl 2>> $O/ab.log \
+     && timeout -k 10 300 python -u tools/shard_balance.py --scene cornell --ns 8 --reps 2 > $O/shard_cornell.json 2> $O/shard.log \
+     && FRT_FINE_TAIL=1 timeout -k 10 300 python -u tools/shard_balance.py --scene cornell --ns 8 --reps 2 > $O/shard_cornell_fine.json 2>> $O/shard.log \
+     && timeout -k 10 400 python -u tools/shard_balance.py --scene cornell_1m --ns 8 --reps 2 > $O/shard_1m.json 2>> $O/shard.log \
+     && FRT_FINE_TAIL=1 timeout -k 10 400 python -u tools/shard_balance.py --scene cornell_1m --ns 8 --reps 2 > $O/shard_1m_fine.json 2>> $O/shard.log ;;
+u)  # the N-way tile split on this round's kernels: every shard (r, N) timed alone on the GPU
+    timeout -k 10 400 python -u tools/shard_balance.py --scene cornell --ns 2,4,8 --reps 2 > $O/shard_cornell.json 2> $O/shard.log \
+     && timeout -k 10 500 python -u tools/shard_balance.py --scene cornell_1m --ns 2,4,8 --reps 2 > $O/shard_1m.json 2>> $O/shard.log ;;
 t)  # the C4 GPU test at the configs' own sample counts (256 / 512 spp on 8,192 oracle pixels)
     pt c4 900 tests/test_gpu_c4.py -m gpu -k config_spp -s ;;
 s)  # the AO and shading-normals integrators on this round's build (Cornell 1080p 512 spp lines)
