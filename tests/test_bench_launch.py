@@ -108,5 +108,17 @@ def test_shared_device_roofline_has_no_fractions():
     res = {"avg_kernel_ms": 100.0, "rays_per_launch": 10 ** 9, "scene_in_lds": False, "scene_bytes": 10 ** 8,
            "launch": {}, "fp64": False}
     out = bench.roofline("path", "cornell_1m:1920x1080", 2, res, 50.0, 2.0, shared_device=True)
-    for k in ("achieved", "frac", "valu_issue_frac", "lds_frac"):
+    for k in ("achieved", "frac", "valu_issue_frac", "lds_frac", "valu_issue_frac_at_clock"):
         assert out.get(k) is None, k
+
+
+def test_roofline_clock_fields():
+    """The profiled clock (roofline_pmc.json clock_ghz, a GRBM_GUI_ACTIVE pass)
+    rescales the VALU fraction from the 2.4-GHz peak to the running clock."""
+    res = {"avg_kernel_ms": 227.0, "rays_per_launch": 7.6e9, "scene_in_lds": True, "scene_bytes": 10 ** 4,
+           "launch": {}, "fp64": False}
+    out = bench.roofline("path", "cornell:1920x1080", 2, res, None, None)
+    pmc = bench.load_profile("roofline_pmc.json", "path:cornell:1920x1080")
+    assert out["bound"] == "valu" and out["clock_ghz"] == round(pmc["clock_ghz"], 3)
+    assert 1.9 < out["clock_ghz"] <= 2.4
+    assert out["valu_issue_frac_at_clock"] == round(out["frac"] * bench.VALU_PEAK_CLOCK_GHZ / pmc["clock_ghz"], 4)
