@@ -131,6 +131,16 @@ r)  # (record; the knob was removed after it) LDS-DMA touches on the 4-wide plan
      && for l in touch touchc touch3; do FRT_LIB_PATH=$E/libfrt_$l.so timeout -k 10 300 python -u tools/perf_ab.py $F \
             --save-films $O/films_$l.npz > /dev/null 2>> $O/ab.log || exit 1; done \
      && python -c "import numpy as np; a=np.load('$O/films_base.npz'); print({l: bool(np.array_equal(a['default'], np.load('$O/films_'+l+'.npz')['default'])) for l in ('touch','touchc','touch3')})" > $O/films_equal.txt ;;
+x)  # (record; the FRT_EXP_TIMELINE knob was removed after it) per-wave timeline of path_megakernel (libfrt_tl.so: entry, LDS scene loaded, first exhausted
+    # queue grab, exit) at 64 and 512 spp, Cornell and cornell_1m
+    FRT_LIB_PATH=$E/libfrt_tl.so timeout -k 10 400 python -u tools/r06/timeline.py > $O/timeline.jsonl 2> $O/timeline.log ;;
+w)  # the per-launch fixed cost: Cornell and cornell_1m 1080p at 64 / 128 / 256 / 512 spp (time = a + b spp)
+    for spp in 64 128 256 512; do
+      timeout -k 10 300 python -u tools/perf_ab.py --scene cornell --spp $spp --rounds 3 --bvh gsah --variants default >> $O/spp_c.jsonl 2>> $O/ab.log || exit 1
+    done \
+     && for spp in 64 128 256 512; do
+      timeout -k 10 300 python -u tools/perf_ab.py --scene cornell_1m --spp $spp --rounds 2 --bvh gsah --variants default >> $O/spp_m.jsonl 2>> $O/ab.log || exit 1
+    done ;;
 v)  # (record; the knob was removed after it) the fine tail (FRT_FINE_TAIL=1: the last chunk's samples cut into 8 chunks queued last): same
     # process at N = 1 (Cornell, cornell_1m), then every shard of N = 8 alone with and without it
     timeout -k 10 400 python -u tools/perf_ab.py --scene cornell --spp 512 --rounds 3 --bvh gsah \
