@@ -131,6 +131,9 @@ r)  # (record; the knob was removed after it) LDS-DMA touches on the 4-wide plan
      && for l in touch touchc touch3; do FRT_LIB_PATH=$E/libfrt_$l.so timeout -k 10 300 python -u tools/perf_ab.py $F \
             --save-films $O/films_$l.npz > /dev/null 2>> $O/ab.log || exit 1; done \
      && python -c "import numpy as np; a=np.load('$O/films_base.npz'); print({l: bool(np.array_equal(a['default'], np.load('$O/films_'+l+'.npz')['default'])) for l in ('touch','touchc','touch3')})" > $O/films_equal.txt ;;
+y)  # the N = 8 code path rehearsed on one GPU: eight gloo ranks sharing the device (tile shards of
+    # 1/8, the gather to rank 0, the PSS-MLT film sum, per_rank fields), the default blocks
+    b gloo8 900 --gpus 8 --backend gloo --steps 2 --warmup 1 ;;
 x)  # (record; the FRT_EXP_TIMELINE knob was removed after it) per-wave timeline of path_megakernel (libfrt_tl.so: entry, LDS scene loaded, first exhausted
     # queue grab, exit) at 64 and 512 spp, Cornell and cornell_1m
     FRT_LIB_PATH=$E/libfrt_tl.so timeout -k 10 400 python -u tools/r06/timeline.py > $O/timeline.jsonl 2> $O/timeline.log ;;
