@@ -131,6 +131,17 @@ r)  # (record; the knob was removed after it) LDS-DMA touches on the 4-wide plan
      && for l in touch touchc touch3; do FRT_LIB_PATH=$E/libfrt_$l.so timeout -k 10 300 python -u tools/perf_ab.py $F \
             --save-films $O/films_$l.npz > /dev/null 2>> $O/ab.log || exit 1; done \
      && python -c "import numpy as np; a=np.load('$O/films_base.npz'); print({l: bool(np.array_equal(a['default'], np.load('$O/films_'+l+'.npz')['default'])) for l in ('touch','touchc','touch3')})" > $O/films_equal.txt ;;
+z)  # (record; the knob was removed after it) the octant node step's store deferred behind the next visit's record reads (libfrt_defer.so,
+    # FRT_EXP_DEFER_PUSH) vs the in-tree build: Cornell 512 spp, PSS-MLT, then films of both libraries
+    F1="--scene cornell --spp 16 --res 480x270 --rounds 1 --variants default"
+    F2="--scene cornell --spp 16 --res 480x270 --rounds 1 --variants default --integrator pssmlt --chains 16384"
+    for k in 1 2; do ab c "" $C && ab c libfrt_defer.so $C || exit 1; done \
+     && for k in 1 2; do ab mlt "" $P && ab mlt libfrt_defer.so $P || exit 1; done \
+     && timeout -k 10 300 python -u tools/perf_ab.py $F1 --save-films $O/fc_base.npz > /dev/null 2>> $O/ab.log \
+     && FRT_LIB_PATH=$E/libfrt_defer.so timeout -k 10 300 python -u tools/perf_ab.py $F1 --save-films $O/fc_exp.npz > /dev/null 2>> $O/ab.log \
+     && timeout -k 10 300 python -u tools/perf_ab.py $F2 --save-films $O/fm_base.npz > /dev/null 2>> $O/ab.log \
+     && FRT_LIB_PATH=$E/libfrt_defer.so timeout -k 10 300 python -u tools/perf_ab.py $F2 --save-films $O/fm_exp.npz > /dev/null 2>> $O/ab.log \
+     && python -c "import numpy as np; print({t: bool(np.array_equal(np.load('$O/f'+t+'_base.npz')['default'], np.load('$O/f'+t+'_exp.npz')['default'])) for t in 'cm'})" > $O/films_equal.txt ;;
 y)  # the N = 8 code path rehearsed on one GPU: eight gloo ranks sharing the device (tile shards of
     # 1/8, the gather to rank 0, the PSS-MLT film sum, per_rank fields), the default blocks
     b gloo8 900 --gpus 8 --backend gloo --steps 2 --warmup 1 ;;
