@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Per-wave timeline of path_megakernel (experiment build with FRT_EXP_TIMELINE=1,
+"""(Record of round 6, stage x; the FRT_EXP_TIMELINE knob was removed after it.)
+Per-wave timeline of path_megakernel (experiment build with FRT_EXP_TIMELINE=1,
 loaded with FRT_LIB_PATH): its frt_stats ray fields carry sums over waves of
 (entry -> first exhausted grab in shader-clock ticks, the same in 100-MHz
 ticks, first exhausted grab -> exit, entry -> exit): the mean clock of the main
