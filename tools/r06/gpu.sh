@@ -131,6 +131,11 @@ r)  # (record; the knob was removed after it) LDS-DMA touches on the 4-wide plan
      && for l in touch touchc touch3; do FRT_LIB_PATH=$E/libfrt_$l.so timeout -k 10 300 python -u tools/perf_ab.py $F \
             --save-films $O/films_$l.npz > /dev/null 2>> $O/ab.log || exit 1; done \
      && python -c "import numpy as np; a=np.load('$O/films_base.npz'); print({l: bool(np.array_equal(a['default'], np.load('$O/films_'+l+'.npz')['default'])) for l in ('touch','touchc','touch3')})" > $O/films_equal.txt ;;
+aa)  # large frames: 4K at 512 spp and 8K at 128 spp on Cornell (the 32-bit queue, the partial-sum
+    # workspace at 5.7 / 22 GB, RMSE on the bench's pixel sample), then 4K on cornell_1m
+    b c4k 600 --res 3840x2160 --spp 512 --steps 3 --warmup 1 --configs off --north-star off \
+     && b c8k 600 --res 7680x4320 --spp 128 --steps 2 --warmup 1 --configs off --north-star off \
+     && b m4k 900 --scene cornell_1m --res 3840x2160 --spp 256 --steps 2 --warmup 1 --configs off --north-star off ;;
 z)  # (record; the knob was removed after it) the octant node step's store deferred behind the next visit's record reads (libfrt_defer.so,
     # FRT_EXP_DEFER_PUSH) vs the in-tree build: Cornell 512 spp, PSS-MLT, then films of both libraries
     F1="--scene cornell --spp 16 --res 480x270 --rounds 1 --variants default"
