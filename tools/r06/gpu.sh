@@ -131,6 +131,10 @@ r)  # (record; the knob was removed after it) LDS-DMA touches on the 4-wide plan
      && for l in touch touchc touch3; do FRT_LIB_PATH=$E/libfrt_$l.so timeout -k 10 300 python -u tools/perf_ab.py $F \
             --save-films $O/films_$l.npz > /dev/null 2>> $O/ab.log || exit 1; done \
      && python -c "import numpy as np; a=np.load('$O/films_base.npz'); print({l: bool(np.array_equal(a['default'], np.load('$O/films_'+l+'.npz')['default'])) for l in ('touch','touchc','touch3')})" > $O/films_equal.txt ;;
+ab)  # short frames back to back in the bench's timed loop (~0.5 ms between launches): Cornell 1080p
+    # at 64 spp, 20 steps, against perf_ab's launches with the film copied to the host in between
+    b s64 300 --spp 64 --steps 20 --warmup 5 --configs off --north-star off --no-cpu-baseline \
+     && timeout -k 10 300 python -u tools/perf_ab.py --scene cornell --spp 64 --rounds 5 --bvh gsah --variants default > $O/ab_s64.jsonl 2>> $O/ab.log ;;
 aa)  # large frames: 4K at 512 spp and 8K at 128 spp on Cornell (the 32-bit queue, the partial-sum
     # workspace at 5.7 / 22 GB, RMSE on the bench's pixel sample), then 4K on cornell_1m
     b c4k 600 --res 3840x2160 --spp 512 --steps 3 --warmup 1 --configs off --north-star off \
