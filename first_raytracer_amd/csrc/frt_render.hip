@@ -2054,6 +2054,7 @@ static bool params_ok(const frt_render_params *p)
           p->shard_index >= 0 && p->shard_index < p->shard_count && p->max_depth >= -1 && p->max_depth < 100000))
         return false;
     if (p->sample_offset < 0 || (int64_t)p->sample_offset + p->spp > (int64_t)0xffffffffLL) return false;
+    if ((int64_t)p->nx * p->ny > (int64_t)INT32_MAX) return false;   // pixel indices are int32 (frt_shard_slots)
     if (p->flags & kRetiredFlags) return false;         // removed A/B plans: fail loudly, not silently
     if (p->integrator == FRT_INTEGRATOR_PATH || p->integrator == FRT_INTEGRATOR_AO ||
         p->integrator == FRT_INTEGRATOR_NORMALS)
@@ -2485,7 +2486,11 @@ static int render_impl(frt_ctx *c, const frt_render_params *p, float *dev_slots,
         return set_err(c, FRT_E_UNSUPPORTED, "ao integrator: metal has no sampling pdf (constant_pdf::generate)");
     const int T = eff_tile(p);
     const int nmt = my_tiles(p);
-    const uint32_t n_slots = (uint32_t)nmt * T * T;
+    // 32-bit slot indices: params_ok caps the frame at 2^31 - 1 pixels, so a shard's padded
+    // slots stay below 2^32 (checked, not assumed: a wrap would render nothing)
+    const uint64_t n_slots64 = (uint64_t)nmt * T * T;
+    if (n_slots64 >= 0xffffffffULL) return set_err(c, FRT_E_UNSUPPORTED, "frame too large for one call: shard it");
+    const uint32_t n_slots = (uint32_t)n_slots64;
     // kernel variant: stack depth, world kind, LDS-resident scene
     Launcher L;
     const bool f64 = use_f64(c, p);

@@ -158,7 +158,8 @@ typedef struct frt_scene_view {
 } frt_scene_view;
 
 typedef struct frt_render_params {
-    int32_t nx, ny;          /* film size (viewer nx, ny)                                  */
+    int32_t nx, ny;          /* film size (viewer nx, ny); nx * ny <= 2^31 - 1 (int32 pixel
+                              * indices), larger frames fail with FRT_E_INVALID             */
     int32_t spp;             /* samples per pixel (viewer ns)                              */
     uint32_t seed;           /* frame seed of the counter RNG (DESIGN.md "RNG stream spec") */
     int32_t max_depth;       /* scatter while depth <= max_depth; reference: 33 (path.cpp:36) */

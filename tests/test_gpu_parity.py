@@ -359,6 +359,19 @@ def test_edge_cases(ctx, cornell_obj, nx, ny, spp, depth):
         assert rmse(film, ref) <= 5 * RMSE_TOL   # tiny frame: one diverged sample weighs more
 
 
+def test_frame_size_limit_gpu(ctx, cornell_obj):
+    """A frame of 2^31 or more pixels fails before anything is allocated or
+    launched (int32 pixel indices; a wrapped slot count would render nothing);
+    the 1 x 1 frame renders."""
+    import torch
+    ctx.upload(frt.HostScene("cornell_box_obj", cornell_obj, 1.0))
+    buf = torch.zeros(16, dtype=torch.float32, device="cuda")
+    with pytest.raises(frt.FrtError):
+        ctx.render_device(frt.RenderParams.make(46341, 46341, 1), buf.data_ptr())
+    film, st = ctx.render(frt.RenderParams.make(1, 1, 4, seed=3))
+    assert st.samples == 4 and st.pixels == 1 and np.isfinite(film).all()
+
+
 def test_unsupported_material_rejected(ctx, cornell_obj):
     """Material types outside frt.h's FRT_MAT_* set fail loudly at upload."""
     import ctypes

@@ -209,3 +209,12 @@ def test_work_granule_bounded_workspace():
     assert k * 64 * 64 <= 48 * lanes_lds and spi >= 1
     # the caller's samples_per_item wins
     assert frt.work_granule(P, 100, slots_1080, lanes_lds, spi_req=7) == (7, 15)
+
+
+def test_frame_size_limit():
+    """Pixel indices are int32 (frt_shard_slots, the kernels' item state): a
+    frame of 2^31 or more pixels is rejected as bad params, not wrapped."""
+    with pytest.raises(frt.FrtError):
+        frt.shard_slots(frt.RenderParams.make(46341, 46341, 1))          # 2,147,488,281 px
+    assert len(frt.shard_slots(frt.RenderParams.make(64, 48, 1, tile_size=16))) == 64 * 48
+
