@@ -131,6 +131,14 @@ r)  # (record; the knob was removed after it) LDS-DMA touches on the 4-wide plan
      && for l in touch touchc touch3; do FRT_LIB_PATH=$E/libfrt_$l.so timeout -k 10 300 python -u tools/perf_ab.py $F \
             --save-films $O/films_$l.npz > /dev/null 2>> $O/ab.log || exit 1; done \
      && python -c "import numpy as np; a=np.load('$O/films_base.npz'); print({l: bool(np.array_equal(a['default'], np.load('$O/films_'+l+'.npz')['default'])) for l in ('touch','touchc','touch3')})" > $O/films_equal.txt ;;
+ac)  # (record; the knob was removed after it) the 4-wide leaf test two triangles a trip, their loads issued together (libfrt_pairs.so,
+    # FRT_EXP_LEAF_PAIRS) vs the in-tree one-at-a-time loop: cornell_1m 256 spp, films of both
+    F="--scene cornell_1m --spp 16 --res 480x270 --rounds 1 --variants default"
+    for k in 1 2; do ab m "" $M && ab m libfrt_pairs.so $M || exit 1; done \
+     && timeout -k 10 300 python -u tools/perf_ab.py $F --save-films $O/films_base.npz > /dev/null 2>> $O/ab.log \
+     && FRT_LIB_PATH=$E/libfrt_pairs.so timeout -k 10 300 python -u tools/perf_ab.py $F --save-films $O/films_exp.npz > /dev/null 2>> $O/ab.log \
+     && python -c "import numpy as np; a=np.load('$O/films_base.npz'); b=np.load('$O/films_exp.npz'); print({k: bool(np.array_equal(a[k], b[k])) for k in a.files})" > $O/films_equal.txt \
+     && FRT_LIB_PATH=$E/libfrt_pairs.so pt c4 600 tests/test_gpu_c4.py tests/test_gpu_parity.py -m gpu -k "small_frame or bvh4 or config_spp" ;;
 ab)  # short frames back to back in the bench's timed loop (~0.5 ms between launches): Cornell 1080p
     # at 64 spp, 20 steps, against perf_ab's launches with the film copied to the host in between
     b s64 300 --spp 64 --steps 20 --warmup 5 --configs off --north-star off --no-cpu-baseline \
